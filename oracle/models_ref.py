@@ -1,0 +1,215 @@
+"""torch-CPU restatement of the reference hot-path modules (TEST INFRASTRUCTURE ONLY).
+
+Each class / function cites the reference file:line it restates.  Parameter and buffer
+names are kept identical to the reference modules so one state_dict (and one PRNG fill,
+``oracle.prng.fill_state_dict``) drives the reference, this oracle and the HIP product.
+Pinned by ``tests/golden/*.npz`` (produced from the real reference code by
+``tests/golden/make_golden.py``) in ``tests/test_oracle_golden.py``.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .medicalnet_ref import ResNetRef
+
+RESNET_OUT = {10: 512, 18: 512, 34: 512, 50: 2048}
+
+
+def build_conv_seg(hparams, n_in):
+    """Replacement ``conv_seg`` head: anat_cnn.py:33-79 (same in pet_resnet_cnn.py:37-81).
+
+    [BN3d(n_in)] -> [Conv3d 'same' -> [BN3d] -> ReLU -> MaxPool3d(2)]* -> GAP -> Flatten
+    -> [Linear -> [BN1d] -> ReLU]* -> Linear(., C) -> ReLU (sic: logits are >= 0).
+    """
+    mods = []
+    if hparams.get("batchnorm_begin"):
+        mods.append(nn.BatchNorm3d(n_in))
+    if "conv_out" in hparams:
+        for n_out, k in zip(hparams["conv_out"], hparams["filter_size"]):
+            mods.append(nn.Conv3d(n_in, n_out, k, padding="same"))
+            if hparams["batchnorm_conv"]:
+                mods.append(nn.BatchNorm3d(n_out))
+            mods += [nn.ReLU(), nn.MaxPool3d(2)]
+            n_in = n_out
+    mods += [nn.AdaptiveAvgPool3d(1), nn.Flatten()]
+    for n_out in hparams["linear_out"]:
+        mods.append(nn.Linear(n_in, n_out))
+        if hparams.get("batchnorm_dense"):
+            mods.append(nn.BatchNorm1d(n_out))
+        mods.append(nn.ReLU())
+        n_in = n_out
+    mods += [nn.Linear(n_in, hparams["n_classes"]), nn.ReLU()]
+    return nn.Sequential(*mods)
+
+
+class FocalLossRef(nn.Module):
+    """pkg/loss_functions/focalloss.py:10-39 with alpha=None (every caller).
+
+    logpt = log_softmax(x)[y]; pt = exp(logpt) DETACHED (focalloss.py:29,
+    ``Variable(logpt.data.exp())``); loss = mean(-(1 - pt)**gamma * logpt).
+    """
+
+    def __init__(self, gamma=0):
+        super().__init__()
+        self.gamma = gamma
+
+    def forward(self, x, y):
+        logpt = F.log_softmax(x, dim=1).gather(1, y.view(-1, 1)).view(-1)
+        pt = logpt.detach().exp()
+        return (-1 * (1 - pt) ** self.gamma * logpt).mean()
+
+
+def make_criterion(hparams):
+    """anat_cnn.py:81-85: focal loss iff hparams['fl_gamma'] is truthy, else weighted CE."""
+    if hparams.get("fl_gamma"):
+        return FocalLossRef(hparams["fl_gamma"])
+    return nn.CrossEntropyLoss(weight=hparams["loss_class_weights"])
+
+
+class _StepMixin:
+    batch_key = "mri"
+
+    def general_step(self, batch, batch_idx=0, mode="train"):
+        """anat_cnn.py:99-109: unsqueeze(1), cast fp32, forward, cast logits fp64, loss."""
+        x = batch[self.batch_key].unsqueeze(1).to(dtype=torch.float32)
+        y = batch["label"]
+        y_hat = self(x).to(dtype=torch.double)
+        return {"loss": self.criterion(y_hat, y), "outputs": y_hat, "labels": y}
+
+
+class AnatCNNRef(_StepMixin, nn.Module):
+    """Anat_CNN (pkg/models/mri_models/anat_cnn.py:13-109) on the MedicalNet restatement."""
+
+    def __init__(self, hparams):
+        super().__init__()
+        self.hparams = dict(hparams)
+        self.model = ResNetRef(hparams["resnet_depth"])
+        self.model.conv_seg = build_conv_seg(hparams, RESNET_OUT[hparams["resnet_depth"]])
+        self.criterion = make_criterion(hparams)
+
+    def forward(self, x):
+        return self.model(x)
+
+
+class PETResNetRef(AnatCNNRef):
+    """PET_CNN_ResNet (pkg/models/pet_models/pet_resnet_cnn.py:12-138): same net, PET key."""
+    batch_key = "pet1451"
+
+
+class SmallPETCNNRef(_StepMixin, nn.Module):
+    """Small_PET_CNN (pkg/models/pet_models/pet_cnn.py:10-70); always weighted CE (:47-48)."""
+    batch_key = "pet1451"
+
+    def __init__(self, hparams):
+        super().__init__()
+        self.hparams = dict(hparams)
+        mods = []
+        n_in = 1
+        n_out = None
+        for n_out, k in zip(hparams["conv_out"], hparams["filter_size"]):
+            mods.append(nn.Conv3d(n_in, n_out, k, padding="same"))
+            if hparams.get("batchnorm"):
+                mods.append(nn.BatchNorm3d(n_out))
+            mods += [nn.ReLU(), nn.MaxPool3d(2)]
+            if "dropout_conv_p" in hparams:
+                mods.append(nn.Dropout(p=hparams["dropout_conv_p"]))
+            n_in = n_out
+        mods += [nn.AdaptiveAvgPool3d(1), nn.Flatten()]
+        if hparams.get("linear_out"):
+            n_out = hparams["linear_out"]
+            if "dropout_dense_p" in hparams:
+                mods.append(nn.Dropout(p=hparams["dropout_dense_p"]))
+            mods += [nn.Linear(n_in, n_out), nn.ReLU()]
+        mods.append(nn.Linear(n_out, hparams["n_classes"]))
+        self.model = nn.Sequential(*mods)
+        self.criterion = nn.CrossEntropyLoss(weight=hparams["loss_class_weights"])
+
+    def forward(self, x):
+        return self.model(x)
+
+
+class AnatPETCNNRef(nn.Module):
+    """Anat_PET_CNN late fusion (pkg/models/fusion_models/anat_pet_fusion.py:11-92).
+
+    ``model_pet`` is a stage-1 Small_PET_CNN cut after GAP+Flatten(+Linear/ReLU)
+    (:28-31), ``model_mri`` a stage-1 Anat_CNN whose conv_seg is cut to [:2] (:32);
+    head: cat(pet 64, reduce_dim_mri(512->64)+ReLU) -> Linear(128,64) -> ReLU ->
+    Linear(64,C) (:42-51), no final ReLU.
+    """
+
+    def __init__(self, hparams, pet_stage1, mri_stage1):
+        super().__init__()
+        self.hparams = dict(hparams)
+        if hparams["n_classes"] == 2:
+            self.model_pet = pet_stage1.model[:-3]
+        else:
+            self.model_pet = pet_stage1.model[:-1]
+        self.model_mri = mri_stage1
+        self.model_mri.model.conv_seg = self.model_mri.model.conv_seg[:2]
+        self.stage2out = nn.Linear(128, 64)
+        self.cls2 = nn.Linear(64, hparams["n_classes"])
+        self.relu = nn.ReLU()
+        self.reduce_dim_mri = nn.Sequential(nn.Linear(512, 64), self.relu)
+        self.model_fuse = nn.Sequential(self.stage2out, self.relu, self.cls2)
+        self.criterion = make_criterion(hparams)
+
+    def forward(self, x_pet, x_mri):
+        bs = x_mri.shape[0]
+        out_pet = self.model_pet(x_pet)
+        out_mri = self.reduce_dim_mri(self.model_mri(x_mri).view(bs, -1))
+        return self.model_fuse(torch.cat((out_pet, out_mri), dim=1))
+
+    def general_step(self, batch, batch_idx=0, mode="train"):
+        """anat_pet_fusion.py:80-92."""
+        x_pet = batch["pet1451"].unsqueeze(1).to(dtype=torch.float32)
+        x_mri = batch["mri"].unsqueeze(1).to(dtype=torch.float32)
+        y = batch["label"]
+        y_hat = self(x_pet, x_mri).to(dtype=torch.double)
+        return {"loss": self.criterion(y_hat, y), "outputs": y_hat, "labels": y}
+
+
+class ResNetPairFusionRef(nn.Module):
+    """BUILD EXTENSION (BASELINE config 3/4): "ResNet-10 x2 + MLP head".
+
+    Both branches are stage-1 ResNet models cut to conv_seg[:2] (512-d), each reduced
+    by Linear(512,64)+ReLU (mirroring ``reduce_dim_mri``, anat_pet_fusion.py:49), then
+    the unchanged Anat_PET_CNN head (anat_pet_fusion.py:42-51).  No reference parity.
+    """
+
+    def __init__(self, hparams, pet_stage1, mri_stage1):
+        super().__init__()
+        self.hparams = dict(hparams)
+        self.model_pet = pet_stage1
+        self.model_pet.model.conv_seg = self.model_pet.model.conv_seg[:2]
+        self.model_mri = mri_stage1
+        self.model_mri.model.conv_seg = self.model_mri.model.conv_seg[:2]
+        self.stage2out = nn.Linear(128, 64)
+        self.cls2 = nn.Linear(64, hparams["n_classes"])
+        self.relu = nn.ReLU()
+        self.reduce_dim_pet = nn.Sequential(nn.Linear(512, 64), self.relu)
+        self.reduce_dim_mri = nn.Sequential(nn.Linear(512, 64), self.relu)
+        self.model_fuse = nn.Sequential(self.stage2out, self.relu, self.cls2)
+        self.criterion = make_criterion(hparams)
+
+    def forward(self, x_pet, x_mri):
+        bs = x_mri.shape[0]
+        out_pet = self.reduce_dim_pet(self.model_pet(x_pet).view(bs, -1))
+        out_mri = self.reduce_dim_mri(self.model_mri(x_mri).view(bs, -1))
+        return self.model_fuse(torch.cat((out_pet, out_mri), dim=1))
+
+    general_step = AnatPETCNNRef.general_step
+
+
+def adam_param_groups(model, hparams):
+    """anat_cnn.py:111-136: head lr = lr; backbone lr = lr_pretrained or frozen."""
+    groups = []
+    for name, p in model.model.named_parameters():
+        if "conv_seg" in name:
+            groups.append({"params": p, "lr": hparams["lr"]})
+        elif not hparams.get("lr_pretrained"):
+            p.requires_grad = False
+            groups.append({"params": p})
+        else:
+            p.requires_grad = True
+            groups.append({"params": p, "lr": hparams["lr_pretrained"]})
+    return groups

@@ -1,0 +1,93 @@
+"""Helpers shared by the parity tests: rebuild the golden cases' models and batches."""
+import os
+
+import numpy as np
+import torch
+
+from oracle import prng, models_ref
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+W2 = [0.20314960629921264, 0.7968503937007874]
+W3 = [0.4651162790697675, 0.6712473572938689, 0.8636363636363636]
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False))
+
+
+def anat_hparams(depth=10, n_classes=2, **kw):
+    h = {"n_classes": n_classes, "resnet_depth": depth, "conv_out": [], "filter_size": [],
+         "batchnorm_begin": False, "batchnorm_dense": False, "linear_out": [],
+         "fl_gamma": None, "lr": 1e-3, "lr_pretrained": 1e-5, "l2_reg": 0,
+         "reduce_factor_lr_schedule": None, "gpu_id": "0",
+         "loss_class_weights": torch.tensor(W2 if n_classes == 2 else W3, dtype=torch.double)}
+    h.update(kw)
+    return h
+
+
+def pet_hparams(n_classes=2, **kw):
+    h = {"n_classes": n_classes, "conv_out": (8, 16, 32, 64), "filter_size": (5, 5, 3, 3),
+         "batchnorm": False, "linear_out": 64, "lr": 1e-3, "reduce_factor_lr_schedule": None,
+         "loss_class_weights": torch.tensor(W2 if n_classes == 2 else W3, dtype=torch.double)}
+    h.update(kw)
+    return h
+
+
+def batch_for(shape, n_classes, seed, keys=("mri",)):
+    b = {"label": torch.from_numpy(prng.labels(seed + 7, shape[0], n_classes))}
+    for i, k in enumerate(keys):
+        gen = prng.mri_volume if k == "mri" else prng.pet_volume
+        b[k] = torch.from_numpy(gen(seed + i, shape)).double()
+    return b
+
+
+def load_prng_weights(model, seed):
+    sd = model.state_dict()
+    vals = prng.fill_state_dict(sd, seed)
+    with torch.no_grad():
+        for k, v in vals.items():
+            sd[k].copy_(torch.from_numpy(v))
+
+
+# name -> (hparams-builder, kind, batch seed, keys); weights seed = fixture 'seed'
+CASES = {
+    "anat_r10_32": (lambda: anat_hparams(10), "anat", 12, ("mri",)),
+    "anat_r10_64": (lambda: anat_hparams(10), "anat", 13, ("mri",)),
+    "anat_r18_head": (lambda: anat_hparams(18, n_classes=3, batchnorm_begin=True,
+                                           batchnorm_dense=True, linear_out=[64, 32],
+                                           fl_gamma=2), "anat", 14, ("mri",)),
+    "anat_r10_focal": (lambda: anat_hparams(10, fl_gamma=5, linear_out=[128]), "anat", 15,
+                       ("mri",)),
+    "pet_resnet_r10": (lambda: anat_hparams(10, fl_gamma=1), "petres", 16, ("pet1451",)),
+    "small_pet": (lambda: pet_hparams(), "smallpet", 18, ("pet1451",)),
+    "small_pet_bn3": (lambda: pet_hparams(n_classes=3, batchnorm=True, conv_out=(16, 32, 64),
+                                          filter_size=(7, 5, 3), linear_out=32),
+                      "smallpet", 20, ("pet1451",)),
+    "anat_pet_fusion": (lambda: anat_hparams(10, fl_gamma=2), "fusion", 22,
+                        ("pet1451", "mri")),
+}
+
+
+def build_oracle(name):
+    hp_fn, kind, _, _ = CASES[name]
+    h = hp_fn()
+    if kind == "anat":
+        return models_ref.AnatCNNRef(h)
+    if kind == "petres":
+        m = models_ref.PETResNetRef(h)
+        return m
+    if kind == "smallpet":
+        return models_ref.SmallPETCNNRef(h)
+    if kind == "fusion":
+        pet = models_ref.SmallPETCNNRef(pet_hparams())
+        mri = models_ref.AnatCNNRef(anat_hparams(10))
+        return models_ref.AnatPETCNNRef(h, pet, mri)
+    raise KeyError(kind)
+
+
+def batch_of(name, g):
+    _, _, bseed, keys = CASES[name]
+    shape = tuple(int(v) for v in g["shape"])
+    n_classes = g["train_logits"].shape[1]
+    return batch_for(shape, n_classes, bseed, keys)

@@ -1,0 +1,281 @@
+"""Generate golden vectors from the REAL reference code (run in the build container only).
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+
+The reference (``/root/reference``, read-only) is imported as a Python package; nothing
+of it is copied.  Its missing third-party dependencies are replaced by the minimal stubs
+below (pytorch_lightning / torchmetrics / torchvision / seaborn: bookkeeping only, no
+arithmetic) and by the oracle's MedicalNet restatement (``oracle/medicalnet_ref.py``),
+because MedicalNet is un-vendored and absent offline.
+
+Every weight, volume and label comes from ``oracle.prng`` so the fixtures hold only
+seeds, shapes and outputs.  The files are data (inputs and expected outputs); the
+reference source never leaves this container.
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+from oracle import prng, medicalnet_ref  # noqa: E402
+
+W2 = [0.20314960629921264, 0.7968503937007874]              # pkg/inference/test_tab.py:25-28
+W3 = [0.4651162790697675, 0.6712473572938689, 0.8636363636363636]   # test_tab.py:36-40
+
+
+def install_stubs():
+    """Bookkeeping-only stand-ins for packages the reference imports but this image lacks."""
+    pl = types.ModuleType("pytorch_lightning")
+
+    class LightningModule(nn.Module):
+        def save_hyperparameters(self, hparams, ignore=()):
+            object.__setattr__(self, "hparams", {k: v for k, v in hparams.items()
+                                                 if k not in ignore})
+
+        def log(self, *a, **k):
+            pass
+
+        def log_dict(self, *a, **k):
+            pass
+
+    pl.LightningModule = LightningModule
+    sys.modules["pytorch_lightning"] = pl
+
+    tm = types.ModuleType("torchmetrics")
+    tmc = types.ModuleType("torchmetrics.classification")
+
+    class _Metric:
+        def __init__(self, *a, **k):
+            pass
+
+        def __call__(self, *a, **k):
+            return None
+
+        def to(self, *a, **k):
+            return self
+
+    for n in ("MulticlassF1Score", "MulticlassMatthewsCorrCoef", "MulticlassConfusionMatrix"):
+        setattr(tmc, n, _Metric)
+    tm.classification = tmc
+    tm.ConfusionMatrix = _Metric
+    sys.modules["torchmetrics"] = tm
+    sys.modules["torchmetrics.classification"] = tmc
+    for n in ("torchvision", "seaborn"):
+        sys.modules[n] = types.ModuleType(n)
+
+    mn = types.ModuleType("MedicalNet")
+    mn_model = types.ModuleType("MedicalNet.model")
+    mn_setting = types.ModuleType("MedicalNet.setting")
+    mn_model.generate_model = medicalnet_ref.generate_model
+    mn_setting.parse_opts = medicalnet_ref.parse_opts
+    mn.model, mn.setting = mn_model, mn_setting
+    sys.modules.update({"MedicalNet": mn, "MedicalNet.model": mn_model,
+                        "MedicalNet.setting": mn_setting})
+    os.environ.setdefault("CUDA_VISIBLE_DEVICES", "0")   # anat_cnn.py:20-24 insists
+    sys.path.insert(0, REF)
+
+
+def load_prng_weights(model, seed):
+    sd = model.state_dict()
+    vals = prng.fill_state_dict(sd, seed)
+    with torch.no_grad():
+        for k, v in vals.items():
+            sd[k].copy_(torch.from_numpy(v))
+
+
+def summarize(prefix, name, t, out, full_limit=4096):
+    a = t.detach().double().numpy().ravel()
+    if a.size <= full_limit:
+        out[f"{prefix}full/{name}"] = a
+    else:
+        out[f"{prefix}head/{name}"] = a[:256].copy()
+        out[f"{prefix}stats/{name}"] = np.array([a.sum(), np.abs(a).sum(), np.sqrt((a * a).sum())])
+
+
+def run_case(model, batch, out):
+    """eval logits on fresh weights, then one train-mode general_step + backward."""
+    model.eval()
+    with torch.no_grad():
+        out["eval_logits"] = model.general_step(batch, 0, "val")["outputs"].numpy()
+    model.train()
+    res = model.general_step(batch, 0, "train")
+    res["loss"].backward()
+    out["train_logits"] = res["outputs"].detach().numpy()
+    out["train_loss"] = np.array(res["loss"].item())
+    for name, p in model.named_parameters():
+        if p.grad is not None:
+            summarize("grad/", name, p.grad, out)
+    for name, b in model.named_buffers():
+        if "running" in name:
+            summarize("buf/", name, b, out)
+    out["state_dict_keys"] = np.array(list(model.state_dict().keys()))
+
+
+def batch_for(shape, n_classes, seed, keys=("mri",)):
+    b = {"label": torch.from_numpy(prng.labels(seed + 7, shape[0], n_classes))}
+    for i, k in enumerate(keys):
+        gen = prng.mri_volume if k == "mri" else prng.pet_volume
+        b[k] = torch.from_numpy(gen(seed + i, shape)).double()   # dataloader yields f64
+    return b
+
+
+def anat_hparams(depth=10, n_classes=2, **kw):
+    h = {"n_classes": n_classes, "resnet_depth": depth, "conv_out": [], "filter_size": [],
+         "batchnorm_begin": False, "batchnorm_dense": False, "linear_out": [],
+         "fl_gamma": None, "lr": 1e-3, "lr_pretrained": 1e-5, "l2_reg": 0,
+         "reduce_factor_lr_schedule": None, "gpu_id": "0",
+         "loss_class_weights": torch.tensor(W2 if n_classes == 2 else W3, dtype=torch.double)}
+    h.update(kw)
+    return h
+
+
+def pet_hparams(n_classes=2, **kw):
+    h = {"n_classes": n_classes, "conv_out": (8, 16, 32, 64), "filter_size": (5, 5, 3, 3),
+         "batchnorm": False, "linear_out": 64, "lr": 1e-3, "reduce_factor_lr_schedule": None,
+         "loss_class_weights": torch.tensor(W2 if n_classes == 2 else W3, dtype=torch.double)}
+    h.update(kw)
+    return h
+
+
+CASES = {}
+
+
+def case(fn):
+    CASES[fn.__name__] = fn
+    return fn
+
+
+@case
+def losses():
+    from pkg.loss_functions.focalloss import FocalLoss
+    out = {}
+    for C in (2, 3):
+        x0 = (prng.uniform(100 + C, 8 * C).astype(np.float64) * 6.0 - 3.0).reshape(8, C)
+        y = torch.from_numpy(prng.labels(200 + C, 8, C))
+        out[f"x_C{C}"], out[f"y_C{C}"] = x0, y.numpy()
+        for g in (0, 1, 2, 5):
+            x = torch.tensor(x0, requires_grad=True)
+            loss = FocalLoss(gamma=g)(x, y)
+            loss.backward()
+            out[f"focal_g{g}_C{C}_loss"] = np.array(loss.item())
+            out[f"focal_g{g}_C{C}_grad"] = x.grad.numpy()
+        w = torch.tensor(W2 if C == 2 else W3, dtype=torch.double)
+        x = torch.tensor(x0, requires_grad=True)
+        loss = nn.CrossEntropyLoss(weight=w)(x, y)
+        loss.backward()
+        out[f"ce_C{C}_loss"] = np.array(loss.item())
+        out[f"ce_C{C}_grad"] = x.grad.numpy()
+    # ReLU'd logits with exact ties (anat_cnn.py:76-77): argmax must take the first index
+    t = torch.tensor([[0.0, 0.0], [0.3, 0.0], [0.0, 0.7], [0.5, 0.5]])
+    out["tie_logits"], out["tie_argmax"] = t.numpy(), torch.argmax(t, 1).numpy()
+    return out
+
+
+def _anat(depth, size, bsz, seed, **kw):
+    from pkg.models.mri_models.anat_cnn import Anat_CNN
+    torch.manual_seed(0)
+    m = Anat_CNN(anat_hparams(depth, **kw))
+    load_prng_weights(m, seed)
+    out = {"seed": np.array(seed), "shape": np.array([bsz, size, size, size])}
+    run_case(m, batch_for((bsz, size, size, size), m.hparams["n_classes"], seed + 1), out)
+    return out
+
+
+@case
+def anat_r10_32():
+    return _anat(10, 32, 2, 11)
+
+
+@case
+def anat_r10_64():                           # BASELINE config 1 (CPU plumbing config)
+    return _anat(10, 64, 2, 12)
+
+
+@case
+def anat_r18_head():
+    return _anat(18, 32, 4, 13, n_classes=3, batchnorm_begin=True, batchnorm_dense=True,
+                 linear_out=[64, 32], fl_gamma=2)
+
+
+@case
+def anat_r10_focal():
+    return _anat(10, 32, 3, 14, fl_gamma=5, linear_out=[128])
+
+
+@case
+def pet_resnet_r10():
+    from pkg.models.pet_models.pet_resnet_cnn import PET_CNN_ResNet
+    m = PET_CNN_ResNet(anat_hparams(10, fl_gamma=1))
+    load_prng_weights(m, 15)
+    out = {"seed": np.array(15), "shape": np.array([2, 32, 32, 32])}
+    run_case(m, batch_for((2, 32, 32, 32), 2, 16, keys=("pet1451",)), out)
+    return out
+
+
+@case
+def small_pet():
+    from pkg.models.pet_models.pet_cnn import Small_PET_CNN
+    m = Small_PET_CNN(pet_hparams())
+    load_prng_weights(m, 17)
+    out = {"seed": np.array(17), "shape": np.array([2, 32, 32, 32])}
+    run_case(m, batch_for((2, 32, 32, 32), 2, 18, keys=("pet1451",)), out)
+    return out
+
+
+@case
+def small_pet_bn3():
+    from pkg.models.pet_models.pet_cnn import Small_PET_CNN
+    m = Small_PET_CNN(pet_hparams(n_classes=3, batchnorm=True, conv_out=(16, 32, 64),
+                                  filter_size=(7, 5, 3), linear_out=32))
+    load_prng_weights(m, 19)
+    out = {"seed": np.array(19), "shape": np.array([2, 32, 32, 32])}
+    run_case(m, batch_for((2, 32, 32, 32), 3, 20, keys=("pet1451",)), out)
+    return out
+
+
+@case
+def anat_pet_fusion():
+    from pkg.models.pet_models.pet_cnn import Small_PET_CNN
+    from pkg.models.mri_models.anat_cnn import Anat_CNN
+    from pkg.models.fusion_models.anat_pet_fusion import Anat_PET_CNN
+    stage1 = {"pet.ckpt": (Small_PET_CNN, pet_hparams()),
+              "mri.ckpt": (Anat_CNN, anat_hparams(10))}
+    orig = {c: c.__dict__.get("load_from_checkpoint") for c in (Small_PET_CNN, Anat_CNN)}
+    for cls in (Small_PET_CNN, Anat_CNN):
+        cls.load_from_checkpoint = classmethod(
+            lambda c, path, **kw: stage1[path][0](stage1[path][1]))
+    try:
+        h = anat_hparams(10, fl_gamma=2, path_pet="pet.ckpt", path_mri="mri.ckpt")
+        m = Anat_PET_CNN(h)
+    finally:
+        for c, f in orig.items():
+            if f is None:
+                del c.load_from_checkpoint
+    load_prng_weights(m, 21)
+    out = {"seed": np.array(21), "shape": np.array([2, 32, 32, 32])}
+    run_case(m, batch_for((2, 32, 32, 32), 2, 22, keys=("pet1451", "mri")), out)
+    return out
+
+
+def main(names=None):
+    install_stubs()
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    for name, fn in CASES.items():
+        if names and name not in names:
+            continue
+        out = fn()
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **out)
+        print(f"{name}: {len(out)} arrays -> {os.path.getsize(path) / 1024:.1f} KiB")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or None)

@@ -1,0 +1,81 @@
+"""Pin the CPU oracle against golden vectors produced by the real reference code.
+
+The fixtures were written by tests/golden/make_golden.py, which imports the reference
+``pkg`` modules (anat_cnn.py, pet_cnn.py, pet_resnet_cnn.py, anat_pet_fusion.py,
+focalloss.py) in the build container.  CPU only; no GPU needed.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import models_ref
+from tests import _golden as G
+
+TOL = dict(rtol=2e-5, atol=2e-6)
+
+
+def run_oracle(name):
+    g = G.load(name)
+    m = G.build_oracle(name)
+    G.load_prng_weights(m, int(g["seed"]))
+    batch = G.batch_of(name, g)
+    out = {}
+    m.eval()
+    with torch.no_grad():
+        out["eval_logits"] = m.general_step(batch, 0, "val")["outputs"].numpy()
+    m.train()
+    res = m.general_step(batch, 0, "train")
+    res["loss"].backward()
+    out["train_logits"] = res["outputs"].detach().numpy()
+    out["train_loss"] = res["loss"].item()
+    return g, m, out
+
+
+@pytest.mark.parametrize("name", list(G.CASES))
+def test_oracle_matches_reference(name):
+    g, m, out = run_oracle(name)
+    assert list(m.state_dict().keys()) == list(g["state_dict_keys"])
+    np.testing.assert_allclose(out["eval_logits"], g["eval_logits"], **TOL)
+    np.testing.assert_allclose(out["train_logits"], g["train_logits"], **TOL)
+    np.testing.assert_allclose(out["train_loss"], g["train_loss"], rtol=1e-6)
+    assert (out["train_logits"].argmax(1) == g["train_logits"].argmax(1)).all()
+    params = dict(m.named_parameters())
+    buffers = dict(m.named_buffers())
+    n_checked = 0
+    for key in g:
+        kind, _, rest = key.partition("/")
+        if kind not in ("grad", "buf"):
+            continue
+        sub, _, pname = rest.partition("/")
+        t = params[pname].grad if kind == "grad" else buffers[pname]
+        a = t.detach().double().numpy().ravel()
+        if sub == "full":
+            np.testing.assert_allclose(a, g[key], rtol=1e-4, atol=1e-6, err_msg=key)
+        elif sub == "head":
+            np.testing.assert_allclose(a[:256], g[key], rtol=1e-4, atol=1e-6, err_msg=key)
+        else:
+            ref = g[key]
+            got = np.array([a.sum(), np.abs(a).sum(), np.sqrt((a * a).sum())])
+            np.testing.assert_allclose(got[1:], ref[1:], rtol=1e-4, err_msg=key)
+            np.testing.assert_allclose(got[0], ref[0], rtol=1e-3, atol=1e-4 * ref[1], err_msg=key)
+        n_checked += 1
+    assert n_checked > 3
+
+
+@pytest.mark.parametrize("C", [2, 3])
+@pytest.mark.parametrize("gamma", [0, 1, 2, 5])
+def test_focal_oracle(C, gamma):
+    g = G.load("losses")
+    x = torch.tensor(g[f"x_C{C}"], requires_grad=True)
+    y = torch.from_numpy(g[f"y_C{C}"])
+    loss = models_ref.FocalLossRef(gamma)(x, y)
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), g[f"focal_g{gamma}_C{C}_loss"], rtol=1e-13)
+    np.testing.assert_allclose(x.grad.numpy(), g[f"focal_g{gamma}_C{C}_grad"], rtol=1e-12,
+                               atol=1e-15)
+
+
+def test_tie_argmax_first_index():
+    g = G.load("losses")
+    assert (torch.from_numpy(g["tie_logits"]).argmax(1).numpy() == g["tie_argmax"]).all()
+    assert list(g["tie_argmax"]) == [0, 0, 1, 0]
