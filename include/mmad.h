@@ -1,0 +1,162 @@
+/*
+ * mmad.h -- C ABI of libmmad_hip.so, the MI355X (gfx950) kernels behind the
+ * multimodal_alzheimer 3D-volume training hot path.
+ *
+ * The reference (Liz490/multimodal_alzheimer) is pure Python: its hot path is the
+ * torch.nn call chain of MedicalNet's 3D-ResNet + the reference heads and losses.
+ * Each entry point below replaces one op of that chain; the reference call site it
+ * stands in for is cited next to it (paths relative to the reference root).  There
+ * is no reference FFI to mirror, so the binding is ctypes (INTEGRATION.md shows it).
+ *
+ * Conventions
+ *   - Every function is asynchronous on the caller's HIP stream (`stream`, a
+ *     hipStream_t passed as void*; NULL = the legacy default stream) and returns an
+ *     int status: MMAD_OK, one of the MMAD_E* codes, or MMAD_EHIP + hipError_t.
+ *   - The library never allocates, frees or synchronises device memory and keeps no
+ *     mutable global state: every buffer (including workspaces sized by the
+ *     *_workspace / *_parts queries) is owned by the caller.
+ *   - Activations are NDHWC ("voxel-major": channels contiguous per voxel) in the
+ *     compute dtype (MMAD_F32 or MMAD_BF16); a logical (N,C,D,H,W) torch tensor in
+ *     torch.channels_last_3d memory format is exactly this layout.
+ *   - Conv weights enter in the torch layout [Co][Ci][kd][kh][kw] fp32 and are packed
+ *     per step (mmad_conv_pack_weight); weight gradients leave in the same torch
+ *     layout, fp32.  BN statistics, scale/shift and all reductions are fp32 (f64 for
+ *     the final per-channel sums); logits and the loss are f64 as in the reference
+ *     (pkg/models/mri_models/anat_cnn.py:104).
+ */
+#ifndef MMAD_H
+#define MMAD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { MMAD_OK = 0, MMAD_EBADSHAPE = 1001, MMAD_EBADDTYPE = 1002, MMAD_ENULL = 1003,
+       MMAD_EUNSUPPORTED = 1004, MMAD_EHIP = 2000 };
+
+enum { MMAD_F32 = 0, MMAD_BF16 = 1, MMAD_F64 = 2 };
+
+/* One 3D convolution (torch.nn.Conv3d semantics, groups = 1).  `do_` is the output
+ * depth (`do` is a C keyword). */
+typedef struct mmad_conv_desc {
+  int32_t n;
+  int32_t ci, di, hi, wi;
+  int32_t co, do_, ho, wo;
+  int32_t kd, kh, kw;
+  int32_t sd, sh, sw;
+  int32_t pd, ph, pw;
+  int32_t dd, dh, dw;
+} mmad_conv_desc;
+
+int mmad_abi_version(void);                 /* == MMAD_ABI_VERSION */
+#define MMAD_ABI_VERSION 1
+const char* mmad_strerror(int status);
+
+/* ---- 3D convolution as MFMA implicit GEMM --------------------------------------
+ * Replaces nn.Conv3d forward/backward: MedicalNet conv1 / BasicBlock / Bottleneck /
+ * shortcut-B convs (used at pkg/models/mri_models/anat_cnn.py:29-31,
+ * pet_resnet_cnn.py:33-35), the 'same'-padded head convs (anat_cnn.py:55-63) and the
+ * Small_PET_CNN convs (pkg/models/pet_models/pet_cnn.py:20-22).
+ * Requirements: ci % 8 == 0 or ci == 1; co % 8 == 0 for dgrad; channel counts powers
+ * of two.  ci == 1 convs run on a W-unfolded input: x must be the output of
+ * mmad_conv_unfold_input (layout [n][di][hi][wo][8]).                              */
+int64_t mmad_conv_packed_elems(const mmad_conv_desc* d, int dtype, int for_dgrad);
+int mmad_conv_pack_weight(const mmad_conv_desc* d, int dtype, const float* w,
+                          void* w_packed, int for_dgrad, void* stream);
+int64_t mmad_conv_unfolded_elems(const mmad_conv_desc* d);
+int mmad_conv_unfold_input(const mmad_conv_desc* d, int in_dtype, const void* x,
+                           int dtype, void* x_unf, void* stream);
+/* rows of the BN-statistics partial buffer written by mmad_conv3d_fwd: [rows][2][co] */
+int64_t mmad_conv3d_stats_rows(const mmad_conv_desc* d, int dtype);
+int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x,
+                    const void* w_packed, const float* bias, void* y, float* stats,
+                    void* stream);
+int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy,
+                      const void* w_packed_t, void* dx, void* stream);
+int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype); /* bytes */
+int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,
+                      float* dw, float* dbias, void* workspace, void* stream);
+
+/* ---- BatchNorm3d / BatchNorm1d (+ fused ReLU and residual add) -------------------
+ * Replaces nn.BatchNorm3d/1d + nn.ReLU + the residual `out += residual; relu`
+ * of MedicalNet BasicBlock, the stem bn1+relu, and the head BNs
+ * (anat_cnn.py:50-51, :69-70).  torch semantics: biased batch variance to normalise,
+ * unbiased variance into running_var, momentum update.  Layout [m][c], m = N*D*H*W.  */
+int64_t mmad_bn_stats_parts(int64_t m, int c);
+int mmad_bn_stats(int dtype, int64_t m, int c, const void* y, float* parts, void* stream);
+int mmad_bn_finalize(int c, int64_t count, int nparts, const float* parts,
+                     const float* gamma, const float* beta, float* running_mean,
+                     float* running_var, float momentum, float eps, int training,
+                     float* mean, float* invstd, float* scale, float* shift, void* stream);
+/* out = act(y*scale + shift + R), R = res*rscale + rshift | res | 0; act = relu|id */
+int mmad_scale_shift_act(int dtype, int64_t m, int c, const void* y, const float* scale,
+                         const float* shift, const void* res, const float* rscale,
+                         const float* rshift, int relu, void* out, void* stream);
+int64_t mmad_bn_bwd_parts(int64_t m, int c);
+/* partial sums of g' and g'*xhat with g' = g * (relu_out > 0 | 1) */
+int mmad_bn_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* relu_out,
+                       const void* y, const float* mean, const float* invstd,
+                       float* parts, void* stream);
+/* dgamma, dbeta (fp32, may be NULL) and the apply coefficients for mmad_bn_bwd_apply */
+int mmad_bn_bwd_finalize(int c, int64_t count, int nparts, const float* parts,
+                         const float* gamma, const float* invstd, int training,
+                         float* dgamma, float* dbeta, float* coef, void* stream);
+/* dy = coef0[c]*g' - coef1[c] - xhat*coef2[c]; optionally also gmask_out = g' */
+int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* relu_out,
+                      const void* y, const float* mean, const float* invstd,
+                      const float* coef, void* dy, void* gmask_out, void* stream);
+int mmad_relu_fwd(int dtype, int64_t n, const void* x, void* y, void* stream);
+int mmad_relu_bwd(int dtype, int64_t n, const void* g, const void* out, void* dx, void* stream);
+int mmad_add(int dtype, int64_t n, const void* a, const void* b, void* out, void* stream);
+
+/* ---- pooling -------------------------------------------------------------------
+ * MaxPool3d(3,2,1) stem pool and MaxPool3d(2) head/PET pools (pet_cnn.py:26),
+ * AdaptiveAvgPool3d(1) (anat_cnn.py:66, pet_cnn.py:33).  Max-pool ties resolve to the
+ * first window position in (kd,kh,kw) scan order, as torch's CPU kernel does.       */
+int mmad_colsum_ws(int dtype, int64_t m, int c, const void* y, float* parts, float* out,
+                   void* stream);   /* out[c] = sum_m y[m][c]; parts: bn_stats_parts rows */
+int mmad_maxpool3d_fwd(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho,
+                       int wo, int k, int s, int p, const void* x, void* y,
+                       uint8_t* argmax, void* stream);
+int mmad_maxpool3d_bwd(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho,
+                       int wo, int k, int s, int p, const void* dy, const uint8_t* argmax,
+                       void* dx, void* stream);
+int mmad_gap_fwd(int dtype, int n, int64_t s, int c, const void* x, float* y, void* stream);
+int mmad_gap_bwd(int dtype, int n, int64_t s, int c, const float* dy, void* dx, void* stream);
+
+/* ---- fusion / classifier MLP head (fp32) ----------------------------------------
+ * nn.Linear (+ReLU) of conv_seg (anat_cnn.py:68-76), reduce_dim_mri / stage2out /
+ * cls2 of Anat_PET_CNN (pkg/models/fusion_models/anat_pet_fusion.py:42-51) and the
+ * concat of the two branch features (anat_pet_fusion.py:76).                       */
+int mmad_linear_fwd(int b, int in, int out, const float* x, const float* w,
+                    const float* bias, int relu, float* y, void* stream);
+int mmad_linear_bwd(int b, int in, int out, const float* x, const float* w,
+                    const float* dy, float* dx, float* dw, float* dbias, void* stream);
+int mmad_concat_cols(int b, int n_in, const float* const* srcs, const int* widths,
+                     float* dst, void* stream);
+int mmad_split_cols(int b, int n_out, const float* src, float* const* dsts,
+                    const int* widths, void* stream);
+
+/* ---- dtype casts / dropout ------------------------------------------------------ */
+int mmad_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);
+int mmad_dropout_fwd(int dtype, int64_t n, float p, uint64_t seed, const void* x, void* y,
+                     uint8_t* keep, void* stream);
+int mmad_dropout_bwd(int dtype, int64_t n, float p, const void* g, const uint8_t* keep,
+                     void* dx, void* stream);
+
+/* ---- losses (f64, one workgroup) -----------------------------------------------
+ * mode 0: weighted cross entropy, nn.CrossEntropyLoss(weight=w) 'mean' reduction
+ *         = sum_i w[y_i]*nll_i / sum_i w[y_i]   (anat_cnn.py:84-85);
+ * mode 1: FocalLoss(gamma), alpha None, mean, with pt DETACHED
+ *         (pkg/loss_functions/focalloss.py:19-39).
+ * Writes the loss and d loss / d logits (the backward is a scale of `dlogits`).     */
+int mmad_loss_fwd(int b, int c, const double* logits, const int64_t* labels,
+                  const double* weight, double gamma, int mode, double* loss,
+                  double* dlogits, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMAD_H */

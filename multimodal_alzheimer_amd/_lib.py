@@ -1,0 +1,135 @@
+"""ctypes binding of libmmad_hip.so (the C ABI declared in include/mmad.h).
+
+torch is imported first on purpose: it loads its bundled HIP runtime
+(``libamdhip64.so.7``), and the library's own dependency on that soname then resolves to
+the same runtime, so torch's streams and allocations are valid handles for our kernels.
+
+There is no fallback: if the library is missing or a call is made on tensors that are not
+on a HIP device, the call raises.
+"""
+import ctypes as C
+import os
+
+import torch
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libmmad_hip.so")
+
+F32, BF16, F64 = 0, 1, 2
+EHIP = 2000
+_HIP_OOM = 2   # hipErrorOutOfMemory
+
+_vp, _i32, _i64, _f32, _f64, _u64 = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_double, C.c_uint64
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "n", "ci", "di", "hi", "wi", "co", "do_", "ho", "wo", "kd", "kh", "kw",
+        "sd", "sh", "sw", "pd", "ph", "pw", "dd", "dh", "dw")]
+
+
+_P = C.POINTER(ConvDesc)
+_SIGS = {
+    "mmad_abi_version": (_i32, []),
+    "mmad_strerror": (C.c_char_p, [_i32]),
+    "mmad_conv_packed_elems": (_i64, [_P, _i32, _i32]),
+    "mmad_conv_pack_weight": (_i32, [_P, _i32, _vp, _vp, _i32, _vp]),
+    "mmad_conv_unfolded_elems": (_i64, [_P]),
+    "mmad_conv_unfold_input": (_i32, [_P, _i32, _vp, _i32, _vp, _vp]),
+    "mmad_conv3d_stats_rows": (_i64, [_P, _i32]),
+    "mmad_conv3d_fwd": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_conv3d_dgrad": (_i32, [_P, _i32, _vp, _vp, _vp, _vp]),
+    "mmad_conv3d_wgrad_workspace": (_i64, [_P, _i32]),
+    "mmad_conv3d_wgrad": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_bn_stats_parts": (_i64, [_i64, _i32]),
+    "mmad_bn_stats": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp]),
+    "mmad_bn_finalize": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _i32,
+                                _vp, _vp, _vp, _vp, _vp]),
+    "mmad_scale_shift_act": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
+                                    _vp]),
+    "mmad_bn_bwd_parts": (_i64, [_i64, _i32]),
+    "mmad_bn_bwd_reduce": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_bn_bwd_finalize": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "mmad_bn_bwd_apply": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_relu_fwd": (_i32, [_i32, _i64, _vp, _vp, _vp]),
+    "mmad_relu_bwd": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp]),
+    "mmad_colsum_ws": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "mmad_add": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp]),
+    "mmad_maxpool3d_fwd": (_i32, [_i32] * 12 + [_vp, _vp, _vp, _vp]),
+    "mmad_maxpool3d_bwd": (_i32, [_i32] * 12 + [_vp, _vp, _vp, _vp]),
+    "mmad_gap_fwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "mmad_gap_bwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "mmad_linear_fwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "mmad_linear_bwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_concat_cols": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp]),
+    "mmad_split_cols": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp]),
+    "mmad_cast": (_i32, [_i32, _i32, _i64, _vp, _vp, _vp]),
+    "mmad_dropout_fwd": (_i32, [_i32, _i64, _f32, _u64, _vp, _vp, _vp, _vp]),
+    "mmad_dropout_bwd": (_i32, [_i32, _i64, _f32, _vp, _vp, _vp, _vp]),
+    "mmad_loss_fwd": (_i32, [_i32, _i32, _vp, _vp, _vp, _f64, _i32, _vp, _vp, _vp]),
+}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+class MMADError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the CDLL; raises if the library has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MMADError(f"{LIB_PATH} is missing: build it with "
+                            "`python -m multimodal_alzheimer_amd._build` (hipcc, gfx950)")
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        if lib.mmad_abi_version() != 1:
+            raise MMADError("libmmad_hip.so ABI version mismatch")
+        _lib = lib
+    return _lib
+
+
+def check(rc, what=""):
+    if rc == 0:
+        return
+    msg = load().mmad_strerror(rc).decode()
+    if rc == EHIP + _HIP_OOM:
+        raise torch.OutOfMemoryError(f"{what}: {msg}")
+    raise MMADError(f"{what} failed ({rc}): {msg}")
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args), name)
+
+
+def stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    if dt == torch.float64:
+        return F64
+    raise MMADError(f"unsupported dtype {dt}")
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and t.device.type != "cuda":
+            raise MMADError("the MI355X hot path runs on HIP devices only "
+                            f"(got a tensor on {t.device}); move the model and batch to "
+                            "'cuda' -- there is no CPU fallback")

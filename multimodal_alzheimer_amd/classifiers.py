@@ -1,0 +1,539 @@
+"""Drop-in replacements for the reference's ``pkg.models`` / ``pkg.loss_functions`` classes.
+
+Same class names, constructor signatures, hparams keys, ``general_step`` contract
+(``{'loss', 'outputs', 'labels'}``), attribute paths (``.model``, ``.model.conv_seg``,
+``.model_fuse``, ``.reduce_dim_mri``, ``.stage2out``, ``.cls2``) and state_dict keys as
+
+  pkg/models/base_model.py                         Base_Model
+  pkg/models/mri_models/anat_cnn.py                Anat_CNN
+  pkg/models/pet_models/pet_cnn.py                 Small_PET_CNN, Random_Benchmark_All_CN
+  pkg/models/pet_models/pet_resnet_cnn.py          PET_CNN_ResNet
+  pkg/models/fusion_models/anat_pet_fusion.py      Anat_PET_CNN
+  pkg/loss_functions/focalloss.py                  FocalLoss
+
+but every forward / backward op runs on the MI355X kernels of libmmad_hip.so.
+
+Additions beyond the reference (documented build extensions, BASELINE configs 3-5):
+  * hparams['precision'] in {'32' (default, the reference's fp32), 'bf16'};
+  * resnet_depth 34 (n_in 512) is accepted (the reference match rejects it,
+    anat_cnn.py:37-46);
+  * PET_MRI_ResNet_Fusion -- "ResNet-10 x2 + MLP head" (config 3/4);
+  * All_Modalities_Fusion -- MRI ResNet + PET ResNet + tabular MLP (config 5; the
+    reference's TabPFN branch is replaced, no reference parity).
+"""
+import os
+from abc import ABC, abstractmethod
+
+import torch
+import torch.nn as nn
+from torch.optim.lr_scheduler import ReduceLROnPlateau
+
+from . import head_ops
+from . import layers as Lyr
+from . import medicalnet
+from .lightning_compat import (LightningModule, MulticlassF1Score, MulticlassMatthewsCorrCoef)
+from .volume_ops import cast
+
+PRETRAIN_TEMPLATE = ("/vol/chameleon/projects/adni/adni_1/MedicalNet/pretrain/"
+                     "resnet_{}_23dataset.pth")      # anat_cnn.py:19
+
+
+# ------------------------------------------------------------------------------ losses
+class FocalLoss(nn.Module):
+    """FocalLoss(gamma, alpha=None, size_average=True) -- pkg/loss_functions/focalloss.py.
+
+    loss = mean_i( -(1 - pt_i)^gamma * log pt_i ), pt detached (focalloss.py:29).
+    """
+
+    def __init__(self, gamma=0, alpha=None, size_average=True):
+        super().__init__()
+        if alpha is not None:
+            raise NotImplementedError("FocalLoss alpha weighting (no reference caller sets it)")
+        self.gamma = gamma
+        self.alpha = alpha
+        self.size_average = size_average
+
+    def forward(self, input, target):
+        loss = head_ops.focal_loss(input, target, self.gamma)
+        if not self.size_average:
+            loss = loss * target.numel()
+        return loss
+
+
+def make_criterion(hparams):
+    """anat_cnn.py:81-85: focal loss iff hparams['fl_gamma'] is truthy, else weighted CE."""
+    if "fl_gamma" in hparams and hparams["fl_gamma"]:
+        return FocalLoss(gamma=hparams["fl_gamma"])
+    return Lyr.CrossEntropyLoss(weight=hparams["loss_class_weights"])
+
+
+def _to_f64(y_hat):
+    return cast(y_hat, torch.float64)
+
+
+# -------------------------------------------------------------------------- base model
+class Base_Model(LightningModule, ABC):
+    """pkg/models/base_model.py:11-239 (metrics / logging surface; hot path in general_step)."""
+
+    def __init__(self, hparams, gpu_id=None):
+        super().__init__()
+        self.save_hyperparameters(hparams, ignore=["gpu_id"])
+        nc = self.hparams["n_classes"]
+        self.label_ind_by_names = ({"CN": 0, "MCI": 1, "AD": 2} if nc == 3
+                                   else {"CN": 0, "AD": 1})
+        for split in ("train", "val", "test"):
+            setattr(self, f"f1_score_{split}", MulticlassF1Score(num_classes=nc, average="macro"))
+            setattr(self, f"f1_score_{split}_per_class",
+                    MulticlassF1Score(num_classes=nc, average="none"))
+
+    @abstractmethod
+    def forward(self, *x):
+        pass
+
+    @abstractmethod
+    def general_step(self, batch, batch_idx, mode) -> dict:
+        pass
+
+    @property
+    def is_cuda(self):
+        return next(self.parameters()).is_cuda
+
+    def save(self, path):
+        print("Saving model... %s" % path)
+        torch.save(self, path)
+
+    def _step(self, batch, batch_idx, split):
+        out = self.general_step(batch, batch_idx, split)
+        getattr(self, f"f1_score_{split}")(out["outputs"], out["labels"])
+        getattr(self, f"f1_score_{split}_per_class")(out["outputs"], out["labels"])
+        return out
+
+    def training_step(self, batch, batch_idx):
+        return self._step(batch, batch_idx, "train")
+
+    def validation_step(self, batch, batch_idx):
+        return self._step(batch, batch_idx, "val")
+
+    def test_step(self, batch, batch_idx):
+        return self._step(batch, batch_idx, "test")
+
+    def predict_step(self, batch, batch_idx):
+        return self.general_step(batch, batch_idx, "pred")
+
+    @abstractmethod
+    def configure_optimizers(self):
+        pass
+
+    def _epoch_end(self, outputs, split):
+        avg = torch.stack([o["loss"].detach() for o in outputs]).mean()
+        f1 = getattr(self, f"f1_score_{split}")
+        f1c = getattr(self, f"f1_score_{split}_per_class")
+        f1_epoch, f1_per_class = f1.compute(), f1c.compute()
+        f1.reset()
+        f1c.reset()
+        d = {f"{split}_loss_epoch": avg, f"{split}_f1_epoch": f1_epoch,
+             "step": float(self.current_epoch)}
+        for i in range(self.hparams["n_classes"]):
+            d[f"{split}_f1_epoch_class_{i}"] = f1_per_class[i]
+        return d
+
+    def training_epoch_end(self, outputs):
+        self.log_dict(self._epoch_end(outputs, "train"))
+
+    def validation_epoch_end(self, outputs):
+        self.log_dict(self._epoch_end(outputs, "val"))
+
+    def test_epoch_end(self, outputs):
+        d = self._epoch_end(outputs, "test")
+        y_hat = torch.cat([o["outputs"].detach() for o in outputs])
+        y = torch.cat([o["labels"] for o in outputs])
+        nc = self.hparams["n_classes"]
+        d["test_f1_epoch_boot"], d["test_f1_epoch_ci"] = self.bootstrap_metric(
+            MulticlassF1Score(num_classes=nc, average="macro"), y_hat, y)
+        d["test_mcc_epoch_boot"], d["test_mcc_epoch_ci"] = self.bootstrap_metric(
+            MulticlassMatthewsCorrCoef(num_classes=nc), y_hat, y)
+        self.log_dict(d)
+
+    def bootstrap_metric(self, metric, y_hat, y_labels, n_drawings=1000):
+        """base_model.py:219-239: mean and 1.96*std over n_drawings resamples."""
+        metric.to(self.device)
+        vals = torch.zeros(n_drawings)
+        n = len(y_hat)
+        for i in range(n_drawings):
+            idx = torch.randint(0, n, (n,))
+            metric(y_hat[idx.to(y_hat.device)], y_labels[idx.to(y_labels.device)])
+            vals[i] = metric.compute()
+            metric.reset()
+        return torch.mean(vals), 1.96 * torch.std(vals)
+
+
+# ---------------------------------------------------------------------------- heads
+def resnet_features(depth):
+    """anat_cnn.py:37-46 depth -> backbone width (34 is a build extension)."""
+    if depth not in medicalnet.FEATURES:
+        raise ValueError("hparams['resnet_depth'] is not in [10, 18, 34, 50]")
+    return medicalnet.FEATURES[depth]
+
+
+def build_conv_seg(hparams, n_in):
+    """Replacement conv_seg head (anat_cnn.py:33-79; pet_resnet_cnn.py:37-81)."""
+    mods = []
+    if hparams.get("batchnorm_begin"):
+        mods.append(Lyr.BatchNorm3d(n_in))
+    if "conv_out" in hparams:
+        for n_out, k in zip(hparams["conv_out"], hparams["filter_size"]):
+            mods.append(Lyr.Conv3d(n_in, n_out, k, padding="same"))
+            if hparams["batchnorm_conv"]:
+                mods.append(Lyr.BatchNorm3d(n_out))
+            mods += [Lyr.ReLU(), Lyr.MaxPool3d(2)]
+            n_in = n_out
+    mods += [Lyr.AdaptiveAvgPool3d(1), nn.Flatten()]
+    for n_out in hparams["linear_out"]:
+        mods.append(Lyr.Linear(n_in, n_out))
+        if hparams.get("batchnorm_dense"):
+            mods.append(Lyr.BatchNorm1d(n_out))
+        mods.append(Lyr.ReLU())
+        n_in = n_out
+    mods += [Lyr.Linear(n_in, hparams["n_classes"]), Lyr.ReLU()]
+    return nn.Sequential(*mods)
+
+
+def _resnet_backbone(hparams):
+    opts = medicalnet.parse_opts()
+    depth = hparams["resnet_depth"]
+    opts.model_depth = depth
+    opts.pretrain_path = hparams.get("pretrain_path") or PRETRAIN_TEMPLATE.format(depth)
+    wrapped, _ = medicalnet.generate_model(opts)
+    return wrapped.module
+
+
+def _adam_groups_backbone(model, hparams):
+    """anat_cnn.py:111-136: head lr; backbone lr_pretrained or frozen (requires_grad off)."""
+    groups = []
+    for name, p in model.named_parameters():
+        if "conv_seg" in name:
+            groups.append({"params": p, "lr": hparams["lr"]})
+        elif not hparams.get("lr_pretrained"):
+            p.requires_grad = False
+            groups.append({"params": p})
+        else:
+            p.requires_grad = True
+            groups.append({"params": p, "lr": hparams["lr_pretrained"]})
+    return groups
+
+
+def _adam(groups, hparams, device):
+    fused = device.type == "cuda"
+    return torch.optim.Adam(groups, weight_decay=hparams.get("l2_reg", 0) or 0, fused=fused)
+
+
+def _with_scheduler(opt, hparams):
+    if hparams.get("reduce_factor_lr_schedule"):
+        return {"optimizer": opt,
+                "lr_scheduler": ReduceLROnPlateau(opt, factor=hparams["reduce_factor_lr_schedule"]),
+                "monitor": "val_loss_epoch"}
+    return opt
+
+
+# ------------------------------------------------------------------------- MRI model
+class Anat_CNN(Base_Model):
+    """MRI classifier: MedicalNet 3D-ResNet + conv_seg head (anat_cnn.py:13-136)."""
+
+    batch_key = "mri"
+
+    def __init__(self, hparams, gpu_id=None):
+        super().__init__(hparams)
+        self.model = _resnet_backbone(hparams)
+        self.model.conv_seg = build_conv_seg(hparams, resnet_features(hparams["resnet_depth"]))
+        self.criterion = make_criterion(hparams)
+        Lyr.set_compute_dtype(self, Lyr.precision_dtype(hparams))
+
+    def forward(self, x):
+        return self.model(x)
+
+    def general_step(self, batch, batch_idx, mode):
+        x = batch[self.batch_key].unsqueeze(1)   # raw f64 volume; conv 1 unfolds + casts it
+        y = batch["label"]
+        y_hat = _to_f64(self.forward(x))
+        loss = self.criterion(y_hat, y)
+        if mode != "pred":
+            self.log(mode + "_loss", loss, on_step=True, prog_bar=True)
+        return {"loss": loss, "outputs": y_hat, "labels": y}
+
+    def configure_optimizers(self):
+        opt = _adam(_adam_groups_backbone(self.model, self.hparams), self.hparams, self.device)
+        return _with_scheduler(opt, self.hparams)
+
+
+class PET_CNN_ResNet(Anat_CNN):
+    """PET classifier on the same backbone (pet_resnet_cnn.py:12-198).
+
+    The reference subclasses LightningModule directly with its own step / epoch-end code;
+    the observable differences kept here: PET batch key, train / val macro-F1 updated inside
+    general_step, no scheduler in configure_optimizers.
+    """
+
+    batch_key = "pet1451"
+
+    def general_step(self, batch, batch_idx, mode):
+        out = super().general_step(batch, batch_idx, mode)
+        if mode in ("train", "val"):
+            getattr(self, f"f1_score_{mode}")(out["outputs"], out["labels"])
+        return out
+
+    def training_step(self, batch, batch_idx):
+        return self.general_step(batch, batch_idx, "train")
+
+    def validation_step(self, batch, batch_idx):
+        return self.general_step(batch, batch_idx, "val")
+
+    def configure_optimizers(self):
+        return _adam(_adam_groups_backbone(self.model, self.hparams), self.hparams, self.device)
+
+
+# ------------------------------------------------------------------------- PET model
+class Small_PET_CNN(Base_Model):
+    """pet_cnn.py:10-82: n x (Conv 'same' (+bias) [BN] ReLU MaxPool(2) [Dropout]) -> GAP ->
+    [Dropout, Linear, ReLU] -> Linear; always weighted CE (pet_cnn.py:47-48)."""
+
+    batch_key = "pet1451"
+
+    def __init__(self, hparams, gpu_id=None):
+        super().__init__(hparams, gpu_id=gpu_id)
+        mods = []
+        n_in, n_out = 1, None
+        for n_out, k in zip(self.hparams["conv_out"], self.hparams["filter_size"]):
+            mods.append(Lyr.Conv3d(n_in, n_out, k, padding="same"))
+            if self.hparams.get("batchnorm"):
+                mods.append(Lyr.BatchNorm3d(n_out))
+            mods += [Lyr.ReLU(), Lyr.MaxPool3d(2)]
+            if "dropout_conv_p" in self.hparams:
+                mods.append(Lyr.Dropout(p=self.hparams["dropout_conv_p"]))
+            n_in = n_out
+        mods += [Lyr.AdaptiveAvgPool3d(1), nn.Flatten()]
+        if self.hparams.get("linear_out"):
+            n_out = self.hparams["linear_out"]
+            if "dropout_dense_p" in self.hparams:
+                mods.append(Lyr.Dropout(p=self.hparams["dropout_dense_p"]))
+            mods += [Lyr.Linear(n_in, n_out), Lyr.ReLU()]
+        mods.append(Lyr.Linear(n_out, self.hparams["n_classes"]))
+        self.model = nn.Sequential(*mods)
+        self.criterion = Lyr.CrossEntropyLoss(weight=hparams["loss_class_weights"])
+        Lyr.set_compute_dtype(self, Lyr.precision_dtype(hparams))
+
+    def forward(self, x):
+        return self.model(x)
+
+    general_step = Anat_CNN.general_step
+
+    def configure_optimizers(self):
+        opt = torch.optim.Adam(self.model.parameters(), lr=self.hparams["lr"],
+                               fused=self.device.type == "cuda")
+        return _with_scheduler(opt, self.hparams)
+
+
+class Random_Benchmark_All_CN(Small_PET_CNN):
+    """pet_cnn.py:85-90: constant 'all CN' prediction baseline."""
+
+    def forward(self, x):
+        y = super().forward(x)
+        one_hot = torch.zeros_like(y)
+        one_hot[..., 0] = 1
+        return one_hot
+
+
+# ---------------------------------------------------------------------- fusion models
+def _freeze(*mods):
+    for m in mods:
+        for p in m.parameters():
+            p.requires_grad = False
+
+
+class Anat_PET_CNN(Base_Model):
+    """PET-MRI late fusion (anat_pet_fusion.py:11-127).
+
+    Stage-1 models come from checkpoints (``path_pet``/``path_anat`` or the hparams
+    ``path_pet``/``path_mri``), or -- an addition for tests / benchmarks -- as live modules
+    via ``pet_model=`` / ``mri_model=``.  ``path_mri=`` is accepted as an alias of
+    ``path_anat`` (pkg/inference/test_anat_pet_fusion.py passes it).
+    """
+
+    def __init__(self, hparams, path_pet=None, path_anat=None, path_mri=None, pet_model=None,
+                 mri_model=None):
+        super().__init__(hparams)
+        path_anat = path_anat or path_mri
+        if pet_model is None or mri_model is None:
+            if path_pet and path_anat:
+                pet_model = Small_PET_CNN.load_from_checkpoint(path_pet)
+                mri_model = Anat_CNN.load_from_checkpoint(path_anat)
+            else:
+                pet_model = Small_PET_CNN.load_from_checkpoint(hparams["path_pet"])
+                mri_model = Anat_CNN.load_from_checkpoint(hparams["path_mri"])
+        cut = -3 if hparams["n_classes"] == 2 else -1
+        self.model_pet = pet_model.model[:cut]
+        self.model_mri = mri_model
+        self.model_mri.model.conv_seg = self.model_mri.model.conv_seg[:2]
+        if not hparams.get("lr_pretrained"):
+            _freeze(self.model_pet, self.model_mri)
+        self.stage2out = Lyr.Linear(64 + 64, 64)
+        self.cls2 = Lyr.Linear(64, hparams["n_classes"])
+        self.relu = Lyr.ReLU()
+        self.reduce_dim_mri = nn.Sequential(Lyr.Linear(512, 64), self.relu)
+        self.model_fuse = nn.Sequential(self.stage2out, self.relu, self.cls2)
+        self.criterion = make_criterion(hparams)
+        Lyr.set_compute_dtype(self, Lyr.precision_dtype(hparams))
+
+    def forward(self, x_pet, x_mri):
+        bs = x_mri.shape[0]
+        out_pet = self.model_pet(x_pet)
+        out_mri = self.reduce_dim_mri(self.model_mri(x_mri).view(bs, -1))
+        return self.model_fuse(head_ops.concat_features(out_pet, out_mri))
+
+    def general_step(self, batch, batch_idx, mode):
+        x_pet = batch["pet1451"].unsqueeze(1)
+        x_mri = batch["mri"].unsqueeze(1)
+        y = batch["label"]
+        y_hat = _to_f64(self(x_pet, x_mri))
+        loss = self.criterion(y_hat, y)
+        self.log(mode + "_loss", loss, on_step=True, prog_bar=True)
+        return {"loss": loss, "outputs": y_hat, "labels": y}
+
+    def _fusion_groups(self):
+        groups = [{"params": p, "lr": self.hparams["lr"]}
+                  for m in (self.model_fuse, self.reduce_dim_mri) for p in m.parameters()]
+        if self.hparams.get("lr_pretrained"):
+            groups += [{"params": p, "lr": self.hparams["lr_pretrained"]}
+                       for m in self._stage1() for p in m.parameters()]
+        return groups
+
+    def _stage1(self):
+        return (self.model_pet, self.model_mri)
+
+    def configure_optimizers(self):
+        return _with_scheduler(_adam(self._fusion_groups(), self.hparams, self.device),
+                               self.hparams)
+
+
+def _stage1_resnet(cls, hparams, depth, precision):
+    h = dict(hparams)
+    h.update({"resnet_depth": depth, "linear_out": [], "conv_out": [], "filter_size": [],
+              "batchnorm_begin": False, "batchnorm_dense": False, "precision": precision})
+    return cls(h)
+
+
+class PET_MRI_ResNet_Fusion(Anat_PET_CNN):
+    """BUILD EXTENSION -- BASELINE config 3/4 "ResNet-10 x2 + MLP head" (SURVEY.md sec. 7).
+
+    PET branch = PET_CNN_ResNet, MRI branch = Anat_CNN, both cut to conv_seg[:2] (512-d),
+    each reduced by Linear(512,64)+ReLU (``reduce_dim_pet`` mirrors ``reduce_dim_mri``,
+    anat_pet_fusion.py:49); head unchanged (anat_pet_fusion.py:42-51).  Stage-1 models from
+    ``path_pet``/``path_anat`` checkpoints, live modules, or fresh from hparams
+    (``resnet_depth_pet`` / ``resnet_depth_mri``, default 10).
+    """
+
+    def __init__(self, hparams, path_pet=None, path_anat=None, pet_model=None, mri_model=None):
+        Base_Model.__init__(self, hparams)
+        prec = hparams.get("precision", "32")
+        if pet_model is None:
+            pet_model = (PET_CNN_ResNet.load_from_checkpoint(path_pet) if path_pet else
+                         _stage1_resnet(PET_CNN_ResNet, hparams,
+                                        hparams.get("resnet_depth_pet", 10), prec))
+        if mri_model is None:
+            mri_model = (Anat_CNN.load_from_checkpoint(path_anat) if path_anat else
+                         _stage1_resnet(Anat_CNN, hparams, hparams.get("resnet_depth_mri", 10),
+                                        prec))
+        self.model_pet = pet_model
+        self.model_pet.model.conv_seg = self.model_pet.model.conv_seg[:2]
+        self.model_mri = mri_model
+        self.model_mri.model.conv_seg = self.model_mri.model.conv_seg[:2]
+        if not hparams.get("lr_pretrained"):
+            _freeze(self.model_pet, self.model_mri)
+        self.stage2out = Lyr.Linear(64 + 64, 64)
+        self.cls2 = Lyr.Linear(64, hparams["n_classes"])
+        self.relu = Lyr.ReLU()
+        self.reduce_dim_pet = nn.Sequential(Lyr.Linear(512, 64), self.relu)
+        self.reduce_dim_mri = nn.Sequential(Lyr.Linear(512, 64), self.relu)
+        self.model_fuse = nn.Sequential(self.stage2out, self.relu, self.cls2)
+        self.criterion = make_criterion(hparams)
+        Lyr.set_compute_dtype(self, Lyr.precision_dtype(hparams))
+
+    def forward(self, x_pet, x_mri):
+        bs = x_mri.shape[0]
+        out_pet = self.reduce_dim_pet(self.model_pet(x_pet).view(bs, -1))
+        out_mri = self.reduce_dim_mri(self.model_mri(x_mri).view(bs, -1))
+        return self.model_fuse(head_ops.concat_features(out_pet, out_mri))
+
+    def _fusion_groups(self):
+        groups = super()._fusion_groups()
+        groups += [{"params": p, "lr": self.hparams["lr"]} for p in self.reduce_dim_pet.parameters()]
+        return groups
+
+
+class Tabular_MLP(nn.Module):
+    """BUILD EXTENSION (config 5): 9 tabular features (dataloader.py:306) -> 64 -> 64."""
+
+    def __init__(self, n_features=9, width=64):
+        super().__init__()
+        self.net = nn.Sequential(Lyr.Linear(n_features, width), Lyr.ReLU(),
+                                 Lyr.Linear(width, width), Lyr.ReLU())
+
+    def forward(self, x):
+        return self.net(x.reshape(x.shape[0], -1))
+
+
+class All_Modalities_Fusion(Base_Model):
+    """Three-branch late fusion (all_modalities_fusion.py:12-137), BUILD EXTENSION form.
+
+    The reference fuses three stage-2 models, two of which embed TabPFN
+    (tabpfn==0.1.8, absent offline, CPU round-trip); BASELINE config 5 replaces that with
+    a tabular MLP.  Branches: MRI ResNet (``resnet_depth_mri``, default 34), PET ResNet
+    (``resnet_depth_pet``, default 18), Tabular_MLP -> 64-d each -> cat 192 ->
+    Linear(192,64) -> ReLU -> Linear(64,C) (the reference's stage-3 head, :50-57).
+    """
+
+    def __init__(self, hparams):
+        super().__init__(hparams)
+        prec = hparams.get("precision", "32")
+        self.model_mri = _stage1_resnet(Anat_CNN, hparams, hparams.get("resnet_depth_mri", 34),
+                                        prec)
+        self.model_mri.model.conv_seg = self.model_mri.model.conv_seg[:2]
+        self.model_pet = _stage1_resnet(PET_CNN_ResNet, hparams,
+                                        hparams.get("resnet_depth_pet", 18), prec)
+        self.model_pet.model.conv_seg = self.model_pet.model.conv_seg[:2]
+        self.model_tabular = Tabular_MLP(hparams.get("n_tabular_features", 9))
+        self.relu = Lyr.ReLU()
+        self.reduce_dim_mri = nn.Sequential(Lyr.Linear(512, 64), self.relu)
+        self.reduce_dim_pet = nn.Sequential(Lyr.Linear(512, 64), self.relu)
+        self.stage3out = Lyr.Linear(64 * 3, 64)
+        self.cls3 = Lyr.Linear(64, hparams["n_classes"])
+        self.model_fuse = nn.Sequential(self.stage3out, self.relu, self.cls3)
+        self.criterion = make_criterion(hparams)
+        Lyr.set_compute_dtype(self, Lyr.precision_dtype(hparams))
+
+    def forward(self, x_pet, x_mri, x_tab):
+        bs = x_mri.shape[0]
+        out_mri = self.reduce_dim_mri(self.model_mri(x_mri).view(bs, -1))
+        out_pet = self.reduce_dim_pet(self.model_pet(x_pet).view(bs, -1))
+        out_tab = self.model_tabular(x_tab)
+        return self.model_fuse(head_ops.concat_features(out_pet, out_mri, out_tab))
+
+    def general_step(self, batch, batch_idx, mode):
+        x_pet = batch["pet1451"].unsqueeze(1)
+        x_mri = batch["mri"].unsqueeze(1)
+        x_tab = cast(batch["tabular"].unsqueeze(1), torch.float32)
+        y = batch["label"]
+        y_hat = _to_f64(self(x_pet, x_mri, x_tab))
+        loss = self.criterion(y_hat, y)
+        self.log(mode + "_loss", loss, on_step=True, prog_bar=True)
+        return {"loss": loss, "outputs": y_hat, "labels": y}
+
+    def configure_optimizers(self):
+        groups = [{"params": p, "lr": self.hparams["lr"]} for p in self.model_fuse.parameters()]
+        rest = (self.model_mri, self.model_pet, self.model_tabular, self.reduce_dim_mri,
+                self.reduce_dim_pet)
+        lr_pre = self.hparams.get("lr_pretrained")
+        for m in rest:
+            for p in m.parameters():
+                p.requires_grad = bool(lr_pre) or m in (self.model_tabular,)
+                groups.append({"params": p, "lr": lr_pre or self.hparams["lr"]})
+        return _with_scheduler(_adam(groups, self.hparams, self.device), self.hparams)

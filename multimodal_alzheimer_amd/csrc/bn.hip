@@ -1,0 +1,412 @@
+// BatchNorm (train / eval) + ReLU + residual add on NDHWC activations, gfx950.
+//
+// Replaces nn.BatchNorm3d / nn.BatchNorm1d + nn.ReLU + MedicalNet's residual
+// `out += residual; out = relu(out)` (BasicBlock), the stem bn1+relu and the head BNs
+// (pkg/models/mri_models/anat_cnn.py:50-51, :69-70).  Layout [m][c], m = N*D*H*W.
+//
+// All per-channel reductions are two-stage and deterministic: a partial pass writes
+// [parts][2][c] fp32 rows (fixed row ranges per block), a finalize pass sums the parts
+// in fixed order in f64.  The conv forward kernel emits the same partial layout from its
+// epilogue, so a BN that follows one of our convs needs no separate statistics pass.
+#include "common.h"
+
+namespace {
+
+constexpr int ROWS_PER_PART = 1024;
+
+// sums over rows [p*RPP, (p+1)*RPP) of y and y^2 (or, for the backward, of g' and
+// g'*xhat) per channel.  Thread layout: P = 256/C row lanes x C channels (C <= 256), or a
+// channel loop for C > 256.
+template <typename T, int MODE>   // MODE 0: stats of y; 1: BN backward sums; 2: sum only
+__global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, const T* __restrict__ y,
+                                                     const T* __restrict__ g,
+                                                     const T* __restrict__ relu_out,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ invstd,
+                                                     float* __restrict__ parts) {
+  __shared__ float red[2][256];
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * ROWS_PER_PART;
+  const int64_t r1 = min(M, r0 + ROWS_PER_PART);
+  const int P = C >= 256 ? 1 : 256 / C;
+  const int cw = C >= 256 ? 256 : C;          // channels covered per pass
+  for (int cbase = 0; cbase < C; cbase += cw) {
+    float s = 0.f, q = 0.f;
+    const int c = cbase + tid % cw;
+    const int rp = tid / cw;
+    const bool active = rp < P && c < C;
+    if (active) {
+      const float mu = MODE == 1 ? mean[c] : 0.f;
+      const float is = MODE == 1 ? invstd[c] : 0.f;
+      for (int64_t r = r0 + rp; r < r1; r += P) {
+        const int64_t i = r * C + c;
+        if (MODE == 1) {
+          float gv = Elt<T>::ld(g, i);
+          if (relu_out != nullptr && !(Elt<T>::ld(relu_out, i) > 0.f)) gv = 0.f;
+          const float xh = (Elt<T>::ld(y, i) - mu) * is;
+          s += gv;
+          q += gv * xh;
+        } else {
+          const float v = Elt<T>::ld(y, i);
+          s += v;
+          if (MODE == 0) q += v * v;
+        }
+      }
+    }
+    red[0][tid] = s;
+    red[1][tid] = q;
+    __syncthreads();
+    if (tid < cw && cbase + tid < C) {
+      float ss = 0.f, qq = 0.f;
+      for (int k = 0; k < P; ++k) { ss += red[0][k * cw + tid]; qq += red[1][k * cw + tid]; }
+      parts[((int64_t)blockIdx.x * 2) * C + cbase + tid] = ss;
+      parts[((int64_t)blockIdx.x * 2 + 1) * C + cbase + tid] = qq;
+    }
+    __syncthreads();
+  }
+}
+
+// f64 sum of the partial rows; block = 64 channels x 16 part-lanes
+__device__ __forceinline__ void sum_parts(int c, int C, int nparts, const float* parts,
+                                          double* sm, double& S, double& Q) {
+  const int cx = threadIdx.x & 63, py = threadIdx.x >> 6;
+  double s = 0.0, q = 0.0;
+  if (c < C)
+    for (int p = py; p < nparts; p += 16) {
+      s += parts[((int64_t)p * 2) * C + c];
+      q += parts[((int64_t)p * 2 + 1) * C + c];
+    }
+  sm[threadIdx.x] = s;
+  sm[1024 + threadIdx.x] = q;
+  __syncthreads();
+  S = 0.0; Q = 0.0;
+  if (py == 0)
+    for (int k = 0; k < 16; ++k) { S += sm[k * 64 + cx]; Q += sm[1024 + k * 64 + cx]; }
+}
+
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(
+    int C, int64_t count, int nparts, const float* __restrict__ parts,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
+    float* running_var, float momentum, float eps, int training, float* mean_out,
+    float* invstd_out, float* scale_out, float* shift_out) {
+  __shared__ double sm[2048];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double S, Q;
+  if (training) {
+    sum_parts(c, C, nparts, parts, sm, S, Q);
+  } else {
+    S = Q = 0.0;
+  }
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
+  double mean, var;
+  if (training) {
+    mean = S / (double)count;
+    var = Q / (double)count - mean * mean;
+    if (var < 0) var = 0;
+    if (running_mean != nullptr) {
+      const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+    }
+  } else {
+    mean = running_mean[c];
+    var = running_var[c];
+  }
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  if (mean_out) mean_out[c] = (float)mean;
+  if (invstd_out) invstd_out[c] = is;
+  if (scale_out) scale_out[c] = gm * is;
+  if (shift_out) shift_out[c] = bt - (float)mean * gm * is;
+}
+
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
+    int C, int64_t count, int nparts, const float* __restrict__ parts,
+    const float* __restrict__ gamma, const float* __restrict__ invstd, int training,
+    float* dgamma, float* dbeta, float* coef) {
+  __shared__ double sm[2048];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double S, Q;
+  sum_parts(c, C, nparts, parts, sm, S, Q);
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
+  if (dbeta) dbeta[c] = (float)S;
+  if (dgamma) dgamma[c] = (float)Q;
+  const double k0 = (double)(gamma ? gamma[c] : 1.f) * invstd[c];
+  coef[c] = (float)k0;
+  coef[C + c] = training ? (float)(k0 * S / (double)count) : 0.f;
+  coef[2 * C + c] = training ? (float)(k0 * Q / (double)count) : 0.f;
+}
+
+__global__ void sum_only_finalize_kernel(int C, int nparts, const float* __restrict__ parts,
+                                         float* out) {
+  __shared__ double sm[2048];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double S, Q;
+  sum_parts(c, C, nparts, parts, sm, S, Q);
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
+  out[c] = (float)S;
+}
+
+// out = act(y*scale + shift + R); vector path when C % EPC == 0
+template <typename T, int RES>   // RES 0: none, 1: identity residual, 2: BN'ed residual
+__global__ void scale_shift_act_kernel(int64_t M, int C, const T* __restrict__ y,
+                                       const float* __restrict__ scale,
+                                       const float* __restrict__ shift,
+                                       const T* __restrict__ res,
+                                       const float* __restrict__ rscale,
+                                       const float* __restrict__ rshift, int relu,
+                                       T* __restrict__ out) {
+  constexpr int N = Chunk<T>::N;
+  const int64_t nchunks = M * C / N;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nchunks;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i0 = q * N;
+    const int c0 = (int)(i0 % C);
+    float v[N], r[N];
+    Chunk<T>::load(y + i0, v);
+    if (RES) Chunk<T>::load(res + i0, r);
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+      const int c = c0 + e;
+      float o = v[e] * scale[c] + shift[c];
+      if (RES == 1) o += r[e];
+      if (RES == 2) o += r[e] * rscale[c] + rshift[c];
+      v[e] = relu ? fmaxf(o, 0.f) : o;
+    }
+    Chunk<T>::store(out + i0, v);
+  }
+}
+
+template <typename T>
+__global__ void scale_shift_act_scalar_kernel(int64_t M, int C, const T* __restrict__ y,
+                                              const float* __restrict__ scale,
+                                              const float* __restrict__ shift,
+                                              const T* __restrict__ res,
+                                              const float* __restrict__ rscale,
+                                              const float* __restrict__ rshift, int relu,
+                                              T* __restrict__ out) {
+  const int64_t n = M * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    float o = Elt<T>::ld(y, i) * scale[c] + shift[c];
+    if (res) o += rscale ? Elt<T>::ld(res, i) * rscale[c] + rshift[c] : Elt<T>::ld(res, i);
+    Elt<T>::st(out, i, relu ? fmaxf(o, 0.f) : o);
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(int64_t M, int C, const T* __restrict__ g,
+                                    const T* __restrict__ relu_out, const T* __restrict__ y,
+                                    const float* __restrict__ mean,
+                                    const float* __restrict__ invstd,
+                                    const float* __restrict__ coef, T* __restrict__ dy,
+                                    T* __restrict__ gmask) {
+  const int64_t n = M * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    float gv = Elt<T>::ld(g, i);
+    if (relu_out != nullptr && !(Elt<T>::ld(relu_out, i) > 0.f)) gv = 0.f;
+    const float xh = (Elt<T>::ld(y, i) - mean[c]) * invstd[c];
+    Elt<T>::st(dy, i, coef[c] * gv - coef[C + c] - xh * coef[2 * C + c]);
+    if (gmask) Elt<T>::st(gmask, i, gv);
+  }
+}
+
+template <typename T>
+__global__ void relu_bwd_kernel(int64_t n, const T* __restrict__ g, const T* __restrict__ out,
+                                T* __restrict__ dx) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    Elt<T>::st(dx, i, Elt<T>::ld(out, i) > 0.f ? Elt<T>::ld(g, i) : 0.f);
+}
+
+template <typename T>
+__global__ void relu_fwd_kernel(int64_t n, const T* __restrict__ x, T* __restrict__ y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = Elt<T>::ld(x, i);
+    Elt<T>::st(y, i, v > 0.f ? v : (v != v ? v : 0.f));
+  }
+}
+
+template <typename T>
+__global__ void add_kernel(int64_t n, const T* __restrict__ a, const T* __restrict__ b,
+                           T* __restrict__ o) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    Elt<T>::st(o, i, Elt<T>::ld(a, i) + Elt<T>::ld(b, i));
+}
+
+unsigned ew_grid(int64_t n) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 256), 256 * 16));
+}
+
+bool dt_ok(int dtype) { return dtype == MMAD_F32 || dtype == MMAD_BF16; }
+
+}  // namespace
+
+extern "C" {
+
+int64_t mmad_bn_stats_parts(int64_t m, int c) {
+  (void)c;
+  return cdiv(m, ROWS_PER_PART);
+}
+int64_t mmad_bn_bwd_parts(int64_t m, int c) { return mmad_bn_stats_parts(m, c); }
+
+int mmad_bn_stats(int dtype, int64_t m, int c, const void* y, float* parts, void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!y || !parts) return MMAD_ENULL;
+  dim3 grid((unsigned)cdiv(m, ROWS_PER_PART));
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL((colsum_kernel<u16, 0>), grid, dim3(256), 0, as_stream(stream), m, c,
+                       (const u16*)y, nullptr, nullptr, nullptr, nullptr, parts);
+  else
+    hipLaunchKernelGGL((colsum_kernel<float, 0>), grid, dim3(256), 0, as_stream(stream), m, c,
+                       (const float*)y, nullptr, nullptr, nullptr, nullptr, parts);
+  return launch_status();
+}
+
+// column sums (conv bias gradient) using `parts` as scratch ([parts][2][c] floats)
+int mmad_colsum_ws(int dtype, int64_t m, int c, const void* y, float* parts, float* out,
+                   void* stream) {
+  int rc = mmad_bn_stats(dtype, m, c, y, parts, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(sum_only_finalize_kernel, dim3((unsigned)cdiv(c, 64)), dim3(1024), 0,
+                     as_stream(stream), c, (int)cdiv(m, ROWS_PER_PART), parts, out);
+  return launch_status();
+}
+
+int mmad_bn_finalize(int c, int64_t count, int nparts, const float* parts, const float* gamma,
+                     const float* beta, float* running_mean, float* running_var,
+                     float momentum, float eps, int training, float* mean, float* invstd,
+                     float* scale, float* shift, void* stream) {
+  if (c <= 0 || count <= 0) return MMAD_EBADSHAPE;
+  if (training && (!parts || nparts <= 0)) return MMAD_ENULL;
+  if (!training && (!running_mean || !running_var)) return MMAD_ENULL;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(c, 64)), dim3(1024), 0,
+                     as_stream(stream), c, count, nparts, parts, gamma, beta, running_mean,
+                     running_var, momentum, eps, training, mean, invstd, scale, shift);
+  return launch_status();
+}
+
+int mmad_scale_shift_act(int dtype, int64_t m, int c, const void* y, const float* scale,
+                         const float* shift, const void* res, const float* rscale,
+                         const float* rshift, int relu, void* out, void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!y || !scale || !shift || !out) return MMAD_ENULL;
+  if ((rscale == nullptr) != (rshift == nullptr)) return MMAD_ENULL;
+  hipStream_t st = as_stream(stream);
+  const int epc = dtype == MMAD_BF16 ? 8 : 4;
+  const int rk = res == nullptr ? 0 : (rscale == nullptr ? 1 : 2);
+  const unsigned grid = ew_grid(m * c / epc);
+#define SSA(T, R)                                                                          \
+  hipLaunchKernelGGL((scale_shift_act_kernel<T, R>), dim3(grid), dim3(256), 0, st, m, c,  \
+                     (const T*)y, scale, shift, (const T*)res, rscale, rshift, relu, (T*)out)
+  if (c % epc == 0) {
+    if (dtype == MMAD_BF16) {
+      if (rk == 0) SSA(u16, 0); else if (rk == 1) SSA(u16, 1); else SSA(u16, 2);
+    } else {
+      if (rk == 0) SSA(float, 0); else if (rk == 1) SSA(float, 1); else SSA(float, 2);
+    }
+  } else if (dtype == MMAD_BF16) {
+    hipLaunchKernelGGL(scale_shift_act_scalar_kernel<u16>, dim3(ew_grid(m * c)), dim3(256), 0,
+                       st, m, c, (const u16*)y, scale, shift, (const u16*)res, rscale, rshift,
+                       relu, (u16*)out);
+  } else {
+    hipLaunchKernelGGL(scale_shift_act_scalar_kernel<float>, dim3(ew_grid(m * c)), dim3(256), 0,
+                       st, m, c, (const float*)y, scale, shift, (const float*)res, rscale,
+                       rshift, relu, (float*)out);
+  }
+#undef SSA
+  return launch_status();
+}
+
+int mmad_bn_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* relu_out,
+                       const void* y, const float* mean, const float* invstd, float* parts,
+                       void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!g || !y || !mean || !invstd || !parts) return MMAD_ENULL;
+  dim3 grid((unsigned)cdiv(m, ROWS_PER_PART));
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL((colsum_kernel<u16, 1>), grid, dim3(256), 0, as_stream(stream), m, c,
+                       (const u16*)y, (const u16*)g, (const u16*)relu_out, mean, invstd, parts);
+  else
+    hipLaunchKernelGGL((colsum_kernel<float, 1>), grid, dim3(256), 0, as_stream(stream), m, c,
+                       (const float*)y, (const float*)g, (const float*)relu_out, mean, invstd,
+                       parts);
+  return launch_status();
+}
+
+int mmad_bn_bwd_finalize(int c, int64_t count, int nparts, const float* parts,
+                         const float* gamma, const float* invstd, int training, float* dgamma,
+                         float* dbeta, float* coef, void* stream) {
+  if (c <= 0 || count <= 0 || nparts <= 0) return MMAD_EBADSHAPE;
+  if (!parts || !invstd || !coef) return MMAD_ENULL;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)cdiv(c, 64)), dim3(1024), 0,
+                     as_stream(stream), c, count, nparts, parts, gamma, invstd, training,
+                     dgamma, dbeta, coef);
+  return launch_status();
+}
+
+int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* relu_out,
+                      const void* y, const float* mean, const float* invstd, const float* coef,
+                      void* dy, void* gmask, void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!g || !y || !mean || !invstd || !coef || !dy) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<u16>, dim3(ew_grid(m * c)), dim3(256), 0,
+                       as_stream(stream), m, c, (const u16*)g, (const u16*)relu_out,
+                       (const u16*)y, mean, invstd, coef, (u16*)dy, (u16*)gmask);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(ew_grid(m * c)), dim3(256), 0,
+                       as_stream(stream), m, c, (const float*)g, (const float*)relu_out,
+                       (const float*)y, mean, invstd, coef, (float*)dy, (float*)gmask);
+  return launch_status();
+}
+
+int mmad_relu_bwd(int dtype, int64_t n, const void* g, const void* out, void* dx, void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (n <= 0) return MMAD_EBADSHAPE;
+  if (!g || !out || !dx) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL(relu_bwd_kernel<u16>, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream),
+                       n, (const u16*)g, (const u16*)out, (u16*)dx);
+  else
+    hipLaunchKernelGGL(relu_bwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0,
+                       as_stream(stream), n, (const float*)g, (const float*)out, (float*)dx);
+  return launch_status();
+}
+
+int mmad_relu_fwd(int dtype, int64_t n, const void* x, void* y, void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (n <= 0) return MMAD_EBADSHAPE;
+  if (!x || !y) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL(relu_fwd_kernel<u16>, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream),
+                       n, (const u16*)x, (u16*)y);
+  else
+    hipLaunchKernelGGL(relu_fwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0,
+                       as_stream(stream), n, (const float*)x, (float*)y);
+  return launch_status();
+}
+
+int mmad_add(int dtype, int64_t n, const void* a, const void* b, void* out, void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (n <= 0) return MMAD_EBADSHAPE;
+  if (!a || !b || !out) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL(add_kernel<u16>, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), n,
+                       (const u16*)a, (const u16*)b, (u16*)out);
+  else
+    hipLaunchKernelGGL(add_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), n,
+                       (const float*)a, (const float*)b, (float*)out);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,84 @@
+// Shared device helpers for libmmad_hip.so (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mmad.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_AS __attribute__((address_space(3)))
+
+// bf16 <-> f32 (round to nearest even; NaN stays NaN) --------------------------------
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ u16 f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u16)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (u16)(u >> 16);
+}
+
+// element access by compute dtype: T = float or u16 (bf16 bits) ----------------------
+template <typename T> struct Elt;
+template <> struct Elt<float> {
+  static __device__ __forceinline__ float ld(const float* p, int64_t i) { return p[i]; }
+  static __device__ __forceinline__ void st(float* p, int64_t i, float v) { p[i] = v; }
+  static constexpr int VEC = 4;   // elements per 16-byte chunk
+};
+template <> struct Elt<u16> {
+  static __device__ __forceinline__ float ld(const u16* p, int64_t i) { return bf2f(p[i]); }
+  static __device__ __forceinline__ void st(u16* p, int64_t i, float v) { p[i] = f2bf(v); }
+  static constexpr int VEC = 8;
+};
+
+// 16-byte chunk <-> 8 (or 4) floats
+template <typename T> struct Chunk;
+template <> struct Chunk<float> {
+  static constexpr int N = 4;
+  static __device__ __forceinline__ void load(const float* p, float* v) {
+    f32x4 c = *reinterpret_cast<const f32x4*>(p);
+    v[0] = c[0]; v[1] = c[1]; v[2] = c[2]; v[3] = c[3];
+  }
+  static __device__ __forceinline__ void store(float* p, const float* v) {
+    f32x4 c; c[0] = v[0]; c[1] = v[1]; c[2] = v[2]; c[3] = v[3];
+    *reinterpret_cast<f32x4*>(p) = c;
+  }
+};
+template <> struct Chunk<u16> {
+  static constexpr int N = 8;
+  static __device__ __forceinline__ void load(const u16* p, float* v) {
+    u16x8 c = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = bf2f(c[i]);
+  }
+  static __device__ __forceinline__ void store(u16* p, const float* v) {
+    u16x8 c;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = f2bf(v[i]);
+    *reinterpret_cast<u16x8*>(p) = c;
+  }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+static inline int hip_status(hipError_t e) { return e == hipSuccess ? MMAD_OK : MMAD_EHIP + (int)e; }
+static inline int launch_status() { return hip_status(hipGetLastError()); }
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static inline bool is_pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
+static inline int ilog2(int64_t v) { int r = 0; while ((int64_t(1) << r) < v) ++r; return r; }

@@ -1,0 +1,352 @@
+// Classifier / late-fusion MLP head, losses, casts and dropout, gfx950.
+//
+// Replaces nn.Linear (+ReLU) of the conv_seg head (pkg/models/mri_models/anat_cnn.py:68-76),
+// reduce_dim_mri / stage2out / cls2 and the feature concat of Anat_PET_CNN
+// (pkg/models/fusion_models/anat_pet_fusion.py:42-51, :76), the focal loss
+// (pkg/loss_functions/focalloss.py:19-39), the weighted cross entropy (anat_cnn.py:84-85),
+// the fp32 input cast / fp64 logits cast of general_step (anat_cnn.py:102-104) and
+// nn.Dropout of Small_PET_CNN (pkg/models/pet_models/pet_cnn.py:27-29, :38-39).
+//
+// The head is tiny (B <= 64 rows, <= 2048 features): one wave per output dot product
+// with lane-strided coalesced reads and a shuffle reduction; no MFMA (a 16-row MFMA
+// tile would be >= 75 % padding at these batch sizes).
+#include "common.h"
+
+namespace {
+
+// y[b][o] = act(sum_i x[b][i] * w[o][i] + bias[o]); one wave per (b, o)
+__global__ __launch_bounds__(256) void linear_fwd_kernel(int B, int IN, int OUT,
+                                                         const float* __restrict__ x,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ bias,
+                                                         int relu, float* __restrict__ y) {
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (wid >= B * OUT) return;
+  const int b = wid / OUT, o = wid % OUT;
+  float s = 0.f;
+  for (int i = lane; i < IN; i += 64) s += x[(int64_t)b * IN + i] * w[(int64_t)o * IN + i];
+  s = wave_sum(s);
+  if (lane == 0) {
+    if (bias) s += bias[o];
+    y[(int64_t)b * OUT + o] = relu ? fmaxf(s, 0.f) : s;
+  }
+}
+
+// dx[b][i] = sum_o dy[b][o] w[o][i]   (thread per (b, i), coalesced over i)
+__global__ void linear_dx_kernel(int B, int IN, int OUT, const float* __restrict__ w,
+                                 const float* __restrict__ dy, float* __restrict__ dx) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * IN) return;
+  const int b = (int)(t / IN), i = (int)(t % IN);
+  float s = 0.f;
+  for (int o = 0; o < OUT; ++o) s += dy[(int64_t)b * OUT + o] * w[(int64_t)o * IN + i];
+  dx[t] = s;
+}
+
+// dw[o][i] = sum_b dy[b][o] x[b][i]; dbias[o] = sum_b dy[b][o]
+__global__ void linear_dw_kernel(int B, int IN, int OUT, const float* __restrict__ x,
+                                 const float* __restrict__ dy, float* __restrict__ dw,
+                                 float* __restrict__ dbias) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t < (int64_t)OUT * IN) {
+    const int o = (int)(t / IN), i = (int)(t % IN);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dy[(int64_t)b * OUT + o] * x[(int64_t)b * IN + i];
+    dw[t] = s;
+  }
+  if (dbias && t < OUT) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dy[(int64_t)b * OUT + t];
+    dbias[t] = s;
+  }
+}
+
+struct ColList {
+  const float* p[8];
+  float* q[8];
+  int w[8];
+  int n;
+};
+
+__global__ void concat_kernel(int B, int total, ColList L, float* __restrict__ dst) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * total) return;
+  const int b = (int)(t / total);
+  int c = (int)(t % total);
+  for (int k = 0; k < L.n; ++k) {
+    if (c < L.w[k]) { dst[t] = L.p[k][(int64_t)b * L.w[k] + c]; return; }
+    c -= L.w[k];
+  }
+}
+
+__global__ void split_kernel(int B, int total, ColList L, const float* __restrict__ src) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * total) return;
+  const int b = (int)(t / total);
+  int c = (int)(t % total);
+  for (int k = 0; k < L.n; ++k) {
+    if (c < L.w[k]) { L.q[k][(int64_t)b * L.w[k] + c] = src[t]; return; }
+    c -= L.w[k];
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(int64_t n, const TI* __restrict__ x, TO* __restrict__ y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if constexpr (sizeof(TO) == 2) {
+      y[i] = f2bf((float)x[i]);                 // f64 -> f32 -> bf16, as torch does
+    } else if constexpr (sizeof(TI) == 2) {
+      y[i] = (TO)bf2f(x[i]);
+    } else {
+      y[i] = (TO)x[i];
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+template <typename T>
+__global__ void dropout_fwd_kernel(int64_t n, float p, uint64_t seed, const T* __restrict__ x,
+                                   T* __restrict__ y, uint8_t* __restrict__ keep) {
+  const float sc = 1.f / (1.f - p);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float u = (float)(mix64(seed * 0xD1342543DE82EF95ull + (uint64_t)i) >> 40) * 0x1p-24f;
+    const bool k = u >= p;
+    keep[i] = k;
+    Elt<T>::st(y, i, k ? Elt<T>::ld(x, i) * sc : 0.f);
+  }
+}
+
+template <typename T>
+__global__ void dropout_bwd_kernel(int64_t n, float p, const T* __restrict__ g,
+                                   const uint8_t* __restrict__ keep, T* __restrict__ dx) {
+  const float sc = 1.f / (1.f - p);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    Elt<T>::st(dx, i, keep[i] ? Elt<T>::ld(g, i) * sc : 0.f);
+}
+
+// mode 0: weighted CE (mean = sum w_y nll / sum w_y); mode 1: focal, pt detached.
+// One block; thread per sample (loop), f64 throughout; block reduction in fixed order.
+__global__ __launch_bounds__(256) void loss_kernel(int B, int C, const double* __restrict__ x,
+                                                   const int64_t* __restrict__ y,
+                                                   const double* __restrict__ w, double gamma,
+                                                   int mode, double* __restrict__ loss,
+                                                   double* __restrict__ dx,
+                                                   int* __restrict__ err) {
+  __shared__ double red[2][256];
+  double num = 0.0, den = 0.0;
+  const int igamma = (int)gamma;
+  const bool int_gamma = (double)igamma == gamma && igamma >= 0 && igamma <= 16;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const int64_t t = y[b];
+    if (t < 0 || t >= C) { if (err) *err = 1; continue; }
+    double mx = -__builtin_inf();
+    for (int c = 0; c < C; ++c) mx = fmax(mx, x[(int64_t)b * C + c]);
+    double se = 0.0;
+    for (int c = 0; c < C; ++c) se += exp(x[(int64_t)b * C + c] - mx);
+    const double lse = mx + log(se);
+    const double logpt = x[(int64_t)b * C + t] - lse;
+    if (mode == 0) {
+      const double wt = w ? w[t] : 1.0;
+      num += wt * -logpt;
+      den += wt;
+    } else {
+      const double pt = exp(logpt);
+      double f;
+      if (int_gamma) { f = 1.0; for (int k = 0; k < igamma; ++k) f *= (1.0 - pt); }
+      else f = pow(1.0 - pt, gamma);
+      num += -f * logpt;
+      den += 1.0;
+    }
+  }
+  red[0][threadIdx.x] = num;
+  red[1][threadIdx.x] = den;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, d = 0.0;
+    for (int k = 0; k < (int)blockDim.x; ++k) { a += red[0][k]; d += red[1][k]; }
+    red[0][0] = a;
+    red[1][0] = d;
+    *loss = a / d;
+  }
+  __syncthreads();
+  const double den_all = red[1][0];
+  // d loss / d x[b][c] = coef_b * (softmax_bc - [c == t_b])
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const int64_t t = y[b];
+    if (t < 0 || t >= C) continue;
+    double mx = -__builtin_inf();
+    for (int c = 0; c < C; ++c) mx = fmax(mx, x[(int64_t)b * C + c]);
+    double se = 0.0;
+    for (int c = 0; c < C; ++c) se += exp(x[(int64_t)b * C + c] - mx);
+    const double lse = mx + log(se);
+    double coef;
+    if (mode == 0) {
+      coef = (w ? w[t] : 1.0) / den_all;
+    } else {
+      const double pt = exp(x[(int64_t)b * C + t] - lse);
+      double f;
+      if (int_gamma) { f = 1.0; for (int k = 0; k < igamma; ++k) f *= (1.0 - pt); }
+      else f = pow(1.0 - pt, gamma);
+      coef = f / den_all;
+    }
+    for (int c = 0; c < C; ++c) {
+      const double sm = exp(x[(int64_t)b * C + c] - lse);
+      dx[(int64_t)b * C + c] = coef * (sm - (c == t ? 1.0 : 0.0));
+    }
+  }
+}
+
+unsigned grid_n(int64_t n, int block = 256) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, block), 256 * 16));
+}
+
+}  // namespace
+
+extern "C" {
+
+int mmad_linear_fwd(int b, int in, int out, const float* x, const float* w, const float* bias,
+                    int relu, float* y, void* stream) {
+  if (b <= 0 || in <= 0 || out <= 0) return MMAD_EBADSHAPE;
+  if (!x || !w || !y) return MMAD_ENULL;
+  hipLaunchKernelGGL(linear_fwd_kernel, dim3((unsigned)cdiv((int64_t)b * out, 4)), dim3(256), 0,
+                     as_stream(stream), b, in, out, x, w, bias, relu, y);
+  return launch_status();
+}
+
+int mmad_linear_bwd(int b, int in, int out, const float* x, const float* w, const float* dy,
+                    float* dx, float* dw, float* dbias, void* stream) {
+  if (b <= 0 || in <= 0 || out <= 0) return MMAD_EBADSHAPE;
+  if (!dy) return MMAD_ENULL;
+  hipStream_t st = as_stream(stream);
+  if (dx) {
+    if (!w) return MMAD_ENULL;
+    hipLaunchKernelGGL(linear_dx_kernel, dim3((unsigned)cdiv((int64_t)b * in, 256)), dim3(256), 0,
+                       st, b, in, out, w, dy, dx);
+    int rc = launch_status();
+    if (rc) return rc;
+  }
+  if (dw || dbias) {
+    if (!x || !dw) return MMAD_ENULL;
+    const int64_t n = std::max<int64_t>((int64_t)out * in, out);
+    hipLaunchKernelGGL(linear_dw_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, b, in,
+                       out, x, dy, dw, dbias);
+  }
+  return launch_status();
+}
+
+int mmad_concat_cols(int b, int n_in, const float* const* srcs, const int* widths, float* dst,
+                     void* stream) {
+  if (b <= 0 || n_in <= 0 || n_in > 8) return MMAD_EBADSHAPE;
+  if (!srcs || !widths || !dst) return MMAD_ENULL;
+  ColList L{};
+  int total = 0;
+  for (int k = 0; k < n_in; ++k) {
+    if (!srcs[k] || widths[k] <= 0) return MMAD_ENULL;
+    L.p[k] = srcs[k]; L.w[k] = widths[k]; total += widths[k];
+  }
+  L.n = n_in;
+  hipLaunchKernelGGL(concat_kernel, dim3((unsigned)cdiv((int64_t)b * total, 256)), dim3(256), 0,
+                     as_stream(stream), b, total, L, dst);
+  return launch_status();
+}
+
+int mmad_split_cols(int b, int n_out, const float* src, float* const* dsts, const int* widths,
+                    void* stream) {
+  if (b <= 0 || n_out <= 0 || n_out > 8) return MMAD_EBADSHAPE;
+  if (!src || !dsts || !widths) return MMAD_ENULL;
+  ColList L{};
+  int total = 0;
+  for (int k = 0; k < n_out; ++k) {
+    if (!dsts[k] || widths[k] <= 0) return MMAD_ENULL;
+    L.q[k] = dsts[k]; L.w[k] = widths[k]; total += widths[k];
+  }
+  L.n = n_out;
+  hipLaunchKernelGGL(split_kernel, dim3((unsigned)cdiv((int64_t)b * total, 256)), dim3(256), 0,
+                     as_stream(stream), b, total, L, src);
+  return launch_status();
+}
+
+int mmad_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream) {
+  if (n <= 0) return MMAD_EBADSHAPE;
+  if (!x || !y) return MMAD_ENULL;
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = grid_n(n);
+#define CAST(TI, TO) \
+  hipLaunchKernelGGL((cast_kernel<TI, TO>), dim3(grid), dim3(256), 0, st, n, (const TI*)x, (TO*)y)
+  if (in_dtype == MMAD_F64 && out_dtype == MMAD_F32) CAST(double, float);
+  else if (in_dtype == MMAD_F64 && out_dtype == MMAD_BF16) CAST(double, u16);
+  else if (in_dtype == MMAD_F32 && out_dtype == MMAD_BF16) CAST(float, u16);
+  else if (in_dtype == MMAD_F32 && out_dtype == MMAD_F64) CAST(float, double);
+  else if (in_dtype == MMAD_BF16 && out_dtype == MMAD_F32) CAST(u16, float);
+  else if (in_dtype == MMAD_BF16 && out_dtype == MMAD_F64) CAST(u16, double);
+  else if (in_dtype == MMAD_F32 && out_dtype == MMAD_F32) CAST(float, float);
+  else if (in_dtype == MMAD_F64 && out_dtype == MMAD_F64) CAST(double, double);
+  else return MMAD_EBADDTYPE;
+#undef CAST
+  return launch_status();
+}
+
+int mmad_dropout_fwd(int dtype, int64_t n, float p, uint64_t seed, const void* x, void* y,
+                     uint8_t* keep, void* stream) {
+  if (n <= 0 || !(p >= 0.f && p < 1.f)) return MMAD_EBADSHAPE;
+  if (!x || !y || !keep) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL(dropout_fwd_kernel<u16>, dim3(grid_n(n)), dim3(256), 0, as_stream(stream),
+                       n, p, seed, (const u16*)x, (u16*)y, keep);
+  else if (dtype == MMAD_F32)
+    hipLaunchKernelGGL(dropout_fwd_kernel<float>, dim3(grid_n(n)), dim3(256), 0,
+                       as_stream(stream), n, p, seed, (const float*)x, (float*)y, keep);
+  else
+    return MMAD_EBADDTYPE;
+  return launch_status();
+}
+
+int mmad_dropout_bwd(int dtype, int64_t n, float p, const void* g, const uint8_t* keep, void* dx,
+                     void* stream) {
+  if (n <= 0 || !(p >= 0.f && p < 1.f)) return MMAD_EBADSHAPE;
+  if (!g || !dx || !keep) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL(dropout_bwd_kernel<u16>, dim3(grid_n(n)), dim3(256), 0, as_stream(stream),
+                       n, p, (const u16*)g, keep, (u16*)dx);
+  else if (dtype == MMAD_F32)
+    hipLaunchKernelGGL(dropout_bwd_kernel<float>, dim3(grid_n(n)), dim3(256), 0,
+                       as_stream(stream), n, p, (const float*)g, keep, (float*)dx);
+  else
+    return MMAD_EBADDTYPE;
+  return launch_status();
+}
+
+int mmad_loss_fwd(int b, int c, const double* logits, const int64_t* labels, const double* weight,
+                  double gamma, int mode, double* loss, double* dlogits, void* stream) {
+  if (b <= 0 || c <= 0 || (mode != 0 && mode != 1)) return MMAD_EBADSHAPE;
+  if (!logits || !labels || !loss || !dlogits) return MMAD_ENULL;
+  hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, as_stream(stream), b, c, logits, labels,
+                     weight, gamma, mode, loss, dlogits, (int*)nullptr);
+  return launch_status();
+}
+
+int mmad_abi_version(void) { return MMAD_ABI_VERSION; }
+
+const char* mmad_strerror(int s) {
+  switch (s) {
+    case MMAD_OK: return "ok";
+    case MMAD_EBADSHAPE: return "bad shape / descriptor";
+    case MMAD_EBADDTYPE: return "unsupported dtype";
+    case MMAD_ENULL: return "null pointer argument";
+    case MMAD_EUNSUPPORTED: return "unsupported configuration";
+    default: break;
+  }
+  if (s >= MMAD_EHIP) return hipGetErrorString((hipError_t)(s - MMAD_EHIP));
+  return "unknown status";
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+"""Autograd ops of the classifier / late-fusion head and the losses (libmmad_hip.so).
+
+Reference ops replaced:
+  linear          nn.Linear            anat_cnn.py:68-76; anat_pet_fusion.py:42-51
+  concat_features torch.cat(dim=1)     anat_pet_fusion.py:76; all_modalities_fusion.py:77
+  dropout         nn.Dropout           pet_cnn.py:27-29, :38-39
+  focal / CE loss FocalLoss, nn.CrossEntropyLoss(weight)   focalloss.py:19-39; anat_cnn.py:81-85
+"""
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+from .volume_ops import cast
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu):
+        L.require_device(x, weight)
+        if x.dtype != torch.float32:
+            x = cast(x, torch.float32)
+        x = x.contiguous()
+        b, n_in = x.shape
+        n_out = weight.shape[0]
+        w = weight.detach().contiguous()
+        bb = None if bias is None else bias.detach().contiguous()
+        y = torch.empty((b, n_out), dtype=torch.float32, device=x.device)
+        L.call("mmad_linear_fwd", b, n_in, n_out, L.ptr(x), L.ptr(w), L.ptr(bb), int(relu),
+               L.ptr(y), L.stream())
+        ctx.save_for_backward(x, weight, y if relu else None)
+        ctx.has_bias = bias is not None
+        ctx.relu = relu
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight, y = ctx.saved_tensors
+        g = g.contiguous()
+        if g.dtype != torch.float32:
+            g = cast(g, torch.float32)
+        b, n_in = x.shape
+        n_out = weight.shape[0]
+        if ctx.relu:
+            gm = torch.empty_like(g)
+            L.call("mmad_relu_bwd", L.F32, g.numel(), L.ptr(g), L.ptr(y), L.ptr(gm), L.stream())
+            g = gm
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+        need_w = ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2])
+        if need_w:
+            dw = torch.empty(weight.shape, dtype=torch.float32, device=g.device)
+            if ctx.has_bias:
+                db = torch.empty(n_out, dtype=torch.float32, device=g.device)
+        L.call("mmad_linear_bwd", b, n_in, n_out, L.ptr(x), L.ptr(weight.detach()), L.ptr(g),
+               L.ptr(dx), L.ptr(dw), L.ptr(db), L.stream())
+        return dx, (dw if ctx.needs_input_grad[1] else None), db, None
+
+
+def linear(x, weight, bias=None, relu=False):
+    return _LinearFn.apply(x, weight, bias, bool(relu))
+
+
+class _ConcatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        L.require_device(*xs)
+        xs = [x if x.dtype == torch.float32 else cast(x, torch.float32) for x in xs]
+        xs = [x.contiguous() for x in xs]
+        b = xs[0].shape[0]
+        widths = [int(x.shape[1]) for x in xs]
+        y = torch.empty((b, sum(widths)), dtype=torch.float32, device=xs[0].device)
+        srcs = (C.c_void_p * len(xs))(*[x.data_ptr() for x in xs])
+        ws = (C.c_int * len(xs))(*widths)
+        L.call("mmad_concat_cols", b, len(xs), srcs, ws, L.ptr(y), L.stream())
+        ctx.widths = widths
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        b = g.shape[0]
+        outs = [torch.empty((b, w), dtype=torch.float32, device=g.device) for w in ctx.widths]
+        dsts = (C.c_void_p * len(outs))(*[o.data_ptr() for o in outs])
+        ws = (C.c_int * len(outs))(*ctx.widths)
+        L.call("mmad_split_cols", b, len(outs), L.ptr(g), dsts, ws, L.stream())
+        return tuple(outs)
+
+
+def concat_features(*xs):
+    """torch.cat(xs, dim=1) for (B, w_k) float32 feature rows."""
+    if len(xs) > 8:
+        raise L.MMADError("concat_features supports at most 8 inputs")
+    return _ConcatFn.apply(*xs)
+
+
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        L.require_device(x)
+        dense = x.is_contiguous() or (x.dim() == 5 and
+                                      x.is_contiguous(memory_format=torch.channels_last_3d))
+        if not dense:
+            x = x.contiguous()
+        y = torch.empty_like(x)
+        keep = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
+        L.call("mmad_dropout_fwd", L.dtype_code(x.dtype), x.numel(), float(p), seed, L.ptr(x),
+               L.ptr(y), L.ptr(keep), L.stream())
+        ctx.save_for_backward(keep)
+        ctx.p = p
+        ctx.like = y
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (keep,) = ctx.saved_tensors
+        g = g.contiguous(memory_format=torch.channels_last_3d) if g.dim() == 5 and \
+            ctx.like.is_contiguous(memory_format=torch.channels_last_3d) else g.contiguous()
+        dx = torch.empty_like(g)
+        L.call("mmad_dropout_bwd", L.dtype_code(g.dtype), g.numel(), float(ctx.p), L.ptr(g),
+               L.ptr(keep), L.ptr(dx), L.stream())
+        return dx, None, None
+
+
+def dropout(x, p, training):
+    if not training or p == 0.0:
+        return x
+    if p >= 1.0:
+        raise L.MMADError("dropout p must be < 1")
+    # host-side seed from torch's CPU generator: reproducible under torch.manual_seed and
+    # never synchronises the device
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    return _DropoutFn.apply(x, float(p), seed)
+
+
+class _LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, weight, gamma, mode):
+        L.require_device(logits, target)
+        x = logits.contiguous()
+        if x.dtype != torch.float64:
+            x = cast(x, torch.float64)
+        t = target.contiguous().to(torch.int64) if target.dtype != torch.int64 else \
+            target.contiguous()
+        b, c = x.shape
+        w = None if weight is None else weight.detach().to(torch.float64).contiguous()
+        loss = torch.empty((), dtype=torch.float64, device=x.device)
+        dx = torch.empty_like(x)
+        L.call("mmad_loss_fwd", b, c, L.ptr(x), L.ptr(t), L.ptr(w), float(gamma), int(mode),
+               L.ptr(loss), L.ptr(dx), L.stream())
+        ctx.save_for_backward(dx)
+        ctx.in_dtype = logits.dtype
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dx,) = ctx.saved_tensors
+        grad = dx * g          # (B, C) x 0-d scale: trivial glue, stays on device
+        if ctx.in_dtype != torch.float64:
+            grad = cast(grad, ctx.in_dtype)
+        return grad, None, None, None, None
+
+
+def weighted_cross_entropy(logits, target, weight=None):
+    """nn.CrossEntropyLoss(weight)(logits, target), 'mean' reduction (anat_cnn.py:84-85)."""
+    if logits.dim() != 2:
+        raise L.MMADError("cross entropy expects (B, C) logits")
+    return _LossFn.apply(logits, target, weight, 0.0, 0)
+
+
+def focal_loss(logits, target, gamma):
+    """FocalLoss(gamma)(logits, target): alpha None, mean, pt detached (focalloss.py:19-39)."""
+    if logits.dim() > 2:
+        n, c = logits.shape[:2]
+        logits = logits.reshape(n, c, -1).transpose(1, 2).reshape(-1, c)
+    return _LossFn.apply(logits, target.reshape(-1), None, float(gamma), 1)

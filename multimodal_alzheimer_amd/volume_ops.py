@@ -1,0 +1,399 @@
+"""Autograd ops over NDHWC volumes, each a thin call into libmmad_hip.so.
+
+A volume tensor is a logical (N, C, D, H, W) torch tensor in ``torch.channels_last_3d``
+memory format -- exactly the NDHWC layout the kernels use -- so any torch code that
+inspects shapes sees the reference's NCDHW semantics.  Compute dtype is float32
+(parity mode, exact-f32 MFMA) or bfloat16 (throughput mode, f32 accumulation).
+
+Reference ops replaced (file:line in the reference tree):
+  conv3d          nn.Conv3d            MedicalNet convs via anat_cnn.py:29-31; pet_cnn.py:20-22
+  batchnorm_act   nn.BatchNorm3d/1d + nn.ReLU (+ residual add)  MedicalNet BasicBlock;
+                                       anat_cnn.py:50-51, :69-70; pet_cnn.py:23-25
+  max_pool3d      nn.MaxPool3d         MedicalNet stem; anat_cnn.py:62; pet_cnn.py:26
+  global_avg_pool nn.AdaptiveAvgPool3d(1)  anat_cnn.py:66; pet_cnn.py:33
+"""
+import torch
+
+from . import _lib as L
+
+CL = torch.channels_last_3d
+
+
+def _cl(t):
+    """dense NDHWC view of a volume gradient (no copy when already channels-last)."""
+    if t.dim() == 5:
+        return t.contiguous(memory_format=CL)
+    return t.contiguous()
+
+
+def _empty_vol(n, c, d, h, w, dtype, device):
+    return torch.empty((n, c, d, h, w), dtype=dtype, device=device, memory_format=CL)
+
+
+def _check_vol(x, dtype=None):
+    L.require_device(x)
+    if x.dim() != 5 or not x.is_contiguous(memory_format=CL):
+        raise L.MMADError("volume tensors must be 5-D channels_last_3d (NDHWC)")
+    if dtype is not None and x.dtype != dtype:
+        raise L.MMADError(f"expected {dtype}, got {x.dtype}")
+    if x.data_ptr() % 16:
+        raise L.MMADError("volume tensors must be 16-byte aligned")
+
+
+# ---------------------------------------------------------------------------------- conv
+def out_extent(i, k, s, p, d):
+    return (i + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+def conv_desc(xshape, wshape, stride, padding, dilation):
+    n, ci, di, hi, wi = xshape
+    co, ci_w, kd, kh, kw = wshape
+    if ci_w != ci:
+        raise L.MMADError(f"conv3d: input has {ci} channels, weight expects {ci_w}")
+    sd, sh, sw = stride
+    pd, ph, pw = padding
+    dd, dh, dw = dilation
+    return L.ConvDesc(n, ci, di, hi, wi, co, out_extent(di, kd, sd, pd, dd),
+                      out_extent(hi, kh, sh, ph, dh), out_extent(wi, kw, sw, pw, dw),
+                      kd, kh, kw, sd, sh, sw, pd, ph, pw, dd, dh, dw)
+
+
+def _desc_tuple(d):
+    return tuple(getattr(d, f) for f, _ in L.ConvDesc._fields_)
+
+
+def pack_weight(d, dt_code, weight, cdtype, for_dgrad):
+    lib = L.load()
+    n = lib.mmad_conv_packed_elems(d, dt_code, int(for_dgrad))
+    if n < 0:
+        raise L.MMADError("conv3d: unsupported geometry")
+    wp = torch.empty(n, dtype=cdtype, device=weight.device)
+    L.call("mmad_conv_pack_weight", d, dt_code, L.ptr(weight.detach().contiguous()), L.ptr(wp),
+           int(for_dgrad), L.stream())
+    return wp
+
+
+class _Conv3dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, geom, cdtype, want_stats):
+        stride, padding, dilation = geom
+        L.require_device(x, weight)
+        if weight.dtype != torch.float32:
+            raise L.MMADError("conv3d master weights must be float32")
+        d = conv_desc(tuple(x.shape), tuple(weight.shape), stride, padding, dilation)
+        dt = L.dtype_code(cdtype)
+        lib = L.load()
+        if d.ci == 1:
+            if ctx.needs_input_grad[0]:
+                raise L.MMADError("conv3d: gradient w.r.t. a 1-channel raw input volume "
+                                  "is not supported (the input never needs one)")
+            xc = x.contiguous()
+            src = torch.empty(lib.mmad_conv_unfolded_elems(d), dtype=cdtype, device=x.device)
+            L.call("mmad_conv_unfold_input", d, L.dtype_code(xc.dtype), L.ptr(xc), dt,
+                   L.ptr(src), L.stream())
+        else:
+            _check_vol(x, cdtype)
+            src = x
+        wp = pack_weight(d, dt, weight, cdtype, False)
+        y = _empty_vol(d.n, d.co, d.do_, d.ho, d.wo, cdtype, x.device)
+        stats = None
+        if want_stats:
+            rows = lib.mmad_conv3d_stats_rows(d, dt)
+            stats = torch.empty((rows, 2, d.co), dtype=torch.float32, device=x.device)
+        b = None if bias is None else bias.detach().contiguous()
+        L.call("mmad_conv3d_fwd", d, dt, L.ptr(src), L.ptr(wp), L.ptr(b), L.ptr(y),
+               L.ptr(stats), L.stream())
+        ctx.save_for_backward(src, weight)
+        ctx.desc = _desc_tuple(d)
+        ctx.cdtype = cdtype
+        ctx.has_bias = bias is not None
+        ctx.xshape = tuple(x.shape)
+        if want_stats:
+            ctx.mark_non_differentiable(stats)
+            return y, stats
+        return y
+
+    @staticmethod
+    def backward(ctx, gy, *_):
+        src, weight = ctx.saved_tensors
+        d = L.ConvDesc(*ctx.desc)
+        cdtype = ctx.cdtype
+        dt = L.dtype_code(cdtype)
+        gy = _cl(gy)
+        if gy.dtype != cdtype:
+            gy = cast(gy, cdtype)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wpt = pack_weight(d, dt, weight, cdtype, True)
+            dx = _empty_vol(d.n, d.ci, d.di, d.hi, d.wi, cdtype, gy.device)
+            L.call("mmad_conv3d_dgrad", d, dt, L.ptr(gy), L.ptr(wpt), L.ptr(dx), L.stream())
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            lib = L.load()
+            ws = torch.empty((lib.mmad_conv3d_wgrad_workspace(d, dt) + 3) // 4,
+                             dtype=torch.float32, device=gy.device)
+            dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
+            db = (torch.empty(d.co, dtype=torch.float32, device=gy.device)
+                  if ctx.has_bias else None)
+            L.call("mmad_conv3d_wgrad", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db),
+                   L.ptr(ws), L.stream())
+            if not ctx.needs_input_grad[1]:
+                dw = None
+        return dx, dw, db, None, None, None
+
+
+def conv3d(x, weight, bias=None, stride=(1, 1, 1), padding=(0, 0, 0), dilation=(1, 1, 1),
+           cdtype=torch.float32, want_stats=False):
+    """nn.functional.conv3d on NDHWC volumes; with want_stats also returns the BN partial
+    sums ([rows][2][Co] fp32) of the output, produced by the conv epilogue."""
+    return _Conv3dFn.apply(x, weight, bias, (tuple(stride), tuple(padding), tuple(dilation)),
+                           cdtype, want_stats)
+
+
+# ----------------------------------------------------------------------------- batchnorm
+def _rows(t):
+    c = t.shape[1]
+    return t.numel() // c, c
+
+
+def _finalize(y, parts, bn, training):
+    """batch (or running) statistics -> mean, invstd, scale, shift; updates running stats."""
+    m, c = _rows(y)
+    dev = y.device
+    mean = torch.empty(c, dtype=torch.float32, device=dev)
+    invstd = torch.empty_like(mean)
+    scale = torch.empty_like(mean)
+    shift = torch.empty_like(mean)
+    gamma = None if bn.weight is None else bn.weight.detach()
+    beta = None if bn.bias is None else bn.bias.detach()
+    use_batch = training or bn.running_mean is None
+    if use_batch:
+        if parts is None:
+            nparts = L.load().mmad_bn_stats_parts(m, c)
+            parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
+            L.call("mmad_bn_stats", L.dtype_code(y.dtype), m, c, L.ptr(y), L.ptr(parts),
+                   L.stream())
+        update = training and bn.track_running_stats and bn.running_mean is not None
+        if update:
+            if bn.momentum is None:
+                raise L.MMADError("BatchNorm momentum=None (cumulative average) unsupported")
+            bn.num_batches_tracked.add_(1)
+        L.call("mmad_bn_finalize", c, m, parts.shape[0], L.ptr(parts), L.ptr(gamma),
+               L.ptr(beta), L.ptr(bn.running_mean if update else None),
+               L.ptr(bn.running_var if update else None), float(bn.momentum or 0.0),
+               float(bn.eps), 1, L.ptr(mean), L.ptr(invstd), L.ptr(scale), L.ptr(shift),
+               L.stream())
+    else:
+        L.call("mmad_bn_finalize", c, m, 0, None, L.ptr(gamma), L.ptr(beta),
+               L.ptr(bn.running_mean), L.ptr(bn.running_var), 0.0, float(bn.eps), 0,
+               L.ptr(mean), L.ptr(invstd), L.ptr(scale), L.ptr(shift), L.stream())
+    return mean, invstd, scale, shift, use_batch
+
+
+def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask):
+    m, c = _rows(y)
+    dev = y.device
+    dt = L.dtype_code(y.dtype)
+    nparts = L.load().mmad_bn_bwd_parts(m, c)
+    parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
+    L.call("mmad_bn_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y), L.ptr(mean),
+           L.ptr(invstd), L.ptr(parts), L.stream())
+    dgamma = torch.empty(c, dtype=torch.float32, device=dev)
+    dbeta = torch.empty_like(dgamma)
+    coef = torch.empty(3 * c, dtype=torch.float32, device=dev)
+    L.call("mmad_bn_bwd_finalize", c, m, nparts, L.ptr(parts), L.ptr(gamma), L.ptr(invstd),
+           int(batch_stats), L.ptr(dgamma), L.ptr(dbeta), L.ptr(coef), L.stream())
+    dy = torch.empty_like(y)
+    gmask = torch.empty_like(y) if want_gmask else None
+    L.call("mmad_bn_bwd_apply", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y), L.ptr(mean),
+           L.ptr(invstd), L.ptr(coef), L.ptr(dy), L.ptr(gmask), L.stream())
+    return dy, dgamma, dbeta, gmask
+
+
+class _BNActFn(torch.autograd.Function):
+    """out = act(bn(y) [+ res | + bn_r(res)]) in one pass over y (and res)."""
+
+    @staticmethod
+    def forward(ctx, y, parts, gamma, beta, res, res_parts, rgamma, rbeta, cfg):
+        bn, relu, training, rbn = cfg
+        L.require_device(y)
+        mean, invstd, scale, shift, batch = _finalize(y, parts, bn, training)
+        rscale = rshift = rmean = rinvstd = None
+        rbatch = False
+        if rbn is not None:
+            rmean, rinvstd, rscale, rshift, rbatch = _finalize(res, res_parts, rbn, training)
+        out = torch.empty_like(y)
+        m, c = _rows(y)
+        L.call("mmad_scale_shift_act", L.dtype_code(y.dtype), m, c, L.ptr(y), L.ptr(scale),
+               L.ptr(shift), L.ptr(res), L.ptr(rscale), L.ptr(rshift), int(relu), L.ptr(out),
+               L.stream())
+        ctx.save_for_backward(y, out if relu else None, mean, invstd, gamma,
+                              res if rbn is not None else None, rmean, rinvstd, rgamma)
+        ctx.cfg = (relu, batch, rbatch, res is not None, rbn is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        y, out, mean, invstd, gamma, rres, rmean, rinvstd, rgamma = ctx.saved_tensors
+        relu, batch, rbatch, has_res, has_rbn = ctx.cfg
+        g = _cl(g) if y.dim() == 5 else g.contiguous()
+        if g.dtype != y.dtype:
+            g = cast(g, y.dtype)
+        gam = None if gamma is None else gamma.detach()
+        dy, dgamma, dbeta, gmask = _bn_backward(g, out, y, mean, invstd, gam, batch,
+                                                has_res and not has_rbn)
+        dres = drg = drb = None
+        if has_rbn:
+            rg = None if rgamma is None else rgamma.detach()
+            dres, drg, drb, _ = _bn_backward(g, out, rres, rmean, rinvstd, rg, rbatch, False)
+        elif has_res:
+            dres = gmask
+        return (dy, None, dgamma if ctx.needs_input_grad[2] else None,
+                dbeta if ctx.needs_input_grad[3] else None, dres, None,
+                drg if ctx.needs_input_grad[6] else None,
+                drb if ctx.needs_input_grad[7] else None, None)
+
+
+def batchnorm_act(y, bn, parts=None, relu=False, res=None, res_bn=None, res_parts=None):
+    """bn(y) (+ res or res_bn(res)) then optional ReLU, torch BatchNorm semantics.
+
+    ``bn`` / ``res_bn`` are nn.BatchNorm modules (parameters + running buffers);
+    ``parts`` are the conv-epilogue partial sums of y when y came from conv3d.
+    """
+    if y.dim() == 5:
+        _check_vol(y)
+    elif not y.is_contiguous():
+        raise L.MMADError("batchnorm_act expects a contiguous (B, C) tensor")
+    if res is not None:
+        if res.shape != y.shape or res.dtype != y.dtype:
+            raise L.MMADError("residual must match the BN input in shape and dtype")
+        if y.dim() == 5:
+            _check_vol(res)
+    training = bn.training or not bn.track_running_stats
+    return _BNActFn.apply(y, parts, bn.weight, bn.bias, res, res_parts,
+                          None if res_bn is None else res_bn.weight,
+                          None if res_bn is None else res_bn.bias,
+                          (bn, relu, training, res_bn))
+
+
+# ------------------------------------------------------------------------------- pooling
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        _check_vol(x)
+        n, c, di, hi, wi = x.shape
+        do, ho, wo = ((v + 2 * p - k) // s + 1 for v in (di, hi, wi))
+        y = _empty_vol(n, c, do, ho, wo, x.dtype, x.device)
+        am = torch.empty((n, do, ho, wo, c), dtype=torch.uint8, device=x.device)
+        L.call("mmad_maxpool3d_fwd", L.dtype_code(x.dtype), n, c, di, hi, wi, do, ho, wo, k, s,
+               p, L.ptr(x), L.ptr(y), L.ptr(am), L.stream())
+        ctx.save_for_backward(am)
+        ctx.geo = (n, c, di, hi, wi, do, ho, wo, k, s, p)
+        ctx.dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (am,) = ctx.saved_tensors
+        n, c, di, hi, wi, do, ho, wo, k, s, p = ctx.geo
+        g = _cl(g)
+        if g.dtype != ctx.dtype:
+            g = cast(g, ctx.dtype)
+        dx = _empty_vol(n, c, di, hi, wi, ctx.dtype, g.device)
+        L.call("mmad_maxpool3d_bwd", L.dtype_code(ctx.dtype), n, c, di, hi, wi, do, ho, wo, k,
+               s, p, L.ptr(g), L.ptr(am), L.ptr(dx), L.stream())
+        return dx, None, None, None
+
+
+def max_pool3d(x, kernel_size, stride=None, padding=0):
+    return _MaxPoolFn.apply(x, int(kernel_size), int(stride or kernel_size), int(padding))
+
+
+class _GapFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        _check_vol(x)
+        n, c = x.shape[:2]
+        s = x.numel() // (n * c)
+        y = torch.empty((n, c, 1, 1, 1), dtype=torch.float32, device=x.device)
+        L.call("mmad_gap_fwd", L.dtype_code(x.dtype), n, s, c, L.ptr(x), L.ptr(y), L.stream())
+        ctx.shape = tuple(x.shape)
+        ctx.dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        n, c = ctx.shape[:2]
+        s = 1
+        for v in ctx.shape[2:]:
+            s *= v
+        g = g.contiguous()
+        if g.dtype != torch.float32:
+            g = cast(g, torch.float32)
+        dx = _empty_vol(*ctx.shape, ctx.dtype, g.device)
+        L.call("mmad_gap_bwd", L.dtype_code(ctx.dtype), n, s, c, L.ptr(g), L.ptr(dx), L.stream())
+        return dx
+
+
+def global_avg_pool(x):
+    """AdaptiveAvgPool3d(1): (N,C,D,H,W) NDHWC -> (N,C,1,1,1) float32."""
+    return _GapFn.apply(x)
+
+
+# --------------------------------------------------------------------- elementwise / cast
+class _ReluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        L.require_device(x)
+        if not (x.is_contiguous() or (x.dim() == 5 and x.is_contiguous(memory_format=CL))):
+            raise L.MMADError("relu expects a dense tensor")
+        y = torch.empty_like(x)
+        L.call("mmad_relu_fwd", L.dtype_code(x.dtype), x.numel(), L.ptr(x), L.ptr(y), L.stream())
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        g = _cl(g) if y.dim() == 5 and y.is_contiguous(memory_format=CL) else g.contiguous()
+        if g.dtype != y.dtype:
+            g = cast(g, y.dtype)
+        dx = torch.empty_like(y)
+        L.call("mmad_relu_bwd", L.dtype_code(y.dtype), y.numel(), L.ptr(g), L.ptr(y), L.ptr(dx),
+               L.stream())
+        return dx
+
+
+def relu(x):
+    return _ReluFn.apply(x)
+
+
+class _CastFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.src = x.dtype
+        return _cast_raw(x, dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _cast_raw(g, ctx.src), None
+
+
+def _cast_raw(x, dtype):
+    L.require_device(x)
+    if x.dtype == dtype:
+        return x
+    if x.dim() == 5 and x.is_contiguous(memory_format=CL) and not x.is_contiguous():
+        y = torch.empty_like(x, dtype=dtype)
+    else:
+        x = x.contiguous()
+        y = torch.empty(x.shape, dtype=dtype, device=x.device)
+    L.call("mmad_cast", L.dtype_code(x.dtype), L.dtype_code(dtype), x.numel(), L.ptr(x),
+           L.ptr(y), L.stream())
+    return y
+
+
+def cast(x, dtype):
+    """dtype conversion on device (f64 -> f32 -> bf16 rounding order, as torch)."""
+    if x.dtype == dtype:
+        return x
+    return _CastFn.apply(x, dtype)

@@ -1,0 +1,247 @@
+"""Per-kernel parity on the MI355X: every HIP op against a torch-CPU float64 reference of
+the same op on the same seeded inputs (fp32 mode to ~1e-5, bf16 mode to bf16 rounding).
+All calls go through libmmad_hip.so (no torch fallback exists)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from multimodal_alzheimer_amd import _lib, head_ops, volume_ops as V
+
+pytestmark = pytest.mark.gpu
+CL = torch.channels_last_3d
+DEV = "cuda"
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(shape, generator=g, dtype=torch.float64) * 2 - 1) * scale
+
+
+def to_vol(x, dtype):
+    return x.to(DEV, dtype).contiguous(memory_format=CL)
+
+
+def close(got, ref, rtol, name=""):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-12
+    assert err <= rtol * scale, f"{name}: max|err| {err:.3e} > {rtol:.1e} * {scale:.3e}"
+
+
+# (N, Ci, D, H, W, Co, k, stride, pad, dil, bias)
+CONV_CASES = [
+    (2, 1, 20, 18, 22, 64, 7, 2, 3, 1, False),     # MedicalNet stem (unfolded path)
+    (2, 64, 8, 10, 6, 64, 3, 1, 1, 1, False),      # layer1
+    (2, 64, 9, 8, 10, 128, 3, 2, 1, 1, False),     # layer2.0.conv1 (stride 2)
+    (2, 128, 6, 7, 5, 256, 3, 1, 2, 2, False),     # layer3 (dilation 2)
+    (1, 256, 6, 6, 6, 512, 3, 1, 4, 4, False),     # layer4 (dilation 4)
+    (2, 64, 9, 8, 10, 128, 1, 2, 0, 1, False),     # shortcut B, stride 2
+    (2, 128, 5, 6, 7, 256, 1, 1, 0, 1, False),     # shortcut B, stride 1
+    (2, 1, 12, 11, 13, 8, 5, 1, 2, 1, True),       # Small_PET_CNN conv 1 (k5 'same')
+    (2, 1, 9, 10, 8, 16, 7, 1, 3, 1, True),        # Small_PET_CNN conv 1 (k7 'same')
+    (2, 8, 10, 9, 11, 16, 5, 1, 2, 1, True),       # Small_PET_CNN conv 2
+    (2, 32, 6, 5, 7, 64, 3, 1, 1, 1, True),        # Small_PET_CNN conv 4
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: f"ci{c[1]}co{c[5]}k{c[6]}s{c[7]}d{c[9]}")
+def test_conv3d_fwd_bwd(case, dtype):
+    n, ci, d, h, w, co, k, s, p, dl, has_bias = case
+    x = rnd(n, ci, d, h, w, seed=1)
+    wt = rnd(co, ci, k, k, k, seed=2, scale=(3.0 / (ci * k ** 3)) ** 0.5)
+    b = rnd(co, seed=3) if has_bias else None
+    if dtype == torch.bfloat16:          # reference on the bf16-rounded operands
+        x = x.to(torch.bfloat16).double()
+        wt = wt.float().to(torch.bfloat16).double()
+    xr = x.clone().requires_grad_(ci > 1)
+    wr = wt.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True) if has_bias else None
+    yr = F.conv3d(xr, wr, br, s, p, dl)
+    gy = rnd(*yr.shape, seed=4)
+    if dtype == torch.bfloat16:
+        gy = gy.to(torch.bfloat16).double()
+    yr.backward(gy)
+
+    xg = (x.to(DEV, torch.float32) if ci == 1 else to_vol(x, dtype)).requires_grad_(ci > 1)
+    wg = wt.float().to(DEV).requires_grad_(True)
+    bg = b.float().to(DEV).requires_grad_(True) if has_bias else None
+    y, stats = V.conv3d(xg, wg, bg, (s,) * 3, (p,) * 3, (dl,) * 3, dtype, want_stats=True)
+    assert y.is_contiguous(memory_format=CL) and y.dtype == dtype
+    y.backward(to_vol(gy, dtype))
+    tol = 2e-5 if dtype == torch.float32 else 1.2e-2
+    close(y, yr, tol, "y")
+    ysum = yr.detach().sum(dim=(0, 2, 3, 4))
+    ysq = (yr.detach() ** 2).sum(dim=(0, 2, 3, 4))
+    close(stats[:, 0].sum(0), ysum, 1e-4 if dtype == torch.float32 else 2e-2, "stats.sum")
+    close(stats[:, 1].sum(0), ysq, 1e-4 if dtype == torch.float32 else 2e-2, "stats.sumsq")
+    gtol = 3e-5 if dtype == torch.float32 else 2e-2
+    close(wg.grad, wr.grad, gtol, "dw")
+    if has_bias:
+        close(bg.grad, br.grad, gtol, "db")
+    if ci > 1:
+        close(xg.grad, xr.grad, gtol, "dx")
+
+
+def test_conv_large_k_split():
+    """wgrad split-K path with many voxels (M >> tile) and Co = 64."""
+    n, ci, co = 2, 64, 64
+    x = rnd(n, ci, 16, 16, 16, seed=5)
+    wt = rnd(co, ci, 3, 3, 3, seed=6, scale=0.05)
+    xr = x.clone().requires_grad_(True)
+    wr = wt.clone().requires_grad_(True)
+    yr = F.conv3d(xr, wr, None, 1, 1, 1)
+    gy = rnd(*yr.shape, seed=7)
+    yr.backward(gy)
+    xg = to_vol(x, torch.float32).requires_grad_(True)
+    wg = wt.float().to(DEV).requires_grad_(True)
+    y = V.conv3d(xg, wg, None, (1,) * 3, (1,) * 3, (1,) * 3, torch.float32)
+    y.backward(to_vol(gy, torch.float32))
+    close(y, yr, 2e-5, "y")
+    close(wg.grad, wr.grad, 3e-5, "dw")
+    close(xg.grad, xr.grad, 3e-5, "dx")
+
+
+class _BN:
+    def __init__(self, c, seed):
+        self.weight = (1 + 0.3 * rnd(c, seed=seed)).float().to(DEV).requires_grad_(True)
+        self.bias = (0.2 * rnd(c, seed=seed + 1)).float().to(DEV).requires_grad_(True)
+        self.running_mean = (0.1 * rnd(c, seed=seed + 2)).float().to(DEV)
+        self.running_var = (1 + 0.5 * rnd(c, seed=seed + 3).abs()).float().to(DEV)
+        self.num_batches_tracked = torch.zeros((), dtype=torch.long, device=DEV)
+        self.momentum, self.eps = 0.1, 1e-5
+        self.training, self.track_running_stats = True, True
+
+
+def _ref_bn(x, bn, training):
+    rm = bn.running_mean.double().cpu().clone()
+    rv = bn.running_var.double().cpu().clone()
+    w = bn.weight.detach().double().cpu().requires_grad_(True)
+    b = bn.bias.detach().double().cpu().requires_grad_(True)
+    y = F.batch_norm(x, rm, rv, w, b, training, bn.momentum, bn.eps)
+    return y, w, b, rm, rv
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mode", ["plain", "relu", "identity_res", "bn_res", "eval"])
+def test_batchnorm_act(mode, dtype):
+    n, c, d, h, w = 2, 64, 5, 6, 7
+    y0 = rnd(n, c, d, h, w, seed=10, scale=2.0) + 0.5
+    r0 = rnd(n, c, d, h, w, seed=11)
+    if dtype == torch.bfloat16:
+        y0, r0 = y0.to(dtype).double(), r0.to(dtype).double()
+    training = mode != "eval"
+    bn, rbn = _BN(c, 20), _BN(c, 30)
+    bn.training = rbn.training = training
+    yr = y0.clone().requires_grad_(True)
+    rr = r0.clone().requires_grad_(True)
+    out_r, w1, b1, rm1, rv1 = _ref_bn(yr, bn, training)
+    if mode == "identity_res":
+        out_r = out_r + rr
+    if mode == "bn_res":
+        o2, w2, b2, rm2, rv2 = _ref_bn(rr, rbn, training)
+        out_r = out_r + o2
+    if mode in ("relu", "identity_res", "bn_res"):
+        out_r = torch.relu(out_r)
+    g = rnd(*out_r.shape, seed=12)
+    if dtype == torch.bfloat16:
+        g = g.to(dtype).double()
+    out_r.backward(g)
+
+    yg = to_vol(y0, dtype).requires_grad_(True)
+    rg = to_vol(r0, dtype).requires_grad_(True)
+    out = V.batchnorm_act(yg, bn, relu=mode in ("relu", "identity_res", "bn_res"),
+                          res=rg if mode in ("identity_res", "bn_res") else None,
+                          res_bn=rbn if mode == "bn_res" else None)
+    out.backward(to_vol(g, dtype))
+    tol = 2e-5 if dtype == torch.float32 else 1.5e-2
+    close(out, out_r, tol, "out")
+    close(yg.grad, yr.grad, 5 * tol, "dy")
+    close(bn.weight.grad, w1.grad, 5 * tol, "dgamma")
+    close(bn.bias.grad, b1.grad, 5 * tol, "dbeta")
+    close(bn.running_mean, rm1, 1e-5, "running_mean")
+    close(bn.running_var, rv1, 1e-5, "running_var")
+    if mode in ("identity_res", "bn_res"):
+        close(rg.grad, rr.grad, 5 * tol, "dres")
+    if mode == "bn_res":
+        close(rbn.weight.grad, w2.grad, 5 * tol, "dgamma_res")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("k,s,p,shape", [(3, 2, 1, (2, 64, 9, 10, 11)), (2, 2, 0, (2, 16, 9, 8, 7))])
+def test_maxpool(k, s, p, shape, dtype):
+    x = rnd(*shape, seed=40)
+    x = torch.relu(x)                          # exact zeros -> ties everywhere
+    x = x.to(dtype).double()
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool3d(xr.float(), k, s, p).double()   # torch CPU kernel = the tie rule
+    g = rnd(*yr.shape, seed=41).to(dtype).double()
+    yr.backward(g)
+    xg = to_vol(x, dtype).requires_grad_(True)
+    y = V.max_pool3d(xg, k, s, p)
+    y.backward(to_vol(g, dtype))
+    assert torch.equal(y.double().cpu(), yr.detach())
+    close(xg.grad, xr.grad, 1e-6 if dtype == torch.float32 else 1e-2, "dx")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_global_avg_pool(dtype):
+    x = rnd(3, 512, 4, 5, 6, seed=50).to(dtype).double()
+    xr = x.clone().requires_grad_(True)
+    yr = F.adaptive_avg_pool3d(xr, 1)
+    g = rnd(3, 512, 1, 1, 1, seed=51)
+    yr.backward(g)
+    xg = to_vol(x, dtype).requires_grad_(True)
+    y = V.global_avg_pool(xg)
+    y.backward(g.float().to(DEV))
+    close(y, yr, 1e-6, "gap")
+    close(xg.grad, xr.grad, 1e-6 if dtype == torch.float32 else 5e-3, "dgap")
+
+
+def test_linear_concat_relu():
+    x1, x2 = rnd(8, 64, seed=60), rnd(8, 64, seed=61)
+    w, b = rnd(64, 128, seed=62, scale=0.1), rnd(64, seed=63)
+    refs = [t.clone().requires_grad_(True) for t in (x1, x2, w, b)]
+    yr = torch.relu(F.linear(torch.cat(refs[:2], 1), refs[2], refs[3]))
+    g = rnd(8, 64, seed=64)
+    yr.backward(g)
+    gs = [t.float().to(DEV).requires_grad_(True) for t in (x1, x2, w, b)]
+    y = V.relu(head_ops.linear(head_ops.concat_features(gs[0], gs[1]), gs[2], gs[3]))
+    y.backward(g.float().to(DEV))
+    close(y, yr, 1e-5, "linear")
+    for a, r, nm in zip(gs, refs, ("dx1", "dx2", "dw", "db")):
+        close(a.grad, r.grad, 1e-5, nm)
+
+
+@pytest.mark.parametrize("C", [2, 3])
+@pytest.mark.parametrize("gamma", [None, 1, 2, 5])
+def test_losses_vs_golden(C, gamma):
+    from tests import _golden as G
+    g = G.load("losses")
+    x = torch.tensor(g[f"x_C{C}"], device=DEV, requires_grad=True)
+    y = torch.from_numpy(g[f"y_C{C}"]).to(DEV)
+    if gamma is None:
+        wts = torch.tensor(G.W2 if C == 2 else G.W3, dtype=torch.float64, device=DEV)
+        loss = head_ops.weighted_cross_entropy(x, y, wts)
+        key = f"ce_C{C}"
+    else:
+        loss = head_ops.focal_loss(x, y, gamma)
+        key = f"focal_g{gamma}_C{C}"
+    loss.backward()
+    assert abs(loss.item() - float(g[key + "_loss"])) <= 1e-12 * max(1, abs(float(g[key + "_loss"])))
+    close(x.grad, torch.from_numpy(g[key + "_grad"]), 1e-12, "dlogits")
+
+
+def test_cast_roundtrip():
+    x = rnd(1000, seed=70).to(DEV)
+    y = V.cast(x, torch.bfloat16)
+    assert torch.equal(y.cpu(), x.cpu().float().to(torch.bfloat16))
+    z = V.cast(V.cast(x, torch.float32), torch.float64)
+    assert torch.equal(z.cpu(), x.cpu().float().double())
+
+
+def test_library_loaded_is_ours():
+    import os
+    lib = _lib.load()
+    assert os.path.samefile(lib._name, _lib.LIB_PATH)
