@@ -1,0 +1,206 @@
+"""Throughput benchmark of the 3D-volume training hot path on MI355X.
+
+BASELINE.json metric: "volumes/sec fwd+bwd, 3D-ResNet-10 @128^3 bf16, 1/2/4/8 MI355X;
+% HBM roofline".  Workload (BASELINE config 2): MRI-only Anat_CNN ResNet-10, synthetic
+1x128^3 volumes (uniform[0,1) like min-max-normalised MRI, resident in HBM as float64 as
+the reference DataLoader delivers them), batch 8 per GPU, weighted CE, bf16 compute with
+fp32 master weights.  One step = general_step (forward + loss) + backward + gradient
+all-reduce (N>1) + Adam; all parameters trainable (lr_pretrained set).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+
+Rank 0 prints one JSON line.  ``roofline`` times the dominant kernel (layer4.0.conv2
+forward, the largest implicit-GEMM launch) with HIP events on the stream it runs on;
+``cpu_baseline`` times the CPU oracle (torch fp32, the reference path) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import multimodal_alzheimer_amd as M  # noqa: E402
+from multimodal_alzheimer_amd import _lib, volume_ops  # noqa: E402
+from multimodal_alzheimer_amd.data_parallel import GradAllReduce  # noqa: E402
+
+W2 = [0.20314960629921264, 0.7968503937007874]
+FLOP_PER_VOL = {128: 424.7e9}            # fwd+bwd ResNet-10 @128^3
+M2_BYTES_PER_VOL = 1.163e9               # unfused eager byte model
+PEAK_BF16 = 2.5e15                       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32 = 157.3e12
+PEAK_HBM = 8.0e12
+
+
+def hparams(precision):
+    return {"n_classes": 2, "resnet_depth": 10, "conv_out": [], "filter_size": [],
+            "batchnorm_begin": False, "batchnorm_dense": False, "linear_out": [],
+            "fl_gamma": None, "lr": 1e-3, "lr_pretrained": 1e-5, "l2_reg": 0,
+            "reduce_factor_lr_schedule": None, "precision": precision,
+            "loss_class_weights": torch.tensor(W2, dtype=torch.float64)}
+
+
+def dominant_kernel_roofline(model, batch, size, dtype, reps=20):
+    """Time layer4.0.conv2's forward implicit GEMM alone with HIP events."""
+    conv = model.model.layer4[0].conv2
+    s = size // 8
+    n = batch
+    x = torch.randn((n, 512, s, s, s), device="cuda", dtype=dtype).contiguous(
+        memory_format=torch.channels_last_3d)
+    d = volume_ops.conv_desc(tuple(x.shape), tuple(conv.weight.shape), (1, 1, 1), (4, 4, 4),
+                             (4, 4, 4))
+    dt = _lib.dtype_code(dtype)
+    wp = volume_ops.pack_weight(d, dt, conv.weight, dtype, False)
+    y = torch.empty((n, 512, s, s, s), device="cuda", dtype=dtype).contiguous(
+        memory_format=torch.channels_last_3d)
+    lib = _lib.load()
+    stats = torch.empty((lib.mmad_conv3d_stats_rows(d, dt), 2, 512), device="cuda")
+    st = torch.cuda.current_stream()
+
+    def launch():
+        _lib.call("mmad_conv3d_fwd", d, dt, _lib.ptr(x), _lib.ptr(wp), None, _lib.ptr(y),
+                  _lib.ptr(stats), _lib.stream())
+
+    for _ in range(3):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        launch()
+    e1.record(st)
+    e1.synchronize()
+    sec = e0.elapsed_time(e1) / 1e3 / reps
+    flops = 2.0 * n * s ** 3 * 512 * 512 * 27
+    peak = PEAK_BF16 if dtype == torch.bfloat16 else PEAK_F32
+    traffic = None
+    tf = os.path.join(REPO, "profiles", "traffic_layer4_conv2_fwd.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    return {"kernel": "igemm_kernel<bf16,128> layer4.0.conv2 fwd (512->512, 3^3 dil 4, "
+                      f"{n}x{s}^3)",
+            "bound": "mfma", "achieved": flops / sec / 1e12, "peak": peak / 1e12,
+            "unit": "TFLOP/s", "frac": flops / sec / peak, "traffic": traffic,
+            "flop_per_launch": flops, "avg_launch_ms": sec * 1e3}
+
+
+def cpu_baseline(size, seconds_budget=20.0):
+    """CPU oracle (torch fp32 restatement of the reference path) fwd+bwd+Adam, B=1."""
+    from oracle import models_ref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    h = hparams("32")
+    m = models_ref.AnatCNNRef(h)
+    opt = torch.optim.Adam(models_ref.adam_param_groups(m, h), weight_decay=0)
+    g = torch.Generator().manual_seed(15)
+    batch = {"mri": torch.rand((1, size, size, size), generator=g, dtype=torch.float64),
+             "label": torch.tensor([1])}
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        m.general_step(batch, 0, "train")["loss"].backward()
+        opt.step()
+
+    step()
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el > seconds_budget or n >= 30:
+            break
+    return {"value": n / el, "unit": "volumes/sec", "cores": threads, "kind": "port",
+            "sample": f"{n} fwd+bwd+Adam steps of the torch-CPU oracle ResNet-10, 1x{size}^3, "
+                      f"batch 1, fp32, {threads} threads ({el:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--size", type=int, default=128)
+    ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    torch.manual_seed(15 + rank)
+    model = M.Anat_CNN(hparams(args.precision)).cuda()
+    opt = model.configure_optimizers()
+    reducer = GradAllReduce(model.parameters()) if world > 1 else None
+    B, S = args.batch, args.size
+    g = torch.Generator(device="cuda").manual_seed(1000 + rank)   # this rank's shard
+    batch = {"mri": torch.rand((B, S, S, S), device="cuda", dtype=torch.float64, generator=g),
+             "label": torch.randint(0, 2, (B,), device="cuda", generator=g)}
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        out = model.general_step(batch, 0, "train")
+        out["loss"].backward()
+        if reducer is not None:
+            reducer.finish()
+        opt.step()
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    ms = el / args.steps * 1e3
+    value = world * B * args.steps / el
+    cdtype = torch.bfloat16 if args.precision == "bf16" else torch.float32
+    result = {
+        "metric": "volumes/sec fwd+bwd, 3D-ResNet-10 @128^3 bf16, 1/2/4/8 MI355X; % HBM roofline",
+        "value": value, "unit": "volumes/sec", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16" if cdtype == torch.bfloat16 else "f32",
+        "data": "synthetic uniform[0,1) f64 volumes resident in HBM, random-init weights",
+        "config": {"workload": f"BASELINE config 2: Anat_CNN ResNet-10 MRI-only, 1x{S}^3, "
+                               f"batch {B}/GPU, weighted CE, Adam, fwd+bwd+step",
+                   "global_batch": B * world, "volume": [1, S, S, S],
+                   "parallelism": f"dp{world}"},
+    }
+    if S in FLOP_PER_VOL:
+        per_gpu = value / world
+        result["step_mfma_frac"] = per_gpu * FLOP_PER_VOL[S] / (
+            PEAK_BF16 if cdtype == torch.bfloat16 else PEAK_F32)
+        result["hbm_roofline_frac_m2"] = per_gpu * M2_BYTES_PER_VOL / PEAK_HBM
+    if rank == 0 and not args.no_roofline:
+        result["roofline"] = dominant_kernel_roofline(model, B, S, cdtype)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(S)
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

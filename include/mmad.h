@@ -86,6 +86,9 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
  * unbiased variance into running_var, momentum update.  Layout [m][c], m = N*D*H*W.  */
 int64_t mmad_bn_stats_parts(int64_t m, int c);
 int mmad_bn_stats(int dtype, int64_t m, int c, const void* y, float* parts, void* stream);
+/* fold groups of `group` partial rows into one: out has cdiv(nparts, group) rows */
+int mmad_bn_parts_fold(int c, int nparts, const float* parts, int group, float* out,
+                       void* stream);
 int mmad_bn_finalize(int c, int64_t count, int nparts, const float* parts,
                      const float* gamma, const float* beta, float* running_mean,
                      float* running_var, float momentum, float eps, int training,

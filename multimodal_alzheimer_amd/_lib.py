@@ -43,6 +43,7 @@ _SIGS = {
     "mmad_conv3d_wgrad": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_bn_stats_parts": (_i64, [_i64, _i32]),
     "mmad_bn_stats": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp]),
+    "mmad_bn_parts_fold": (_i32, [_i32, _i32, _vp, _i32, _vp, _vp]),
     "mmad_bn_finalize": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _i32,
                                 _vp, _vp, _vp, _vp, _vp]),
     "mmad_scale_shift_act": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp,

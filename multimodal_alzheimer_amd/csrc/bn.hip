@@ -12,58 +12,120 @@
 
 namespace {
 
-constexpr int ROWS_PER_PART = 1024;
+// Row ranges per partial-sum block: <= 1024 parts so the f64 finalize stays short, and
+// >= 64 rows per part so each block streams a useful amount.
+struct PartPlan {
+  int64_t rpp;
+  int nparts;
+};
+PartPlan part_plan(int64_t M) {
+  int n = (int)std::min<int64_t>(1024, std::max<int64_t>(1, cdiv(M, 64)));
+  const int64_t rpp = cdiv(M, n);
+  return {rpp, (int)cdiv(M, rpp)};
+}
 
-// sums over rows [p*RPP, (p+1)*RPP) of y and y^2 (or, for the backward, of g' and
-// g'*xhat) per channel.  Thread layout: P = 256/C row lanes x C channels (C <= 256), or a
-// channel loop for C > 256.
-template <typename T, int MODE>   // MODE 0: stats of y; 1: BN backward sums; 2: sum only
-__global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, const T* __restrict__ y,
+// Per-channel sums over rows [p*rpp, (p+1)*rpp) of
+//   MODE 0: y and y^2          (BN forward statistics)
+//   MODE 1: g' and g'*xhat     (BN backward), g' = g * (relu_out > 0 | 1)
+//   MODE 2: y                  (conv bias gradient)
+// V channels per thread (16-byte vectors when C % VEC == 0), C / V lanes per row and
+// 256 / (C / V) rows in flight per block; one LDS pass folds the row lanes.
+template <typename T, int MODE, int V>
+__global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t rpp,
+                                                     const T* __restrict__ y,
                                                      const T* __restrict__ g,
                                                      const T* __restrict__ relu_out,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ invstd,
                                                      float* __restrict__ parts) {
-  __shared__ float red[2][256];
+  __shared__ float red[2][2048];
   const int tid = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * ROWS_PER_PART;
-  const int64_t r1 = min(M, r0 + ROWS_PER_PART);
-  const int P = C >= 256 ? 1 : 256 / C;
-  const int cw = C >= 256 ? 256 : C;          // channels covered per pass
-  for (int cbase = 0; cbase < C; cbase += cw) {
-    float s = 0.f, q = 0.f;
-    const int c = cbase + tid % cw;
-    const int rp = tid / cw;
-    const bool active = rp < P && c < C;
-    if (active) {
-      const float mu = MODE == 1 ? mean[c] : 0.f;
-      const float is = MODE == 1 ? invstd[c] : 0.f;
-      for (int64_t r = r0 + rp; r < r1; r += P) {
-        const int64_t i = r * C + c;
-        if (MODE == 1) {
-          float gv = Elt<T>::ld(g, i);
-          if (relu_out != nullptr && !(Elt<T>::ld(relu_out, i) > 0.f)) gv = 0.f;
-          const float xh = (Elt<T>::ld(y, i) - mu) * is;
-          s += gv;
-          q += gv * xh;
-        } else {
-          const float v = Elt<T>::ld(y, i);
-          s += v;
-          if (MODE == 0) q += v * v;
+  const int lpr = C / V;
+  const int rpar = 256 / lpr;
+  const int cl = tid % lpr, rl = tid / lpr;
+  const int64_t r0 = (int64_t)blockIdx.x * rpp;
+  const int64_t r1 = min(M, r0 + rpp);
+  float s[V], q[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  if (rl < rpar) {
+    float mu[V], is[V];
+    if (MODE == 1) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) { mu[e] = mean[cl * V + e]; is[e] = invstd[cl * V + e]; }
+    }
+    for (int64_t r = r0 + rl; r < r1; r += rpar) {
+      const int64_t i = r * C + cl * V;
+      float yv[V];
+      if constexpr (V == Chunk<T>::N) Chunk<T>::load(y + i, yv);
+      else for (int e = 0; e < V; ++e) yv[e] = Elt<T>::ld(y, i + e);
+      if (MODE == 1) {
+        float gv[V], ov[V];
+        if constexpr (V == Chunk<T>::N) Chunk<T>::load(g + i, gv);
+        else for (int e = 0; e < V; ++e) gv[e] = Elt<T>::ld(g, i + e);
+        if (relu_out != nullptr) {
+          if constexpr (V == Chunk<T>::N) Chunk<T>::load(relu_out + i, ov);
+          else for (int e = 0; e < V; ++e) ov[e] = Elt<T>::ld(relu_out, i + e);
+#pragma unroll
+          for (int e = 0; e < V; ++e) gv[e] = ov[e] > 0.f ? gv[e] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          s[e] += gv[e];
+          q[e] += gv[e] * ((yv[e] - mu[e]) * is[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          s[e] += yv[e];
+          if (MODE == 0) q[e] += yv[e] * yv[e];
         }
       }
     }
-    red[0][tid] = s;
-    red[1][tid] = q;
-    __syncthreads();
-    if (tid < cw && cbase + tid < C) {
-      float ss = 0.f, qq = 0.f;
-      for (int k = 0; k < P; ++k) { ss += red[0][k * cw + tid]; qq += red[1][k * cw + tid]; }
-      parts[((int64_t)blockIdx.x * 2) * C + cbase + tid] = ss;
-      parts[((int64_t)blockIdx.x * 2 + 1) * C + cbase + tid] = qq;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      red[0][rl * C + cl * V + e] = s[e];
+      red[1][rl * C + cl * V + e] = q[e];
     }
-    __syncthreads();
   }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float ss = 0.f, qq = 0.f;
+    for (int k = 0; k < rpar; ++k) { ss += red[0][k * C + c]; qq += red[1][k * C + c]; }
+    parts[((int64_t)blockIdx.x * 2) * C + c] = ss;
+    parts[((int64_t)blockIdx.x * 2 + 1) * C + c] = qq;
+  }
+}
+
+// Fold groups of `group` partial rows into one (fixed order): keeps the finalize short
+// when the parts come from the conv epilogue (one row per 128-voxel tile).
+__global__ void parts_fold_kernel(int C, int nparts, int group, const float* __restrict__ in,
+                                  float* __restrict__ out) {
+  const int o = blockIdx.x;
+  for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
+    float s = 0.f;
+    const int p1 = min(nparts, (o + 1) * group);
+    for (int p = o * group; p < p1; ++p) s += in[(int64_t)p * 2 * C + c];
+    out[(int64_t)o * 2 * C + c] = s;
+  }
+}
+
+template <typename T, int MODE>
+int launch_colsum(int64_t M, int C, const void* y, const void* g, const void* ro,
+                  const float* mean, const float* invstd, float* parts, hipStream_t st) {
+  const PartPlan pp = part_plan(M);
+  constexpr int VEC = Chunk<T>::N;
+  dim3 grid((unsigned)pp.nparts);
+  if (C % VEC == 0 && C / VEC <= 256) {
+    hipLaunchKernelGGL((colsum_kernel<T, MODE, VEC>), grid, dim3(256), 0, st, M, C, pp.rpp,
+                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts);
+  } else if (C <= 256) {
+    hipLaunchKernelGGL((colsum_kernel<T, MODE, 1>), grid, dim3(256), 0, st, M, C, pp.rpp,
+                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts);
+  } else {
+    return MMAD_EUNSUPPORTED;
+  }
+  return launch_status();
 }
 
 // f64 sum of the partial rows; block = 64 channels x 16 part-lanes
@@ -195,22 +257,46 @@ __global__ void scale_shift_act_scalar_kernel(int64_t M, int C, const T* __restr
   }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ void bn_bwd_apply_kernel(int64_t M, int C, const T* __restrict__ g,
                                     const T* __restrict__ relu_out, const T* __restrict__ y,
                                     const float* __restrict__ mean,
                                     const float* __restrict__ invstd,
                                     const float* __restrict__ coef, T* __restrict__ dy,
                                     T* __restrict__ gmask) {
-  const int64_t n = M * C;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    float gv = Elt<T>::ld(g, i);
-    if (relu_out != nullptr && !(Elt<T>::ld(relu_out, i) > 0.f)) gv = 0.f;
-    const float xh = (Elt<T>::ld(y, i) - mean[c]) * invstd[c];
-    Elt<T>::st(dy, i, coef[c] * gv - coef[C + c] - xh * coef[2 * C + c]);
-    if (gmask) Elt<T>::st(gmask, i, gv);
+  const int64_t nv = M * C / V;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nv;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = q * V;
+    const int c0 = (int)(i % C);
+    float gv[V], yv[V], ov[V], dv[V];
+    if constexpr (V == Chunk<T>::N) {
+      Chunk<T>::load(g + i, gv);
+      Chunk<T>::load(y + i, yv);
+      if (relu_out) Chunk<T>::load(relu_out + i, ov);
+    } else {
+      for (int e = 0; e < V; ++e) {
+        gv[e] = Elt<T>::ld(g, i + e);
+        yv[e] = Elt<T>::ld(y, i + e);
+        if (relu_out) ov[e] = Elt<T>::ld(relu_out, i + e);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int c = c0 + e;
+      if (relu_out && !(ov[e] > 0.f)) gv[e] = 0.f;
+      const float xh = (yv[e] - mean[c]) * invstd[c];
+      dv[e] = coef[c] * gv[e] - coef[C + c] - xh * coef[2 * C + c];
+    }
+    if constexpr (V == Chunk<T>::N) {
+      Chunk<T>::store(dy + i, dv);
+      if (gmask) Chunk<T>::store(gmask + i, gv);
+    } else {
+      for (int e = 0; e < V; ++e) {
+        Elt<T>::st(dy, i + e, dv[e]);
+        if (gmask) Elt<T>::st(gmask, i + e, gv[e]);
+      }
+    }
   }
 }
 
@@ -251,7 +337,7 @@ extern "C" {
 
 int64_t mmad_bn_stats_parts(int64_t m, int c) {
   (void)c;
-  return cdiv(m, ROWS_PER_PART);
+  return m > 0 ? part_plan(m).nparts : -1;
 }
 int64_t mmad_bn_bwd_parts(int64_t m, int c) { return mmad_bn_stats_parts(m, c); }
 
@@ -259,23 +345,36 @@ int mmad_bn_stats(int dtype, int64_t m, int c, const void* y, float* parts, void
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
   if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
   if (!y || !parts) return MMAD_ENULL;
-  dim3 grid((unsigned)cdiv(m, ROWS_PER_PART));
   if (dtype == MMAD_BF16)
-    hipLaunchKernelGGL((colsum_kernel<u16, 0>), grid, dim3(256), 0, as_stream(stream), m, c,
-                       (const u16*)y, nullptr, nullptr, nullptr, nullptr, parts);
-  else
-    hipLaunchKernelGGL((colsum_kernel<float, 0>), grid, dim3(256), 0, as_stream(stream), m, c,
-                       (const float*)y, nullptr, nullptr, nullptr, nullptr, parts);
+    return launch_colsum<u16, 0>(m, c, y, nullptr, nullptr, nullptr, nullptr, parts,
+                                 as_stream(stream));
+  return launch_colsum<float, 0>(m, c, y, nullptr, nullptr, nullptr, nullptr, parts,
+                                 as_stream(stream));
+}
+
+int mmad_bn_parts_fold(int c, int nparts, const float* parts, int group, float* out,
+                       void* stream) {
+  if (c <= 0 || nparts <= 0 || group <= 0) return MMAD_EBADSHAPE;
+  if (!parts || !out) return MMAD_ENULL;
+  hipLaunchKernelGGL(parts_fold_kernel, dim3((unsigned)cdiv(nparts, group)), dim3(256), 0,
+                     as_stream(stream), c, nparts, group, parts, out);
   return launch_status();
 }
 
 // column sums (conv bias gradient) using `parts` as scratch ([parts][2][c] floats)
 int mmad_colsum_ws(int dtype, int64_t m, int c, const void* y, float* parts, float* out,
                    void* stream) {
-  int rc = mmad_bn_stats(dtype, m, c, y, parts, stream);
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!y || !parts || !out) return MMAD_ENULL;
+  int rc = dtype == MMAD_BF16
+               ? launch_colsum<u16, 2>(m, c, y, nullptr, nullptr, nullptr, nullptr, parts,
+                                       as_stream(stream))
+               : launch_colsum<float, 2>(m, c, y, nullptr, nullptr, nullptr, nullptr, parts,
+                                         as_stream(stream));
   if (rc) return rc;
   hipLaunchKernelGGL(sum_only_finalize_kernel, dim3((unsigned)cdiv(c, 64)), dim3(1024), 0,
-                     as_stream(stream), c, (int)cdiv(m, ROWS_PER_PART), parts, out);
+                     as_stream(stream), c, part_plan(m).nparts, parts, out);
   return launch_status();
 }
 
@@ -331,15 +430,9 @@ int mmad_bn_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* r
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
   if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
   if (!g || !y || !mean || !invstd || !parts) return MMAD_ENULL;
-  dim3 grid((unsigned)cdiv(m, ROWS_PER_PART));
   if (dtype == MMAD_BF16)
-    hipLaunchKernelGGL((colsum_kernel<u16, 1>), grid, dim3(256), 0, as_stream(stream), m, c,
-                       (const u16*)y, (const u16*)g, (const u16*)relu_out, mean, invstd, parts);
-  else
-    hipLaunchKernelGGL((colsum_kernel<float, 1>), grid, dim3(256), 0, as_stream(stream), m, c,
-                       (const float*)y, (const float*)g, (const float*)relu_out, mean, invstd,
-                       parts);
-  return launch_status();
+    return launch_colsum<u16, 1>(m, c, y, g, relu_out, mean, invstd, parts, as_stream(stream));
+  return launch_colsum<float, 1>(m, c, y, g, relu_out, mean, invstd, parts, as_stream(stream));
 }
 
 int mmad_bn_bwd_finalize(int c, int64_t count, int nparts, const float* parts,
@@ -359,14 +452,17 @@ int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* re
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
   if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
   if (!g || !y || !mean || !invstd || !coef || !dy) return MMAD_ENULL;
-  if (dtype == MMAD_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<u16>, dim3(ew_grid(m * c)), dim3(256), 0,
-                       as_stream(stream), m, c, (const u16*)g, (const u16*)relu_out,
-                       (const u16*)y, mean, invstd, coef, (u16*)dy, (u16*)gmask);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(ew_grid(m * c)), dim3(256), 0,
-                       as_stream(stream), m, c, (const float*)g, (const float*)relu_out,
-                       (const float*)y, mean, invstd, coef, (float*)dy, (float*)gmask);
+  hipStream_t st = as_stream(stream);
+#define APPLY(T, V)                                                                          \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, V>), dim3(ew_grid(m * c / V)), dim3(256), 0, st, \
+                     m, c, (const T*)g, (const T*)relu_out, (const T*)y, mean, invstd, coef,  \
+                     (T*)dy, (T*)gmask)
+  if (dtype == MMAD_BF16) {
+    if (c % 8 == 0) APPLY(u16, 8); else APPLY(u16, 1);
+  } else {
+    if (c % 4 == 0) APPLY(float, 4); else APPLY(float, 1);
+  }
+#undef APPLY
   return launch_status();
 }
 

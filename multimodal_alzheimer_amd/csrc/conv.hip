@@ -710,7 +710,7 @@ int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype) {
   const Geom g = fwd_geom(d, dtype);
   const WSplit sp = wgrad_split(g);
   const int64_t slabs = (int64_t)sp.splits * g.Nd * g.K * 4;
-  const int64_t parts = cdiv(g.M, 1024) * 2 * g.Nd * 4;   // bias-gradient column sums
+  const int64_t parts = (int64_t)1024 * 2 * g.Nd * 4;   // bias-gradient column sums
   return std::max(slabs, parts);
 }
 

@@ -5,11 +5,12 @@
 // pkg/models/mri_models/anat_cnn.py:62) and nn.AdaptiveAvgPool3d(1)
 // (anat_cnn.py:66, pet_cnn.py:33).
 //
-// Max pool: consecutive threads walk consecutive channels of one voxel (coalesced).
-// Ties resolve to the FIRST window position in (kd, kh, kw) scan order with a strict
-// `>` (NaN always wins), exactly torch's CPU kernel; the window index is kept as one
-// byte per output so the backward is a deterministic gather (no atomics) that adds the
-// contributions of the overlapping windows in output order, as torch's CPU backward does.
+// Every thread owns V consecutive channels of one voxel (16-byte vectors when C % VEC ==
+// 0), so all loads and stores are coalesced vectors.  Max-pool ties resolve to the FIRST
+// window position in (kd, kh, kw) scan order with a strict `>` (NaN always wins), exactly
+// torch's CPU kernel; the window index is kept as one byte per output so the backward is
+// a deterministic gather (no atomics) that adds the contributions of the overlapping
+// windows in output order, as torch's CPU backward does.
 #include "common.h"
 
 namespace {
@@ -18,21 +19,36 @@ struct PoolG {
   int n, c, di, hi, wi, do_, ho, wo, k, s, p;
 };
 
-template <typename T>
+template <typename T, int V>
+__device__ __forceinline__ void load_v(const T* p, float* v) {
+  if constexpr (V == Chunk<T>::N) Chunk<T>::load(p, v);
+  else for (int e = 0; e < V; ++e) v[e] = Elt<T>::ld(p, e);
+}
+template <typename T, int V>
+__device__ __forceinline__ void store_v(T* p, const float* v) {
+  if constexpr (V == Chunk<T>::N) Chunk<T>::store(p, v);
+  else for (int e = 0; e < V; ++e) Elt<T>::st(p, e, v[e]);
+}
+
+template <typename T, int V>
 __global__ void maxpool_fwd_kernel(PoolG g, const T* __restrict__ x, T* __restrict__ y,
                                    uint8_t* __restrict__ am) {
-  const int64_t total = (int64_t)g.n * g.do_ * g.ho * g.wo * g.c;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % g.c);
-    int64_t v = i / g.c;
+  const int cv = g.c / V;
+  const int64_t total = (int64_t)g.n * g.do_ * g.ho * g.wo * cv;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(t % cv) * V;
+    int64_t v = t / cv;
+    const int64_t ovox = v;
     const int ow = (int)(v % g.wo); v /= g.wo;
     const int oh = (int)(v % g.ho); v /= g.ho;
     const int od = (int)(v % g.do_);
     const int64_t nb = v / g.do_;
     const int z0 = od * g.s - g.p, y0 = oh * g.s - g.p, x0 = ow * g.s - g.p;
-    float best = -__builtin_inff();
-    int bi = -1;
+    float best[V];
+    int bi[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { best[e] = -__builtin_inff(); bi[e] = -1; }
     for (int kd = 0; kd < g.k; ++kd) {
       const int z = z0 + kd;
       if ((unsigned)z >= (unsigned)g.di) continue;
@@ -42,82 +58,131 @@ __global__ void maxpool_fwd_kernel(PoolG g, const T* __restrict__ x, T* __restri
         for (int kw = 0; kw < g.k; ++kw) {
           const int xx = x0 + kw;
           if ((unsigned)xx >= (unsigned)g.wi) continue;
-          const float val = Elt<T>::ld(x, (((nb * g.di + z) * g.hi + yy) * g.wi + xx) * g.c + c);
+          float val[V];
+          load_v<T, V>(x + (((nb * g.di + z) * g.hi + yy) * g.wi + xx) * g.c + c0, val);
           const int wi = (kd * g.k + kh) * g.k + kw;
-          if (bi < 0) bi = wi;
-          if (val > best || val != val) { best = val; bi = wi; }
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            if (bi[e] < 0) bi[e] = wi;
+            if (val[e] > best[e] || val[e] != val[e]) { best[e] = val[e]; bi[e] = wi; }
+          }
         }
       }
     }
-    Elt<T>::st(y, i, best);
-    am[i] = (uint8_t)bi;
+    store_v<T, V>(y + ovox * g.c + c0, best);
+#pragma unroll
+    for (int e = 0; e < V; ++e) am[ovox * g.c + c0 + e] = (uint8_t)bi[e];
   }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ void maxpool_bwd_kernel(PoolG g, const T* __restrict__ dy,
                                    const uint8_t* __restrict__ am, T* __restrict__ dx) {
-  const int64_t total = (int64_t)g.n * g.di * g.hi * g.wi * g.c;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % g.c);
-    int64_t v = i / g.c;
+  const int cv = g.c / V;
+  const int64_t total = (int64_t)g.n * g.di * g.hi * g.wi * cv;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(t % cv) * V;
+    int64_t v = t / cv;
+    const int64_t ivox = v;
     const int iw = (int)(v % g.wi); v /= g.wi;
     const int ih = (int)(v % g.hi); v /= g.hi;
     const int id = (int)(v % g.di);
     const int64_t nb = v / g.di;
     // outputs whose window covers this input: o*s - p <= i <= o*s - p + k - 1
-    auto lo = [&](int ii) { int t = ii + g.p - (g.k - 1); return t <= 0 ? 0 : (t + g.s - 1) / g.s; };
-    auto hi = [&](int ii, int lim) { int t = (ii + g.p) / g.s; return t < lim - 1 ? t : lim - 1; };
+    auto lo = [&](int ii) { int q = ii + g.p - (g.k - 1); return q <= 0 ? 0 : (q + g.s - 1) / g.s; };
+    auto hi = [&](int ii, int lim) { int q = (ii + g.p) / g.s; return q < lim - 1 ? q : lim - 1; };
     const int d0 = lo(id), d1 = hi(id, g.do_);
     const int h0 = lo(ih), h1 = hi(ih, g.ho);
     const int w0 = lo(iw), w1 = hi(iw, g.wo);
-    float acc = 0.f;
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
     for (int od = d0; od <= d1; ++od)
       for (int oh = h0; oh <= h1; ++oh)
         for (int ow = w0; ow <= w1; ++ow) {
           const int wi = ((id - (od * g.s - g.p)) * g.k + (ih - (oh * g.s - g.p))) * g.k +
                          (iw - (ow * g.s - g.p));
-          const int64_t o = (((nb * g.do_ + od) * g.ho + oh) * g.wo + ow) * g.c + c;
-          if (am[o] == wi) acc += Elt<T>::ld(dy, o);
+          const int64_t o = (((nb * g.do_ + od) * g.ho + oh) * g.wo + ow) * g.c + c0;
+          uint8_t a[V];
+          if constexpr (V == 8) {
+            const uint64_t w = *reinterpret_cast<const uint64_t*>(am + o);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] = (uint8_t)(w >> (8 * e));
+          } else if constexpr (V == 4) {
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(am + o);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a[e] = (uint8_t)(w >> (8 * e));
+          } else {
+            for (int e = 0; e < V; ++e) a[e] = am[o + e];
+          }
+          bool any = false;
+#pragma unroll
+          for (int e = 0; e < V; ++e) any |= a[e] == wi;
+          if (!any) continue;
+          float gv[V];
+          load_v<T, V>(dy + o, gv);
+#pragma unroll
+          for (int e = 0; e < V; ++e)
+            if (a[e] == wi) acc[e] += gv[e];
         }
-    Elt<T>::st(dx, i, acc);
+    store_v<T, V>(dx + ivox * g.c + c0, acc);
   }
 }
 
-// GAP: one block per (n, 64-channel group); 4 row-lanes per channel, fp32 partial sums
-template <typename T>
-__global__ __launch_bounds__(256) void gap_fwd_kernel(int64_t S, int C, const T* __restrict__ x,
-                                                     float* __restrict__ y) {
-  __shared__ float red[256];
+// GAP: one block per (n, channel chunk of up to 256); V channels per thread,
+// 256 / (chunk / V) voxel lanes; fp32 partial sums folded through LDS.
+template <typename T, int V>
+__global__ __launch_bounds__(1024) void gap_fwd_kernel(int64_t S, int C, int CB,
+                                                      const T* __restrict__ x,
+                                                      float* __restrict__ y) {
+  __shared__ float red[1024 * 8];
   const int n = blockIdx.y;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rl = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < C)
-    for (int64_t v = rl; v < S; v += 4) s += Elt<T>::ld(x, ((int64_t)n * S + v) * C + c);
-  red[threadIdx.x] = s;
+  const int cb0 = blockIdx.x * CB;
+  const int cw = min(CB, C - cb0);
+  const int lpr = cw / V;
+  const int rpar = (int)blockDim.x / lpr;
+  const int cl = threadIdx.x % lpr, rl = threadIdx.x / lpr;
+  float s[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) s[e] = 0.f;
+  if (rl < rpar) {
+    for (int64_t v = rl; v < S; v += rpar) {
+      float val[V];
+      load_v<T, V>(x + ((int64_t)n * S + v) * C + cb0 + cl * V, val);
+#pragma unroll
+      for (int e = 0; e < V; ++e) s[e] += val[e];
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) red[rl * cw + cl * V + e] = s[e];
+  }
   __syncthreads();
-  if (rl == 0 && c < C)
-    y[(int64_t)n * C + c] = (red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] +
-                             red[threadIdx.x + 192]) / (float)S;
+  for (int c = threadIdx.x; c < cw; c += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < rpar; ++k) acc += red[k * cw + c];
+    y[(int64_t)n * C + cb0 + c] = acc / (float)S;
+  }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ void gap_bwd_kernel(int n, int64_t S, int C, const float* __restrict__ dy,
                                T* __restrict__ dx) {
-  const int64_t total = (int64_t)n * S * C;
+  const int cv = C / V;
+  const int64_t total = (int64_t)n * S * cv;
   const float inv = 1.f / (float)S;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const int64_t nb = i / ((int64_t)S * C);
-    Elt<T>::st(dx, i, dy[nb * C + c] * inv);
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(t % cv) * V;
+    const int64_t nb = t / ((int64_t)S * cv);
+    float v[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] = dy[nb * C + c0 + e] * inv;
+    store_v<T, V>(dx + (t / cv) * C + c0, v);
   }
 }
 
 unsigned grid_of(int64_t n) {
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 256), 256 * 16));
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 256), 256 * 32));
 }
 
 bool pool_ok(const PoolG& g) {
@@ -126,6 +191,61 @@ bool pool_ok(const PoolG& g) {
     return false;
   auto ext = [&](int i) { return (i + 2 * g.p - g.k) / g.s + 1; };
   return ext(g.di) == g.do_ && ext(g.hi) == g.ho && ext(g.wi) == g.wo;
+}
+
+template <typename T>
+int pool_fwd(const PoolG& g, const void* x, void* y, uint8_t* am, hipStream_t st) {
+  constexpr int VEC = Chunk<T>::N;
+  const int64_t vox = (int64_t)g.n * g.do_ * g.ho * g.wo;
+  if (g.c % VEC == 0)
+    hipLaunchKernelGGL((maxpool_fwd_kernel<T, VEC>), dim3(grid_of(vox * g.c / VEC)), dim3(256),
+                       0, st, g, (const T*)x, (T*)y, am);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_kernel<T, 1>), dim3(grid_of(vox * g.c)), dim3(256), 0, st,
+                       g, (const T*)x, (T*)y, am);
+  return launch_status();
+}
+
+template <typename T>
+int pool_bwd(const PoolG& g, const void* dy, const uint8_t* am, void* dx, hipStream_t st) {
+  constexpr int VEC = Chunk<T>::N;
+  const int64_t vox = (int64_t)g.n * g.di * g.hi * g.wi;
+  if (g.c % VEC == 0)
+    hipLaunchKernelGGL((maxpool_bwd_kernel<T, VEC>), dim3(grid_of(vox * g.c / VEC)), dim3(256),
+                       0, st, g, (const T*)dy, am, (T*)dx);
+  else
+    hipLaunchKernelGGL((maxpool_bwd_kernel<T, 1>), dim3(grid_of(vox * g.c)), dim3(256), 0, st,
+                       g, (const T*)dy, am, (T*)dx);
+  return launch_status();
+}
+
+template <typename T>
+int gap_fwd(int n, int64_t s, int c, const void* x, float* y, hipStream_t st) {
+  constexpr int VEC = Chunk<T>::N;
+  if (c % VEC == 0) {
+    const int cb = std::min(c, 256);
+    if (cb % VEC) return MMAD_EUNSUPPORTED;
+    hipLaunchKernelGGL((gap_fwd_kernel<T, VEC>), dim3((unsigned)cdiv(c, cb), (unsigned)n),
+                       dim3(1024), 0, st, s, c, cb, (const T*)x, y);
+  } else {
+    const int cb = std::min(c, 1024);
+    hipLaunchKernelGGL((gap_fwd_kernel<T, 1>), dim3((unsigned)cdiv(c, cb), (unsigned)n),
+                       dim3(1024), 0, st, s, c, cb, (const T*)x, y);
+  }
+  return launch_status();
+}
+
+template <typename T>
+int gap_bwd(int n, int64_t s, int c, const float* dy, void* dx, hipStream_t st) {
+  constexpr int VEC = Chunk<T>::N;
+  const int64_t tot = (int64_t)n * s * c;
+  if (c % VEC == 0)
+    hipLaunchKernelGGL((gap_bwd_kernel<T, VEC>), dim3(grid_of(tot / VEC)), dim3(256), 0, st, n,
+                       s, c, dy, (T*)dx);
+  else
+    hipLaunchKernelGGL((gap_bwd_kernel<T, 1>), dim3(grid_of(tot)), dim3(256), 0, st, n, s, c,
+                       dy, (T*)dx);
+  return launch_status();
 }
 
 }  // namespace
@@ -138,16 +258,9 @@ int mmad_maxpool3d_fwd(int dtype, int n, int c, int di, int hi, int wi, int do_,
   PoolG g{n, c, di, hi, wi, do_, ho, wo, k, s, p};
   if (!pool_ok(g)) return MMAD_EBADSHAPE;
   if (!x || !y || !argmax) return MMAD_ENULL;
-  const unsigned grid = grid_of((int64_t)n * do_ * ho * wo * c);
-  if (dtype == MMAD_BF16)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<u16>, dim3(grid), dim3(256), 0, as_stream(stream), g,
-                       (const u16*)x, (u16*)y, argmax);
-  else if (dtype == MMAD_F32)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(grid), dim3(256), 0, as_stream(stream),
-                       g, (const float*)x, (float*)y, argmax);
-  else
-    return MMAD_EBADDTYPE;
-  return launch_status();
+  if (dtype == MMAD_BF16) return pool_fwd<u16>(g, x, y, argmax, as_stream(stream));
+  if (dtype == MMAD_F32) return pool_fwd<float>(g, x, y, argmax, as_stream(stream));
+  return MMAD_EBADDTYPE;
 }
 
 int mmad_maxpool3d_bwd(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho, int wo,
@@ -156,46 +269,25 @@ int mmad_maxpool3d_bwd(int dtype, int n, int c, int di, int hi, int wi, int do_,
   PoolG g{n, c, di, hi, wi, do_, ho, wo, k, s, p};
   if (!pool_ok(g)) return MMAD_EBADSHAPE;
   if (!dy || !dx || !argmax) return MMAD_ENULL;
-  const unsigned grid = grid_of((int64_t)n * di * hi * wi * c);
-  if (dtype == MMAD_BF16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<u16>, dim3(grid), dim3(256), 0, as_stream(stream), g,
-                       (const u16*)dy, argmax, (u16*)dx);
-  else if (dtype == MMAD_F32)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(grid), dim3(256), 0, as_stream(stream),
-                       g, (const float*)dy, argmax, (float*)dx);
-  else
-    return MMAD_EBADDTYPE;
-  return launch_status();
+  if (dtype == MMAD_BF16) return pool_bwd<u16>(g, dy, argmax, dx, as_stream(stream));
+  if (dtype == MMAD_F32) return pool_bwd<float>(g, dy, argmax, dx, as_stream(stream));
+  return MMAD_EBADDTYPE;
 }
 
 int mmad_gap_fwd(int dtype, int n, int64_t s, int c, const void* x, float* y, void* stream) {
   if (n <= 0 || s <= 0 || c <= 0) return MMAD_EBADSHAPE;
   if (!x || !y) return MMAD_ENULL;
-  dim3 grid((unsigned)cdiv(c, 64), (unsigned)n);
-  if (dtype == MMAD_BF16)
-    hipLaunchKernelGGL(gap_fwd_kernel<u16>, grid, dim3(256), 0, as_stream(stream), s, c,
-                       (const u16*)x, y);
-  else if (dtype == MMAD_F32)
-    hipLaunchKernelGGL(gap_fwd_kernel<float>, grid, dim3(256), 0, as_stream(stream), s, c,
-                       (const float*)x, y);
-  else
-    return MMAD_EBADDTYPE;
-  return launch_status();
+  if (dtype == MMAD_BF16) return gap_fwd<u16>(n, s, c, x, y, as_stream(stream));
+  if (dtype == MMAD_F32) return gap_fwd<float>(n, s, c, x, y, as_stream(stream));
+  return MMAD_EBADDTYPE;
 }
 
 int mmad_gap_bwd(int dtype, int n, int64_t s, int c, const float* dy, void* dx, void* stream) {
   if (n <= 0 || s <= 0 || c <= 0) return MMAD_EBADSHAPE;
   if (!dy || !dx) return MMAD_ENULL;
-  const unsigned grid = grid_of((int64_t)n * s * c);
-  if (dtype == MMAD_BF16)
-    hipLaunchKernelGGL(gap_bwd_kernel<u16>, dim3(grid), dim3(256), 0, as_stream(stream), n, s, c,
-                       dy, (u16*)dx);
-  else if (dtype == MMAD_F32)
-    hipLaunchKernelGGL(gap_bwd_kernel<float>, dim3(grid), dim3(256), 0, as_stream(stream), n, s,
-                       c, dy, (float*)dx);
-  else
-    return MMAD_EBADDTYPE;
-  return launch_status();
+  if (dtype == MMAD_BF16) return gap_bwd<u16>(n, s, c, dy, dx, as_stream(stream));
+  if (dtype == MMAD_F32) return gap_bwd<float>(n, s, c, dy, dx, as_stream(stream));
+  return MMAD_EBADDTYPE;
 }
 
 }  // extern "C"

@@ -1,0 +1,94 @@
+"""Data parallelism for the 3D-volume training step: one process per GPU, RCCL over xGMI.
+
+The reference trains on one GPU (``pl.Trainer(devices=1)``, train_anat_cnn.py) and has no
+collective at all; this is new work.  Samples (single volumes or PET-MRI pairs / triples
+merged by MultiModalDataset, pkg/utils/dataloader.py:124-156) are independent, so the
+only exchange per step is the gradient all-reduce:
+
+* ``shard_indices`` -- DistributedSampler-style sharding of the sample-pair index list
+  (seeded shuffle per epoch, equal shard sizes by padding with wrap-around samples);
+* ``GradAllReduce`` -- gradient buckets (~32 MiB, reverse registration order so the
+  last layers' gradients, ready first in backward, go first) all-reduced asynchronously
+  from post-accumulate-grad hooks while backward continues; ``finish()`` waits, averages
+  and writes the reduced gradients back.  BN statistics stay per replica (as DDP).
+
+Backend "nccl" is RCCL on ROCm; "gloo" runs the same code on CPU for the tests.
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_indices(n_samples, rank, world, epoch=0, shuffle=True, seed=15):
+    """Indices of this rank's shard (torch DistributedSampler semantics, drop_last=False)."""
+    if shuffle:
+        g = torch.Generator()
+        g.manual_seed(seed + epoch)
+        order = torch.randperm(n_samples, generator=g).tolist()
+    else:
+        order = list(range(n_samples))
+    per = -(-n_samples // world)
+    total = per * world
+    order += order[: total - n_samples] if total > n_samples else []
+    return order[rank:total:world]
+
+
+class GradAllReduce:
+    def __init__(self, params, bucket_mb=32.0, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.params = [p for p in params if p.requires_grad]
+        cap = int(bucket_mb * (1 << 20))
+        self.buckets = []
+        cur, size = [], 0
+        for p in reversed(self.params):          # backward produces the last layers first
+            cur.append(p)
+            size += p.numel() * p.element_size()
+            if size >= cap:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self._owner = {}
+        for bi, b in enumerate(self.buckets):
+            for p in b:
+                self._owner[p] = bi
+        self._hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
+        self.reset()
+
+    def reset(self):
+        self._pending = [len(b) for b in self.buckets]
+        self._inflight = {}
+
+    def _ready(self, p):
+        bi = self._owner[p]
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0:
+            self._launch(bi)
+
+    def _launch(self, bi):
+        flat = torch.cat([p.grad.reshape(-1) for p in self.buckets[bi]])
+        work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._inflight[bi] = (flat, work)
+
+    def finish(self):
+        """Wait for every bucket (launching any whose grads never all arrived), then
+        write grad = mean over ranks back into each parameter."""
+        for bi, b in enumerate(self.buckets):
+            if bi not in self._inflight:
+                for p in b:
+                    if p.grad is None:
+                        p.grad = torch.zeros_like(p)
+                self._launch(bi)
+        for bi, (flat, work) in sorted(self._inflight.items()):
+            work.wait()
+            flat.div_(self.world)
+            off = 0
+            for p in self.buckets[bi]:
+                n = p.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                off += n
+        self.reset()
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()

@@ -172,6 +172,13 @@ def _finalize(y, parts, bn, training):
             parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
             L.call("mmad_bn_stats", L.dtype_code(y.dtype), m, c, L.ptr(y), L.ptr(parts),
                    L.stream())
+        if parts.shape[0] > 1024:        # conv-epilogue partials: one row per 128 voxels
+            group = -(-parts.shape[0] // 512)
+            folded = torch.empty((-(-parts.shape[0] // group), 2, c), dtype=torch.float32,
+                                 device=dev)
+            L.call("mmad_bn_parts_fold", c, parts.shape[0], L.ptr(parts), group, L.ptr(folded),
+                   L.stream())
+            parts = folded
         update = training and bn.track_running_stats and bn.running_mean is not None
         if update:
             if bn.momentum is None:

@@ -1,0 +1,71 @@
+"""CPU-side checks of the C ABI: the library loads (no GPU needed) and exports exactly the
+functions include/mmad.h declares, with the ctypes table in _lib.py covering all of them.
+No kernel is launched here."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from multimodal_alzheimer_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "mmad.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mmad_\w+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        from multimodal_alzheimer_amd import _build
+        _build.build()
+    return _lib.load()
+
+
+def test_header_matches_binding_table():
+    assert header_functions() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_header_symbol(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (mmad_\w+)", out))
+    missing = set(header_functions()) - exported
+    assert not missing, f"not exported: {sorted(missing)}"
+    for name in header_functions():
+        assert hasattr(lib, name)
+
+
+def test_abi_version_and_errors(lib):
+    assert lib.mmad_abi_version() == 1
+    assert lib.mmad_strerror(0) == b"ok"
+    assert b"shape" in lib.mmad_strerror(1001)
+
+
+def test_host_side_shape_queries(lib):
+    from multimodal_alzheimer_amd.volume_ops import conv_desc
+    d = conv_desc((8, 64, 32, 32, 32), (128, 64, 3, 3, 3), (2, 2, 2), (1, 1, 1), (1, 1, 1))
+    assert (d.do_, d.ho, d.wo) == (16, 16, 16)
+    assert lib.mmad_conv_packed_elems(d, _lib.BF16, 0) == 128 * 27 * 64
+    assert lib.mmad_conv_packed_elems(d, _lib.BF16, 1) == 64 * 27 * 128
+    assert lib.mmad_conv3d_stats_rows(d, _lib.BF16) == 8 * 16 ** 3 // 128
+    assert lib.mmad_conv3d_wgrad_workspace(d, _lib.BF16) > 0
+    stem = conv_desc((8, 1, 128, 128, 128), (64, 1, 7, 7, 7), (2, 2, 2), (3, 3, 3), (1, 1, 1))
+    assert lib.mmad_conv_unfolded_elems(stem) == 8 * 128 * 128 * 64 * 8
+    assert lib.mmad_conv_packed_elems(stem, _lib.BF16, 0) == 64 * 416   # 49 taps x 8 -> 416
+    bad = conv_desc((1, 64, 8, 8, 8), (64, 64, 3, 3, 3), (1, 1, 1), (1, 1, 1), (1, 1, 1))
+    bad.wo = 9   # inconsistent with the torch output-extent formula
+    assert lib.mmad_conv_packed_elems(bad, _lib.F32, 0) == -1
+
+
+def test_bad_arguments_are_rejected_without_launching(lib):
+    from multimodal_alzheimer_amd.volume_ops import conv_desc
+    d = conv_desc((1, 64, 8, 8, 8), (64, 64, 3, 3, 3), (1, 1, 1), (1, 1, 1), (1, 1, 1))
+    assert lib.mmad_conv3d_fwd(d, 7, None, None, None, None, None, None) == 1002
+    assert lib.mmad_conv3d_fwd(d, _lib.F32, None, None, None, None, None, None) == 1003
+    assert lib.mmad_loss_fwd(0, 2, None, None, None, 0.0, 0, None, None, None) == 1001

@@ -1,0 +1,68 @@
+"""Data-parallel path on CPU with the gloo backend, world_size 2 (the same code runs over
+RCCL on GPUs): bucketed asynchronous gradient all-reduce == mean of per-rank gradients ==
+the single-process gradient of the concatenated batch; sample-pair sharding is a disjoint
+cover of the dataset."""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+
+from multimodal_alzheimer_amd.data_parallel import GradAllReduce, shard_indices
+
+
+def _model():
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Linear(16, 64), nn.ReLU(), nn.Linear(64, 64), nn.Tanh(),
+                         nn.Linear(64, 3))
+
+
+def _data():
+    g = torch.Generator().manual_seed(1)
+    return torch.randn(8, 16, generator=g), torch.randint(0, 3, (8,), generator=g)
+
+
+def _worker(rank, world, init_file, out_file):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank,
+                            world_size=world)
+    m = _model()
+    red = GradAllReduce(m.parameters(), bucket_mb=0.004)   # several tiny buckets
+    assert len(red.buckets) > 1
+    x, y = _data()
+    idx = shard_indices(8, rank, world, shuffle=False)
+    for _ in range(2):                                       # hooks re-arm every step
+        m.zero_grad(set_to_none=True)
+        nn.functional.cross_entropy(m(x[idx]), y[idx]).backward()
+        red.finish()
+    if rank == 0:
+        torch.save({k: p.grad.clone() for k, p in m.named_parameters()}, out_file)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_matches_full_batch():
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        init_file = os.path.join(td, "init")
+        out_file = os.path.join(td, "grads.pt")
+        mp.spawn(_worker, args=(world, init_file, out_file), nprocs=world, join=True)
+        got = torch.load(out_file, weights_only=True)
+    m = _model()
+    x, y = _data()
+    nn.functional.cross_entropy(m(x), y).backward()   # mean over 8 == mean of 2 shard means
+    for k, p in m.named_parameters():
+        torch.testing.assert_close(got[k], p.grad, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,world", [(10, 2), (8, 4), (7, 8), (1946, 8)])
+def test_shard_indices_cover(n, world):
+    shards = [shard_indices(n, r, world, epoch=3) for r in range(world)]
+    assert len({len(s) for s in shards}) == 1
+    flat = [i for s in shards for i in s]
+    assert set(flat) == set(range(n))
+    assert len(flat) == -(-n // world) * world
+    assert shard_indices(n, 0, world, epoch=3) == shards[0]
+    assert shard_indices(n, 0, world, epoch=4) != shards[0] or n < 3

@@ -1,0 +1,124 @@
+"""Drop-in surface checks on CPU (no kernel launches): class names / constructor signatures
+/ state_dict keys match the reference (pinned by the golden fixtures), PL-1.7.7-format
+checkpoint round trip, reference import paths, and "no CPU fallback"."""
+import inspect
+
+import numpy as np
+import pytest
+import torch
+
+import multimodal_alzheimer_amd as M
+from multimodal_alzheimer_amd import _lib
+from tests import _golden as G
+from tests.test_model_parity_gpu import build_product
+
+
+@pytest.mark.parametrize("name", list(G.CASES))
+def test_state_dict_keys_match_reference(name):
+    g = G.load(name)
+    m = build_product(name)
+    assert list(m.state_dict().keys()) == list(g["state_dict_keys"])
+    ref = G.build_oracle(name)
+    for (k1, v1), (k2, v2) in zip(m.state_dict().items(), ref.state_dict().items()):
+        assert k1 == k2 and v1.shape == v2.shape and v1.dtype == v2.dtype, k1
+
+
+def test_reference_import_paths():
+    from pkg.loss_functions.focalloss import FocalLoss
+    from pkg.models.base_model import Base_Model
+    from pkg.models.fusion_models.anat_pet_fusion import Anat_PET_CNN
+    from pkg.models.mri_models.anat_cnn import Anat_CNN
+    from pkg.models.pet_models.pet_cnn import Small_PET_CNN
+    from pkg.models.pet_models.pet_resnet_cnn import PET_CNN_ResNet
+    from MedicalNet.model import generate_model
+    from MedicalNet.setting import parse_opts
+    assert Anat_CNN is M.Anat_CNN and FocalLoss is M.FocalLoss
+    assert issubclass(Anat_CNN, Base_Model)
+    assert list(inspect.signature(Anat_CNN).parameters) == ["hparams", "gpu_id"]
+    assert list(inspect.signature(Small_PET_CNN).parameters) == ["hparams", "gpu_id"]
+    assert list(inspect.signature(PET_CNN_ResNet).parameters) == ["hparams", "gpu_id"]
+    assert list(inspect.signature(Anat_PET_CNN).parameters)[:3] == ["hparams", "path_pet",
+                                                                     "path_anat"]
+    assert list(inspect.signature(FocalLoss).parameters) == ["gamma", "alpha", "size_average"]
+    opts = parse_opts()
+    opts.model_depth = 18
+    net, _ = generate_model(opts)
+    assert len(net.module.layer1) == 2
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    h = G.anat_hparams(10, linear_out=[64], batchnorm_dense=True)
+    m = M.Anat_CNN(h)
+    G.load_prng_weights(m, 3)
+    path = tmp_path / "epoch=0-val_loss=0.5.ckpt"
+    m.save_checkpoint(str(path))
+    ck = torch.load(path, weights_only=True)
+    for k in ("state_dict", "hyper_parameters", "epoch", "global_step",
+              "pytorch-lightning_version", "optimizer_states", "lr_schedulers", "callbacks",
+              "loops"):
+        assert k in ck
+    m2 = M.Anat_CNN.load_from_checkpoint(str(path))
+    for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k
+    assert m2.hparams["linear_out"] == [64]
+
+
+def test_fusion_loads_stage1_checkpoints(tmp_path):
+    pet = M.Small_PET_CNN(G.pet_hparams())
+    mri = M.Anat_CNN(G.anat_hparams(10))
+    G.load_prng_weights(pet, 1)
+    G.load_prng_weights(mri, 2)
+    pet.save_checkpoint(str(tmp_path / "pet.ckpt"))
+    mri.save_checkpoint(str(tmp_path / "mri.ckpt"))
+    h = G.anat_hparams(10, fl_gamma=2, path_pet=str(tmp_path / "pet.ckpt"),
+                       path_mri=str(tmp_path / "mri.ckpt"))
+    f = M.Anat_PET_CNN(h)
+    assert len(f.model_pet) == len(pet.model) - 3          # anat_pet_fusion.py:28-29
+    assert len(f.model_mri.model.conv_seg) == 2             # anat_pet_fusion.py:32
+    assert torch.equal(f.model_mri.model.conv1.weight, mri.model.conv1.weight)
+    f2 = M.Anat_PET_CNN(h, path_pet=str(tmp_path / "pet.ckpt"),
+                        path_mri=str(tmp_path / "mri.ckpt"))   # test_anat_pet_fusion.py alias
+    assert list(f2.state_dict()) == list(f.state_dict())
+
+
+def test_frozen_backbone_without_lr_pretrained():
+    h = G.anat_hparams(10, lr_pretrained=None)
+    m = M.Anat_CNN(h)
+    m.configure_optimizers()
+    assert not m.model.conv1.weight.requires_grad
+    assert all(p.requires_grad for p in m.model.conv_seg.parameters())
+
+
+def test_no_cpu_fallback():
+    m = M.Anat_CNN(G.anat_hparams(10))
+    batch = G.batch_for((1, 16, 16, 16), 2, 0)
+    with pytest.raises(_lib.MMADError, match="HIP devices only"):
+        m.general_step(batch, 0, "train")
+
+
+def test_precision_switch():
+    m = M.Anat_CNN(G.anat_hparams(10, precision="bf16"))
+    assert m.model.layer4[0].conv2.compute_dtype == torch.bfloat16
+    m = M.Anat_CNN(G.anat_hparams(10))
+    assert m.model.layer4[0].conv2.compute_dtype == torch.float32
+    with pytest.raises(ValueError):
+        M.Anat_CNN(G.anat_hparams(10, precision="fp8"))
+
+
+def test_depth_table():
+    for depth, blocks in ((10, 1), (18, 2), (34, 3)):
+        m = M.Anat_CNN(G.anat_hparams(depth))
+        assert len(m.model.layer1) == blocks
+        assert m.model.conv_seg[-2].in_features == 512
+    m = M.Anat_CNN(G.anat_hparams(50))
+    assert m.model.conv_seg[-2].in_features == 2048
+    with pytest.raises(ValueError):
+        M.Anat_CNN(G.anat_hparams(26))
+
+
+def test_metrics_fallback_f1():
+    from multimodal_alzheimer_amd.lightning_compat import MulticlassF1Score
+    f = MulticlassF1Score(num_classes=2, average="macro")
+    f(torch.tensor([[0.9, 0.1], [0.2, 0.8], [0.3, 0.7], [0.6, 0.4]]), torch.tensor([0, 1, 0, 0]))
+    # class 0: tp=2 fp=0 fn=1 -> 0.8; class 1: tp=1 fp=1 fn=0 -> 0.667
+    np.testing.assert_allclose(f.compute().item(), (0.8 + 2 / 3) / 2, rtol=1e-6)
