@@ -144,11 +144,25 @@ __global__ __launch_bounds__(256) void igemm_kernel(Geom g, const T* __restrict_
 
   const int wm = wave & 1, wn = wave >> 1;
   const int lr = lane & 15, lk = lane >> 4;
-  f32x4 acc[4][TN];
+  // fp32 mode sums K in two levels (a fresh partial per FLUSH K-steps, then acc += part):
+  // one f32 MFMA chain over K = 27*512 terms would grow the rounding error ~K-fold.
+  constexpr int FLUSH = 8;
+  f32x4 acc[4][TN], part[4][TN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto flush = [&]() {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] += part[i][j];
+          part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+  };
 
   auto compute = [&](int buf) {
     const char* a = As + buf * BM * ROWB + (wm * 64 + lr) * ROWB;
@@ -180,7 +194,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(Geom g, const T* __restrict_
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], part[i][j], 0, 0, 0);
       }
     }
   };
@@ -193,9 +207,11 @@ __global__ __launch_bounds__(256) void igemm_kernel(Geom g, const T* __restrict_
     const int cur = ks & 1;
     if (ks + 1 < nk) load_tiles((ks + 1) * BK);
     compute(cur);
+    if (ks % FLUSH == FLUSH - 1) flush();
     if (ks + 1 < nk) store_tiles(cur ^ 1);
     __syncthreads();
   }
+  flush();
 
   // epilogue: bias, store, BN partial sums over this block's valid rows
   float cs[TN], cq[TN];
@@ -347,11 +363,23 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Geom g, const T* __restrict_
 
   const int wm = wave & 1, wn = wave >> 1;
   const int lr = lane & 15, lk = lane >> 4;
-  f32x4 acc[TI][TJ];
+  constexpr int FLUSH = 4;    // fp32: fresh partial every 4 K-steps (128 voxels)
+  f32x4 acc[TI][TJ], part[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TJ; ++j) acc[i][j] = part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto flush = [&]() {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          acc[i][j] += part[i][j];
+          part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+  };
 
   auto compute = [&](int buf) {
     const char* a = As + buf * WBK * AROW;
@@ -394,7 +422,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Geom g, const T* __restrict_
         for (int i = 0; i < TI; ++i)
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], part[i][j], 0, 0, 0);
       }
     }
   };
@@ -408,10 +436,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Geom g, const T* __restrict_
       const int cur = ks & 1;
       if (ks + 1 < nk) load_tiles(mbeg + (ks + 1) * WBK);
       compute(cur);
+      if (ks % FLUSH == FLUSH - 1) flush();
       if (ks + 1 < nk) store_tiles(cur ^ 1);
       __syncthreads();
     }
   }
+  flush();
   float* out = ws + (int64_t)blockIdx.z * g.Nd * g.K;
 #pragma unroll
   for (int i = 0; i < TI; ++i)

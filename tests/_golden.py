@@ -54,6 +54,8 @@ def load_prng_weights(model, seed):
 CASES = {
     "anat_r10_32": (lambda: anat_hparams(10), "anat", 12, ("mri",)),
     "anat_r10_64": (lambda: anat_hparams(10), "anat", 13, ("mri",)),
+    "anat_r10_32_live": (lambda: anat_hparams(10), "anat", 32, ("mri",)),
+    "anat_r10_64_live": (lambda: anat_hparams(10), "anat", 33, ("mri",)),
     "anat_r18_head": (lambda: anat_hparams(18, n_classes=3, batchnorm_begin=True,
                                            batchnorm_dense=True, linear_out=[64, 32],
                                            fl_gamma=2), "anat", 14, ("mri",)),

@@ -80,7 +80,15 @@ def install_stubs():
     sys.modules.update({"MedicalNet": mn, "MedicalNet.model": mn_model,
                         "MedicalNet.setting": mn_setting})
     os.environ.setdefault("CUDA_VISIBLE_DEVICES", "0")   # anat_cnn.py:20-24 insists
+    # The reference's `pkg` is a namespace package (no __init__.py); this repo's `pkg/`
+    # import shim is a regular package and would shadow it, so drop the repo from the path
+    # (the oracle modules are already imported) and any cached `pkg` modules.
+    sys.path[:] = [p for p in sys.path if os.path.abspath(p or ".") != REPO]
+    for name in [m for m in sys.modules if m == "pkg" or m.startswith("pkg.")]:
+        del sys.modules[name]
     sys.path.insert(0, REF)
+    import pkg.models.base_model as _bm
+    assert _bm.__file__.startswith(REF), _bm.__file__
 
 
 def load_prng_weights(model, seed):
@@ -190,13 +198,34 @@ def _anat(depth, size, bsz, seed, **kw):
 
 
 @case
-def anat_r10_32():
+def anat_r10_32():                           # all logits ReLU'd to 0: argmax tie case
     return _anat(10, 32, 2, 11)
 
 
 @case
 def anat_r10_64():                           # BASELINE config 1 (CPU plumbing config)
     return _anat(10, 64, 2, 12)
+
+
+def _anat_live(depth, size, bsz, seed, **kw):
+    """Weight seed (searched upwards in steps of 1000) whose train logits keep a positive
+    entry in every sample, so gradients reach the backbone (the final ReLU,
+    anat_cnn.py:77, otherwise zeroes them all)."""
+    for s in range(seed, seed + 50000, 1000):
+        out = _anat(depth, size, bsz, s, **kw)
+        if (out["train_logits"] > 0).any(axis=1).all():
+            return out
+    raise RuntimeError("no live seed")
+
+
+@case
+def anat_r10_32_live():
+    return _anat_live(10, 32, 2, 31)
+
+
+@case
+def anat_r10_64_live():                      # BASELINE config 1 with live gradients
+    return _anat_live(10, 64, 2, 32)
 
 
 @case

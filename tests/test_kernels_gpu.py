@@ -168,6 +168,40 @@ def test_batchnorm_act(mode, dtype):
         close(rbn.weight.grad, w2.grad, 5 * tol, "dgamma_res")
 
 
+@pytest.mark.parametrize("shape,dil", [((2, 512, 4, 4, 4), 4), ((2, 256, 4, 4, 4), 2),
+                                       ((2, 64, 8, 8, 8), 1)])
+def test_conv_bn_relu_chain(shape, dil):
+    """conv (epilogue BN partial sums) -> BN(train) + ReLU -> conv, forward and backward,
+    fp32, against torch float64 -- the fused block structure of MedicalNet's BasicBlock."""
+    n, c, d, h, w = shape
+    x = rnd(*shape, seed=80)
+    w1 = rnd(c, c, 3, 3, 3, seed=81, scale=(3.0 / (27 * c)) ** 0.5)
+    w2 = rnd(c, c, 3, 3, 3, seed=82, scale=(3.0 / (27 * c)) ** 0.5)
+    bn = _BN(c, 83)
+    xr = x.clone().requires_grad_(True)
+    w1r, w2r = w1.clone().requires_grad_(True), w2.clone().requires_grad_(True)
+    c1 = F.conv3d(xr, w1r, None, 1, dil, dil)
+    a1, gw, gb, rm, rv = _ref_bn(c1, bn, True)
+    a1 = torch.relu(a1)
+    out = F.conv3d(a1, w2r, None, 1, dil, dil)
+    gy = rnd(*out.shape, seed=84)
+    out.backward(gy)
+
+    xg = to_vol(x, torch.float32).requires_grad_(True)
+    w1g = w1.float().to(DEV).requires_grad_(True)
+    w2g = w2.float().to(DEV).requires_grad_(True)
+    y1, parts = V.conv3d(xg, w1g, None, (1,) * 3, (dil,) * 3, (dil,) * 3, torch.float32, True)
+    h1 = V.batchnorm_act(y1, bn, parts, relu=True)
+    o = V.conv3d(h1, w2g, None, (1,) * 3, (dil,) * 3, (dil,) * 3, torch.float32)
+    o.backward(to_vol(gy, torch.float32))
+    close(o, out, 2e-5, "out")
+    close(bn.bias.grad, gb.grad, 1e-4, "dbeta")
+    close(bn.weight.grad, gw.grad, 1e-4, "dgamma")
+    close(w1g.grad, w1r.grad, 1e-4, "dw1")
+    close(w2g.grad, w2r.grad, 1e-4, "dw2")
+    close(xg.grad, xr.grad, 1e-4, "dx")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("k,s,p,shape", [(3, 2, 1, (2, 64, 9, 10, 11)), (2, 2, 0, (2, 16, 9, 8, 7))])
 def test_maxpool(k, s, p, shape, dtype):
