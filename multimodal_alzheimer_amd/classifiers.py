@@ -222,8 +222,26 @@ def _adam_groups_backbone(model, hparams):
     return groups
 
 
+def _merge_groups(groups):
+    """The reference builds one Adam param group per tensor (anat_cnn.py:112-126); groups
+    that share a learning rate are merged (Adam is element-wise, so the update is
+    identical) so the fused optimizer runs one multi-tensor launch per learning rate
+    instead of one per tensor."""
+    merged = {}
+    for grp in groups:
+        params = grp["params"]
+        params = list(params) if not isinstance(params, torch.Tensor) else [params]
+        key = grp.get("lr", None)
+        merged.setdefault(key, []).extend(params)
+    out = []
+    for lr, params in merged.items():
+        out.append({"params": params} if lr is None else {"params": params, "lr": lr})
+    return out
+
+
 def _adam(groups, hparams, device):
     fused = device.type == "cuda"
+    groups = _merge_groups(groups)
     return torch.optim.Adam(groups, weight_decay=hparams.get("l2_reg", 0) or 0, fused=fused)
 
 

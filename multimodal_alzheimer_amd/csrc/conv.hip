@@ -265,6 +265,274 @@ __global__ __launch_bounds__(256) void igemm_kernel(Geom g, const T* __restrict_
   }
 }
 
+// ---- implicit GEMM v2: LDS-DMA staging ----------------------------------------------
+// Same GEMM view as igemm_kernel, restructured for gfx950:
+//  * operands go global -> LDS directly with global_load_lds_dwordx4 (no VGPR staging):
+//    one wave instruction fills 8 tile rows x 128 B; each lane supplies its own source
+//    address, so the implicit-GEMM row gather and the zero padding (lanes pointed at a
+//    128-B zero block in the code object) cost no extra LDS writes;
+//  * 128-B K-slices per stage (64 bf16 / 32 f32) in a 2-stage ring, one barrier per stage;
+//  * XOR-swizzled LDS rows (chunk c of row r lives in slot c ^ (r & 7)), applied on the
+//    source address so the DMA image stays lane-linear, which spreads the fragment reads
+//    of 16 consecutive rows over 8 slots;
+//  * XCD-aware tile order: each XCD walks a contiguous range of (m, n) tiles with n
+//    fastest, so the n-tiles that share an A panel (and neighbouring m-tiles that share
+//    halo voxels) meet in the same L2.
+__device__ const u32x4 g_zero_chunk[8] = {};
+
+constexpr int RB2 = 128;   // K bytes per stage row
+
+template <typename T, int BN, bool TRANS, int BM2, int NST>
+__global__ __launch_bounds__(256, NST == 2 ? 2 : 1) void igemm2_kernel(
+    Geom g, const T* __restrict__ src, const T* __restrict__ wgt, const float* __restrict__ bias,
+    T* __restrict__ dst, float* __restrict__ stats, int nbm, int nbn) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  constexpr int BK = RB2 / (int)sizeof(T);
+  constexpr int TM = BM2 / 32, TN = BN / 32;
+  constexpr int A_BYTES = BM2 * RB2, B_BYTES = BN * RB2, STAGE = A_BYTES + B_BYTES;
+  constexpr int AI = A_BYTES / 4096, BI = B_BYTES / 4096;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* tapoff = reinterpret_cast<int*>(smem);
+  char* ring = smem + TAPB;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int mt = tile / nbn, nt = tile % nbn;
+  const int m0 = mt * BM2, n0 = nt * BN;
+  fill_taps(g, tapoff, TRANS);
+
+  // this lane's A rows: one per DMA instruction, row = (wave*AI + i)*8 + lane/8
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;          // logical K chunk this lane fetches
+  int rz[AI], ry[AI], rx[AI];
+  int64_t rbase[AI];
+  bool rok[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int m = m0 + (wave * AI + i) * 8 + lrow;
+    rok[i] = m < g.M;
+    const int mm = rok[i] ? m : 0;
+    const int xw = mm % g.Wd;
+    int t1 = mm / g.Wd;
+    const int yh = t1 % g.Hd;
+    t1 /= g.Hd;
+    const int zd = t1 % g.Dd, nb = t1 / g.Dd;
+    if (!TRANS) {
+      rz[i] = zd * g.sd - g.pd; ry[i] = yh * g.sh - g.ph; rx[i] = xw * g.sw - g.pw;
+    } else {
+      rz[i] = zd + g.pd; ry[i] = yh + g.ph; rx[i] = xw + g.pw;
+    }
+    rbase[i] = (int64_t)nb * g.Ds;
+  }
+  __syncthreads();
+
+  auto issue = [&](int stage, int k0) {
+    char* sbase = ring + stage * STAGE;
+    const int k = k0 + lchunk * EPC;
+    const bool kok = k < g.K;
+    const int tap = k >> g.cs_shift, ci = k & (g.Cs - 1);
+    const int to = kok ? tapoff[tap] : 0;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const void* p = g_zero_chunk;
+      int z, y, x;
+      if (rok[i] && kok && src_voxel<TRANS>(g, rz[i], ry[i], rx[i], to, z, y, x)) {
+        const int64_t vox = ((rbase[i] + z) * g.Hs + y) * g.Ws + x;
+        p = src + (vox << g.cs_shift) + ci;
+      }
+      __builtin_amdgcn_global_load_lds(p, (LDS_AS void*)(sbase + (wave * AI + i) * 1024), 16,
+                                       0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int co = n0 + (wave * BI + i) * 8 + lrow;
+      const void* p = co < g.Nd ? (const void*)(wgt + (int64_t)co * g.Kpad + k0 + lchunk * EPC)
+                                : (const void*)g_zero_chunk;
+      __builtin_amdgcn_global_load_lds(
+          p, (LDS_AS void*)(sbase + A_BYTES + (wave * BI + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  const int wm = wave & 1, wn = wave >> 1;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int sw = lr & 7;                          // swizzle of every row this lane reads
+  constexpr int FLUSH = 8;
+  f32x4 acc[TM][TN], part[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int stage) {
+    const char* a = ring + stage * STAGE + (wm * (BM2 / 2) + lr) * RB2;
+    const char* b = ring + stage * STAGE + A_BYTES + (wn * (BN / 2) + lr) * RB2;
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int s = 0; s < BK / 32; ++s) {
+        const int off = ((4 * s + lk) ^ sw) << 4;
+        bf16x8 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8*>(a + i * 16 * RB2 + off);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8*>(b + j * 16 * RB2 + off);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < BK / 4; ++s) {
+        const int off = ((s ^ sw) << 4) + lk * 4;
+        float fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[i] = *reinterpret_cast<const float*>(a + i * 16 * RB2 + off);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const float*>(b + j * 16 * RB2 + off);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], part[i][j], 0, 0, 0);
+      }
+    }
+  };
+  auto flush = [&]() {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] += part[i][j];
+          part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+  };
+
+  const int nk = g.Kpad / BK;
+  if constexpr (NST == 2) {
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ks = 0; ks < nk; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < nk) issue(cur ^ 1, (ks + 1) * BK);
+      compute(cur);
+      if (ks % FLUSH == FLUSH - 1) flush();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // 3-stage ring: stage ks+2 is issued while stage ks is consumed; the counted wait
+    // vmcnt(AI+BI) at the end of an iteration retires stage ks+1 and leaves ks+2 in flight
+    // across the raw barrier (a __syncthreads() would drain it: vmcnt(0)).
+    constexpr int NI = AI + BI;
+    issue(0, 0);
+    if (nk > 1) {
+      issue(1, BK);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    int cur = 0;
+    for (int ks = 0; ks < nk; ++ks) {
+      const int nxt2 = cur == 0 ? 2 : cur - 1;          // (ks + 2) % 3
+      if (ks + 2 < nk) issue(nxt2, (ks + 2) * BK);
+      compute(cur);
+      if (ks % FLUSH == FLUSH - 1) flush();
+      if (ks + 2 < nk)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NI) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      cur = cur == 2 ? 0 : cur + 1;
+    }
+  }
+  flush();
+
+  // epilogue: bias, store, BN partial sums over this tile's valid rows.  bf16 tiles are
+  // transposed through LDS so the global stores are whole 16-byte channel vectors (the
+  // MFMA C layout gives each lane 4 voxels x 1 channel).
+  constexpr int CROW = BN * 2 + 16;
+  const bool lds_out = sizeof(T) == 2 && (g.Nd & 7) == 0;
+  u16* ctile = reinterpret_cast<u16*>(ring + 1024);
+  float cs[TN], cq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    cs[j] = 0.f; cq[j] = 0.f;
+    const int col = wn * (BN / 2) + j * 16 + lr;
+    const int co = n0 + col;
+    const float bv = (bias != nullptr && co < g.Nd) ? bias[co] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * (BM2 / 2) + i * 16 + lk * 4 + r;
+        const int m = m0 + row;
+        const float v = acc[i][j][r] + bv;
+        if (lds_out) ctile[row * (CROW / 2) + col] = f2bf(v);
+        if (m < g.M && co < g.Nd) {
+          if (!lds_out) Elt<T>::st(dst, (int64_t)m * g.Nd + co, v);
+          cs[j] += v;
+          cq[j] += v * v;
+        }
+      }
+  }
+  if (lds_out) {
+    __syncthreads();
+    constexpr int CPR = BN / 8;
+#pragma unroll
+    for (int h = 0; h < BM2 * CPR / 256; ++h) {
+      const int q = tid + 256 * h;
+      const int row = q / CPR, c8 = q % CPR;
+      const int m = m0 + row, co = n0 + c8 * 8;
+      if (m < g.M && co < g.Nd)
+        *reinterpret_cast<u32x4*>(reinterpret_cast<u16*>(dst) + (int64_t)m * g.Nd + co) =
+            *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) + row * CROW +
+                                            c8 * 16);
+    }
+  }
+  if (stats != nullptr) {
+    float* red = reinterpret_cast<float*>(ring);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      cs[j] += __shfl_xor(cs[j], 16, 64);
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 16, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+    }
+    if (wm == 1 && lk == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (BN / 2) + j * 16 + lr;
+        red[col] = cs[j];
+        red[BN + col] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && lk == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (BN / 2) + j * 16 + lr;
+        const int co = n0 + col;
+        if (co < g.Nd) {
+          stats[((int64_t)mt * 2) * g.Nd + co] = cs[j] + red[col];
+          stats[((int64_t)mt * 2 + 1) * g.Nd + co] = cq[j] + red[BN + col];
+        }
+      }
+    }
+  }
+}
+
 // ---- weight gradient --------------------------------------------------------------
 // dW[co][k] = sum_m dY[m][co] * X(m, k): block tile BMW (co) x 128 (k), K-step = 32
 // voxels, split over m into `splits` slices -> fp32 partial slabs ws[s][co][k].
@@ -456,6 +724,206 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Geom g, const T* __restrict_
     }
 }
 
+// ---- weight gradient v2: LDS-DMA staging ---------------------------------------------
+// Same GEMM as wgrad_kernel.  Both tiles are m-major images ([m][co] of dY, [m][k] of the
+// gathered X) filled by global_load_lds_dwordx4: a wave instruction writes 1 KB = RPI
+// m-rows.  Rows are XOR-swizzled in 16-byte slots (swizzle applied to the source address,
+// image stays lane-linear) so the transposing fragment reads of 8 m-rows x 16 columns
+// (bf16: ds_read_b64_tr_b16) or 2 m-rows x 16 columns (f32: ds_read_b32) hit distinct
+// banks.  2-stage ring, one barrier per 32-voxel stage.
+template <typename T, int ROWB>
+__device__ __forceinline__ int wswz(int r) {
+  if constexpr (sizeof(T) == 4) return 4 * (r & 1);
+  else if constexpr (ROWB >= 256) return 2 * (r & 3) + 8 * ((r >> 3) & 1);
+  else return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
+}
+
+template <typename T, int BMW>
+__global__ __launch_bounds__(256, 2) void wgrad2_kernel(Geom g, const T* __restrict__ src,
+                                                        const T* __restrict__ dy,
+                                                        float* __restrict__ ws, int m_per_split) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  constexpr int AROWB = BMW * (int)sizeof(T), BROWB = WBN * (int)sizeof(T);
+  constexpr int A_BYTES = WBK * AROWB, B_BYTES = WBK * BROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int ARPI = 1024 / AROWB, BRPI = 1024 / BROWB;      // rows per DMA instruction
+  constexpr int ALPR = AROWB / 16, BLPR = BROWB / 16;         // lanes per row
+  constexpr int AIPW = A_BYTES / 4096, BIPW = B_BYTES / 4096; // instructions per wave
+  constexpr int TI = BMW / 32, TJ = WBN / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* tapoff = reinterpret_cast<int*>(smem);
+  char* ring = smem + TAPB;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k0 = blockIdx.x * WBN, co0 = blockIdx.y * BMW;
+  const int mbeg = blockIdx.z * m_per_split;
+  const int mend = min(g.M, mbeg + m_per_split);
+  fill_taps(g, tapoff, false);
+  __syncthreads();
+
+  // A (dY) rows / chunks of this lane
+  int arow[AIPW], aco[AIPW];
+#pragma unroll
+  for (int i = 0; i < AIPW; ++i) {
+    arow[i] = (wave * AIPW + i) * ARPI + lane / ALPR;
+    aco[i] = co0 + ((lane % ALPR) ^ wswz<T, AROWB>(arow[i])) * EPC;
+  }
+  // B (gathered X) rows / chunks of this lane: fixed (tap, ci) per instruction, rows advance
+  int brow[BIPW], bto[BIPW], bci[BIPW], bx[BIPW], by[BIPW], bz[BIPW], bn[BIPW];
+  bool bkok[BIPW];
+#pragma unroll
+  for (int i = 0; i < BIPW; ++i) {
+    brow[i] = (wave * BIPW + i) * BRPI + lane / BLPR;
+    const int k = k0 + ((lane % BLPR) ^ wswz<T, BROWB>(brow[i])) * EPC;
+    bkok[i] = k < g.K;
+    bci[i] = k & (g.Cs - 1);
+    bto[i] = tapoff[bkok[i] ? (k >> g.cs_shift) : 0];
+    int m = mbeg + brow[i];
+    bx[i] = m % g.Wd; m /= g.Wd;
+    by[i] = m % g.Hd; m /= g.Hd;
+    bz[i] = m % g.Dd; bn[i] = m / g.Dd;
+  }
+
+  auto issue = [&](int stage, int mk) {
+    char* sbase = ring + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < AIPW; ++i) {
+      const int m = mk + arow[i];
+      const void* p = (m < mend && aco[i] < g.Nd)
+                          ? (const void*)(dy + (int64_t)m * g.Nd + aco[i])
+                          : (const void*)g_zero_chunk;
+      __builtin_amdgcn_global_load_lds(p, (LDS_AS void*)(sbase + (wave * AIPW + i) * 1024), 16,
+                                       0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BIPW; ++i) {
+      const int m = mk + brow[i];
+      const void* p = g_zero_chunk;
+      int z, y, x;
+      if (m < mend && bkok[i] &&
+          src_voxel<false>(g, bz[i] * g.sd - g.pd, by[i] * g.sh - g.ph, bx[i] * g.sw - g.pw,
+                           bto[i], z, y, x)) {
+        const int64_t vox = (((int64_t)bn[i] * g.Ds + z) * g.Hs + y) * g.Ws + x;
+        p = src + (vox << g.cs_shift) + bci[i];
+      }
+      __builtin_amdgcn_global_load_lds(
+          p, (LDS_AS void*)(sbase + A_BYTES + (wave * BIPW + i) * 1024), 16, 0, 0);
+      bx[i] += WBK;
+      while (bx[i] >= g.Wd) {
+        bx[i] -= g.Wd;
+        if (++by[i] == g.Hd) { by[i] = 0; if (++bz[i] == g.Dd) { bz[i] = 0; ++bn[i]; } }
+      }
+    }
+  };
+
+  const int wm = wave & 1, wn = wave >> 1;
+  const int lr = lane & 15, lk = lane >> 4;
+  constexpr int FLUSH = 4;
+  f32x4 acc[TI][TJ], part[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int stage) {
+    const char* a = ring + stage * STAGE;
+    const char* b = a + A_BYTES;
+    if constexpr (sizeof(T) == 2) {
+      // lane 4q+p of each 16-lane group lk reads m-rows 8lk+q (+4), columns 4p..4p+3
+      const int q = (lane & 15) >> 2, p = lane & 3;
+      const int r0 = 8 * lk + q, r1 = r0 + 4;
+      bf16x8 fa[TI], fb[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int col = wm * (BMW / 2) + i * 16 + 4 * p;          // element column
+        const int ch = col >> 3, hb = (col & 7) * 2;
+        const char* lo = a + r0 * AROWB + ((ch ^ wswz<T, AROWB>(r0)) << 4) + hb;
+        const char* hi = a + r1 * AROWB + ((ch ^ wswz<T, AROWB>(r1)) << 4) + hb;
+        bf16x4 vlo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)lo);
+        bf16x4 vhi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)hi);
+        fa[i] = __builtin_shufflevector(vlo, vhi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int col = wn * (WBN / 2) + j * 16 + 4 * p;
+        const int ch = col >> 3, hb = (col & 7) * 2;
+        const char* lo = b + r0 * BROWB + ((ch ^ wswz<T, BROWB>(r0)) << 4) + hb;
+        const char* hi = b + r1 * BROWB + ((ch ^ wswz<T, BROWB>(r1)) << 4) + hb;
+        bf16x4 vlo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)lo);
+        bf16x4 vhi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)hi);
+        fb[j] = __builtin_shufflevector(vlo, vhi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < WBK / 4; ++s) {
+        const int row = s * 4 + lk;
+        float fa[TI], fb[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int col = wm * (BMW / 2) + i * 16 + lr;
+          fa[i] = *reinterpret_cast<const float*>(
+              a + row * AROWB + (((col >> 2) ^ wswz<T, AROWB>(row)) << 4) + (col & 3) * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int col = wn * (WBN / 2) + j * 16 + lr;
+          fb[j] = *reinterpret_cast<const float*>(
+              b + row * BROWB + (((col >> 2) ^ wswz<T, BROWB>(row)) << 4) + (col & 3) * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], part[i][j], 0, 0, 0);
+      }
+    }
+  };
+  auto flush = [&]() {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          acc[i][j] += part[i][j];
+          part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+  };
+
+  const int nk = (mend - mbeg + WBK - 1) / WBK;
+  if (nk > 0) {
+    issue(0, mbeg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ks = 0; ks < nk; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < nk) issue(cur ^ 1, mbeg + (ks + 1) * WBK);
+      compute(cur);
+      if (ks % FLUSH == FLUSH - 1) flush();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  flush();
+  float* out = ws + (int64_t)blockIdx.z * g.Nd * g.K;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = k0 + wn * (WBN / 2) + j * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * (BMW / 2) + i * 16 + lk * 4 + r;
+        if (co < g.Nd && k < g.K) out[(int64_t)co * g.K + k] = acc[i][j][r];
+      }
+    }
+}
+
 // sum the split-K slabs in fixed order and scatter into the torch [co][ci][kd][kh][kw]
 // layout.  unf_kw > 0: the conv ran on a W-unfolded Cin=1 input (k = (kd,kh)*8 + j).
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
@@ -526,7 +994,8 @@ __global__ void unfold_w_kernel(const TI* __restrict__ x, TO* __restrict__ xu, i
 }
 
 // ---- host-side geometry -----------------------------------------------------------
-int bk_of(int dtype) { return dtype == MMAD_BF16 ? 32 : 16; }
+// packed-weight row stride granule: one 128-byte K-slice (igemm2's stage row)
+int bk_of(int dtype) { return dtype == MMAD_BF16 ? 64 : 32; }
 
 bool desc_ok(const mmad_conv_desc* d) {
   if (!d) return false;
@@ -593,7 +1062,7 @@ WSplit wgrad_split(const Geom& g) {
   WSplit s{};
   s.bmw = g.Nd <= 64 ? 64 : 128;
   const int64_t tiles = cdiv(g.Nd, s.bmw) * cdiv(g.K, WBN);
-  int64_t want = cdiv(2048, tiles);
+  int64_t want = cdiv(1024, tiles);     // ~4 blocks per CU: 2 resident + a second wave
   const int64_t max_split = std::max<int64_t>(1, cdiv(g.M, WBK * 8));
   want = std::max<int64_t>(1, std::min(want, max_split));
   // keep the slab workspace bounded (<= 512 MiB)
@@ -613,10 +1082,66 @@ int launch_igemm(const Geom& g, const void* src, const void* w, const float* bia
   return launch_status();
 }
 
+// tile rows: 64 when 128-row tiles would leave the 256 CUs under two blocks each
+int igemm_bm(const Geom& g) {
+  const int64_t tiles = cdiv(g.M, 128) * cdiv(g.Nd, bn_of(g));
+  return tiles < 512 ? 64 : 128;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+template <typename T, int BN, bool TRANS, int BMT, int NST>
+int launch_igemm2_bm(const Geom& g, const void* src, const void* w, const float* bias,
+                     void* dst, float* stats, hipStream_t st) {
+  const size_t lds = TAPB + NST * (BMT + BN) * RB2;
+  static const bool attr_ok =
+      lds <= 65536 || hipFuncSetAttribute((const void*)igemm2_kernel<T, BN, TRANS, BMT, NST>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)lds) == hipSuccess;
+  if (!attr_ok) return MMAD_EUNSUPPORTED;
+  const int nbm = (int)cdiv(g.M, BMT), nbn = (int)cdiv(g.Nd, BN);
+  hipLaunchKernelGGL((igemm2_kernel<T, BN, TRANS, BMT, NST>), dim3((unsigned)(nbm * nbn)),
+                     dim3(256), lds, st, g, (const T*)src, (const T*)w, bias, (T*)dst, stats,
+                     nbm, nbn);
+  return launch_status();
+}
+
+template <typename T, int BN, bool TRANS>
+int launch_igemm2(const Geom& g, const void* src, const void* w, const float* bias, void* dst,
+                  float* stats, hipStream_t st) {
+  // ring depth for 128-row tiles: 3 stages need 96 KB (1 block/CU) and measured 0.6x of
+  // the 2-stage / 2-blocks-per-CU configuration, so 2 is the default
+  static const int nst = env_int("MMAD_NST", 2);
+  if (igemm_bm(g) == 64)
+    return launch_igemm2_bm<T, BN, TRANS, 64, 2>(g, src, w, bias, dst, stats, st);
+  if (nst == 3)
+    return launch_igemm2_bm<T, BN, TRANS, 128, 3>(g, src, w, bias, dst, stats, st);
+  return launch_igemm2_bm<T, BN, TRANS, 128, 2>(g, src, w, bias, dst, stats, st);
+}
+
+// MMAD_IGEMM=1 selects the register-staged v1 kernel (kept for A/B measurements)
+bool use_v1() {
+  static const bool v = [] {
+    const char* e = getenv("MMAD_IGEMM");
+    return e != nullptr && e[0] == '1';
+  }();
+  return v;
+}
+
 template <bool TRANS>
 int run_igemm(const Geom& g, int dtype, const void* src, const void* w, const float* bias,
               void* dst, float* stats, hipStream_t st) {
   const int bn = bn_of(g);
+  if (!use_v1()) {
+    if (dtype == MMAD_BF16)
+      return bn == 64 ? launch_igemm2<u16, 64, TRANS>(g, src, w, bias, dst, stats, st)
+                      : launch_igemm2<u16, 128, TRANS>(g, src, w, bias, dst, stats, st);
+    return bn == 64 ? launch_igemm2<float, 64, TRANS>(g, src, w, bias, dst, stats, st)
+                    : launch_igemm2<float, 128, TRANS>(g, src, w, bias, dst, stats, st);
+  }
   if (dtype == MMAD_BF16)
     return bn == 64 ? launch_igemm<u16, 64, TRANS>(g, src, w, bias, dst, stats, st)
                     : launch_igemm<u16, 128, TRANS>(g, src, w, bias, dst, stats, st);
@@ -627,6 +1152,18 @@ int run_igemm(const Geom& g, int dtype, const void* src, const void* w, const fl
 template <typename T, int BMW>
 int launch_wgrad(const Geom& g, const WSplit& sp, const void* x, const void* dy, float* ws,
                  hipStream_t st) {
+  if (!use_v1()) {
+    const size_t lds2 = TAPB + 2 * WBK * (BMW + WBN) * sizeof(T);
+    static const bool ok2 =
+        lds2 <= 65536 || hipFuncSetAttribute((const void*)wgrad2_kernel<T, BMW>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds2) == hipSuccess;
+    if (!ok2) return MMAD_EUNSUPPORTED;
+    dim3 grid2((unsigned)cdiv(g.K, WBN), (unsigned)cdiv(g.Nd, BMW), (unsigned)sp.splits);
+    hipLaunchKernelGGL((wgrad2_kernel<T, BMW>), grid2, dim3(256), lds2, st, g, (const T*)x,
+                       (const T*)dy, ws, sp.m_per_split);
+    return launch_status();
+  }
   const size_t arow = BMW * sizeof(T) + 16, brow = WBN * sizeof(T) + 16;
   const size_t lds = TAPB + 2 * WBK * (arow + brow);
   if (lds > 65536) {
@@ -711,7 +1248,8 @@ int mmad_conv_unfold_input(const mmad_conv_desc* d, int in_dtype, const void* x,
 
 int64_t mmad_conv3d_stats_rows(const mmad_conv_desc* d, int dtype) {
   if (!desc_ok(d)) return -1;
-  return cdiv(fwd_geom(d, dtype).M, BM);
+  const Geom g = fwd_geom(d, dtype);
+  return cdiv(g.M, use_v1() ? BM : igemm_bm(g));
 }
 
 int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x, const void* wp,

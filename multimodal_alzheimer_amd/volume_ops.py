@@ -104,6 +104,7 @@ class _Conv3dFn(torch.autograd.Function):
         L.call("mmad_conv3d_fwd", d, dt, L.ptr(src), L.ptr(wp), L.ptr(b), L.ptr(y),
                L.ptr(stats), L.stream())
         ctx.save_for_backward(src, weight)
+        ctx.set_materialize_grads(False)   # the stats output never gets a gradient
         ctx.desc = _desc_tuple(d)
         ctx.cdtype = cdtype
         ctx.has_bias = bias is not None
@@ -115,6 +116,8 @@ class _Conv3dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy, *_):
+        if gy is None:
+            return None, None, None, None, None, None
         src, weight = ctx.saved_tensors
         d = L.ConvDesc(*ctx.desc)
         cdtype = ctx.cdtype
