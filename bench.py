@@ -11,7 +11,8 @@ all-reduce (N>1) + Adam; all parameters trainable (lr_pretrained set).
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
 Rank 0 prints one JSON line.  ``roofline`` times the dominant kernel (layer4.0.conv2
-forward, the largest implicit-GEMM launch) with HIP events on the stream it runs on;
+forward, the largest implicit-GEMM launch) with HIP events recorded around each of its
+launches inside the timed region, on the stream it runs on;
 ``cpu_baseline`` times the CPU oracle (torch fp32, the reference path) on a bounded sample.
 """
 import argparse
@@ -46,48 +47,33 @@ def hparams(precision):
             "loss_class_weights": torch.tensor(W2, dtype=torch.float64)}
 
 
-def dominant_kernel_roofline(model, batch, size, dtype, reps=20):
-    """Time layer4.0.conv2's forward implicit GEMM alone with HIP events."""
-    conv = model.model.layer4[0].conv2
+def dominant_desc(batch, size):
+    """layer4.0.conv2 (512->512, 3^3, dilation 4, 16^3 at 128^3 input): the largest
+    implicit-GEMM launch of the step."""
     s = size // 8
-    n = batch
-    x = torch.randn((n, 512, s, s, s), device="cuda", dtype=dtype).contiguous(
-        memory_format=torch.channels_last_3d)
-    d = volume_ops.conv_desc(tuple(x.shape), tuple(conv.weight.shape), (1, 1, 1), (4, 4, 4),
-                             (4, 4, 4))
-    dt = _lib.dtype_code(dtype)
-    wp = volume_ops.pack_weight(d, dt, conv.weight, dtype, False)
-    y = torch.empty((n, 512, s, s, s), device="cuda", dtype=dtype).contiguous(
-        memory_format=torch.channels_last_3d)
-    lib = _lib.load()
-    stats = torch.empty((lib.mmad_conv3d_stats_rows(d, dt), 2, 512), device="cuda")
-    st = torch.cuda.current_stream()
+    d = volume_ops.conv_desc((batch, 512, s, s, s), (512, 512, 3, 3, 3), (1, 1, 1),
+                             (4, 4, 4), (4, 4, 4))
+    return volume_ops._desc_tuple(d), 2.0 * batch * s ** 3 * 512 * 512 * 27
 
-    def launch():
-        _lib.call("mmad_conv3d_fwd", d, dt, _lib.ptr(x), _lib.ptr(wp), None, _lib.ptr(y),
-                  _lib.ptr(stats), _lib.stream())
 
-    for _ in range(3):
-        launch()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(reps):
-        launch()
-    e1.record(st)
-    e1.synchronize()
-    sec = e0.elapsed_time(e1) / 1e3 / reps
-    flops = 2.0 * n * s ** 3 * 512 * 512 * 27
+def dominant_kernel_roofline(events, batch, size, dtype):
+    """Average duration of the dominant kernel's launches inside the timed region, from the
+    HIP event pairs volume_ops recorded around each launch on its own stream."""
+    _, flops = dominant_desc(batch, size)
+    if not events:
+        return None
+    sec = sum(a.elapsed_time(b) for a, b in events) / len(events) / 1e3
     peak = PEAK_BF16 if dtype == torch.bfloat16 else PEAK_F32
     traffic = None
     tf = os.path.join(REPO, "profiles", "traffic_layer4_conv2_fwd.json")
     if os.path.exists(tf):
         with open(tf) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
-    return {"kernel": "igemm_kernel<bf16,128> layer4.0.conv2 fwd (512->512, 3^3 dil 4, "
-                      f"{n}x{s}^3)",
+    s = size // 8
+    return {"kernel": f"igemm_kernel layer4.0.conv2 fwd (512->512, 3^3 dil 4, {batch}x{s}^3)",
             "bound": "mfma", "achieved": flops / sec / 1e12, "peak": peak / 1e12,
             "unit": "TFLOP/s", "frac": flops / sec / peak, "traffic": traffic,
-            "flop_per_launch": flops, "avg_launch_ms": sec * 1e3}
+            "flop_per_launch": flops, "avg_launch_ms": sec * 1e3, "launches": len(events)}
 
 
 def cpu_baseline(size, seconds_budget=20.0):
@@ -161,11 +147,15 @@ def main():
         step()
     if world > 1:
         dist.barrier()
+    events = []
+    if rank == 0 and not args.no_roofline:
+        volume_ops.FWD_PROBES[dominant_desc(B, S)[0]] = events
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
+    volume_ops.FWD_PROBES.clear()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -193,7 +183,7 @@ def main():
             PEAK_BF16 if cdtype == torch.bfloat16 else PEAK_F32)
         result["hbm_roofline_frac_m2"] = per_gpu * M2_BYTES_PER_VOL / PEAK_HBM
     if rank == 0 and not args.no_roofline:
-        result["roofline"] = dominant_kernel_roofline(model, B, S, cdtype)
+        result["roofline"] = dominant_kernel_roofline(events, B, S, cdtype)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(S)
     if rank == 0:

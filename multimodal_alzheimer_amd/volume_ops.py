@@ -62,6 +62,11 @@ def _desc_tuple(d):
     return tuple(getattr(d, f) for f, _ in L.ConvDesc._fields_)
 
 
+# Live kernel timing: map a conv descriptor tuple to a list; every forward launch with that
+# geometry appends a (start, end) HIP event pair recorded on the launch stream around it.
+FWD_PROBES = {}
+
+
 def pack_weight(d, dt_code, weight, cdtype, for_dgrad):
     lib = L.load()
     n = lib.mmad_conv_packed_elems(d, dt_code, int(for_dgrad))
@@ -101,8 +106,15 @@ class _Conv3dFn(torch.autograd.Function):
             rows = lib.mmad_conv3d_stats_rows(d, dt)
             stats = torch.empty((rows, 2, d.co), dtype=torch.float32, device=x.device)
         b = None if bias is None else bias.detach().contiguous()
+        probe = FWD_PROBES.get(_desc_tuple(d)) if FWD_PROBES else None
+        if probe is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         L.call("mmad_conv3d_fwd", d, dt, L.ptr(src), L.ptr(wp), L.ptr(b), L.ptr(y),
                L.ptr(stats), L.stream())
+        if probe is not None:
+            e1.record()
+            probe.append((e0, e1))
         ctx.save_for_backward(src, weight)
         ctx.set_materialize_grads(False)   # the stats output never gets a gradient
         ctx.desc = _desc_tuple(d)

@@ -53,11 +53,14 @@ def test_host_side_shape_queries(lib):
     assert (d.do_, d.ho, d.wo) == (16, 16, 16)
     assert lib.mmad_conv_packed_elems(d, _lib.BF16, 0) == 128 * 27 * 64
     assert lib.mmad_conv_packed_elems(d, _lib.BF16, 1) == 64 * 27 * 128
-    assert lib.mmad_conv3d_stats_rows(d, _lib.BF16) == 8 * 16 ** 3 // 128
+    # one BN partial row per output tile: 128-voxel tiles, or 64 for grids under 512 tiles
+    assert lib.mmad_conv3d_stats_rows(d, _lib.BF16) == 8 * 16 ** 3 // 64
     assert lib.mmad_conv3d_wgrad_workspace(d, _lib.BF16) > 0
     stem = conv_desc((8, 1, 128, 128, 128), (64, 1, 7, 7, 7), (2, 2, 2), (3, 3, 3), (1, 1, 1))
     assert lib.mmad_conv_unfolded_elems(stem) == 8 * 128 * 128 * 64 * 8
-    assert lib.mmad_conv_packed_elems(stem, _lib.BF16, 0) == 64 * 416   # 49 taps x 8 -> 416
+    assert lib.mmad_conv3d_stats_rows(stem, _lib.BF16) == 8 * 64 ** 3 // 128
+    # 49 (kd, kh) taps x 8 unfolded kw "channels" = 392, padded to a 128-byte K slice
+    assert lib.mmad_conv_packed_elems(stem, _lib.BF16, 0) == 64 * 448
     bad = conv_desc((1, 64, 8, 8, 8), (64, 64, 3, 3, 3), (1, 1, 1), (1, 1, 1), (1, 1, 1))
     bad.wo = 9   # inconsistent with the torch output-extent formula
     assert lib.mmad_conv_packed_elems(bad, _lib.F32, 0) == -1

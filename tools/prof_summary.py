@@ -1,0 +1,92 @@
+"""Summaries of rocprofv3 csv output, written into profiles/.
+
+    python tools/prof_summary.py stats    <dir> [top]      kernel_stats table
+    python tools/prof_summary.py dominant <dir> <grid_x>   per-dispatch durations of the
+                                                           forward igemm launches with that
+                                                           grid (one line per step position)
+    python tools/prof_summary.py traffic  <fetch_dir> <write_dir>   HBM bytes per launch of
+                                                           the probe kernel (json)
+
+FETCH_SIZE is doubled: on gfx950 it reports half the bytes of 16-B-per-lane streaming
+reads, including buffer/global_load ... lds (MI355X_MICROARCH.md, HBM section).
+WRITE_SIZE is taken as is (exact for 16-B-per-lane stores).
+"""
+import collections
+import csv
+import json
+import statistics
+import sys
+
+
+def short(name):
+    return name.replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::",
+                                                                      "")
+
+
+def stats(d, top=30):
+    rows = list(csv.DictReader(open(f"{d}/run_kernel_stats.csv")))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    out = [f"{'total ms':>9} {'%':>5} {'calls':>6} {'avg us':>9}  kernel"]
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
+        out.append(f"{float(r['TotalDurationNs']) / 1e6:9.3f} {float(r['Percentage']):5.1f} "
+                   f"{r['Calls']:>6} {float(r['AverageNs']) / 1e3:9.1f}  {short(r['Name'])[:110]}")
+    out.append(f"all kernels: {tot / 1e6:.3f} ms")
+    return "\n".join(out)
+
+
+def dominant(d, grid_x):
+    """Forward igemm dispatches (MODE 0) in launch order; those with the given grid are
+    grouped by their position inside a step so the layer each one belongs to is visible."""
+    rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+    fwd = [r for r in rows if "igemm_kernel" in r["Kernel_Name"]
+           and r["Kernel_Name"].split("<")[1].split(",")[2].strip() == "0"]
+    fwd.sort(key=lambda r: int(r["Start_Timestamp"]))
+    sel = [r for r in fwd if int(r["Grid_Size_X"]) == grid_x]
+    out = [f"{len(fwd)} forward igemm dispatches, {len(sel)} with grid_x={grid_x}"]
+    # consecutive matching dispatches inside one step form a fixed-length group
+    groups = collections.defaultdict(list)
+    per = None
+    for n in (3, 2, 1):
+        if len(sel) % n == 0:
+            per = n
+            break
+    for i, r in enumerate(sel):
+        groups[i % per].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    for k in sorted(groups):
+        v = groups[k]
+        out.append(f"position {k} of {per}: n={len(v)} avg={statistics.mean(v):.1f} us "
+                   f"median={statistics.median(v):.1f} us min={min(v):.1f} max={max(v):.1f}")
+    return "\n".join(out)
+
+
+def counter(d, name):
+    rows = list(csv.DictReader(open(f"{d}/run_counter_collection.csv")))
+    vals = [float(r["Counter_Value"]) for r in rows
+            if "igemm_kernel" in r["Kernel_Name"] and r["Counter_Name"] == name]
+    return vals
+
+
+def traffic(fetch_dir, write_dir):
+    f = counter(fetch_dir, "FETCH_SIZE")
+    w = counter(write_dir, "WRITE_SIZE")
+    # rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB
+    fb = statistics.median(f) * 1024 * 2
+    wb = statistics.median(w) * 1024
+    return {"kernel": "igemm_kernel layer4.0.conv2 fwd (bf16, 8x512x16^3, 3^3 dil 4)",
+            "launches": [len(f), len(w)],
+            "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+            "hbm_bytes_per_launch": fb + wb,
+            "raw_fetch_size_kib": f, "raw_write_size_kib": w,
+            "correction": "FETCH_SIZE x2 (gfx950 half-count of 16B/lane reads); "
+                          "WRITE_SIZE as reported; median over launches; on-die cache "
+                          "scrubbed before each launch (cold)"}
+
+
+if __name__ == "__main__":
+    mode = sys.argv[1]
+    if mode == "stats":
+        print(stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 30))
+    elif mode == "dominant":
+        print(dominant(sys.argv[2], int(sys.argv[3])))
+    elif mode == "traffic":
+        print(json.dumps(traffic(sys.argv[2], sys.argv[3]), indent=1))
