@@ -126,6 +126,21 @@ int mmad_maxpool3d_fwd(int dtype, int n, int c, int di, int hi, int wi, int do_,
 int mmad_maxpool3d_bwd(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho,
                        int wo, int k, int s, int p, const void* dy, const uint8_t* argmax,
                        void* dx, void* stream);
+/* Fused MedicalNet stem tail maxpool(relu(bn1(conv1 y))) (MedicalNet resnet.py forward:
+ * conv1 -> bn1 -> relu -> maxpool, reached from anat_cnn.py:29-31): the full-resolution
+ * BN+ReLU output is never written.  argmax = window index | 0x80 when the max passed the
+ * ReLU; ymax = the raw y at the argmax.  Backward: mmad_bnpool_bwd_reduce over the pooled
+ * grid -> mmad_bn_bwd_finalize (count = full-resolution rows) -> mmad_bnpool_bwd_apply. */
+int mmad_bnpool_fwd(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho, int wo,
+                    int k, int s, int p, const void* y, const float* scale, const float* shift,
+                    void* out, uint8_t* argmax, void* ymax, void* stream);
+int mmad_bnpool_bwd_reduce(int dtype, int64_t m, int c, const void* g, const uint8_t* argmax,
+                           const void* ymax, const float* mean, const float* invstd,
+                           float* parts, void* stream);   /* m = pooled rows */
+int mmad_bnpool_bwd_apply(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho,
+                          int wo, int k, int s, int p, const void* g, const uint8_t* argmax,
+                          const void* y, const float* mean, const float* invstd,
+                          const float* coef, void* dy, void* stream);
 int mmad_gap_fwd(int dtype, int n, int64_t s, int c, const void* x, float* y, void* stream);
 int mmad_gap_bwd(int dtype, int n, int64_t s, int c, const float* dy, void* dx, void* stream);
 

@@ -28,6 +28,8 @@ PartPlan part_plan(int64_t M) {
 //   MODE 0: y and y^2          (BN forward statistics)
 //   MODE 1: g' and g'*xhat     (BN backward), g' = g * (relu_out > 0 | 1)
 //   MODE 2: y                  (conv bias gradient)
+//   MODE 3: as MODE 1 with the mask from bit 7 of act[] (fused BN+ReLU+max-pool backward,
+//           rows = pooled outputs, y = the pre-BN value at each window's argmax)
 // V channels per thread (16-byte vectors when C % VEC == 0), C / V lanes per row and
 // 256 / (C / V) rows in flight per block; one LDS pass folds the row lanes.
 template <typename T, int MODE, int V>
@@ -37,7 +39,8 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
                                                      const T* __restrict__ relu_out,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ invstd,
-                                                     float* __restrict__ parts) {
+                                                     float* __restrict__ parts,
+                                                     const uint8_t* __restrict__ act) {
   __shared__ float red[2][2048];
   const int tid = threadIdx.x;
   const int lpr = C / V;
@@ -50,7 +53,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
   for (int e = 0; e < V; ++e) { s[e] = 0.f; q[e] = 0.f; }
   if (rl < rpar) {
     float mu[V], is[V];
-    if (MODE == 1) {
+    if (MODE == 1 || MODE == 3) {
 #pragma unroll
       for (int e = 0; e < V; ++e) { mu[e] = mean[cl * V + e]; is[e] = invstd[cl * V + e]; }
     }
@@ -59,11 +62,14 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
       float yv[V];
       if constexpr (V == Chunk<T>::N) Chunk<T>::load(y + i, yv);
       else for (int e = 0; e < V; ++e) yv[e] = Elt<T>::ld(y, i + e);
-      if (MODE == 1) {
+      if (MODE == 1 || MODE == 3) {
         float gv[V], ov[V];
         if constexpr (V == Chunk<T>::N) Chunk<T>::load(g + i, gv);
         else for (int e = 0; e < V; ++e) gv[e] = Elt<T>::ld(g, i + e);
-        if (relu_out != nullptr) {
+        if (MODE == 3) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) gv[e] = (act[i + e] & 0x80) ? gv[e] : 0.f;
+        } else if (relu_out != nullptr) {
           if constexpr (V == Chunk<T>::N) Chunk<T>::load(relu_out + i, ov);
           else for (int e = 0; e < V; ++e) ov[e] = Elt<T>::ld(relu_out, i + e);
 #pragma unroll
@@ -112,38 +118,59 @@ __global__ void parts_fold_kernel(int C, int nparts, int group, const float* __r
 
 template <typename T, int MODE>
 int launch_colsum(int64_t M, int C, const void* y, const void* g, const void* ro,
-                  const float* mean, const float* invstd, float* parts, hipStream_t st) {
+                  const float* mean, const float* invstd, float* parts, hipStream_t st,
+                  const uint8_t* act = nullptr) {
   const PartPlan pp = part_plan(M);
   constexpr int VEC = Chunk<T>::N;
   dim3 grid((unsigned)pp.nparts);
   if (C % VEC == 0 && C / VEC <= 256) {
     hipLaunchKernelGGL((colsum_kernel<T, MODE, VEC>), grid, dim3(256), 0, st, M, C, pp.rpp,
-                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts);
+                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act);
   } else if (C <= 256) {
     hipLaunchKernelGGL((colsum_kernel<T, MODE, 1>), grid, dim3(256), 0, st, M, C, pp.rpp,
-                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts);
+                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act);
   } else {
     return MMAD_EUNSUPPORTED;
   }
   return launch_status();
 }
 
-// f64 sum of the partial rows; block = 64 channels x 16 part-lanes
+// f64 sum of the partial rows; block = FC channels x 64 part-lanes (1024 threads), loads
+// unrolled 4 deep, then a fixed-shape LDS tree over the part-lanes (deterministic).
+constexpr int FC = 16;
 __device__ __forceinline__ void sum_parts(int c, int C, int nparts, const float* parts,
                                           double* sm, double& S, double& Q) {
-  const int cx = threadIdx.x & 63, py = threadIdx.x >> 6;
+  const int cx = threadIdx.x % FC, py = threadIdx.x / FC;
   double s = 0.0, q = 0.0;
-  if (c < C)
-    for (int p = py; p < nparts; p += 16) {
+  if (c < C) {
+    int p = py;
+    for (; p + 192 < nparts; p += 256) {
+      float a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = parts[((int64_t)(p + 64 * u) * 2) * C + c];
+        b[u] = parts[((int64_t)(p + 64 * u) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s += a[u]; q += b[u]; }
+    }
+    for (; p < nparts; p += 64) {
       s += parts[((int64_t)p * 2) * C + c];
       q += parts[((int64_t)p * 2 + 1) * C + c];
     }
+  }
   sm[threadIdx.x] = s;
   sm[1024 + threadIdx.x] = q;
   __syncthreads();
-  S = 0.0; Q = 0.0;
-  if (py == 0)
-    for (int k = 0; k < 16; ++k) { S += sm[k * 64 + cx]; Q += sm[1024 + k * 64 + cx]; }
+  for (int half = 32; half >= 1; half >>= 1) {
+    if (py < half) {
+      sm[threadIdx.x] += sm[threadIdx.x + half * FC];
+      sm[1024 + threadIdx.x] += sm[1024 + threadIdx.x + half * FC];
+    }
+    __syncthreads();
+  }
+  S = sm[cx];
+  Q = sm[1024 + cx];
 }
 
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(
@@ -152,14 +179,14 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
     float* running_var, float momentum, float eps, int training, float* mean_out,
     float* invstd_out, float* scale_out, float* shift_out) {
   __shared__ double sm[2048];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int c = blockIdx.x * FC + (threadIdx.x % FC);
   double S, Q;
   if (training) {
     sum_parts(c, C, nparts, parts, sm, S, Q);
   } else {
     S = Q = 0.0;
   }
-  if ((threadIdx.x >> 6) != 0 || c >= C) return;
+  if (threadIdx.x >= FC || c >= C) return;
   double mean, var;
   if (training) {
     mean = S / (double)count;
@@ -187,10 +214,10 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     const float* __restrict__ gamma, const float* __restrict__ invstd, int training,
     float* dgamma, float* dbeta, float* coef) {
   __shared__ double sm[2048];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int c = blockIdx.x * FC + (threadIdx.x % FC);
   double S, Q;
   sum_parts(c, C, nparts, parts, sm, S, Q);
-  if ((threadIdx.x >> 6) != 0 || c >= C) return;
+  if (threadIdx.x >= FC || c >= C) return;
   if (dbeta) dbeta[c] = (float)S;
   if (dgamma) dgamma[c] = (float)Q;
   const double k0 = (double)(gamma ? gamma[c] : 1.f) * invstd[c];
@@ -202,10 +229,10 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
 __global__ void sum_only_finalize_kernel(int C, int nparts, const float* __restrict__ parts,
                                          float* out) {
   __shared__ double sm[2048];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int c = blockIdx.x * FC + (threadIdx.x % FC);
   double S, Q;
   sum_parts(c, C, nparts, parts, sm, S, Q);
-  if ((threadIdx.x >> 6) != 0 || c >= C) return;
+  if (threadIdx.x >= FC || c >= C) return;
   out[c] = (float)S;
 }
 
@@ -230,7 +257,7 @@ __global__ void scale_shift_act_kernel(int64_t M, int C, const T* __restrict__ y
 #pragma unroll
     for (int e = 0; e < N; ++e) {
       const int c = c0 + e;
-      float o = v[e] * scale[c] + shift[c];
+      float o = bn_affine(v[e], scale[c], shift[c]);
       if (RES == 1) o += r[e];
       if (RES == 2) o += r[e] * rscale[c] + rshift[c];
       v[e] = relu ? fmaxf(o, 0.f) : o;
@@ -251,7 +278,7 @@ __global__ void scale_shift_act_scalar_kernel(int64_t M, int C, const T* __restr
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
-    float o = Elt<T>::ld(y, i) * scale[c] + shift[c];
+    float o = bn_affine(Elt<T>::ld(y, i), scale[c], shift[c]);
     if (res) o += rscale ? Elt<T>::ld(res, i) * rscale[c] + rshift[c] : Elt<T>::ld(res, i);
     Elt<T>::st(out, i, relu ? fmaxf(o, 0.f) : o);
   }
@@ -373,7 +400,7 @@ int mmad_colsum_ws(int dtype, int64_t m, int c, const void* y, float* parts, flo
                : launch_colsum<float, 2>(m, c, y, nullptr, nullptr, nullptr, nullptr, parts,
                                          as_stream(stream));
   if (rc) return rc;
-  hipLaunchKernelGGL(sum_only_finalize_kernel, dim3((unsigned)cdiv(c, 64)), dim3(1024), 0,
+  hipLaunchKernelGGL(sum_only_finalize_kernel, dim3((unsigned)cdiv(c, FC)), dim3(1024), 0,
                      as_stream(stream), c, part_plan(m).nparts, parts, out);
   return launch_status();
 }
@@ -385,7 +412,7 @@ int mmad_bn_finalize(int c, int64_t count, int nparts, const float* parts, const
   if (c <= 0 || count <= 0) return MMAD_EBADSHAPE;
   if (training && (!parts || nparts <= 0)) return MMAD_ENULL;
   if (!training && (!running_mean || !running_var)) return MMAD_ENULL;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(c, 64)), dim3(1024), 0,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(c, FC)), dim3(1024), 0,
                      as_stream(stream), c, count, nparts, parts, gamma, beta, running_mean,
                      running_var, momentum, eps, training, mean, invstd, scale, shift);
   return launch_status();
@@ -435,12 +462,25 @@ int mmad_bn_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* r
   return launch_colsum<float, 1>(m, c, y, g, relu_out, mean, invstd, parts, as_stream(stream));
 }
 
+int mmad_bnpool_bwd_reduce(int dtype, int64_t m, int c, const void* g, const uint8_t* argmax,
+                           const void* ymax, const float* mean, const float* invstd,
+                           float* parts, void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!g || !argmax || !ymax || !mean || !invstd || !parts) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    return launch_colsum<u16, 3>(m, c, ymax, g, nullptr, mean, invstd, parts, as_stream(stream),
+                                 argmax);
+  return launch_colsum<float, 3>(m, c, ymax, g, nullptr, mean, invstd, parts, as_stream(stream),
+                                 argmax);
+}
+
 int mmad_bn_bwd_finalize(int c, int64_t count, int nparts, const float* parts,
                          const float* gamma, const float* invstd, int training, float* dgamma,
                          float* dbeta, float* coef, void* stream) {
   if (c <= 0 || count <= 0 || nparts <= 0) return MMAD_EBADSHAPE;
   if (!parts || !invstd || !coef) return MMAD_ENULL;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)cdiv(c, 64)), dim3(1024), 0,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)cdiv(c, FC)), dim3(1024), 0,
                      as_stream(stream), c, count, nparts, parts, gamma, invstd, training,
                      dgamma, dbeta, coef);
   return launch_status();

@@ -15,6 +15,50 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define LDS_AS __attribute__((address_space(3)))
 
+// Wait until at most N vector-memory ops (incl. LDS-DMA) of this wave are outstanding and
+// all LDS ops have completed; N must be a compile-time constant (it is an immediate).
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+  static_assert(N >= 0 && N <= 12, "vmcnt immediate");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 11) asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+}
+
+// Workgroup barrier that does NOT drain in-flight LDS-DMA (unlike __syncthreads, whose
+// fence waits vmcnt(0)); pair it with wait_vm_lgkm0<N>() for the stage being consumed.
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// 16-byte LDS-DMA (global_load_lds_dwordx4) issued from inline asm: hipcc does not count it,
+// so it never inserts its own vmcnt(0) drain before a later LDS read (which it does for
+// the builtin ahead of ds_read_*_tr reads); the caller waits with wait_vm_lgkm0<N>().
+// lds_addr = wave-uniform LDS byte address of this wave's 1 KiB destination.
+__device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const LDS_AS void*)p);
+}
+
 // bf16 <-> f32 (round to nearest even; NaN stays NaN) --------------------------------
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
 __device__ __forceinline__ u16 f2bf(float f) {
@@ -64,6 +108,18 @@ template <> struct Chunk<u16> {
     *reinterpret_cast<u16x8*>(p) = c;
   }
 };
+
+// BN affine (+ReLU) of one value, shared by every kernel that applies a BN so the fused and
+// unfused paths round identically: o = fma(y, scale, shift), relu -> max(o, 0).
+__device__ __forceinline__ float bn_affine(float y, float scale, float shift) {
+  return __builtin_fmaf(y, scale, shift);
+}
+// value as stored in dtype T (bf16 rounding for u16)
+template <typename T>
+__device__ __forceinline__ float as_stored(float v) {
+  if constexpr (sizeof(T) == 2) return bf2f(f2bf(v));
+  else return v;
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -396,7 +396,9 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
 // transposing fragment reads of 8 m-rows x 16 columns (bf16: ds_read_b64_tr_b16) or
 // 2 m-rows x 16 columns (f32: ds_read_b32) hit distinct banks.
 constexpr int WBN = 128;
-constexpr int WBK = 32;
+template <typename T>
+constexpr int wbk() { return 32; }
+int wbk_of(int) { return 32; }   // 64 measured slower (fewer blocks per CU)
 
 template <typename T, int ROWB>
 __device__ __forceinline__ int wswz(int r) {
@@ -405,7 +407,7 @@ __device__ __forceinline__ int wswz(int r) {
   else return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
 }
 
-template <typename T, int BMW>
+template <typename T, int BMW, int WBK, int NST>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restrict__ src,
                                                        const T* __restrict__ dy,
                                                        float* __restrict__ ws, int m_per_split) {
@@ -428,23 +430,32 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
   fill_taps_fwd(g, tapoff);
   __syncthreads();
 
-  int arow[AIPW], aco[AIPW];
+  int aco[AIPW];
 #pragma unroll
   for (int i = 0; i < AIPW; ++i) {
-    arow[i] = (wave * AIPW + i) * ARPI + lane / ALPR;
-    aco[i] = co0 + ((lane % ALPR) ^ wswz<T, AROWB>(arow[i])) * EPC;
+    const int arow = (wave * AIPW + i) * ARPI + lane / ALPR;
+    aco[i] = co0 + ((lane % ALPR) ^ wswz<T, AROWB>(arow)) * EPC;
   }
-  // B chunks: fixed (tap, ci) per instruction, rows advance WBK voxels per stage
-  int brow[BIPW], bto[BIPW], bci[BIPW], bx[BIPW], by[BIPW], bz[BIPW], bn[BIPW];
+  // B chunks: fixed (tap, ci) per instruction, rows advance WBK voxels per stage as a
+  // mixed-radix (x, y, z, n) add with at most one carry per digit (step digits < radix)
+  const int sx = WBK % g.Wd;
+  int qq = WBK / g.Wd;
+  const int sy = qq % g.Hd;
+  qq /= g.Hd;
+  const int sz = qq % g.Dd, sn = qq / g.Dd;
+  int bci[BIPW], bx[BIPW], by[BIPW], bz[BIPW], bn[BIPW], box[BIPW], boy[BIPW], boz[BIPW];
   bool bkok[BIPW];
 #pragma unroll
   for (int i = 0; i < BIPW; ++i) {
-    brow[i] = (wave * BIPW + i) * BRPI + lane / BLPR;
-    const int k = k0 + ((lane % BLPR) ^ wswz<T, BROWB>(brow[i])) * EPC;
+    const int brow = (wave * BIPW + i) * BRPI + lane / BLPR;
+    const int k = k0 + ((lane % BLPR) ^ wswz<T, BROWB>(brow)) * EPC;
     bkok[i] = k < g.K;
     bci[i] = k & (g.Cs - 1);
-    bto[i] = tapoff[bkok[i] ? (k >> g.cs_shift) : 0];
-    int m = mbeg + brow[i];
+    const int to = tapoff[bkok[i] ? (k >> g.cs_shift) : 0];
+    box[i] = ((to >> 16) & 255) - 128 - g.pw;
+    boy[i] = ((to >> 8) & 255) - 128 - g.ph;
+    boz[i] = (to & 255) - 128 - g.pd;
+    int m = mbeg + brow;
     bx[i] = m % g.Wd; m /= g.Wd;
     by[i] = m % g.Hd; m /= g.Hd;
     bz[i] = m % g.Dd; bn[i] = m / g.Dd;
@@ -454,31 +465,33 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
     char* sbase = ring + stage * STAGE;
 #pragma unroll
     for (int i = 0; i < AIPW; ++i) {
-      const int m = mk + arow[i];
+      const int m = mk + (wave * AIPW + i) * ARPI + lane / ALPR;
       const void* p = (m < mend && aco[i] < g.Nd)
                           ? (const void*)(dy + (int64_t)m * g.Nd + aco[i])
                           : (const void*)g_zero_chunk;
-      __builtin_amdgcn_global_load_lds(p, (LDS_AS void*)(sbase + (wave * AIPW + i) * 1024), 16,
-                                       0, 0);
+      glds16_asm(p, lds_addr_of(sbase + (wave * AIPW + i) * 1024));
     }
 #pragma unroll
     for (int i = 0; i < BIPW; ++i) {
-      const int m = mk + brow[i];
-      const void* p = g_zero_chunk;
-      int z, y, x;
-      if (m < mend && bkok[i] &&
-          src_voxel(g, bz[i] * g.sd - g.pd, by[i] * g.sh - g.ph, bx[i] * g.sw - g.pw, bto[i], z,
-                    y, x)) {
-        const int64_t vox = (((int64_t)bn[i] * g.Ds + z) * g.Hs + y) * g.Ws + x;
-        p = src + (vox << g.cs_shift) + bci[i];
-      }
-      __builtin_amdgcn_global_load_lds(
-          p, (LDS_AS void*)(sbase + A_BYTES + (wave * BIPW + i) * 1024), 16, 0, 0);
-      bx[i] += WBK;
-      while (bx[i] >= g.Wd) {
-        bx[i] -= g.Wd;
-        if (++by[i] == g.Hd) { by[i] = 0; if (++bz[i] == g.Dd) { bz[i] = 0; ++bn[i]; } }
-      }
+      const int m = mk + (wave * BIPW + i) * BRPI + lane / BLPR;
+      const int z = bz[i] * g.sd + boz[i], y = by[i] * g.sh + boy[i];
+      const int x = bx[i] * g.sw + box[i];
+      const bool ok = m < mend && bkok[i] && (unsigned)z < (unsigned)g.Ds &&
+                      (unsigned)y < (unsigned)g.Hs && (unsigned)x < (unsigned)g.Ws;
+      const int vox = ((bn[i] * g.Ds + z) * g.Hs + y) * g.Ws + x;   // < 2^31 (host check)
+      const void* p = ok ? (const void*)(src + ((int64_t)vox << g.cs_shift) + bci[i])
+                         : (const void*)g_zero_chunk;
+      glds16_asm(p, lds_addr_of(sbase + A_BYTES + (wave * BIPW + i) * 1024));
+      bx[i] += sx;
+      const int cx = bx[i] >= g.Wd;
+      bx[i] -= cx ? g.Wd : 0;
+      by[i] += sy + cx;
+      const int cy = by[i] >= g.Hd;
+      by[i] -= cy ? g.Hd : 0;
+      bz[i] += sz + cy;
+      const int cz = bz[i] >= g.Dd;
+      bz[i] -= cz ? g.Dd : 0;
+      bn[i] += sn + cz;
     }
   };
 
@@ -491,14 +504,19 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int stage) {
+  // bf16: every fragment of a stage is read into registers first (the transposing LDS reads
+  // make hipcc wait for all LDS-DMA in flight, so the next stage's DMA is issued after
+  // them), then the MFMAs run while that DMA lands.
+  constexpr int KH = WBK / 32;
+  bf16x8 fa[KH][TI], fb[KH][TJ];
+  auto read_frags = [&](int stage) {
     const char* a = ring + stage * STAGE;
     const char* b = a + A_BYTES;
-    if constexpr (sizeof(T) == 2) {
-      // lane 4q+p of each 16-lane group lk reads m-rows 8lk+q (+4), columns 4p..4p+3
-      const int q = (lane & 15) >> 2, p = lane & 3;
-      const int r0 = 8 * lk + q, r1 = r0 + 4;
-      bf16x8 fa[TI], fb[TJ];
+    // lane 4q+p of each 16-lane group lk reads m-rows 8lk+q (+4), columns 4p..4p+3
+    const int q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh) {
+      const int r0 = 32 * kh + 8 * lk + q, r1 = r0 + 4;
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int col = wm * (BMW / 2) + i * 16 + 4 * p;
@@ -507,7 +525,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
         const char* hi = a + r1 * AROWB + ((ch ^ wswz<T, AROWB>(r1)) << 4) + hb;
         bf16x4 vlo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)lo);
         bf16x4 vhi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)hi);
-        fa[i] = __builtin_shufflevector(vlo, vhi, 0, 1, 2, 3, 4, 5, 6, 7);
+        fa[kh][i] = __builtin_shufflevector(vlo, vhi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
@@ -517,13 +535,26 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
         const char* hi = b + r1 * BROWB + ((ch ^ wswz<T, BROWB>(r1)) << 4) + hb;
         bf16x4 vlo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)lo);
         bf16x4 vhi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)hi);
-        fb[j] = __builtin_shufflevector(vlo, vhi, 0, 1, 2, 3, 4, 5, 6, 7);
+        fb[kh][j] = __builtin_shufflevector(vlo, vhi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
+    }
+  };
+  auto mma_frags = [&]() {
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh)
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kh][i], fb[kh][j], acc[i][j],
+                                                              0, 0, 0);
+  };
+
+  auto compute = [&](int stage) {
+    const char* a = ring + stage * STAGE;
+    const char* b = a + A_BYTES;
+    if constexpr (sizeof(T) == 2) {
+      (void)a; (void)b;
     } else {
 #pragma unroll
       for (int s = 0; s < WBK / 4; ++s) {
@@ -561,18 +592,37 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
     }
   };
 
+  // NST-deep ring, NST-1 stages of DMA in flight (asm DMA: hipcc adds no drains).  At the
+  // top of step ks: wait until only the younger stages' DMA is outstanding, barrier (all
+  // waves' DMA for ks landed; all waves done reading ks-1), refill buffer (ks-1) % NST.
   const int nk = (mend - mbeg + WBK - 1) / WBK;
+  constexpr int LPS = AIPW + BIPW;          // DMA instructions per stage per wave
+  constexpr int PD = NST - 1;
   if (nk > 0) {
-    issue(0, mbeg);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+      if (s < nk) issue(s, mbeg + s * WBK);
     for (int ks = 0; ks < nk; ++ks) {
-      const int cur = ks & 1;
-      if (ks + 1 < nk) issue(cur ^ 1, mbeg + (ks + 1) * WBK);
-      compute(cur);
-      if (ks % FLUSH == FLUSH - 1) flush();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      const int younger = min(PD - 1, nk - 1 - ks);
+      if constexpr (PD >= 3) {
+        if (younger >= 2) wait_vm_lgkm0<2 * LPS>();
+        else if (younger == 1) wait_vm_lgkm0<LPS>();
+        else wait_vm_lgkm0<0>();
+      } else if constexpr (PD == 2) {
+        if (younger >= 1) wait_vm_lgkm0<LPS>();
+        else wait_vm_lgkm0<0>();
+      } else {
+        wait_vm_lgkm0<0>();
+      }
+      raw_barrier();
+      if (ks + PD < nk) issue((ks + PD) % NST, mbeg + (ks + PD) * WBK);
+      if constexpr (sizeof(T) == 2) {
+        read_frags(ks % NST);
+        mma_frags();
+      } else {
+        compute(ks % NST);
+        if (ks % FLUSH == FLUSH - 1) flush();
+      }
     }
   }
   flush();
@@ -611,6 +661,29 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
   }
 }
 
+// Same sum, for the plain (not unfolded) layout: one block per (co, 64-channel slice);
+// slab reads run along ci (coalesced), the [ci][taps] result goes out through LDS as one
+// contiguous run of the torch tensor.
+__global__ __launch_bounds__(256) void wgrad_reduce_t_kernel(const float* __restrict__ ws,
+                                                             float* __restrict__ dw, int splits,
+                                                             int Nd, int K, int Cs, int taps) {
+  __shared__ float tile[64 * 33];
+  const int ct = min(64, Cs), groups = 256 / ct;
+  const int co = blockIdx.y, c0 = blockIdx.x * ct;
+  const int e = threadIdx.x % ct, tg = threadIdx.x / ct;
+  const int64_t total = (int64_t)Nd * K;
+  const float* base = ws + (int64_t)co * K + c0 + e;
+  for (int t = tg; t < taps; t += groups) {
+    float s = 0.f;
+    for (int sp = 0; sp < splits; ++sp) s += base[sp * total + (int64_t)t * Cs];
+    tile[e * (taps + 1) + t] = s;
+  }
+  __syncthreads();
+  float* out = dw + ((int64_t)co * Cs + c0) * taps;
+  for (int l = threadIdx.x; l < ct * taps; l += 256)
+    out[l] = tile[(l / taps) * (taps + 1) + l % taps];
+}
+
 // ---- weight packing / input unfolding -------------------------------------------------
 template <typename T>
 __global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ wp, int rows,
@@ -632,6 +705,36 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ 
       }
     }
     Elt<T>::st(wp, idx, v);
+  }
+}
+
+// Coalesced packing for unpadded rows (Kpad == K): the input is read as [B][R][Cc]
+// (contiguous along Cc) through a 64x64 LDS tile and element (b, i, j) is written to
+// b*ob + (j / jd)*oj1 + (j % jd)*oj2 + i  (contiguous along i).
+//   forward: B = Co, R = Ci, Cc = taps           -> [co][tap][ci]
+//   dgrad:   B = 1,  R = Co, Cc = Ci*taps (jd = taps) -> [ci][tap][co]
+template <typename T>
+__global__ __launch_bounds__(256) void pack_transpose_kernel(const float* __restrict__ w,
+                                                             T* __restrict__ wp, int R, int Cc,
+                                                             int64_t ob, int jd, int64_t oj1,
+                                                             int oj2) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.z;
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const float* src = w + (int64_t)b * R * Cc;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = ty; r < 64; r += 4) {
+    const int i = i0 + r, j = j0 + tx;
+    tile[r][tx] = (i < R && j < Cc) ? src[(int64_t)i * Cc + j] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = ty; c < 64; c += 4) {
+    const int j = j0 + c, i = i0 + tx;
+    if (i < R && j < Cc)
+      Elt<T>::st(wp, (int64_t)b * ob + (int64_t)(j / jd) * oj1 + (int64_t)(j % jd) * oj2 + i,
+                 tile[tx][c]);
   }
 }
 
@@ -722,7 +825,10 @@ Geom dgrad_geom(const mmad_conv_desc* d, int dtype) {
 
 bool geom_ok(const Geom& g, int dtype) {
   const int epc = dtype == MMAD_BF16 ? 8 : 4;
-  return is_pow2(g.Cs) && g.Cs % epc == 0 && (int64_t)g.M * g.Nd < (int64_t(1) << 40);
+  const int64_t src_vox = (int64_t)g.nb * g.Ds * g.Hs * g.Ws;
+  const int64_t dst_vox = (int64_t)g.nb * g.Dd * g.Hd * g.Wd;
+  return is_pow2(g.Cs) && g.Cs % epc == 0 && (int64_t)g.M * g.Nd < (int64_t(1) << 40) &&
+         src_vox < (int64_t(1) << 31) && dst_vox < (int64_t(1) << 31);   // 32-bit voxel ids
 }
 
 int bn_of(const Geom& g) { return g.Nd <= 64 ? 64 : 128; }
@@ -733,7 +839,8 @@ int igemm_bm(int64_t m, const Geom& g) {
 }
 
 struct WSplit { int bmw, splits, m_per_split; };
-WSplit wgrad_split(const Geom& g) {
+WSplit wgrad_split(const Geom& g, int dtype) {
+  const int WBK = wbk_of(dtype);
   WSplit s{};
   s.bmw = g.Nd <= 64 ? 64 : 128;
   const int64_t tiles = cdiv(g.Nd, s.bmw) * cdiv(g.K, WBN);
@@ -785,16 +892,23 @@ int run_igemm(const Geom& g, int dtype, int64_t m_max, int classes, const void* 
   return run_igemm_t<float, MODE>(g, m_max, classes, src, w, bias, dst, stats, st);
 }
 
+template <typename T, int BMW, int WBK, int NST>
+int launch_wgrad_k(const Geom& g, const WSplit& sp, const void* x, const void* dy, float* ws,
+                 hipStream_t st) {
+  const size_t lds = TAPB + NST * WBK * (BMW + WBN) * sizeof(T);
+  static const bool ok = set_lds(wgrad_kernel<T, BMW, WBK, NST>, lds);
+  if (!ok) return MMAD_EUNSUPPORTED;
+  dim3 grid((unsigned)cdiv(g.K, WBN), (unsigned)cdiv(g.Nd, BMW), (unsigned)sp.splits);
+  hipLaunchKernelGGL((wgrad_kernel<T, BMW, WBK, NST>), grid, dim3(256), lds, st, g, (const T*)x,
+                     (const T*)dy, ws, sp.m_per_split);
+  return launch_status();
+}
+
 template <typename T, int BMW>
 int launch_wgrad(const Geom& g, const WSplit& sp, const void* x, const void* dy, float* ws,
                  hipStream_t st) {
-  const size_t lds = TAPB + 2 * WBK * (BMW + WBN) * sizeof(T);
-  static const bool ok = set_lds(wgrad_kernel<T, BMW>, lds);
-  if (!ok) return MMAD_EUNSUPPORTED;
-  dim3 grid((unsigned)cdiv(g.K, WBN), (unsigned)cdiv(g.Nd, BMW), (unsigned)sp.splits);
-  hipLaunchKernelGGL((wgrad_kernel<T, BMW>), grid, dim3(256), lds, st, g, (const T*)x,
-                     (const T*)dy, ws, sp.m_per_split);
-  return launch_status();
+  // ring depth 2: deeper rings (3, 4) cost blocks per CU and measured 10-30 % slower
+  return launch_wgrad_k<T, BMW, 32, 2>(g, sp, x, dy, ws, st);
 }
 
 unsigned grid_for(int64_t total, int block = 256) {
@@ -822,6 +936,22 @@ int mmad_conv_pack_weight(const mmad_conv_desc* d, int dtype, const float* w, vo
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
   const int mode = for_dgrad ? 1 : (unfolded(d) ? 2 : 0);
   const int64_t total = (int64_t)g.Nd * g.Kpad;
+  if (mode != 2 && g.Kpad == g.K) {
+    // forward: per co, [Ci][taps] -> [taps][Ci]; dgrad: [Co][Ci*taps] -> [Ci][taps][Co]
+    const int R = mode == 0 ? d->ci : d->co;
+    const int Cc = mode == 0 ? g.taps : d->ci * g.taps;
+    const int B = mode == 0 ? d->co : 1;
+    const int64_t ob = mode == 0 ? g.Kpad : 0, oj1 = mode == 0 ? 0 : g.Kpad;
+    const int jd = g.taps, oj2 = mode == 0 ? d->ci : d->co;
+    dim3 grid((unsigned)cdiv(Cc, 64), (unsigned)cdiv(R, 64), (unsigned)B);
+    if (dtype == MMAD_BF16)
+      hipLaunchKernelGGL(pack_transpose_kernel<u16>, grid, dim3(256), 0, as_stream(stream), w,
+                         (u16*)wp, R, Cc, ob, jd, oj1, oj2);
+    else
+      hipLaunchKernelGGL(pack_transpose_kernel<float>, grid, dim3(256), 0, as_stream(stream), w,
+                         (float*)wp, R, Cc, ob, jd, oj1, oj2);
+    return launch_status();
+  }
   if (dtype == MMAD_BF16)
     hipLaunchKernelGGL(pack_weight_kernel<u16>, dim3(grid_for(total)), dim3(256), 0,
                        as_stream(stream), w, (u16*)wp, g.Nd, g.Kpad, g.K, g.Cs, g.cs_shift,
@@ -897,7 +1027,7 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
 int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype) {
   if (!desc_ok(d)) return -1;
   const Geom g = fwd_geom(d, dtype);
-  const WSplit sp = wgrad_split(g);
+  const WSplit sp = wgrad_split(g, dtype);
   const int64_t slabs = (int64_t)sp.splits * g.Nd * g.K * 4;
   const int64_t parts = (int64_t)1024 * 2 * g.Nd * 4;   // bias-gradient column sums
   return std::max(slabs, parts);
@@ -913,7 +1043,7 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
   if (!x || !dy || !dw || !workspace) return MMAD_ENULL;
   const Geom g = fwd_geom(d, dtype);
   if (!geom_ok(g, dtype) || g.Nd % (dtype == MMAD_BF16 ? 8 : 4)) return MMAD_EUNSUPPORTED;
-  const WSplit sp = wgrad_split(g);
+  const WSplit sp = wgrad_split(g, dtype);
   hipStream_t st = as_stream(stream);
   int rc;
   if (dtype == MMAD_BF16)
@@ -924,9 +1054,14 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
                       : launch_wgrad<float, 128>(g, sp, x, dy, (float*)workspace, st);
   if (rc) return rc;
   const int64_t total = (int64_t)g.Nd * g.K;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, st,
-                     (const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.cs_shift,
-                     g.taps, unfolded(d) ? d->kw : 0);
+  if (!unfolded(d) && g.taps <= 32 && sp.splits <= 8)
+    hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)cdiv(g.Cs, 64), (unsigned)g.Nd),
+                       dim3(256), 0, st, (const float*)workspace, dw, sp.splits, g.Nd, g.K,
+                       g.Cs, g.taps);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, st,
+                       (const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.cs_shift,
+                       g.taps, unfolded(d) ? d->kw : 0);
   rc = launch_status();
   if (rc) return rc;
   if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, stream);

@@ -130,6 +130,131 @@ __global__ void maxpool_bwd_kernel(PoolG g, const T* __restrict__ dy,
   }
 }
 
+// Fused MedicalNet stem tail: out = maxpool(relu(bn(y))) straight from the conv output y.
+// The BN+ReLU value is rounded to T before the comparison, so out and the argmax equal the
+// unfused scale_shift_act -> maxpool_fwd chain bit for bit.  am = window index | 0x80 when
+// the max is > 0 (ReLU passed it); ymax = the raw y at the argmax (backward x-hat).
+template <typename T, int V>
+__global__ void bnpool_fwd_kernel(PoolG g, const T* __restrict__ y,
+                                  const float* __restrict__ scale,
+                                  const float* __restrict__ shift, T* __restrict__ out,
+                                  uint8_t* __restrict__ am, T* __restrict__ ymax) {
+  const int cv = g.c / V;
+  const int64_t total = (int64_t)g.n * g.do_ * g.ho * g.wo * cv;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(t % cv) * V;
+    int64_t v = t / cv;
+    const int64_t ovox = v;
+    const int ow = (int)(v % g.wo); v /= g.wo;
+    const int oh = (int)(v % g.ho); v /= g.ho;
+    const int od = (int)(v % g.do_);
+    const int64_t nb = v / g.do_;
+    const int z0 = od * g.s - g.p, y0 = oh * g.s - g.p, x0 = ow * g.s - g.p;
+    float sc[V], sh[V], best[V], braw[V];
+    int bi[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e];
+      best[e] = -__builtin_inff(); braw[e] = 0.f; bi[e] = -1;
+    }
+    for (int kd = 0; kd < g.k; ++kd) {
+      const int z = z0 + kd;
+      if ((unsigned)z >= (unsigned)g.di) continue;
+      for (int kh = 0; kh < g.k; ++kh) {
+        const int yy = y0 + kh;
+        if ((unsigned)yy >= (unsigned)g.hi) continue;
+        for (int kw = 0; kw < g.k; ++kw) {
+          const int xx = x0 + kw;
+          if ((unsigned)xx >= (unsigned)g.wi) continue;
+          float raw[V];
+          load_v<T, V>(y + (((nb * g.di + z) * g.hi + yy) * g.wi + xx) * g.c + c0, raw);
+          const int wi = (kd * g.k + kh) * g.k + kw;
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            const float val = as_stored<T>(fmaxf(bn_affine(raw[e], sc[e], sh[e]), 0.f));
+            if (bi[e] < 0) { bi[e] = wi; braw[e] = raw[e]; }
+            if (val > best[e] || val != val) { best[e] = val; bi[e] = wi; braw[e] = raw[e]; }
+          }
+        }
+      }
+    }
+    store_v<T, V>(out + ovox * g.c + c0, best);
+    store_v<T, V>(ymax + ovox * g.c + c0, braw);
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+      am[ovox * g.c + c0 + e] = (uint8_t)(bi[e] | (best[e] > 0.f ? 0x80 : 0));
+  }
+}
+
+// Fused backward, dense pass: for every input voxel, g' = sum of the pooled gradients of the
+// windows whose argmax it is (and whose max passed the ReLU), then the BN input gradient
+// dy = coef0 * g' - coef1 - xhat * coef2 (coef from the pooled-grid reduction).
+template <typename T, int V>
+__global__ void bnpool_bwd_apply_kernel(PoolG g, const T* __restrict__ gp,
+                                        const uint8_t* __restrict__ am, const T* __restrict__ y,
+                                        const float* __restrict__ mean,
+                                        const float* __restrict__ invstd,
+                                        const float* __restrict__ coef, T* __restrict__ dy) {
+  const int cv = g.c / V;
+  const int64_t total = (int64_t)g.n * g.di * g.hi * g.wi * cv;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(t % cv) * V;
+    int64_t v = t / cv;
+    const int64_t ivox = v;
+    const int iw = (int)(v % g.wi); v /= g.wi;
+    const int ih = (int)(v % g.hi); v /= g.hi;
+    const int id = (int)(v % g.di);
+    const int64_t nb = v / g.di;
+    auto lo = [&](int ii) { int q = ii + g.p - (g.k - 1); return q <= 0 ? 0 : (q + g.s - 1) / g.s; };
+    auto hi = [&](int ii, int lim) { int q = (ii + g.p) / g.s; return q < lim - 1 ? q : lim - 1; };
+    const int d0 = lo(id), d1 = hi(id, g.do_);
+    const int h0 = lo(ih), h1 = hi(ih, g.ho);
+    const int w0 = lo(iw), w1 = hi(iw, g.wo);
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+    for (int od = d0; od <= d1; ++od)
+      for (int oh = h0; oh <= h1; ++oh)
+        for (int ow = w0; ow <= w1; ++ow) {
+          const int wi = 0x80 | (((id - (od * g.s - g.p)) * g.k + (ih - (oh * g.s - g.p))) * g.k +
+                                 (iw - (ow * g.s - g.p)));
+          const int64_t o = (((nb * g.do_ + od) * g.ho + oh) * g.wo + ow) * g.c + c0;
+          uint8_t a[V];
+          if constexpr (V == 8) {
+            const uint64_t w = *reinterpret_cast<const uint64_t*>(am + o);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] = (uint8_t)(w >> (8 * e));
+          } else if constexpr (V == 4) {
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(am + o);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a[e] = (uint8_t)(w >> (8 * e));
+          } else {
+            for (int e = 0; e < V; ++e) a[e] = am[o + e];
+          }
+          bool any = false;
+#pragma unroll
+          for (int e = 0; e < V; ++e) any |= a[e] == wi;
+          if (!any) continue;
+          float gv[V];
+          load_v<T, V>(gp + o, gv);
+#pragma unroll
+          for (int e = 0; e < V; ++e)
+            if (a[e] == wi) acc[e] += gv[e];
+        }
+    float yv[V], dv[V];
+    load_v<T, V>(y + ivox * g.c + c0, yv);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int c = c0 + e;
+      const float xh = (yv[e] - mean[c]) * invstd[c];
+      dv[e] = coef[c] * acc[e] - coef[g.c + c] - xh * coef[2 * g.c + c];
+    }
+    store_v<T, V>(dy + ivox * g.c + c0, dv);
+  }
+}
+
 // GAP: one block per (n, channel chunk of up to 256); V channels per thread,
 // 256 / (chunk / V) voxel lanes; fp32 partial sums folded through LDS.
 template <typename T, int V>
@@ -220,6 +345,36 @@ int pool_bwd(const PoolG& g, const void* dy, const uint8_t* am, void* dx, hipStr
 }
 
 template <typename T>
+int bnpool_fwd(const PoolG& g, const void* y, const float* scale, const float* shift, void* out,
+               uint8_t* am, void* ymax, hipStream_t st) {
+  constexpr int VEC = Chunk<T>::N;
+  const int64_t vox = (int64_t)g.n * g.do_ * g.ho * g.wo;
+  if (g.c % VEC == 0)
+    hipLaunchKernelGGL((bnpool_fwd_kernel<T, VEC>), dim3(grid_of(vox * g.c / VEC)), dim3(256),
+                       0, st, g, (const T*)y, scale, shift, (T*)out, am, (T*)ymax);
+  else
+    hipLaunchKernelGGL((bnpool_fwd_kernel<T, 1>), dim3(grid_of(vox * g.c)), dim3(256), 0, st, g,
+                       (const T*)y, scale, shift, (T*)out, am, (T*)ymax);
+  return launch_status();
+}
+
+template <typename T>
+int bnpool_bwd_apply(const PoolG& g, const void* gp, const uint8_t* am, const void* y,
+                     const float* mean, const float* invstd, const float* coef, void* dy,
+                     hipStream_t st) {
+  constexpr int VEC = Chunk<T>::N;
+  const int64_t vox = (int64_t)g.n * g.di * g.hi * g.wi;
+  if (g.c % VEC == 0)
+    hipLaunchKernelGGL((bnpool_bwd_apply_kernel<T, VEC>), dim3(grid_of(vox * g.c / VEC)),
+                       dim3(256), 0, st, g, (const T*)gp, am, (const T*)y, mean, invstd, coef,
+                       (T*)dy);
+  else
+    hipLaunchKernelGGL((bnpool_bwd_apply_kernel<T, 1>), dim3(grid_of(vox * g.c)), dim3(256), 0,
+                       st, g, (const T*)gp, am, (const T*)y, mean, invstd, coef, (T*)dy);
+  return launch_status();
+}
+
+template <typename T>
 int gap_fwd(int n, int64_t s, int c, const void* x, float* y, hipStream_t st) {
   constexpr int VEC = Chunk<T>::N;
   if (c % VEC == 0) {
@@ -271,6 +426,33 @@ int mmad_maxpool3d_bwd(int dtype, int n, int c, int di, int hi, int wi, int do_,
   if (!dy || !dx || !argmax) return MMAD_ENULL;
   if (dtype == MMAD_BF16) return pool_bwd<u16>(g, dy, argmax, dx, as_stream(stream));
   if (dtype == MMAD_F32) return pool_bwd<float>(g, dy, argmax, dx, as_stream(stream));
+  return MMAD_EBADDTYPE;
+}
+
+int mmad_bnpool_fwd(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho, int wo,
+                    int k, int s, int p, const void* y, const float* scale, const float* shift,
+                    void* out, uint8_t* argmax, void* ymax, void* stream) {
+  PoolG g{n, c, di, hi, wi, do_, ho, wo, k, s, p};
+  if (!pool_ok(g) || k * k * k > 127) return MMAD_EBADSHAPE;
+  if (!y || !scale || !shift || !out || !argmax || !ymax) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    return bnpool_fwd<u16>(g, y, scale, shift, out, argmax, ymax, as_stream(stream));
+  if (dtype == MMAD_F32)
+    return bnpool_fwd<float>(g, y, scale, shift, out, argmax, ymax, as_stream(stream));
+  return MMAD_EBADDTYPE;
+}
+
+int mmad_bnpool_bwd_apply(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho,
+                          int wo, int k, int s, int p, const void* g, const uint8_t* argmax,
+                          const void* y, const float* mean, const float* invstd,
+                          const float* coef, void* dy, void* stream) {
+  PoolG pg{n, c, di, hi, wi, do_, ho, wo, k, s, p};
+  if (!pool_ok(pg) || k * k * k > 127) return MMAD_EBADSHAPE;
+  if (!g || !argmax || !y || !mean || !invstd || !coef || !dy) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    return bnpool_bwd_apply<u16>(pg, g, argmax, y, mean, invstd, coef, dy, as_stream(stream));
+  if (dtype == MMAD_F32)
+    return bnpool_bwd_apply<float>(pg, g, argmax, y, mean, invstd, coef, dy, as_stream(stream));
   return MMAD_EBADDTYPE;
 }
 

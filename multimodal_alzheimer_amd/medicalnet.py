@@ -135,8 +135,11 @@ class ResNet(nn.Module):
 
     def forward_features(self, x):
         """stem + 4 stages: (N,1,D,H,W) raw volume (f64/f32) -> (N,C,D/8,H/8,W/8) NDHWC."""
-        x = _conv_bn_act(self.conv1, self.bn1, x)
-        x = self.maxpool(x)
+        # conv1 -> bn1 -> relu -> maxpool: BN, ReLU and the pool run as one pass over the
+        # conv output (volume_ops.batchnorm_relu_maxpool)
+        y, parts = self.conv1.forward_stats(x)
+        mp = self.maxpool
+        x = V.batchnorm_relu_maxpool(y, self.bn1, parts, mp.kernel_size, mp.stride, mp.padding)
         return self.layer4(self.layer3(self.layer2(self.layer1(x))))
 
     def forward(self, x):

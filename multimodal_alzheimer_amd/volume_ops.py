@@ -297,6 +297,63 @@ def batchnorm_act(y, bn, parts=None, relu=False, res=None, res_bn=None, res_part
                           (bn, relu, training, res_bn))
 
 
+class _BNReluPoolFn(torch.autograd.Function):
+    """maxpool(relu(bn(y))) in one pass; the full-resolution BN+ReLU output never exists."""
+
+    @staticmethod
+    def forward(ctx, y, parts, gamma, beta, cfg):
+        bn, training, k, s, p = cfg
+        mean, invstd, scale, shift, batch = _finalize(y, parts, bn, training)
+        n, c, di, hi, wi = y.shape
+        do, ho, wo = ((v + 2 * p - k) // s + 1 for v in (di, hi, wi))
+        out = _empty_vol(n, c, do, ho, wo, y.dtype, y.device)
+        ymax = torch.empty_like(out)
+        am = torch.empty((n, do, ho, wo, c), dtype=torch.uint8, device=y.device)
+        L.call("mmad_bnpool_fwd", L.dtype_code(y.dtype), n, c, di, hi, wi, do, ho, wo, k, s, p,
+               L.ptr(y), L.ptr(scale), L.ptr(shift), L.ptr(out), L.ptr(am), L.ptr(ymax),
+               L.stream())
+        ctx.save_for_backward(y, am, ymax, mean, invstd, gamma)
+        ctx.geo = (n, c, di, hi, wi, do, ho, wo, k, s, p)
+        ctx.batch = batch
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        y, am, ymax, mean, invstd, gamma = ctx.saved_tensors
+        n, c, di, hi, wi, do, ho, wo, k, s, p = ctx.geo
+        g = _cl(g)
+        if g.dtype != y.dtype:
+            g = cast(g, y.dtype)
+        dt = L.dtype_code(y.dtype)
+        dev = y.device
+        mp = n * do * ho * wo
+        nparts = L.load().mmad_bn_bwd_parts(mp, c)
+        parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
+        L.call("mmad_bnpool_bwd_reduce", dt, mp, c, L.ptr(g), L.ptr(am), L.ptr(ymax),
+               L.ptr(mean), L.ptr(invstd), L.ptr(parts), L.stream())
+        dgamma = torch.empty(c, dtype=torch.float32, device=dev)
+        dbeta = torch.empty_like(dgamma)
+        coef = torch.empty(3 * c, dtype=torch.float32, device=dev)
+        gam = None if gamma is None else gamma.detach()
+        L.call("mmad_bn_bwd_finalize", c, n * di * hi * wi, nparts, L.ptr(parts), L.ptr(gam),
+               L.ptr(invstd), int(ctx.batch), L.ptr(dgamma), L.ptr(dbeta), L.ptr(coef),
+               L.stream())
+        dy = torch.empty_like(y)
+        L.call("mmad_bnpool_bwd_apply", dt, n, c, di, hi, wi, do, ho, wo, k, s, p, L.ptr(g),
+               L.ptr(am), L.ptr(y), L.ptr(mean), L.ptr(invstd), L.ptr(coef), L.ptr(dy),
+               L.stream())
+        return (dy, None, dgamma if ctx.needs_input_grad[2] else None,
+                dbeta if ctx.needs_input_grad[3] else None, None)
+
+
+def batchnorm_relu_maxpool(y, bn, parts, kernel_size, stride, padding):
+    """max_pool3d(relu(bn(y)), k, s, p) fused (MedicalNet stem: bn1 -> relu -> maxpool)."""
+    _check_vol(y)
+    training = bn.training or not bn.track_running_stats
+    return _BNReluPoolFn.apply(y, parts, bn.weight, bn.bias,
+                               (bn, training, int(kernel_size), int(stride), int(padding)))
+
+
 # ------------------------------------------------------------------------------- pooling
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod

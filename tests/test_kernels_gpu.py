@@ -168,6 +168,50 @@ def test_batchnorm_act(mode, dtype):
         close(rbn.weight.grad, w2.grad, 5 * tol, "dgamma_res")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("training", [True, False])
+def test_bn_relu_maxpool_fused(dtype, training):
+    """Fused stem tail maxpool(relu(bn(y))) == the unfused batchnorm_act -> max_pool3d chain
+    (forward bit-exact incl. ties on ReLU zeros; backward to rounding), and both against
+    torch float64."""
+    n, c, d, h, w = 2, 64, 9, 10, 11
+    y0 = rnd(n, c, d, h, w, seed=70, scale=2.0)
+    if dtype == torch.bfloat16:
+        y0 = y0.to(dtype).double()
+    bn_a, bn_b, bn_r = _BN(c, 71), _BN(c, 71), _BN(c, 71)
+    for b_ in (bn_a, bn_b, bn_r):
+        b_.training = training
+    yr = y0.clone().requires_grad_(True)
+    out_r, w_r, b_r, rm_r, rv_r = _ref_bn(yr, bn_r, training)
+    pr = F.max_pool3d(torch.relu(out_r), 3, 2, 1)
+    g = rnd(*pr.shape, seed=72)
+    if dtype == torch.bfloat16:
+        g = g.to(dtype).double()
+    pr.backward(g)
+
+    ya = to_vol(y0, dtype).requires_grad_(True)
+    pa = V.max_pool3d(V.batchnorm_act(ya, bn_a, relu=True), 3, 2, 1)
+    pa.backward(to_vol(g, dtype))
+    yb = to_vol(y0, dtype).requires_grad_(True)
+    pb = V.batchnorm_relu_maxpool(yb, bn_b, None, 3, 2, 1)
+    pb.backward(to_vol(g, dtype))
+
+    assert torch.equal(pa, pb), "fused forward differs from the unfused chain"
+    tol = 2e-5 if dtype == torch.float32 else 1.5e-2
+    close(pb, pr, tol, "out")
+    close(yb.grad, ya.grad, tol, "dy fused vs unfused")
+    close(bn_b.weight.grad, bn_a.weight.grad, tol, "dgamma fused vs unfused")
+    close(bn_b.bias.grad, bn_a.bias.grad, tol, "dbeta fused vs unfused")
+    if dtype == torch.float32:
+        # (bf16: rounding the BN output before the max moves argmaxes between near-equal
+        # values, which routes gradient elsewhere -- compared against the unfused chain only)
+        close(yb.grad, yr.grad, 5 * tol, "dy")
+        close(bn_b.weight.grad, w_r.grad, 5 * tol, "dgamma")
+        close(bn_b.bias.grad, b_r.grad, 5 * tol, "dbeta")
+    close(bn_b.running_mean, rm_r, 1e-5, "running_mean")
+    close(bn_b.running_var, rv_r, 1e-5, "running_var")
+
+
 @pytest.mark.parametrize("shape,dil", [((2, 512, 4, 4, 4), 4), ((2, 256, 4, 4, 4), 2),
                                        ((2, 64, 8, 8, 8), 1)])
 def test_conv_bn_relu_chain(shape, dil):

@@ -1,0 +1,71 @@
+"""Run one conv pass of one ResNet-10 @128^3 layer (batch 8, bf16) a few times, for rocprofv3
+counter passes on a single kernel:
+
+    rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY ... -d gpurun_out/pmc_x -o run \
+        --output-format csv -- python3 tools/probe_kernel.py --layer l4c2 --op wgrad
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from multimodal_alzheimer_amd import _lib, volume_ops  # noqa: E402
+
+# name: (cin, cout, size at 128^3 input, k, stride, pad, dil)
+LAYERS = {
+    "stem": (1, 64, 128, 7, 2, 3, 1),
+    "l1c": (64, 64, 32, 3, 1, 1, 1),
+    "l2c1": (64, 128, 32, 3, 2, 1, 1),
+    "l3c2": (256, 256, 16, 3, 1, 2, 2),
+    "l4c1": (256, 512, 16, 3, 1, 4, 4),
+    "l4c2": (512, 512, 16, 3, 1, 4, 4),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layer", default="l4c2", choices=sorted(LAYERS))
+    ap.add_argument("--op", default="wgrad", choices=["fwd", "dgrad", "wgrad"])
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    ci, co, s, k, st, p, dl = LAYERS[a.layer]
+    dtype = torch.bfloat16
+    xs = (a.batch, ci, s, s, s)
+    ws = (co, ci, k, k, k)
+    d = volume_ops.conv_desc(xs, ws, (st,) * 3, (p,) * 3, (dl,) * 3)
+    dt = _lib.dtype_code(dtype)
+    lib = _lib.load()
+    w = torch.randn(ws, device="cuda") * 0.02
+    if ci == 1:
+        raw = torch.rand(xs, device="cuda")
+        x = torch.empty(lib.mmad_conv_unfolded_elems(d), dtype=dtype, device="cuda")
+        _lib.call("mmad_conv_unfold_input", d, _lib.dtype_code(raw.dtype), _lib.ptr(raw), dt,
+                  _lib.ptr(x), _lib.stream())
+    else:
+        x = torch.randn(xs, device="cuda", dtype=dtype).contiguous(
+            memory_format=torch.channels_last_3d)
+    y = torch.randn((a.batch, co, d.do_, d.ho, d.wo), device="cuda", dtype=dtype).contiguous(
+        memory_format=torch.channels_last_3d)
+    for _ in range(a.reps):
+        if a.op == "fwd":
+            wp = volume_ops.pack_weight(d, dt, w, dtype, False)
+            _lib.call("mmad_conv3d_fwd", d, dt, _lib.ptr(x), _lib.ptr(wp), None, _lib.ptr(y),
+                      None, _lib.stream())
+        elif a.op == "dgrad":
+            wp = volume_ops.pack_weight(d, dt, w, dtype, True)
+            _lib.call("mmad_conv3d_dgrad", d, dt, _lib.ptr(y), _lib.ptr(wp), _lib.ptr(x),
+                      _lib.stream())
+        else:
+            wsp = torch.empty((lib.mmad_conv3d_wgrad_workspace(d, dt) + 3) // 4, device="cuda")
+            dw = torch.empty(ws, device="cuda")
+            _lib.call("mmad_conv3d_wgrad", d, dt, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dw), None,
+                      _lib.ptr(wsp), _lib.stream())
+    torch.cuda.synchronize()
+    print("ok", a.layer, a.op, a.reps)
+
+
+if __name__ == "__main__":
+    main()
