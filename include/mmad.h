@@ -65,6 +65,21 @@ const char* mmad_strerror(int status);
 int64_t mmad_conv_packed_elems(const mmad_conv_desc* d, int dtype, int for_dgrad);
 int mmad_conv_pack_weight(const mmad_conv_desc* d, int dtype, const float* w,
                           void* w_packed, int for_dgrad, void* stream);
+/* Batched packing: one launch repacks every listed weight (a model's whole conv set per
+ * step).  mmad_conv_pack_job fills one job on the host (MMAD_EUNSUPPORTED when this
+ * geometry needs the per-call path: padded K rows or a ci == 1 conv); the job array is
+ * copied to device memory once and reused while the pointers stay valid.            */
+typedef struct mmad_pack_job {
+  const float* w;
+  void* w_packed;
+  int32_t rows, cols, batch, jdiv, ostride_j2, tiles_x, tiles_y, pad_;
+  int64_t ostride_b, ostride_j1, tile0;
+} mmad_pack_job;
+int mmad_conv_pack_job(const mmad_conv_desc* d, int dtype, int for_dgrad, const float* w,
+                       void* w_packed, int64_t tile0, mmad_pack_job* job);
+int64_t mmad_pack_job_tiles(const mmad_pack_job* job);
+int mmad_conv_pack_batch(int dtype, int njobs, const mmad_pack_job* jobs_device,
+                         int64_t total_tiles, void* stream);
 int64_t mmad_conv_unfolded_elems(const mmad_conv_desc* d);
 int mmad_conv_unfold_input(const mmad_conv_desc* d, int in_dtype, const void* x,
                            int dtype, void* x_unf, void* stream);
@@ -92,7 +107,9 @@ int mmad_bn_parts_fold(int c, int nparts, const float* parts, int group, float* 
 int mmad_bn_finalize(int c, int64_t count, int nparts, const float* parts,
                      const float* gamma, const float* beta, float* running_mean,
                      float* running_var, float momentum, float eps, int training,
-                     float* mean, float* invstd, float* scale, float* shift, void* stream);
+                     float* mean, float* invstd, float* scale, float* shift,
+                     int64_t* num_batches_tracked, void* stream);
+                     /* num_batches_tracked (nullable) += 1 with the running-stat update */
 /* out = act(y*scale + shift + R), R = res*rscale + rshift | res | 0; act = relu|id */
 int mmad_scale_shift_act(int dtype, int64_t m, int c, const void* y, const float* scale,
                          const float* shift, const void* res, const float* rscale,

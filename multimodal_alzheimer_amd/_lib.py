@@ -28,12 +28,24 @@ class ConvDesc(C.Structure):
         "sd", "sh", "sw", "pd", "ph", "pw", "dd", "dh", "dw")]
 
 
+class PackJob(C.Structure):
+    """mirror of mmad_pack_job (include/mmad.h)"""
+    _fields_ = ([("w", C.c_void_p), ("w_packed", C.c_void_p)] +
+                [(n, C.c_int32) for n in ("rows", "cols", "batch", "jdiv", "ostride_j2",
+                                          "tiles_x", "tiles_y", "pad_")] +
+                [(n, C.c_int64) for n in ("ostride_b", "ostride_j1", "tile0")])
+
+
 _P = C.POINTER(ConvDesc)
+_PJ = C.POINTER(PackJob)
 _SIGS = {
     "mmad_abi_version": (_i32, []),
     "mmad_strerror": (C.c_char_p, [_i32]),
     "mmad_conv_packed_elems": (_i64, [_P, _i32, _i32]),
     "mmad_conv_pack_weight": (_i32, [_P, _i32, _vp, _vp, _i32, _vp]),
+    "mmad_conv_pack_job": (_i32, [_P, _i32, _i32, _vp, _vp, _i64, _PJ]),
+    "mmad_pack_job_tiles": (_i64, [_PJ]),
+    "mmad_conv_pack_batch": (_i32, [_i32, _i32, _vp, _i64, _vp]),
     "mmad_conv_unfolded_elems": (_i64, [_P]),
     "mmad_conv_unfold_input": (_i32, [_P, _i32, _vp, _i32, _vp, _vp]),
     "mmad_conv3d_stats_rows": (_i64, [_P, _i32]),
@@ -45,7 +57,7 @@ _SIGS = {
     "mmad_bn_stats": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_bn_parts_fold": (_i32, [_i32, _i32, _vp, _i32, _vp, _vp]),
     "mmad_bn_finalize": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _i32,
-                                _vp, _vp, _vp, _vp, _vp]),
+                                _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_scale_shift_act": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
                                     _vp]),
     "mmad_bn_bwd_parts": (_i64, [_i64, _i32]),

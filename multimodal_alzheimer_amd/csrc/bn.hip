@@ -177,7 +177,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
     int C, int64_t count, int nparts, const float* __restrict__ parts,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
     float* running_var, float momentum, float eps, int training, float* mean_out,
-    float* invstd_out, float* scale_out, float* shift_out) {
+    float* invstd_out, float* scale_out, float* shift_out, int64_t* nbt) {
   __shared__ double sm[2048];
   const int c = blockIdx.x * FC + (threadIdx.x % FC);
   double S, Q;
@@ -193,6 +193,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
     var = Q / (double)count - mean * mean;
     if (var < 0) var = 0;
     if (running_mean != nullptr) {
+      if (nbt != nullptr && c == 0) *nbt += 1;
       const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
       running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
       running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
@@ -408,13 +409,14 @@ int mmad_colsum_ws(int dtype, int64_t m, int c, const void* y, float* parts, flo
 int mmad_bn_finalize(int c, int64_t count, int nparts, const float* parts, const float* gamma,
                      const float* beta, float* running_mean, float* running_var,
                      float momentum, float eps, int training, float* mean, float* invstd,
-                     float* scale, float* shift, void* stream) {
+                     float* scale, float* shift, int64_t* num_batches_tracked, void* stream) {
   if (c <= 0 || count <= 0) return MMAD_EBADSHAPE;
   if (training && (!parts || nparts <= 0)) return MMAD_ENULL;
   if (!training && (!running_mean || !running_var)) return MMAD_ENULL;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(c, FC)), dim3(1024), 0,
                      as_stream(stream), c, count, nparts, parts, gamma, beta, running_mean,
-                     running_var, momentum, eps, training, mean, invstd, scale, shift);
+                     running_var, momentum, eps, training, mean, invstd, scale, shift,
+                     num_batches_tracked);
   return launch_status();
 }
 

@@ -738,6 +738,45 @@ __global__ __launch_bounds__(256) void pack_transpose_kernel(const float* __rest
   }
 }
 
+// Batched form: blockIdx.x walks the concatenated tile ranges of all jobs.
+template <typename T>
+__global__ __launch_bounds__(256) void pack_batch_kernel(const mmad_pack_job* __restrict__ jobs,
+                                                         int njobs) {
+  __shared__ float tile[64][65];
+  // job lookup: last job with tile0 <= blockIdx.x (jobs sorted by tile0)
+  int lo = 0, hi = njobs - 1;
+  const int64_t bid = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].tile0 <= bid) lo = mid; else hi = mid - 1;
+  }
+  const mmad_pack_job& jb = jobs[lo];
+  int64_t t = bid - jb.tile0;
+  const int bx = (int)(t % jb.tiles_x);
+  t /= jb.tiles_x;
+  const int by = (int)(t % jb.tiles_y);
+  const int b = (int)(t / jb.tiles_y);
+  const int R = jb.rows, Cc = jb.cols, jd = jb.jdiv, oj2 = jb.ostride_j2;
+  const int i0 = by * 64, j0 = bx * 64;
+  const float* src = jb.w + (int64_t)b * R * Cc;
+  T* wp = reinterpret_cast<T*>(jb.w_packed);
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = ty; r < 64; r += 4) {
+    const int i = i0 + r, j = j0 + tx;
+    tile[r][tx] = (i < R && j < Cc) ? src[(int64_t)i * Cc + j] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = ty; c < 64; c += 4) {
+    const int j = j0 + c, i = i0 + tx;
+    if (i < R && j < Cc)
+      Elt<T>::st(wp, (int64_t)b * jb.ostride_b + (int64_t)(j / jd) * jb.ostride_j1 +
+                         (int64_t)(j % jd) * oj2 + i,
+                 tile[tx][c]);
+  }
+}
+
 template <typename TI, typename TO>
 __global__ void unfold_w_kernel(const TI* __restrict__ x, TO* __restrict__ xu, int64_t rows,
                                 int Wi, int Wo, int KW, int sw, int pw, int dw) {
@@ -960,6 +999,51 @@ int mmad_conv_pack_weight(const mmad_conv_desc* d, int dtype, const float* w, vo
     hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0,
                        as_stream(stream), w, (float*)wp, g.Nd, g.Kpad, g.K, g.Cs, g.cs_shift,
                        g.taps, mode, d->ci, d->kw);
+  return launch_status();
+}
+
+int mmad_conv_pack_job(const mmad_conv_desc* d, int dtype, int for_dgrad, const float* w,
+                       void* wp, int64_t tile0, mmad_pack_job* job) {
+  if (!desc_ok(d)) return MMAD_EBADSHAPE;
+  if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
+  if (!w || !wp || !job) return MMAD_ENULL;
+  if (unfolded(d)) return MMAD_EUNSUPPORTED;
+  const Geom g = for_dgrad ? dgrad_geom(d, dtype) : fwd_geom(d, dtype);
+  if (!geom_ok(g, dtype) || g.Kpad != g.K) return MMAD_EUNSUPPORTED;
+  const bool fw = !for_dgrad;
+  mmad_pack_job j{};
+  j.w = w;
+  j.w_packed = wp;
+  j.rows = fw ? d->ci : d->co;
+  j.cols = fw ? g.taps : d->ci * g.taps;
+  j.batch = fw ? d->co : 1;
+  j.jdiv = g.taps;
+  j.ostride_j2 = fw ? d->ci : d->co;
+  j.ostride_b = fw ? g.Kpad : 0;
+  j.ostride_j1 = fw ? 0 : g.Kpad;
+  j.tiles_x = (int)cdiv(j.cols, 64);
+  j.tiles_y = (int)cdiv(j.rows, 64);
+  j.tile0 = tile0;
+  *job = j;
+  return MMAD_OK;
+}
+
+int64_t mmad_pack_job_tiles(const mmad_pack_job* job) {
+  return job ? (int64_t)job->tiles_x * job->tiles_y * job->batch : -1;
+}
+
+int mmad_conv_pack_batch(int dtype, int njobs, const mmad_pack_job* jobs, int64_t total_tiles,
+                         void* stream) {
+  if (njobs <= 0 || total_tiles <= 0 || total_tiles > INT32_MAX) return MMAD_EBADSHAPE;
+  if (!jobs) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL(pack_batch_kernel<u16>, dim3((unsigned)total_tiles), dim3(256), 0,
+                       as_stream(stream), jobs, njobs);
+  else if (dtype == MMAD_F32)
+    hipLaunchKernelGGL(pack_batch_kernel<float>, dim3((unsigned)total_tiles), dim3(256), 0,
+                       as_stream(stream), jobs, njobs);
+  else
+    return MMAD_EBADDTYPE;
   return launch_status();
 }
 

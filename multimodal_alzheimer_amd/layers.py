@@ -38,6 +38,14 @@ class Conv3d(nn.Conv3d):
             return tuple(pads)
         return _triple(self.padding)
 
+    _prepacked = None     # (fwd, dgrad) packed weights from volume_ops.PackPlan.run
+
+    def _stride3(self):
+        return _triple(self.stride)
+
+    def _dilation3(self):
+        return _triple(self.dilation)
+
     def forward_stats(self, x):
         """(y, bn partial sums): the conv epilogue also reduces the output per channel."""
         return self._run(x, True)
@@ -48,8 +56,9 @@ class Conv3d(nn.Conv3d):
         cd = self.compute_dtype
         if x.shape[1] != 1 and x.dtype != cd:
             x = volume_ops.cast(x, cd)
+        packed, self._prepacked = self._prepacked, None     # valid for one forward only
         return volume_ops.conv3d(x, self.weight, self.bias, _triple(self.stride), self._pads(),
-                                 _triple(self.dilation), cd, want_stats)
+                                 _triple(self.dilation), cd, want_stats, packed)
 
     def forward(self, x):
         return self._run(x, False)

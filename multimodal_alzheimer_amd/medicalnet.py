@@ -137,6 +137,8 @@ class ResNet(nn.Module):
         """stem + 4 stages: (N,1,D,H,W) raw volume (f64/f32) -> (N,C,D/8,H/8,W/8) NDHWC."""
         # conv1 -> bn1 -> relu -> maxpool: BN, ReLU and the pool run as one pass over the
         # conv output (volume_ops.batchnorm_relu_maxpool)
+        if self.conv1.weight.is_cuda:
+            V.prepack(self)          # every conv weight repacked in one launch per step
         y, parts = self.conv1.forward_stats(x)
         mp = self.maxpool
         x = V.batchnorm_relu_maxpool(y, self.bn1, parts, mp.kernel_size, mp.stride, mp.padding)

@@ -78,9 +78,89 @@ def pack_weight(d, dt_code, weight, cdtype, for_dgrad):
     return wp
 
 
+def _weight_desc(weight, stride, padding, dilation):
+    """a descriptor for packing only: the packed layouts depend on the weight shape and the
+    conv's stride/padding/dilation, not on the volume extent, so any consistent extent does."""
+    co, ci, kd, kh, kw = weight.shape
+    ext = [max(16, (k - 1) * d + 1) for k, d in zip((kd, kh, kw), dilation)]
+    return conv_desc((1, ci, *ext), tuple(weight.shape), stride, padding, dilation)
+
+
+class PackPlan:
+    """Repack a set of conv weights (forward layout, and the dgrad layout when gradients
+    are on) with ONE kernel launch per step instead of one or two per conv.
+
+    ``convs``: layers.Conv3d modules sharing one compute dtype.  ``run()`` refreshes every
+    packed copy from the current fp32 master weights and hands each conv its buffers for
+    its next forward (``conv._prepacked``).  Convs the batched kernel does not cover (a
+    ci == 1 stem, padded K rows) keep packing per call."""
+
+    def __init__(self, convs, cdtype, with_dgrad):
+        lib = L.load()
+        dt = L.dtype_code(cdtype)
+        self.cdtype, self.dt = cdtype, dt
+        self.entries = []
+        jobs = []
+        tiles = 0
+        for conv in convs:
+            w = conv.weight
+            d = _weight_desc(w, conv._stride3(), conv._pads(), conv._dilation3())
+            bufs = []
+            for fd in ((0, 1) if with_dgrad else (0,)):
+                n = lib.mmad_conv_packed_elems(d, dt, fd)
+                wp = torch.empty(max(n, 0), dtype=cdtype, device=w.device)
+                job = L.PackJob()
+                rc = lib.mmad_conv_pack_job(d, dt, fd, L.ptr(w), L.ptr(wp), tiles, job)
+                if rc != 0:
+                    bufs.append(None)
+                    continue
+                tiles += lib.mmad_pack_job_tiles(job)
+                jobs.append(job)
+                bufs.append(wp)
+            if not with_dgrad:
+                bufs.append(None)
+            self.entries.append((conv, w.data_ptr(), bufs[0], bufs[1]))
+        self.njobs, self.tiles = len(jobs), tiles
+        if jobs:
+            raw = (L.PackJob * len(jobs))(*jobs)
+            host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
+            self.table = host.to(convs[0].weight.device)
+        self.with_dgrad = with_dgrad
+
+    def valid_for(self, convs, cdtype, with_dgrad):
+        return (cdtype == self.cdtype and with_dgrad == self.with_dgrad and
+                len(convs) == len(self.entries) and
+                all(c is e[0] and c.weight.data_ptr() == e[1]
+                    for c, e in zip(convs, self.entries)))
+
+    def run(self):
+        if self.njobs:
+            L.call("mmad_conv_pack_batch", self.dt, self.njobs, L.ptr(self.table), self.tiles,
+                   L.stream())
+        for conv, _, wp, wpt in self.entries:
+            conv._prepacked = (wp, wpt) if wp is not None or wpt is not None else None
+
+
+def prepack(module, convs=None):
+    """Batched weight repack for every layers.Conv3d under ``module`` (see PackPlan)."""
+    from .layers import Conv3d
+    if convs is None:
+        convs = [m for m in module.modules() if isinstance(m, Conv3d) and m.weight.is_cuda]
+    if not convs:
+        return
+    cdtype = convs[0].compute_dtype
+    convs = [c for c in convs if c.compute_dtype == cdtype]
+    with_dgrad = torch.is_grad_enabled()
+    plan = getattr(module, "_mmad_pack_plan", None)
+    if plan is None or not plan.valid_for(convs, cdtype, with_dgrad):
+        plan = PackPlan(convs, cdtype, with_dgrad)
+        module._mmad_pack_plan = plan
+    plan.run()
+
+
 class _Conv3dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, geom, cdtype, want_stats):
+    def forward(ctx, x, weight, bias, geom, cdtype, want_stats, packed=None):
         stride, padding, dilation = geom
         L.require_device(x, weight)
         if weight.dtype != torch.float32:
@@ -99,7 +179,9 @@ class _Conv3dFn(torch.autograd.Function):
         else:
             _check_vol(x, cdtype)
             src = x
-        wp = pack_weight(d, dt, weight, cdtype, False)
+        wp, wpt = packed if packed is not None else (None, None)
+        if wp is None:
+            wp = pack_weight(d, dt, weight, cdtype, False)
         y = _empty_vol(d.n, d.co, d.do_, d.ho, d.wo, cdtype, x.device)
         stats = None
         if want_stats:
@@ -116,6 +198,7 @@ class _Conv3dFn(torch.autograd.Function):
             e1.record()
             probe.append((e0, e1))
         ctx.save_for_backward(src, weight)
+        ctx.wpt = wpt                      # prepacked dgrad layout (or None: pack in bwd)
         ctx.set_materialize_grads(False)   # the stats output never gets a gradient
         ctx.desc = _desc_tuple(d)
         ctx.cdtype = cdtype
@@ -129,7 +212,7 @@ class _Conv3dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, *_):
         if gy is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         src, weight = ctx.saved_tensors
         d = L.ConvDesc(*ctx.desc)
         cdtype = ctx.cdtype
@@ -139,7 +222,7 @@ class _Conv3dFn(torch.autograd.Function):
             gy = cast(gy, cdtype)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            wpt = pack_weight(d, dt, weight, cdtype, True)
+            wpt = ctx.wpt if ctx.wpt is not None else pack_weight(d, dt, weight, cdtype, True)
             dx = _empty_vol(d.n, d.ci, d.di, d.hi, d.wi, cdtype, gy.device)
             L.call("mmad_conv3d_dgrad", d, dt, L.ptr(gy), L.ptr(wpt), L.ptr(dx), L.stream())
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
@@ -153,15 +236,16 @@ class _Conv3dFn(torch.autograd.Function):
                    L.ptr(ws), L.stream())
             if not ctx.needs_input_grad[1]:
                 dw = None
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
 def conv3d(x, weight, bias=None, stride=(1, 1, 1), padding=(0, 0, 0), dilation=(1, 1, 1),
-           cdtype=torch.float32, want_stats=False):
+           cdtype=torch.float32, want_stats=False, packed=None):
     """nn.functional.conv3d on NDHWC volumes; with want_stats also returns the BN partial
-    sums ([rows][2][Co] fp32) of the output, produced by the conv epilogue."""
+    sums ([rows][2][Co] fp32) of the output, produced by the conv epilogue.  ``packed``:
+    (forward, dgrad) packed weights refreshed this step by PackPlan.run (either None)."""
     return _Conv3dFn.apply(x, weight, bias, (tuple(stride), tuple(padding), tuple(dilation)),
-                           cdtype, want_stats)
+                           cdtype, want_stats, packed)
 
 
 # ----------------------------------------------------------------------------- batchnorm
@@ -198,16 +282,20 @@ def _finalize(y, parts, bn, training):
         if update:
             if bn.momentum is None:
                 raise L.MMADError("BatchNorm momentum=None (cumulative average) unsupported")
-            bn.num_batches_tracked.add_(1)
+        nbt = None
+        if update and getattr(bn, "num_batches_tracked", None) is not None:
+            nbt = bn.num_batches_tracked
+            if nbt.dtype != torch.int64 or nbt.device != dev:
+                raise L.MMADError("num_batches_tracked must be an int64 tensor on the device")
         L.call("mmad_bn_finalize", c, m, parts.shape[0], L.ptr(parts), L.ptr(gamma),
                L.ptr(beta), L.ptr(bn.running_mean if update else None),
                L.ptr(bn.running_var if update else None), float(bn.momentum or 0.0),
                float(bn.eps), 1, L.ptr(mean), L.ptr(invstd), L.ptr(scale), L.ptr(shift),
-               L.stream())
+               L.ptr(nbt), L.stream())
     else:
         L.call("mmad_bn_finalize", c, m, 0, None, L.ptr(gamma), L.ptr(beta),
                L.ptr(bn.running_mean), L.ptr(bn.running_var), 0.0, float(bn.eps), 0,
-               L.ptr(mean), L.ptr(invstd), L.ptr(scale), L.ptr(shift), L.stream())
+               L.ptr(mean), L.ptr(invstd), L.ptr(scale), L.ptr(shift), None, L.stream())
     return mean, invstd, scale, shift, use_batch
 
 
