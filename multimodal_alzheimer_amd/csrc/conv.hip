@@ -74,8 +74,10 @@ __device__ __forceinline__ void fill_taps_fwd(const Geom& g, int* tapoff) {
 }
 
 // ---- implicit GEMM (forward / per-parity-class dgrad) --------------------------------
-template <typename T, int BN, int MODE, int BM>
-__global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restrict__ src,
+// Block = WGM x WGN waves, tile BM voxels x BN channels, NST-deep LDS ring with NST-1 stages
+// of LDS-DMA in flight (asm DMA + counted vmcnt + raw barrier, see wgrad_kernel).
+template <typename T, int BN, int MODE, int BM, int WGM = 2, int WGN = 2, int NST = 2>
+__global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* __restrict__ src,
                                                        const T* __restrict__ wgt,
                                                        const float* __restrict__ bias,
                                                        T* __restrict__ dst,
@@ -83,9 +85,12 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
                                                        int nbn) {
   constexpr int EPC = 16 / (int)sizeof(T);
   constexpr int BK = RB / (int)sizeof(T);
-  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int NW = WGM * WGN, NT = 64 * NW;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;          // per-wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int A_BYTES = BM * RB, B_BYTES = BN * RB, STAGE = A_BYTES + B_BYTES;
-  constexpr int AI = A_BYTES / 4096, BI = B_BYTES / 4096;
+  constexpr int AI = A_BYTES / (1024 * NW), BI = B_BYTES / (1024 * NW);
+  static_assert(AI * 1024 * NW == A_BYTES && BI * 1024 * NW == B_BYTES, "tile/wave split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* tapoff = reinterpret_cast<int*>(smem);
   int* tapidx = tapoff + MAXTAPS;
@@ -170,7 +175,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
   uint64_t rmask[AI];
   int64_t rvox[AI];
   if (use_mask) {
-    for (int t = tid; t < ntap; t += 256) {
+    for (int t = tid; t < ntap; t += NT) {
       const int to = tapoff[t];
       tapdelta[t] = (((to & 255) - 128) * g.Hs + (((to >> 8) & 255) - 128)) * g.Ws +
                     (((to >> 16) & 255) - 128);
@@ -200,8 +205,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
       for (int i = 0; i < AI; ++i) {
         const void* p = g_zero_chunk;
         if (kok && ((rmask[i] >> ti) & 1)) p = src + ((rvox[i] + td) << g.cs_shift) + ci;
-        __builtin_amdgcn_global_load_lds(p, (LDS_AS void*)(sbase + (wave * AI + i) * 1024), 16,
-                                         0, 0);
+        glds16_asm(p, lds_addr_of(sbase + (wave * AI + i) * 1024));
       }
     } else {
       const int to = kok ? tapoff[ti] : 0;
@@ -213,8 +217,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
           const int64_t vox = ((rbase[i] + z) * g.Hs + y) * g.Ws + x;
           p = src + (vox << g.cs_shift) + ci;
         }
-        __builtin_amdgcn_global_load_lds(p, (LDS_AS void*)(sbase + (wave * AI + i) * 1024), 16,
-                                         0, 0);
+        glds16_asm(p, lds_addr_of(sbase + (wave * AI + i) * 1024));
       }
     }
     const int woff = MODE == FWD ? k : (kok ? (tapidx[ti] << g.cs_shift) + ci : 0);
@@ -223,12 +226,11 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
       const int co = n0 + (wave * BI + i) * 8 + lrow;
       const void* p = (co < g.Nd && kok) ? (const void*)(wgt + (int64_t)co * g.Kpad + woff)
                                          : (const void*)g_zero_chunk;
-      __builtin_amdgcn_global_load_lds(
-          p, (LDS_AS void*)(sbase + A_BYTES + (wave * BI + i) * 1024), 16, 0, 0);
+      glds16_asm(p, lds_addr_of(sbase + A_BYTES + (wave * BI + i) * 1024));
     }
   };
 
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave % WGM, wn = wave / WGM;
   const int lr = lane & 15, lk = lane >> 4;
   const int sw8 = lr & 7;                          // swizzle of every row this lane reads
   // fp32 mode sums K in two levels (fresh partial every FLUSH stages): one f32 MFMA chain
@@ -241,8 +243,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
     for (int j = 0; j < TN; ++j) acc[i][j] = part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int stage) {
-    const char* a = ring + stage * STAGE + (wm * (BM / 2) + lr) * RB;
-    const char* b = ring + stage * STAGE + A_BYTES + (wn * (BN / 2) + lr) * RB;
+    const char* a = ring + stage * STAGE + (wm * WTM + lr) * RB;
+    const char* b = ring + stage * STAGE + A_BYTES + (wn * WTN + lr) * RB;
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int s = 0; s < BK / 32; ++s) {
@@ -288,20 +290,32 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
   };
 
   const int nk = (Kc + BK - 1) / BK;
+  constexpr int LPS = AI + BI;                   // DMA instructions per stage per wave
+  constexpr int PD = NST - 1;                    // stages in flight
   if (nk > 0) {
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+      if (s < nk) issue(s, s * BK);
     for (int ks = 0; ks < nk; ++ks) {
-      const int cur = ks & 1;
-      if (ks + 1 < nk) issue(cur ^ 1, (ks + 1) * BK);
-      compute(cur);
+      const int younger = min(PD - 1, nk - 1 - ks);
+      if constexpr (PD >= 3) {
+        if (younger >= 2) wait_vm_lgkm0<2 * LPS>();
+        else if (younger == 1) wait_vm_lgkm0<LPS>();
+        else wait_vm_lgkm0<0>();
+      } else if constexpr (PD == 2) {
+        if (younger >= 1) wait_vm_lgkm0<LPS>();
+        else wait_vm_lgkm0<0>();
+      } else {
+        wait_vm_lgkm0<0>();
+      }
+      raw_barrier();
+      if (ks + PD < nk) issue((ks + PD) % NST, (ks + PD) * BK);
+      compute(ks % NST);
       if (ks % FLUSH == FLUSH - 1) flush();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
     }
   }
   flush();
+  __syncthreads();                               // ring reused by the epilogue
 
   // dst voxel of a tile row
   auto dst_row = [&](int m) -> int64_t {
@@ -325,14 +339,14 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     cs[j] = 0.f; cq[j] = 0.f;
-    const int col = wn * (BN / 2) + j * 16 + lr;
+    const int col = wn * WTN + j * 16 + lr;
     const int co = n0 + col;
     const float bv = (bias != nullptr && co < g.Nd) ? bias[co] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wm * (BM / 2) + i * 16 + lk * 4 + r;
+        const int row = wm * WTM + i * 16 + lk * 4 + r;
         const int m = m0 + row;
         const float v = acc[i][j][r] + bv;
         if (lds_out) ctile[row * (CROW / 2) + col] = f2bf(v);
@@ -347,8 +361,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
     __syncthreads();
     constexpr int CPR = BN / 8;
 #pragma unroll
-    for (int h = 0; h < BM * CPR / 256; ++h) {
-      const int q = tid + 256 * h;
+    for (int h = 0; h < BM * CPR / NT; ++h) {
+      const int q = tid + NT * h;
       const int row = q / CPR, c8 = q % CPR;
       const int m = m0 + row, co = n0 + c8 * 8;
       if (m < Mc && co < g.Nd)
@@ -358,7 +372,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
     }
   }
   if (stats != nullptr) {
-    float* red = reinterpret_cast<float*>(ring);
+    float* red = reinterpret_cast<float*>(ring + 1024 + BM * CROW);   // past the C tile
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       cs[j] += __shfl_xor(cs[j], 16, 64);
@@ -366,23 +380,28 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(Geom g, const T* __restri
       cq[j] += __shfl_xor(cq[j], 16, 64);
       cq[j] += __shfl_xor(cq[j], 32, 64);
     }
-    if (wm == 1 && lk == 0) {
+    if (wm > 0 && lk == 0) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = wn * (BN / 2) + j * 16 + lr;
-        red[col] = cs[j];
-        red[BN + col] = cq[j];
+        const int col = wn * WTN + j * 16 + lr;
+        red[(wm - 1) * 2 * BN + col] = cs[j];
+        red[(wm - 1) * 2 * BN + BN + col] = cq[j];
       }
     }
     __syncthreads();
     if (wm == 0 && lk == 0) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = wn * (BN / 2) + j * 16 + lr;
+        const int col = wn * WTN + j * 16 + lr;
         const int co = n0 + col;
+        float ss = cs[j], qs = cq[j];
+        for (int w = 1; w < WGM; ++w) {        // fixed order: deterministic
+          ss += red[(w - 1) * 2 * BN + col];
+          qs += red[(w - 1) * 2 * BN + BN + col];
+        }
         if (co < g.Nd) {
-          stats[((int64_t)mt * 2) * g.Nd + co] = cs[j] + red[col];
-          stats[((int64_t)mt * 2 + 1) * g.Nd + co] = cq[j] + red[BN + col];
+          stats[((int64_t)mt * 2) * g.Nd + co] = ss;
+          stats[((int64_t)mt * 2 + 1) * g.Nd + co] = qs;
         }
       }
     }
@@ -688,7 +707,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_t_kernel(const float* __rest
 template <typename T>
 __global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ wp, int rows,
                                    int Kpad, int K, int Cs, int cs_shift, int taps, int mode,
-                                   int Ci, int unf_kw) {
+                                   int Ci, int unf_kw, int flip) {
   const int64_t total = (int64_t)rows * Kpad;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
@@ -698,8 +717,8 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ 
       const int tap = k >> cs_shift, c = k & (Cs - 1);
       if (mode == 0) {            // forward: row = co, c = ci
         v = w[((int64_t)r * Ci + c) * taps + tap];
-      } else if (mode == 1) {     // dgrad: row = ci, c = co
-        v = w[((int64_t)c * Ci + r) * taps + tap];
+      } else if (mode == 1) {     // dgrad: row = ci, c = co (flip: taps in reverse order)
+        v = w[((int64_t)c * Ci + r) * taps + (flip ? taps - 1 - tap : tap)];
       } else {                    // unfolded Cin=1 forward: tap = kd*KH+kh, c = kw
         v = c < unf_kw ? w[((int64_t)r * taps + tap) * unf_kw + c] : 0.f;
       }
@@ -717,7 +736,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void pack_transpose_kernel(const float* __restrict__ w,
                                                              T* __restrict__ wp, int R, int Cc,
                                                              int64_t ob, int jd, int64_t oj1,
-                                                             int oj2) {
+                                                             int oj2, int flip) {
   __shared__ float tile[64][65];
   const int b = blockIdx.z;
   const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
@@ -733,7 +752,8 @@ __global__ __launch_bounds__(256) void pack_transpose_kernel(const float* __rest
   for (int c = ty; c < 64; c += 4) {
     const int j = j0 + c, i = i0 + tx;
     if (i < R && j < Cc)
-      Elt<T>::st(wp, (int64_t)b * ob + (int64_t)(j / jd) * oj1 + (int64_t)(j % jd) * oj2 + i,
+      Elt<T>::st(wp, (int64_t)b * ob + (int64_t)(j / jd) * oj1 +
+                         (int64_t)(flip ? jd - 1 - j % jd : j % jd) * oj2 + i,
                  tile[tx][c]);
   }
 }
@@ -772,7 +792,7 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const mmad_pack_job* __
     const int j = j0 + c, i = i0 + tx;
     if (i < R && j < Cc)
       Elt<T>::st(wp, (int64_t)b * jb.ostride_b + (int64_t)(j / jd) * jb.ostride_j1 +
-                         (int64_t)(j % jd) * oj2 + i,
+                         (int64_t)(jb.pad_ ? jd - 1 - j % jd : j % jd) * oj2 + i,
                  tile[tx][c]);
   }
 }
@@ -862,6 +882,24 @@ Geom dgrad_geom(const mmad_conv_desc* d, int dtype) {
   return g;
 }
 
+// A stride-1 conv's input gradient is itself a forward conv: dY (Co channels) against the
+// weights with the taps reversed, padding (k-1)*dil - pad.  It then runs on the forward
+// kernels (tap masks, large tiles) instead of the parity-class path.
+bool dgrad_as_fwd(const mmad_conv_desc* d) {
+  return d->sd == 1 && d->sh == 1 && d->sw == 1 && !unfolded(d) &&
+         (d->kd - 1) * d->dd - d->pd >= 0 && (d->kh - 1) * d->dh - d->ph >= 0 &&
+         (d->kw - 1) * d->dw - d->pw >= 0;
+}
+
+Geom dgrad_fwd_geom(const mmad_conv_desc* d, int dtype) {
+  Geom g = dgrad_geom(d, dtype);
+  g.sd = g.sh = g.sw = 1;
+  g.pd = (d->kd - 1) * d->dd - d->pd;
+  g.ph = (d->kh - 1) * d->dh - d->ph;
+  g.pw = (d->kw - 1) * d->dw - d->pw;
+  return g;
+}
+
 bool geom_ok(const Geom& g, int dtype) {
   const int epc = dtype == MMAD_BF16 ? 8 : 4;
   const int64_t src_vox = (int64_t)g.nb * g.Ds * g.Hs * g.Ws;
@@ -899,22 +937,63 @@ bool set_lds(F* kern, size_t lds) {
                                              (int)lds) == hipSuccess;
 }
 
-template <typename T, int BN, int MODE, int BMT>
+template <typename T, int BN, int MODE, int BMT, int WGM = 2, int WGN = 2, int NST = 2>
 int launch_igemm_bm(const Geom& g, int64_t m_max, int classes, const void* src, const void* w,
                     const float* bias, void* dst, float* stats, hipStream_t st) {
-  const size_t lds = TAPB + 2 * (BMT + BN) * RB;
-  static const bool ok = set_lds(igemm_kernel<T, BN, MODE, BMT>, lds);
+  const size_t ring = (size_t)NST * (BMT + BN) * RB;
+  const size_t epi = 1024 + (size_t)BMT * (BN * 2 + 16) + (size_t)(WGM - 1) * 2 * BN * 4;
+  const size_t lds = TAPB + std::max(ring, epi);
+  static const bool ok = set_lds(igemm_kernel<T, BN, MODE, BMT, WGM, WGN, NST>, lds);
   if (!ok) return MMAD_EUNSUPPORTED;
   const int nbm = (int)cdiv(m_max, BMT), nbn = (int)cdiv(g.Nd, BN);
-  hipLaunchKernelGGL((igemm_kernel<T, BN, MODE, BMT>), dim3((unsigned)(nbm * nbn),
-                     (unsigned)classes), dim3(256), lds, st, g, (const T*)src, (const T*)w,
-                     bias, (T*)dst, stats, nbm, nbn);
+  hipLaunchKernelGGL((igemm_kernel<T, BN, MODE, BMT, WGM, WGN, NST>),
+                     dim3((unsigned)(nbm * nbn), (unsigned)classes), dim3(64 * WGM * WGN), lds,
+                     st, g, (const T*)src, (const T*)w, bias, (T*)dst, stats, nbm, nbn);
   return launch_status();
+}
+
+// experiment switch for the large-tile configurations (bf16, >= 256 output channels)
+int big_cfg() {
+  static const int v = [] { const char* e = getenv("MMAD_IGEMM_BIG"); return e ? atoi(e) : 0; }();
+  return v;
+}
+int big_cfg_for(const Geom& g, int dtype, int64_t m_max, int classes) {
+  if (dtype != MMAD_BF16) return 0;
+  int cfg = big_cfg();
+  if (cfg < 0) return 0;                        // MMAD_IGEMM_BIG=-1: 128 x 128 tiles only
+  if (cfg == 0)   // default: 256 x 256 tiles (8 waves) when they give every CU a block
+    return g.Nd % 256 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 256) >= 256 ? 2 : 0;
+  if (cfg == 4) return g.Nd % 128 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 128) >= 256 ? 4 : 0;
+  return g.Nd % 256 == 0 && cdiv(m_max, 128) * classes * (g.Nd / 256) >= 256 ? cfg : 0;
+}
+// rows per M tile of a forward launch (= rows of the BN partial-sum buffer per tile)
+int fwd_tile_rows(const Geom& g, int dtype) {
+  const int cfg = big_cfg_for(g, dtype, g.M, 1);
+  if (cfg == 2 || cfg == 4) return 256;
+  if (cfg) return 128;
+  return igemm_bm(g.M, g);
 }
 
 template <typename T, int MODE>
 int run_igemm_t(const Geom& g, int64_t m_max, int classes, const void* src, const void* w,
                 const float* bias, void* dst, float* stats, hipStream_t st) {
+  if constexpr (sizeof(T) == 2 && MODE == FWD) {
+    const int cfg = big_cfg_for(g, MMAD_BF16, m_max, classes);
+    if (cfg) {
+      if (cfg == 1)   // 128 x 256 tile, 8 waves (2 x 4), 3-deep ring, 1 block per CU
+        return launch_igemm_bm<T, 256, MODE, 128, 2, 4, 3>(g, m_max, classes, src, w, bias,
+                                                          dst, stats, st);
+      if (cfg == 2)   // 256 x 256 tile, 8 waves (2 x 4) of 128 x 64, 2-deep ring
+        return launch_igemm_bm<T, 256, MODE, 256, 2, 4, 2>(g, m_max, classes, src, w, bias,
+                                                          dst, stats, st);
+      if (cfg == 3)   // 128 x 128 tile, 4 waves, 3-deep ring (1 block per CU)
+        return launch_igemm_bm<T, 128, MODE, 128, 2, 2, 3>(g, m_max, classes, src, w, bias,
+                                                          dst, stats, st);
+      if (cfg == 4)   // 256 x 128 tile, 8 waves (4 x 2), 2-deep ring
+        return launch_igemm_bm<T, 128, MODE, 256, 4, 2, 2>(g, m_max, classes, src, w, bias,
+                                                          dst, stats, st);
+    }
+  }
   const bool small = igemm_bm(m_max * classes, g) == 64;
   if (bn_of(g) == 64)
     return small ? launch_igemm_bm<T, 64, MODE, 64>(g, m_max, classes, src, w, bias, dst, stats, st)
@@ -974,6 +1053,7 @@ int mmad_conv_pack_weight(const mmad_conv_desc* d, int dtype, const float* w, vo
   const Geom g = for_dgrad ? dgrad_geom(d, dtype) : fwd_geom(d, dtype);
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
   const int mode = for_dgrad ? 1 : (unfolded(d) ? 2 : 0);
+  const int flip = for_dgrad && dgrad_as_fwd(d);
   const int64_t total = (int64_t)g.Nd * g.Kpad;
   if (mode != 2 && g.Kpad == g.K) {
     // forward: per co, [Ci][taps] -> [taps][Ci]; dgrad: [Co][Ci*taps] -> [Ci][taps][Co]
@@ -985,20 +1065,20 @@ int mmad_conv_pack_weight(const mmad_conv_desc* d, int dtype, const float* w, vo
     dim3 grid((unsigned)cdiv(Cc, 64), (unsigned)cdiv(R, 64), (unsigned)B);
     if (dtype == MMAD_BF16)
       hipLaunchKernelGGL(pack_transpose_kernel<u16>, grid, dim3(256), 0, as_stream(stream), w,
-                         (u16*)wp, R, Cc, ob, jd, oj1, oj2);
+                         (u16*)wp, R, Cc, ob, jd, oj1, oj2, flip);
     else
       hipLaunchKernelGGL(pack_transpose_kernel<float>, grid, dim3(256), 0, as_stream(stream), w,
-                         (float*)wp, R, Cc, ob, jd, oj1, oj2);
+                         (float*)wp, R, Cc, ob, jd, oj1, oj2, flip);
     return launch_status();
   }
   if (dtype == MMAD_BF16)
     hipLaunchKernelGGL(pack_weight_kernel<u16>, dim3(grid_for(total)), dim3(256), 0,
                        as_stream(stream), w, (u16*)wp, g.Nd, g.Kpad, g.K, g.Cs, g.cs_shift,
-                       g.taps, mode, d->ci, d->kw);
+                       g.taps, mode, d->ci, d->kw, flip);
   else
     hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0,
                        as_stream(stream), w, (float*)wp, g.Nd, g.Kpad, g.K, g.Cs, g.cs_shift,
-                       g.taps, mode, d->ci, d->kw);
+                       g.taps, mode, d->ci, d->kw, flip);
   return launch_status();
 }
 
@@ -1023,6 +1103,7 @@ int mmad_conv_pack_job(const mmad_conv_desc* d, int dtype, int for_dgrad, const 
   j.ostride_j1 = fw ? 0 : g.Kpad;
   j.tiles_x = (int)cdiv(j.cols, 64);
   j.tiles_y = (int)cdiv(j.rows, 64);
+  j.pad_ = for_dgrad && dgrad_as_fwd(d);       // reversed tap order (see dgrad_as_fwd)
   j.tile0 = tile0;
   *job = j;
   return MMAD_OK;
@@ -1081,7 +1162,7 @@ int mmad_conv_unfold_input(const mmad_conv_desc* d, int in_dtype, const void* x,
 int64_t mmad_conv3d_stats_rows(const mmad_conv_desc* d, int dtype) {
   if (!desc_ok(d)) return -1;
   const Geom g = fwd_geom(d, dtype);
-  return cdiv(g.M, igemm_bm(g.M, g));
+  return cdiv(g.M, fwd_tile_rows(g, dtype));
 }
 
 int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x, const void* wp,
@@ -1100,6 +1181,12 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!dy || !wpt || !dx) return MMAD_ENULL;
   if (unfolded(d)) return MMAD_EUNSUPPORTED;   // the raw input never needs a gradient
+  if (dgrad_as_fwd(d)) {
+    const Geom gf = dgrad_fwd_geom(d, dtype);
+    if (!geom_ok(gf, dtype)) return MMAD_EUNSUPPORTED;
+    return run_igemm<FWD>(gf, dtype, gf.M, 1, dy, wpt, nullptr, dx, nullptr,
+                          as_stream(stream));
+  }
   const Geom g = dgrad_geom(d, dtype);
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
   // the largest parity class (0,0,0) sizes the grid
