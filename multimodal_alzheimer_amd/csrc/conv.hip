@@ -426,24 +426,26 @@ __device__ __forceinline__ int wswz(int r) {
   else return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
 }
 
-template <typename T, int BMW, int WBK, int NST>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restrict__ src,
+template <typename T, int BMW, int WBK, int NST, int WBNT = WBN, int WGM = 2, int WGN = 2>
+__global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* __restrict__ src,
                                                        const T* __restrict__ dy,
                                                        float* __restrict__ ws, int m_per_split) {
   constexpr int EPC = 16 / (int)sizeof(T);
-  constexpr int AROWB = BMW * (int)sizeof(T), BROWB = WBN * (int)sizeof(T);
+  constexpr int NW = WGM * WGN;
+  constexpr int AROWB = BMW * (int)sizeof(T), BROWB = WBNT * (int)sizeof(T);
   constexpr int A_BYTES = WBK * AROWB, B_BYTES = WBK * BROWB, STAGE = A_BYTES + B_BYTES;
   constexpr int ARPI = 1024 / AROWB, BRPI = 1024 / BROWB;      // rows per DMA instruction
   constexpr int ALPR = AROWB / 16, BLPR = BROWB / 16;         // lanes per row
-  constexpr int AIPW = A_BYTES / 4096, BIPW = B_BYTES / 4096; // instructions per wave
-  constexpr int TI = BMW / 32, TJ = WBN / 32;
+  constexpr int AIPW = A_BYTES / (1024 * NW), BIPW = B_BYTES / (1024 * NW);   // per wave
+  static_assert(AIPW * 1024 * NW == A_BYTES && BIPW * 1024 * NW == B_BYTES, "wave split");
+  constexpr int TI = BMW / WGM / 16, TJ = WBNT / WGN / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* tapoff = reinterpret_cast<int*>(smem);
   char* ring = smem + TAPB;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int k0 = blockIdx.x * WBN, co0 = blockIdx.y * BMW;
+  const int k0 = blockIdx.x * WBNT, co0 = blockIdx.y * BMW;
   const int mbeg = blockIdx.z * m_per_split;
   const int mend = min(g.M, mbeg + m_per_split);
   fill_taps_fwd(g, tapoff);
@@ -514,7 +516,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
     }
   };
 
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave % WGM, wn = wave / WGM;
   const int lr = lane & 15, lk = lane >> 4;
   constexpr int FLUSH = 4;    // fp32: fresh partial every 4 stages (128 voxels)
   f32x4 acc[TI][TJ], part[TI][TJ];
@@ -538,7 +540,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
       const int r0 = 32 * kh + 8 * lk + q, r1 = r0 + 4;
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        const int col = wm * (BMW / 2) + i * 16 + 4 * p;
+        const int col = wm * (BMW / WGM) + i * 16 + 4 * p;
         const int ch = col >> 3, hb = (col & 7) * 2;
         const char* lo = a + r0 * AROWB + ((ch ^ wswz<T, AROWB>(r0)) << 4) + hb;
         const char* hi = a + r1 * AROWB + ((ch ^ wswz<T, AROWB>(r1)) << 4) + hb;
@@ -548,7 +550,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
-        const int col = wn * (WBN / 2) + j * 16 + 4 * p;
+        const int col = wn * (WBNT / WGN) + j * 16 + 4 * p;
         const int ch = col >> 3, hb = (col & 7) * 2;
         const char* lo = b + r0 * BROWB + ((ch ^ wswz<T, BROWB>(r0)) << 4) + hb;
         const char* hi = b + r1 * BROWB + ((ch ^ wswz<T, BROWB>(r1)) << 4) + hb;
@@ -581,13 +583,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
         float fa[TI], fb[TJ];
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
-          const int col = wm * (BMW / 2) + i * 16 + lr;
+          const int col = wm * (BMW / WGM) + i * 16 + lr;
           fa[i] = *reinterpret_cast<const float*>(
               a + row * AROWB + (((col >> 2) ^ wswz<T, AROWB>(row)) << 4) + (col & 3) * 4);
         }
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-          const int col = wn * (WBN / 2) + j * 16 + lr;
+          const int col = wn * (WBNT / WGN) + j * 16 + lr;
           fb[j] = *reinterpret_cast<const float*>(
               b + row * BROWB + (((col >> 2) ^ wswz<T, BROWB>(row)) << 4) + (col & 3) * 4);
         }
@@ -650,10 +652,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Geom g, const T* __restri
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
-      const int k = k0 + wn * (WBN / 2) + j * 16 + lr;
+      const int k = k0 + wn * (WBNT / WGN) + j * 16 + lr;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * (BMW / 2) + i * 16 + lk * 4 + r;
+        const int co = co0 + wm * (BMW / WGM) + i * 16 + lk * 4 + r;
         if (co < g.Nd && k < g.K) out[(int64_t)co * g.K + k] = acc[i][j][r];
       }
     }
@@ -916,12 +918,23 @@ int igemm_bm(int64_t m, const Geom& g) {
 }
 
 struct WSplit { int bmw, splits, m_per_split; };
+// 256 x 256 wgrad tiles (8 waves, one block per CU): measured 10-15 % SLOWER than the
+// 4-wave 128 x 128 tiles on layer3/4 (more split-K slabs, less latency hiding), so off
+// unless MMAD_WGRAD_BIG=1 (kept as the A/B switch for tuning).
+bool wgrad_big(const Geom& g, int dtype) {
+  static const int v = [] { const char* e = getenv("MMAD_WGRAD_BIG"); return e ? atoi(e) : 0; }();
+  return v && dtype == MMAD_BF16 && g.Nd % 256 == 0 && g.K >= 256 * 8;
+}
+
 WSplit wgrad_split(const Geom& g, int dtype) {
   const int WBK = wbk_of(dtype);
   WSplit s{};
-  s.bmw = g.Nd <= 64 ? 64 : 128;
-  const int64_t tiles = cdiv(g.Nd, s.bmw) * cdiv(g.K, WBN);
-  int64_t want = cdiv(1024, tiles);     // ~4 blocks per CU: 2 resident + a second wave
+  const bool big = wgrad_big(g, dtype);
+  s.bmw = big ? 256 : (g.Nd <= 64 ? 64 : 128);
+  const int wbn = big ? 256 : WBN;
+  const int64_t tiles = cdiv(g.Nd, s.bmw) * cdiv(g.K, wbn);
+  // ~4 blocks per CU for the 4-wave tiles (2 resident + a second wave), ~2 for 8-wave ones
+  int64_t want = cdiv(big ? 512 : 1024, tiles);
   const int64_t max_split = std::max<int64_t>(1, cdiv(g.M, WBK * 8));
   want = std::max<int64_t>(1, std::min(want, max_split));
   while (want > 1 && want * g.Nd * (int64_t)g.K * 4 > (int64_t(512) << 20)) --want;
@@ -1010,15 +1023,16 @@ int run_igemm(const Geom& g, int dtype, int64_t m_max, int classes, const void* 
   return run_igemm_t<float, MODE>(g, m_max, classes, src, w, bias, dst, stats, st);
 }
 
-template <typename T, int BMW, int WBK, int NST>
+template <typename T, int BMW, int WBK, int NST, int WBNT = WBN, int WGM = 2, int WGN = 2>
 int launch_wgrad_k(const Geom& g, const WSplit& sp, const void* x, const void* dy, float* ws,
-                 hipStream_t st) {
-  const size_t lds = TAPB + NST * WBK * (BMW + WBN) * sizeof(T);
-  static const bool ok = set_lds(wgrad_kernel<T, BMW, WBK, NST>, lds);
+                   hipStream_t st) {
+  const size_t lds = TAPB + NST * WBK * (BMW + WBNT) * sizeof(T);
+  static const bool ok = set_lds(wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN>, lds);
   if (!ok) return MMAD_EUNSUPPORTED;
-  dim3 grid((unsigned)cdiv(g.K, WBN), (unsigned)cdiv(g.Nd, BMW), (unsigned)sp.splits);
-  hipLaunchKernelGGL((wgrad_kernel<T, BMW, WBK, NST>), grid, dim3(256), lds, st, g, (const T*)x,
-                     (const T*)dy, ws, sp.m_per_split);
+  dim3 grid((unsigned)cdiv(g.K, WBNT), (unsigned)cdiv(g.Nd, BMW), (unsigned)sp.splits);
+  hipLaunchKernelGGL((wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN>), grid,
+                     dim3(64 * WGM * WGN), lds, st, g, (const T*)x, (const T*)dy, ws,
+                     sp.m_per_split);
   return launch_status();
 }
 
@@ -1218,7 +1232,9 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
   hipStream_t st = as_stream(stream);
   int rc;
   if (dtype == MMAD_BF16)
-    rc = sp.bmw == 64 ? launch_wgrad<u16, 64>(g, sp, x, dy, (float*)workspace, st)
+    rc = sp.bmw == 256 ? launch_wgrad_k<u16, 256, 32, 2, 256, 2, 4>(g, sp, x, dy,
+                                                                   (float*)workspace, st)
+       : sp.bmw == 64 ? launch_wgrad<u16, 64>(g, sp, x, dy, (float*)workspace, st)
                       : launch_wgrad<u16, 128>(g, sp, x, dy, (float*)workspace, st);
   else
     rc = sp.bmw == 64 ? launch_wgrad<float, 64>(g, sp, x, dy, (float*)workspace, st)
