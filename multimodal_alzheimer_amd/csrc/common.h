@@ -19,20 +19,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // all LDS ops have completed; N must be a compile-time constant (it is an immediate).
 template <int N>
 __device__ __forceinline__ void wait_vm_lgkm0() {
-  static_assert(N >= 0 && N <= 12, "vmcnt immediate");
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
-  else if constexpr (N == 11) asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+  static_assert(N >= 0 && N <= 63, "vmcnt immediate (6 bits)");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(N) : "memory");
 }
 
 // Workgroup barrier that does NOT drain in-flight LDS-DMA (unlike __syncthreads, whose
@@ -61,12 +49,13 @@ __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
 
 // bf16 <-> f32 (round to nearest even; NaN stays NaN) --------------------------------
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
-__device__ __forceinline__ u16 f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (u16)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (u16)(u >> 16);
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair (v_cvt_pk_bf16_f32, round to nearest even)
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
 }
+__device__ __forceinline__ u16 f2bf(float f) { return (u16)(pack_bf16x2(f, 0.f) & 0xffffu); }
 
 // element access by compute dtype: T = float or u16 (bf16 bits) ----------------------
 template <typename T> struct Elt;
@@ -102,10 +91,10 @@ template <> struct Chunk<u16> {
     for (int i = 0; i < 8; ++i) v[i] = bf2f(c[i]);
   }
   static __device__ __forceinline__ void store(u16* p, const float* v) {
-    u16x8 c;
+    u32x4 c;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) c[i] = f2bf(v[i]);
-    *reinterpret_cast<u16x8*>(p) = c;
+    for (int i = 0; i < 4; ++i) c[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+    *reinterpret_cast<u32x4*>(p) = c;
   }
 };
 

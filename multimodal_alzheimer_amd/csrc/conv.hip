@@ -33,6 +33,7 @@
 //  * epilogue: bias, BN partial sums (sum, sum of squares per channel) from the fp32
 //    accumulators, bf16 tile transposed through LDS into 16-byte channel-vector stores.
 #include "common.h"
+#include "stem.h"
 
 namespace {
 
@@ -979,6 +980,11 @@ int big_cfg_for(const Geom& g, int dtype, int64_t m_max, int classes) {
   if (cfg == 4) return g.Nd % 128 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 128) >= 256 ? 4 : 0;
   return g.Nd % 256 == 0 && cdiv(m_max, 128) * classes * (g.Nd / 256) >= 256 ? cfg : 0;
 }
+// MMAD_STEM=0 routes the MedicalNet stem through the generic implicit GEMM (A/B switch)
+bool stem_kernel_on() {
+  static const bool v = [] { const char* e = getenv("MMAD_STEM"); return !e || atoi(e) != 0; }();
+  return v;
+}
 // rows per M tile of a forward launch (= rows of the BN partial-sum buffer per tile)
 int fwd_tile_rows(const Geom& g, int dtype) {
   const int cfg = big_cfg_for(g, dtype, g.M, 1);
@@ -1175,6 +1181,8 @@ int mmad_conv_unfold_input(const mmad_conv_desc* d, int in_dtype, const void* x,
 
 int64_t mmad_conv3d_stats_rows(const mmad_conv_desc* d, int dtype) {
   if (!desc_ok(d)) return -1;
+  if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on())
+    return mmad_stem::fwd_stats_rows(d);
   const Geom g = fwd_geom(d, dtype);
   return cdiv(g.M, fwd_tile_rows(g, dtype));
 }
@@ -1184,6 +1192,8 @@ int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x, const voi
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!x || !wp || !y) return MMAD_ENULL;
+  if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on())
+    return mmad_stem::fwd(d, x, wp, bias, y, stats, stream);
   const Geom g = fwd_geom(d, dtype);
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
   return run_igemm<FWD>(g, dtype, g.M, 1, x, wp, bias, y, stats, as_stream(stream));

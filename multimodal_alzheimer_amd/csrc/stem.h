@@ -1,0 +1,16 @@
+// Dedicated MedicalNet stem convolution (conv1: Cin 1 -> 64, 7x7x7, stride 2, pad 3) on the
+// W-unfolded input (layout [n][di][hi][wo][8], see mmad_conv_unfold_input).  Internal to
+// libmmad_hip.so: mmad_conv3d_fwd routes a matching descriptor here.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/mmad.h"
+
+namespace mmad_stem {
+// true when the descriptor/dtype is handled by the stem kernel
+bool fwd_ok(const mmad_conv_desc* d, int dtype);
+// rows of the BN partial-sum buffer the stem kernel writes ([rows][2][64])
+int64_t fwd_stats_rows(const mmad_conv_desc* d);
+int fwd(const mmad_conv_desc* d, const void* x_unf, const void* w_packed, const float* bias,
+        void* y, float* stats, void* stream);
+}  // namespace mmad_stem

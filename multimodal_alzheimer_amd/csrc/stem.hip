@@ -1,0 +1,306 @@
+// Dedicated MedicalNet stem convolution, gfx950.
+//
+// conv1 of MedicalNet's ResNet (nn.Conv3d(1, 64, 7, stride 2, padding 3), reached from
+// pkg/models/mri_models/anat_cnn.py:29-31 and pet_resnet_cnn.py:33-35) runs on the
+// W-unfolded input U[n][z][y][xo][8] (8 = the kw taps of output column xo, see
+// mmad_conv_unfold_input), so the conv is a (7, 7, 1) stencil over 16-byte rows of U.
+//
+// The generic implicit GEMM gathers 49 x 16 B per output voxel from L2 and runs only 7
+// K-stages per tile, which leaves it latency-bound (~250 TFLOP/s).  Here a block owns two
+// output rows (y, y+1) x all 64 output columns x all 64 channels and walks the whole z
+// range: the (kd) input planes it needs sit in an LDS ring of KD + sd planes (each plane
+// = the 9 input rows those two output rows touch, 1 KiB each), so each input row is
+// fetched from memory about once per block instead of ~12 times, and the next z-step's
+// sd new planes are DMA'd (asm LDS-DMA) while the MFMAs of the current step run.  The
+// weights (64 x 448 bf16) stay in LDS for the block's lifetime.  Per z-step the epilogue
+// writes the 128 x 64 bf16 output tile as 16-byte vectors and one row of BN partial sums,
+// exactly like the implicit-GEMM epilogue, so the BN that follows is unchanged.  The MFMA
+// runs transposed (channels x voxels) so each lane stores 4 adjacent channels directly.
+#include "common.h"
+#include "stem.h"
+
+namespace {
+
+constexpr int CO = 64;            // output channels
+constexpr int YT = 2;             // output rows per block
+constexpr int XW = 64;            // output columns per row (max)
+constexpr int ROWB = XW * 16;     // one unfolded input row in LDS (1 KiB)
+constexpr int CROW = CO * 2 + 16; // C tile row (bf16, padded)
+
+__device__ const u32x4 g_zero_kb[64] = {};   // 1 KiB of zeros: DMA source for padding rows
+
+struct StemG {
+  int n, di, hi, wo, do_, ho;
+  int sd, sh, pd, ph;
+  int kpad, wrow;                 // packed weight row (elements), LDS weight row (bytes)
+  int rz, yin, nks;               // ring planes, rows per plane, K-steps of 32
+  int nyb, nzc, zsteps;           // y-pairs, z-chunks, z-steps per block
+  int ring_off, c_off, red_off;   // LDS offsets (bytes)
+};
+
+template <int KD, int KH, int SD, int SH>
+__global__ __launch_bounds__(320) void stem_fwd_kernel(StemG g, const u16* __restrict__ U,
+                                                       const u16* __restrict__ wp,
+                                                       const float* __restrict__ bias,
+                                                       u16* __restrict__ y,
+                                                       float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wimg = smem;
+  char* ring = smem + g.ring_off;
+  char* ctile = smem + g.c_off;
+  float* red = reinterpret_cast<float*>(smem + g.red_off);
+  constexpr int NTAP = KD * KH, NKS = (NTAP + 3) / 4;   // K-steps of 4 taps (32)
+  constexpr int NTHR = 320;                               // 4 compute waves + 1 loader
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware block order: neighbouring y-pairs (sharing input rows) meet in one L2
+  const int nwg = gridDim.x, bid0 = blockIdx.x;
+  const int xcd = bid0 & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid0 >> 3);
+  const int zc = bid % g.nzc;
+  const int yb = (bid / g.nzc) % g.nyb;
+  const int nb = bid / (g.nzc * g.nyb);
+  const int oz0 = zc * g.zsteps;
+  const int oz1 = min(g.do_, oz0 + g.zsteps);
+
+  // weights -> LDS once: 64 rows of kpad bf16, row stride wrow bytes (bank-spread pad)
+  {
+    const int cpr = g.kpad / 8;                   // 16-byte chunks per row
+    for (int q = tid; q < CO * cpr; q += NTHR) {
+      const int r = q / cpr, c = q % cpr;
+      *reinterpret_cast<u32x4*>(wimg + r * g.wrow + c * 16) =
+          *reinterpret_cast<const u32x4*>(wp + (int64_t)r * g.kpad + c * 8);
+    }
+  }
+
+  // Wave 4 is the loader: it alone issues the plane DMAs, so its vmcnt counts nothing but
+  // them (the compute waves' output stores would otherwise sit in the same counter and
+  // turn every counted wait into a full drain).
+  constexpr int YIN = (YT - 1) * SH + KH, RSTEP = SD * YIN;
+  const int ybase = yb * YT * SH - g.ph;
+  const bool loader = wave == 4;
+  auto load_row = [&](int zi, int slot, int t) __attribute__((always_inline)) {
+    const int yi = ybase + t;
+    const bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi &&
+                    lane < g.wo;
+    const void* p = ok ? (const void*)(U + ((((int64_t)nb * g.di + zi) * g.hi + yi) * g.wo +
+                                            lane) * 8)
+                       : (const void*)(g_zero_kb + lane);
+    glds16_asm(p, lds_addr_of(ring + (slot * YIN + t) * ROWB));
+  };
+  // the SD new planes of z-step ozn (RSTEP row DMAs)
+  auto load_step = [&](int ozn) __attribute__((always_inline)) {
+#pragma unroll
+    for (int f = 0; f < RSTEP; ++f) {
+      const int kd = KD - SD + f / YIN;
+      load_row(ozn * SD - g.pd + kd, (ozn * SD + kd) % g.rz, f % YIN);
+    }
+  };
+  if (loader) {
+    // prologue: all KD planes of the first z-step
+#pragma unroll 1
+    for (int kd = 0; kd < KD; ++kd)
+#pragma unroll 1
+      for (int t = 0; t < YIN; ++t) load_row(oz0 * SD - g.pd + kd, (oz0 * SD + kd) % g.rz, t);
+  }
+
+  const int yl = (wave >> 1) & 1, xh = wave & 1;  // compute wave: output row yl, cols xh*32..
+  const int lr = lane & 15, lk = lane >> 4;
+  // per K-step s, this lane's A tap (kd, kh) and B k offset
+  int a_kd[NKS], a_kh[NKS];
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    const int t = min(4 * s + lk, NTAP - 1);     // taps past NTAP have zero weights
+    a_kd[s] = t / KH;
+    a_kh[s] = t % KH;
+  }
+
+  // BN partial sums accumulate in registers over the block's whole z range (one partial
+  // row per block, written at the end): per-z-step reductions cost more than the MFMAs
+  float cs[4][4], cq[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { cs[j][r] = 0.f; cq[j][r] = 0.f; }
+  float bv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = bias != nullptr ? bias[j * 16 + lk * 4 + r] : 0.f;
+  const int oy = yb * YT + yl;
+  const bool yok = oy < g.ho;
+
+#pragma unroll 1
+  for (int oz = oz0; oz < oz1; ++oz) {
+    // planes of oz landed; every wave done with step oz-1 (including its C-tile reads)
+    if (loader) {
+      wait_vm_lgkm0<0>();
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    raw_barrier();
+    if (loader) {
+      if (oz + 1 < oz1) load_step(oz + 1);      // next z-step's planes land during this one
+      raw_barrier();                            // matches the compute waves' C-tile barrier
+      continue;
+    }
+    const int sbase = (oz * SD) % g.rz;
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      int slot = sbase + a_kd[s];
+      slot -= slot >= g.rz ? g.rz : 0;
+      const char* arow = ring + (slot * YIN + yl * SH + a_kh[s]) * ROWB + (xh * 32 + lr) * 16;
+      bf16x8 fa[2], fb[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(arow + i * 256);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(wimg + (j * 16 + lr) * g.wrow +
+                                                 (32 * s + 8 * lk) * 2);
+      // transposed product (channels x voxels): each lane ends with 4 consecutive output
+      // channels of one voxel
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+
+    // epilogue: 8-byte runs into the LDS C tile, then whole 16-byte lines to the output
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int x = xh * 32 + i * 16 + lr;
+      const bool ok = yok && x < g.wo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[i][j][r] + bv[j][r];
+          if (ok) {                              // (fp32 values, as the igemm epilogue)
+            cs[j][r] += v[r];
+            cq[j][r] += v[r] * v[r];
+          }
+        }
+        uint2 pk;
+        pk.x = pack_bf16x2(v[0], v[1]);
+        pk.y = pack_bf16x2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(ctile + (yl * XW + x) * CROW + (j * 16 + lk * 4) * 2) = pk;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {                // 128 rows x 8 chunks, 256 compute threads
+      const int q = tid + 256 * h;
+      const int row = q >> 3, c8 = q & 7;
+      const int ry = row >> 6, x = row & 63;
+      const int yy = yb * YT + ry;
+      if (x < g.wo && yy < g.ho)
+        *reinterpret_cast<u32x4*>(y + ((((int64_t)nb * g.do_ + oz) * g.ho + yy) * g.wo + x) * CO +
+                                  c8 * 8) =
+            *reinterpret_cast<const u32x4*>(ctile + row * CROW + c8 * 16);
+    }
+  }
+
+  // one partial row per block: sum the 16 voxel lanes, then the 4 compute waves
+  if (stats != nullptr) {
+    if (!loader) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            cs[j][r] += __shfl_xor(cs[j][r], o, 64);
+            cq[j][r] += __shfl_xor(cq[j][r], o, 64);
+          }
+          if (lr == 0) {
+            red[(wave * 2) * CO + j * 16 + lk * 4 + r] = cs[j][r];
+            red[(wave * 2 + 1) * CO + j * 16 + lk * 4 + r] = cq[j][r];
+          }
+        }
+    }
+    __syncthreads();
+    if (tid < CO) {
+      float ss = 0.f, sq = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {              // fixed order: deterministic
+        ss += red[(w * 2) * CO + tid];
+        sq += red[(w * 2 + 1) * CO + tid];
+      }
+      stats[((int64_t)bid * 2) * CO + tid] = ss;
+      stats[((int64_t)bid * 2 + 1) * CO + tid] = sq;
+    }
+  }
+}
+
+bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds) {
+  if (d->ci != 1 || d->co != CO || d->kd != 7 || d->kh != 7 || d->kw > 8) return false;
+  if (d->sd != 2 || d->sh != 2) return false;     // the instantiated form (MedicalNet)
+  if (d->dd != 1 || d->dh != 1 || d->dw != 1 || d->wo > XW || d->wo < 1) return false;
+  g = StemG{};
+  g.n = d->n; g.di = d->di; g.hi = d->hi; g.wo = d->wo; g.do_ = d->do_; g.ho = d->ho;
+  g.sd = d->sd; g.sh = d->sh; g.pd = d->pd; g.ph = d->ph;
+  const int ntap = d->kd * d->kh;
+  g.kpad = (int)cdiv(ntap * 8, 64) * 64;        // as mmad_conv_pack_weight (mode 2)
+  g.wrow = g.kpad * 2 + 16;
+  g.rz = d->kd + g.sd;                           // planes of this and the next z-step
+  g.yin = (YT - 1) * g.sh + d->kh;
+  g.nks = (int)cdiv(ntap, 4);
+  if (g.nks > 16 || g.kpad < g.nks * 32) return false;
+  g.nyb = (int)cdiv(g.ho, YT);
+  const int64_t base = (int64_t)g.n * g.nyb;
+  g.nzc = (int)std::max<int64_t>(1, std::min<int64_t>(g.do_, cdiv(256, base)));
+  g.zsteps = (int)cdiv(g.do_, g.nzc);
+  g.nzc = (int)cdiv(g.do_, g.zsteps);
+  g.ring_off = CO * g.wrow;
+  g.c_off = g.ring_off + g.rz * g.yin * ROWB;
+  g.red_off = g.c_off + YT * XW * CROW;
+  lds = (size_t)g.red_off + 4 * 2 * CO * sizeof(float);
+  blocks = (int)(base * g.nzc);
+  return lds <= 160 * 1024 && base * g.nzc < (int64_t(1) << 31);
+}
+
+}  // namespace
+
+namespace mmad_stem {
+
+bool fwd_ok(const mmad_conv_desc* d, int dtype) {
+  StemG g;
+  int blocks;
+  size_t lds;
+  return dtype == MMAD_BF16 && geom_for(d, g, blocks, lds);
+}
+
+int64_t fwd_stats_rows(const mmad_conv_desc* d) {
+  StemG g;
+  int blocks;
+  size_t lds;
+  if (!geom_for(d, g, blocks, lds)) return -1;
+  return blocks;                                 // one BN partial row per block
+}
+
+int fwd(const mmad_conv_desc* d, const void* x_unf, const void* w_packed, const float* bias,
+        void* y, float* stats, void* stream) {
+  StemG g;
+  int blocks;
+  size_t lds;
+  if (!geom_for(d, g, blocks, lds)) return MMAD_EUNSUPPORTED;
+  static const bool ok = hipFuncSetAttribute((const void*)stem_fwd_kernel<7, 7, 2, 2>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             160 * 1024) == hipSuccess;
+  if (!ok) return MMAD_EUNSUPPORTED;
+  hipLaunchKernelGGL((stem_fwd_kernel<7, 7, 2, 2>), dim3((unsigned)blocks), dim3(320), lds,
+                     as_stream(stream), g, (const u16*)x_unf, (const u16*)w_packed, bias, (u16*)y,
+                     stats);
+  return launch_status();
+}
+
+}  // namespace mmad_stem

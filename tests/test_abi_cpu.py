@@ -58,7 +58,9 @@ def test_host_side_shape_queries(lib):
     assert lib.mmad_conv3d_wgrad_workspace(d, _lib.BF16) > 0
     stem = conv_desc((8, 1, 128, 128, 128), (64, 1, 7, 7, 7), (2, 2, 2), (3, 3, 3), (1, 1, 1))
     assert lib.mmad_conv_unfolded_elems(stem) == 8 * 128 * 128 * 64 * 8
-    assert lib.mmad_conv3d_stats_rows(stem, _lib.BF16) == 8 * 64 ** 3 // 128
+    # bf16 stem runs on the dedicated stem kernel: one BN partial row per (n, y-pair) block
+    assert lib.mmad_conv3d_stats_rows(stem, _lib.BF16) == 8 * 64 // 2
+    assert lib.mmad_conv3d_stats_rows(stem, _lib.F32) == 8 * 64 ** 3 // 128
     # 49 (kd, kh) taps x 8 unfolded kw "channels" = 392, padded to a 128-byte K slice
     assert lib.mmad_conv_packed_elems(stem, _lib.BF16, 0) == 64 * 448
     bad = conv_desc((1, 64, 8, 8, 8), (64, 64, 3, 3, 3), (1, 1, 1), (1, 1, 1), (1, 1, 1))
