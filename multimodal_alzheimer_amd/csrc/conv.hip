@@ -666,12 +666,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
 // layout.  unf_kw > 0: the conv ran on a W-unfolded Cin=1 input (k = (kd,kh)*8 + j).
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
                                     int splits, int Nd, int K, int Cs, int cs_shift, int taps,
-                                    int unf_kw) {
+                                    int unf_kw, int stride) {
   const int64_t total = (int64_t)Nd * K;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += ws[sp * total + idx];
+    for (int sp = 0; sp < splits; sp += stride) s += ws[sp * total + idx];
     const int co = (int)(idx / K), k = (int)(idx % K);
     if (unf_kw > 0) {
       const int j = k & 7, tkh = k >> 3;   // tkh = kd*KH + kh
@@ -680,6 +680,22 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
       const int tap = k >> cs_shift, ci = k & (Cs - 1);
       dw[((int64_t)co * Cs + ci) * taps + tap] = s;
     }
+  }
+}
+
+// First level of a two-level slab sum (many slabs): slab[g*G] += slabs g*G+1 .. g*G+G-1,
+// in place and in fixed order; the second level sums every G-th slab.
+__global__ void slab_group_sum_kernel(float* __restrict__ ws, int splits, int64_t total, int G) {
+  const int ng = (splits + G - 1) / G;
+  const int64_t n = total * ng;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int gi = (int)(t / total);
+    const int64_t idx = t % total;
+    float s = 0.f;
+    const int s1 = min(splits, (gi + 1) * G);
+    for (int sp = gi * G; sp < s1; ++sp) s += ws[sp * total + idx];
+    ws[(int64_t)gi * G * total + idx] = s;
   }
 }
 
@@ -1223,7 +1239,9 @@ int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype) {
   if (!desc_ok(d)) return -1;
   const Geom g = fwd_geom(d, dtype);
   const WSplit sp = wgrad_split(g, dtype);
-  const int64_t slabs = (int64_t)sp.splits * g.Nd * g.K * 4;
+  int64_t slabs = (int64_t)sp.splits * g.Nd * g.K * 4;
+  if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on())
+    slabs = std::max<int64_t>(slabs, mmad_stem::wgrad_blocks(d) * g.Nd * g.K * 4);
   const int64_t parts = (int64_t)1024 * 2 * g.Nd * 4;   // bias-gradient column sums
   return std::max(slabs, parts);
 }
@@ -1238,9 +1256,26 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
   if (!x || !dy || !dw || !workspace) return MMAD_ENULL;
   const Geom g = fwd_geom(d, dtype);
   if (!geom_ok(g, dtype) || g.Nd % (dtype == MMAD_BF16 ? 8 : 4)) return MMAD_EUNSUPPORTED;
-  const WSplit sp = wgrad_split(g, dtype);
   hipStream_t st = as_stream(stream);
   int rc;
+  if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on() && g.K == 392) {
+    rc = mmad_stem::wgrad(d, x, dy, (float*)workspace, stream);
+    if (rc) return rc;
+    // (one slab per block: sum 16-slab groups in place first, so no thread walks them all)
+    const int nb = (int)mmad_stem::wgrad_blocks(d);
+    const int64_t total = (int64_t)g.Nd * g.K;
+    constexpr int G = 16;
+    hipLaunchKernelGGL(slab_group_sum_kernel, dim3(grid_for(total * cdiv(nb, G))), dim3(256), 0,
+                       st, (float*)workspace, nb, total, G);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, st,
+                       (const float*)workspace, dw, nb, g.Nd, g.K, g.Cs, g.cs_shift, g.taps,
+                       d->kw, G);
+    rc = launch_status();
+    if (rc) return rc;
+    if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, stream);
+    return MMAD_OK;
+  }
+  const WSplit sp = wgrad_split(g, dtype);
   if (dtype == MMAD_BF16)
     rc = sp.bmw == 256 ? launch_wgrad_k<u16, 256, 32, 2, 256, 2, 4>(g, sp, x, dy,
                                                                    (float*)workspace, st)
@@ -1258,7 +1293,7 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
   else
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, st,
                        (const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.cs_shift,
-                       g.taps, unfolded(d) ? d->kw : 0);
+                       g.taps, unfolded(d) ? d->kw : 0, 1);
   rc = launch_status();
   if (rc) return rc;
   if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, stream);

@@ -13,4 +13,7 @@ bool fwd_ok(const mmad_conv_desc* d, int dtype);
 int64_t fwd_stats_rows(const mmad_conv_desc* d);
 int fwd(const mmad_conv_desc* d, const void* x_unf, const void* w_packed, const float* bias,
         void* y, float* stats, void* stream);
+// weight gradient: one fp32 partial slab [64][392] per block into ws (see wgrad_blocks)
+int64_t wgrad_blocks(const mmad_conv_desc* d);
+int wgrad(const mmad_conv_desc* d, const void* x_unf, const void* dy, float* ws, void* stream);
 }  // namespace mmad_stem

@@ -241,6 +241,156 @@ __global__ __launch_bounds__(320) void stem_fwd_kernel(StemG g, const u16* __res
   }
 }
 
+// ---- stem weight gradient ----------------------------------------------------------------
+// dW[co][k] = sum over output voxels m of dY[m][co] * U(m, k), k = (kd*7 + kh)*8 + kw.
+// Same block walk as the forward (n, y-pair, z range; the U planes in an LDS ring), plus
+// the block's 128 x 64 dY tile per z-step DMA'd into a 2-deep LDS ring (rows XOR-swizzled
+// for the transposing reads).  8 waves; each keeps a 32 (co) x 112 (k) slice of dW in
+// registers for the whole z range and issues 1/8 of the next step's DMAs (these waves
+// store nothing inside the loop, so a plain vmcnt(0) waits only for DMA).  The only output
+// is one fp32 partial slab per block, summed by wgrad_reduce_kernel.
+constexpr int WK = 392;            // 49 taps x 8 (unfolded kw)
+constexpr int WKW = 112;           // k columns per compute wave (7 MFMA tiles)
+
+__device__ __forceinline__ int dswz(int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); }
+
+template <int KD, int KH, int SD, int SH>
+__global__ __launch_bounds__(512) void stem_wgrad_kernel(StemG g, const u16* __restrict__ U,
+                                                         const u16* __restrict__ dy,
+                                                         float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int YIN = (YT - 1) * SH + KH, RSTEP = SD * YIN;
+  constexpr int DYB = YT * XW * CO * 2;            // one dY tile: 128 rows x 128 B
+  char* ring = smem;                               // U planes
+  char* dyr = smem + g.ring_off;                   // 2 dY tiles (ring_off reused as offset)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwg = gridDim.x, bid0 = blockIdx.x;
+  const int xcd = bid0 & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid0 >> 3);
+  const int zc = bid % g.nzc;
+  const int yb = (bid / g.nzc) % g.nyb;
+  const int nb = bid / (g.nzc * g.nyb);
+  const int oz0 = zc * g.zsteps;
+  const int oz1 = min(g.do_, oz0 + g.zsteps);
+  const int ybase = yb * YT * SH - g.ph;
+
+  auto load_row = [&](int zi, int slot, int t) __attribute__((always_inline)) {
+    const int yi = ybase + t;
+    const bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi &&
+                    lane < g.wo;
+    const void* p = ok ? (const void*)(U + ((((int64_t)nb * g.di + zi) * g.hi + yi) * g.wo +
+                                            lane) * 8)
+                       : (const void*)(g_zero_kb + lane);
+    glds16_asm(p, lds_addr_of(ring + (slot * YIN + t) * ROWB));
+  };
+  // dY tile of z-step oz: 128 rows (voxel m = yl*64 + x) of 64 channels; one DMA
+  // instruction = 8 rows; lane chunk swizzled so the transposing reads are conflict-free
+  auto load_dy = [&](int oz, int buf, int q) __attribute__((always_inline)) {
+    {
+      const int row = q * 8 + (lane >> 3);
+      const int ry = row >> 6, x = row & 63, yy = yb * YT + ry;
+      const int ch = (lane & 7) ^ dswz(row);
+      const bool ok = x < g.wo && yy < g.ho;
+      const void* p = ok ? (const void*)(dy + ((((int64_t)nb * g.do_ + oz) * g.ho + yy) * g.wo +
+                                              x) * CO + ch * 8)
+                         : (const void*)(g_zero_kb + lane);
+      glds16_asm(p, lds_addr_of(dyr + buf * DYB + q * 1024));
+    }
+  };
+  // the new planes + dY tile of z-step ozn: RSTEP + 16 DMAs spread over the 8 waves
+  auto load_step = [&](int ozn) __attribute__((always_inline)) {
+#pragma unroll 1
+    for (int f = wave; f < RSTEP + 16; f += 8) {
+      if (f < RSTEP) {
+        const int kd = KD - SD + f / YIN;
+        load_row(ozn * SD - g.pd + kd, (ozn * SD + kd) % g.rz, f % YIN);
+      } else {
+        load_dy(ozn, ozn & 1, f - RSTEP);
+      }
+    }
+  };
+  if (oz0 < oz1) {
+#pragma unroll 1
+    for (int f = wave; f < (KD - SD) * YIN; f += 8) {
+      const int kd = f / YIN;
+      load_row(oz0 * SD - g.pd + kd, (oz0 * SD + kd) % g.rz, f % YIN);
+    }
+    load_step(oz0);
+  }
+
+  // compute wave w: channels [32*(w&1), +32), k columns [112*(w>>1), +112) = 14 taps
+  const int q = (lane & 15) >> 2, p = lane & 3, lk = lane >> 4;
+  const int wc = wave & 1, wk = wave >> 1;
+  f32x4 acc[2][7];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // this lane's B columns: k-tile j covers taps 2*(7w + j) + (p >> 1), kw 4*(p & 1)..+3
+  // packed per k-tile: plane kd in bits 20+, byte offset (kh row + kw half) below
+  int b_off[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int t = min(2 * (7 * wk + j) + (p >> 1), KD * KH - 1);
+    b_off[j] = ((t / KH) << 20) | ((t % KH) * ROWB + (p & 1) * 8);
+  }
+
+#pragma unroll 1
+  for (int oz = oz0; oz < oz1; ++oz) {
+    wait_vm_lgkm0<0>();                            // this wave's DMAs for oz landed
+    raw_barrier();                                 // ... and everyone's; step oz-1 done
+    if (oz + 1 < oz1) load_step(oz + 1);          // lands while the MFMAs of oz run
+    const int sbase = (oz * SD) % g.rz;
+    const char* dyt = dyr + (oz & 1) * DYB;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {               // 32 voxels per K-step
+      const int yl = ks >> 1;
+      const int r0 = 32 * ks + 8 * lk + q, r1 = r0 + 4;
+      bf16x8 fa[2], fb[7];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {                // dY^T: co tile i of this wave's half
+        const int col = wc * 32 + i * 16 + 4 * p;
+        const int ch = col >> 3, cb = (col & 7) * 2;
+        const char* lo = dyt + r0 * 128 + ((ch ^ dswz(r0)) << 4) + cb;
+        const char* hi = dyt + r1 * 128 + ((ch ^ dswz(r1)) << 4) + cb;
+        bf16x4 vlo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)lo);
+        bf16x4 vhi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)hi);
+        fa[i] = __builtin_shufflevector(vlo, vhi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+      const int x0 = (r0 & 63), x1 = (r1 & 63);
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {                // U: k tile j
+        int slot = sbase + (b_off[j] >> 20);
+        slot -= slot >= g.rz ? g.rz : 0;
+        const char* rowp = ring + (slot * YIN + yl * SH) * ROWB + (b_off[j] & 0xfffff);
+        bf16x4 vlo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)(rowp + x0 * 16));
+        bf16x4 vhi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)(rowp + x1 * 16));
+        fb[j] = __builtin_shufflevector(vlo, vhi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 7; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // this block's partial slab: ws[bid][co][k], k < 392
+  float* out = ws + (int64_t)bid * CO * WK;
+  const int lr = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int k = wk * WKW + j * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = wc * 32 + i * 16 + lk * 4 + r;
+        if (k < WK) out[(int64_t)co * WK + k] = acc[i][j][r];
+      }
+    }
+}
+
 bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds) {
   if (d->ci != 1 || d->co != CO || d->kd != 7 || d->kh != 7 || d->kw > 8) return false;
   if (d->sd != 2 || d->sh != 2) return false;     // the instantiated form (MedicalNet)
@@ -285,6 +435,31 @@ int64_t fwd_stats_rows(const mmad_conv_desc* d) {
   size_t lds;
   if (!geom_for(d, g, blocks, lds)) return -1;
   return blocks;                                 // one BN partial row per block
+}
+
+int64_t wgrad_blocks(const mmad_conv_desc* d) {
+  StemG g;
+  int blocks;
+  size_t lds;
+  if (!geom_for(d, g, blocks, lds)) return -1;
+  return blocks;
+}
+
+int wgrad(const mmad_conv_desc* d, const void* x_unf, const void* dy, float* ws, void* stream) {
+  StemG g;
+  int blocks;
+  size_t lds;
+  if (!geom_for(d, g, blocks, lds)) return MMAD_EUNSUPPORTED;
+  // LDS: U plane ring, then two dY tiles
+  g.ring_off = g.rz * g.yin * ROWB;
+  const size_t wl = (size_t)g.ring_off + 2 * YT * XW * CO * 2;
+  static const bool ok = hipFuncSetAttribute((const void*)stem_wgrad_kernel<7, 7, 2, 2>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             160 * 1024) == hipSuccess;
+  if (!ok || wl > 160 * 1024) return MMAD_EUNSUPPORTED;
+  hipLaunchKernelGGL((stem_wgrad_kernel<7, 7, 2, 2>), dim3((unsigned)blocks), dim3(512), wl,
+                     as_stream(stream), g, (const u16*)x_unf, (const u16*)dy, ws);
+  return launch_status();
 }
 
 int fwd(const mmad_conv_desc* d, const void* x_unf, const void* w_packed, const float* bias,
