@@ -1,9 +1,10 @@
 """Summaries of rocprofv3 csv output, written into profiles/.
 
     python tools/prof_summary.py stats    <dir> [top]      kernel_stats table
-    python tools/prof_summary.py dominant <dir> <grid_x>   per-dispatch durations of the
-                                                           forward igemm launches with that
-                                                           grid (one line per step position)
+    python tools/prof_summary.py dominant <dir> <grid_x> [name]  per-dispatch durations of
+                                                           the forward igemm launches with
+                                                           that grid and kernel-name prefix
+                                                           (one line per step position)
     python tools/prof_summary.py traffic  <fetch_dir> <write_dir>   HBM bytes per launch of
                                                            the probe kernel (json)
 
@@ -34,20 +35,21 @@ def stats(d, top=30):
     return "\n".join(out)
 
 
-def dominant(d, grid_x):
-    """Forward igemm dispatches (MODE 0) in launch order; those with the given grid are
-    grouped by their position inside a step so the layer each one belongs to is visible."""
+def dominant(d, grid_x, name="igemm_kernel<unsigned short, 256, 0, 256"):
+    """Forward igemm dispatches (MODE 0) in launch order; those with the given grid and
+    kernel-name prefix are grouped by their position inside a step so the layer each one
+    belongs to is visible."""
     rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
     fwd = [r for r in rows if "igemm_kernel" in r["Kernel_Name"]
            and r["Kernel_Name"].split("<")[1].split(",")[2].strip() == "0"]
     fwd.sort(key=lambda r: int(r["Start_Timestamp"]))
-    sel = [r for r in fwd if int(r["Grid_Size_X"]) == grid_x]
+    sel = [r for r in fwd if int(r["Grid_Size_X"]) == grid_x and name in r["Kernel_Name"]]
     out = [f"{len(fwd)} forward igemm dispatches, {len(sel)} with grid_x={grid_x}"]
     # consecutive matching dispatches inside one step form a fixed-length group
     groups = collections.defaultdict(list)
     per = None
-    for n in (3, 2, 1):
-        if len(sel) % n == 0:
+    for n in (4, 3, 2, 1):
+        if len(sel) % n == 0 and len(sel) // n in (13, 10, 20, 25):   # steps+warmup
             per = n
             break
     for i, r in enumerate(sel):
@@ -87,6 +89,6 @@ if __name__ == "__main__":
     if mode == "stats":
         print(stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 30))
     elif mode == "dominant":
-        print(dominant(sys.argv[2], int(sys.argv[3])))
+        print(dominant(sys.argv[2], int(sys.argv[3]), *sys.argv[4:5]))
     elif mode == "traffic":
         print(json.dumps(traffic(sys.argv[2], sys.argv[3]), indent=1))
