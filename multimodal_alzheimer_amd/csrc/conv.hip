@@ -683,6 +683,35 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
   }
 }
 
+// Same sum for many slabs: 4 groups of 64 lanes take every 4th slab of 64 consecutive
+// elements (independent load streams instead of one serial chain of `splits` loads per
+// thread -- 128 slabs of a 1x1x1 conv took 32 us as a chain), combined in fixed order.
+__global__ __launch_bounds__(256) void wgrad_reduce_wide_kernel(
+    const float* __restrict__ ws, float* __restrict__ dw, int splits, int Nd, int K, int Cs,
+    int cs_shift, int taps, int unf_kw, int stride) {
+  __shared__ float red[4][64];
+  const int64_t total = (int64_t)Nd * K;
+  const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t idx = (int64_t)blockIdx.x * 64 + e;
+  float s = 0.f;
+  if (idx < total) {
+#pragma unroll 4
+    for (int sp = grp * stride; sp < splits; sp += 4 * stride) s += ws[sp * total + idx];
+  }
+  red[grp][e] = s;
+  __syncthreads();
+  if (grp != 0 || idx >= total) return;
+  s = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+  const int co = (int)(idx / K), k = (int)(idx % K);
+  if (unf_kw > 0) {
+    const int j = k & 7, tkh = k >> 3;
+    if (j < unf_kw) dw[((int64_t)co * taps + tkh) * unf_kw + j] = s;
+  } else {
+    const int tap = k >> cs_shift, ci = k & (Cs - 1);
+    dw[((int64_t)co * Cs + ci) * taps + tap] = s;
+  }
+}
+
 // First level of a two-level slab sum (many slabs): slab[g*G] += slabs g*G+1 .. g*G+G-1,
 // in place and in fixed order; the second level sums every G-th slab.
 __global__ void slab_group_sum_kernel(float* __restrict__ ws, int splits, int64_t total, int G) {
@@ -938,9 +967,9 @@ struct WSplit { int bmw, splits, m_per_split; };
 // 256 x 256 wgrad tiles (8 waves, one block per CU): measured 10-15 % SLOWER than the
 // 4-wave 128 x 128 tiles on layer3/4 (more split-K slabs, less latency hiding), so off
 // unless MMAD_WGRAD_BIG=1 (kept as the A/B switch for tuning).
-bool wgrad_big(const Geom& g, int dtype) {
+int wgrad_big(const Geom& g, int dtype) {
   static const int v = [] { const char* e = getenv("MMAD_WGRAD_BIG"); return e ? atoi(e) : 0; }();
-  return v && dtype == MMAD_BF16 && g.Nd % 256 == 0 && g.K >= 256 * 8;
+  return (v && dtype == MMAD_BF16 && g.Nd % 256 == 0 && g.K >= 256 * 8) ? v : 0;
 }
 
 WSplit wgrad_split(const Geom& g, int dtype) {
@@ -950,11 +979,28 @@ WSplit wgrad_split(const Geom& g, int dtype) {
   s.bmw = big ? 256 : (g.Nd <= 64 ? 64 : 128);
   const int wbn = big ? 256 : WBN;
   const int64_t tiles = cdiv(g.Nd, s.bmw) * cdiv(g.K, wbn);
-  // ~4 blocks per CU for the 4-wave tiles (2 resident + a second wave), ~2 for 8-wave ones
-  int64_t want = cdiv(big ? 512 : 1024, tiles);
-  const int64_t max_split = std::max<int64_t>(1, cdiv(g.M, WBK * 8));
-  want = std::max<int64_t>(1, std::min(want, max_split));
-  while (want > 1 && want * g.Nd * (int64_t)g.K * 4 > (int64_t(512) << 20)) --want;
+  // Split count from a small cost model (measured on MI355X, tools/exp_wgrad.sh):
+  //   rounds(s) * stages_per_split(s) * c  +  s * slab_MB * r
+  // rounds = ceil(blocks / resident slots): 4 blocks per CU for the 4-wave tiles (LDS
+  // 36 KB, <128 VGPRs), 1 for the 8-wave ones.  A block count just past a multiple of the
+  // slots costs a whole extra round (the old "cdiv(1024, tiles)" rule always landed there:
+  // l4c1 1080 blocks ran 19 % slower than 864).  c ~ 0.93 us per 32-voxel stage of a
+  // 128-wide tile, r ~ 0.2 us per MB of fp32 slab written and re-read by the reduce.
+  const int64_t slots = big ? 256 : 1024;
+  const int64_t max_split = std::max<int64_t>(1, std::min<int64_t>(cdiv(g.M, WBK * 8), 512));
+  const double c = 0.93 * s.bmw / 128.0, r = 0.2;
+  const double slab_mb = (double)g.Nd * g.K * 4 / 1e6;
+  int64_t want = 1;
+  double best = 1e30;
+  for (int64_t sp = 1; sp <= max_split; ++sp) {
+    if (sp > 1 && sp * g.Nd * (int64_t)g.K * 4 > (int64_t(512) << 20)) break;
+    const int64_t stages = cdiv(cdiv(g.M, sp), WBK);
+    const int64_t nsp = cdiv(g.M, stages * WBK);          // splits actually produced
+    const double cost = (double)cdiv(tiles * nsp, slots) * stages * c + nsp * slab_mb * r;
+    if (cost < best * 0.999) { best = cost; want = sp; }
+  }
+  static const int force = [] { const char* e = getenv("MMAD_WGRAD_SPLITS"); return e ? atoi(e) : 0; }();
+  if (force > 0) want = std::min<int64_t>(force, max_split);
   s.m_per_split = (int)(cdiv(cdiv(g.M, want), WBK) * WBK);
   s.splits = (int)cdiv(g.M, s.m_per_split);
   return s;
@@ -1277,8 +1323,11 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
   }
   const WSplit sp = wgrad_split(g, dtype);
   if (dtype == MMAD_BF16)
-    rc = sp.bmw == 256 ? launch_wgrad_k<u16, 256, 32, 2, 256, 2, 4>(g, sp, x, dy,
-                                                                   (float*)workspace, st)
+    rc = sp.bmw == 256 ? (wgrad_big(g, dtype) == 3
+                              ? launch_wgrad_k<u16, 256, 32, 3, 256, 2, 4>(g, sp, x, dy,
+                                                                          (float*)workspace, st)
+                              : launch_wgrad_k<u16, 256, 32, 2, 256, 2, 4>(g, sp, x, dy,
+                                                                          (float*)workspace, st))
        : sp.bmw == 64 ? launch_wgrad<u16, 64>(g, sp, x, dy, (float*)workspace, st)
                       : launch_wgrad<u16, 128>(g, sp, x, dy, (float*)workspace, st);
   else
@@ -1290,6 +1339,10 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
     hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)cdiv(g.Cs, 64), (unsigned)g.Nd),
                        dim3(256), 0, st, (const float*)workspace, dw, sp.splits, g.Nd, g.K,
                        g.Cs, g.taps);
+  else if (sp.splits >= 8)
+    hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)cdiv(total, 64)), dim3(256), 0,
+                       st, (const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.cs_shift,
+                       g.taps, unfolded(d) ? d->kw : 0, 1);
   else
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, st,
                        (const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.cs_shift,

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--layers", default="", help="comma-separated subset of layer names")
+    ap.add_argument("--tag", default="", help="label printed on every row")
     args = ap.parse_args()
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     code = L.dtype_code(dt)
@@ -53,7 +55,10 @@ def main():
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     print(f"{'layer':6s} {'GFLOP':>7s} | {'fwd us':>8s} {'TF/s':>6s} | {'dgrad us':>8s} {'TF/s':>6s} |"
           f" {'wgrad us':>8s} {'TF/s':>6s} | {'miopen f/d/w TF/s':>20s}")
+    pick = set(args.layers.split(",")) if args.layers else None
     for name, (n, ci, s), co, k, st, p, dl in LAYERS:
+        if pick is not None and name not in pick:
+            continue
         x = torch.randn((n, ci, s, s, s), device="cuda").to(dt)
         if ci > 1:
             x = x.contiguous(memory_format=CL)
@@ -95,7 +100,7 @@ def main():
         tot["fwd"] += t_f
         tot["dgrad"] += 0 if t_d != t_d else t_d
         tot["wgrad"] += t_w
-        print(f"{name:6s} {flop / 1e9:7.1f} | {t_f * 1e6:8.1f} {flop / t_f / 1e12:6.0f} | "
+        print(f"{args.tag}{name:6s} {flop / 1e9:7.1f} | {t_f * 1e6:8.1f} {flop / t_f / 1e12:6.0f} | "
               f"{t_d * 1e6:8.1f} {flop / t_d / 1e12:6.0f} | {t_w * 1e6:8.1f} {flop / t_w / 1e12:6.0f} | {mio}")
     print("totals ms:", {k: round(v * 1e3, 3) for k, v in tot.items()},
           "sum", round(sum(tot.values()) * 1e3, 3))
