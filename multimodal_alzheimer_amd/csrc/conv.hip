@@ -33,6 +33,7 @@
 //  * epilogue: bias, BN partial sums (sum, sum of squares per channel) from the fp32
 //    accumulators, bf16 tile transposed through LDS into 16-byte channel-vector stores.
 #include "common.h"
+#include "patchconv.h"
 #include "stem.h"
 
 namespace {
@@ -956,6 +957,16 @@ bool geom_ok(const Geom& g, int dtype) {
          src_vox < (int64_t(1) << 31) && dst_vox < (int64_t(1) << 31);   // 32-bit voxel ids
 }
 
+// the patch-resident kernel (patchconv.hip) for narrow stride-1 bf16 convs
+mmad_patch::Geo patch_geo(const Geom& g) {
+  return mmad_patch::Geo{g.nb, g.Cs, g.Nd, g.Kpad, g.Ds, g.Hs, g.Ws, g.Dd, g.Hd, g.Wd,
+                         g.KD, g.KH, g.KW, g.pd, g.ph, g.pw, g.dd, g.dh, g.dw};
+}
+bool use_patch(const Geom& g, int dtype) {
+  return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
+         mmad_patch::ok(patch_geo(g));
+}
+
 int bn_of(const Geom& g) { return g.Nd <= 64 ? 64 : 128; }
 
 // tile rows: 64 when 128-row tiles would leave the 256 CUs with under two blocks each
@@ -1246,6 +1257,7 @@ int64_t mmad_conv3d_stats_rows(const mmad_conv_desc* d, int dtype) {
   if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on())
     return mmad_stem::fwd_stats_rows(d);
   const Geom g = fwd_geom(d, dtype);
+  if (!unfolded(d) && use_patch(g, dtype)) return mmad_patch::tiles(patch_geo(g));
   return cdiv(g.M, fwd_tile_rows(g, dtype));
 }
 
@@ -1258,6 +1270,8 @@ int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x, const voi
     return mmad_stem::fwd(d, x, wp, bias, y, stats, stream);
   const Geom g = fwd_geom(d, dtype);
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
+  if (!unfolded(d) && use_patch(g, dtype))
+    return mmad_patch::fwd(patch_geo(g), x, wp, bias, y, stats, stream);
   return run_igemm<FWD>(g, dtype, g.M, 1, x, wp, bias, y, stats, as_stream(stream));
 }
 
@@ -1270,6 +1284,8 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
   if (dgrad_as_fwd(d)) {
     const Geom gf = dgrad_fwd_geom(d, dtype);
     if (!geom_ok(gf, dtype)) return MMAD_EUNSUPPORTED;
+    if (use_patch(gf, dtype))
+      return mmad_patch::fwd(patch_geo(gf), dy, wpt, nullptr, dx, nullptr, stream);
     return run_igemm<FWD>(gf, dtype, gf.M, 1, dy, wpt, nullptr, dx, nullptr,
                           as_stream(stream));
   }

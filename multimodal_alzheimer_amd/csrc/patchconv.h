@@ -1,0 +1,22 @@
+// Patch-resident stride-1 3D convolution for narrow layers (bf16), internal to
+// libmmad_hip.so: mmad_conv3d_fwd / mmad_conv3d_dgrad route matching geometries here
+// (see patchconv.hip for the design).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/mmad.h"
+
+namespace mmad_patch {
+// stride-1 conv over NDHWC bf16 volumes; weights packed [Nd][Kpad] with k = tap*Cs + ci
+struct Geo {
+  int nb, Cs, Nd, Kpad;           // input channels, output channels, packed weight row
+  int Ds, Hs, Ws, Dd, Hd, Wd;     // source / destination extents
+  int KD, KH, KW, pd, ph, pw, dd, dh, dw;
+};
+// true when the geometry is handled (and the kernel is switched on, MMAD_PATCH)
+bool ok(const Geo& g);
+// M tiles of one launch = rows of the BN partial-sum buffer it writes ([rows][2][Nd])
+int64_t tiles(const Geo& g);
+int fwd(const Geo& g, const void* src, const void* wp, const float* bias, void* dst,
+        float* stats, void* stream);
+}  // namespace mmad_patch
