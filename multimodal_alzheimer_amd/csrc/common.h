@@ -43,6 +43,19 @@ __device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t lds_addr) 
       : "v"(gsrc), "s"(lds_addr)
       : "memory");
 }
+// Same through a buffer resource: lane byte offset `voff` (32-bit); an offset past the
+// resource's size reads 16 zero bytes (hardware range check), which is how padding and
+// out-of-range rows are fed without a pointer select.
+__device__ __forceinline__ void buf_lds16_asm(uint32_t voff, __amdgpu_buffer_rsrc_t rsrc,
+                                              uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds_addr)
+      : "memory");
+}
 __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
   return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const LDS_AS void*)p);
 }

@@ -11,6 +11,8 @@
 // torch's CPU kernel; the window index is kept as one byte per output so the backward is
 // a deterministic gather (no atomics) that adds the contributions of the overlapping
 // windows in output order, as torch's CPU backward does.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -191,6 +193,60 @@ __global__ void bnpool_fwd_kernel(PoolG g, const T* __restrict__ y,
 // together (clamped addresses for padding positions, masked out of the comparison); the
 // argmax bytes of a channel vector leave in one store.
 template <typename T, int V>
+__device__ __forceinline__ void bnpool3_fwd_one(const PoolG& g, const T* __restrict__ y,
+                                                const float* __restrict__ scale,
+                                                const float* __restrict__ shift,
+                                                T* __restrict__ out, uint8_t* __restrict__ am,
+                                                T* __restrict__ ymax, int64_t nb, int od,
+                                                int oh, int ow, int c0) {
+  const int64_t ovox = ((nb * g.do_ + od) * g.ho + oh) * g.wo + ow;
+  const int z0 = od * g.s - g.p, y0 = oh * g.s - g.p, x0 = ow * g.s - g.p;
+  float sc[V], sh[V], best[V], braw[V];
+  int bi[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e];
+    best[e] = -__builtin_inff(); braw[e] = 0.f; bi[e] = -1;
+  }
+  for (int kd = 0; kd < 3; ++kd) {
+    const int z = z0 + kd;
+    if ((unsigned)z >= (unsigned)g.di) continue;
+    float raw[9][V];
+    bool ok[9];
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+      const int yy = y0 + w / 3, xx = x0 + w % 3;
+      ok[w] = (unsigned)yy < (unsigned)g.hi && (unsigned)xx < (unsigned)g.wi;
+      const int yc = min(max(yy, 0), g.hi - 1), xc = min(max(xx, 0), g.wi - 1);
+      load_v<T, V>(y + (((nb * g.di + z) * g.hi + yc) * g.wi + xc) * g.c + c0, raw[w]);
+    }
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+      if (!ok[w]) continue;
+      const int wi = kd * 9 + w;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float val = as_stored<T>(fmaxf(bn_affine(raw[w][e], sc[e], sh[e]), 0.f));
+        if (bi[e] < 0) { bi[e] = wi; braw[e] = raw[w][e]; }
+        if (val > best[e] || val != val) { best[e] = val; bi[e] = wi; braw[e] = raw[w][e]; }
+      }
+    }
+  }
+  store_v<T, V>(out + ovox * g.c + c0, best);
+  store_v<T, V>(ymax + ovox * g.c + c0, braw);
+  uint64_t packed = 0;
+#pragma unroll
+  for (int e = 0; e < V; ++e)
+    packed |= (uint64_t)(uint8_t)(bi[e] | (best[e] > 0.f ? 0x80 : 0)) << (8 * e);
+  if constexpr (V == 8) *reinterpret_cast<uint64_t*>(am + ovox * g.c + c0) = packed;
+  else if constexpr (V == 4) *reinterpret_cast<uint32_t*>(am + ovox * g.c + c0) = (uint32_t)packed;
+  else for (int e = 0; e < V; ++e) am[ovox * g.c + c0 + e] = (uint8_t)(packed >> (8 * e));
+}
+
+// k = 3 form of bnpool_fwd_kernel: per window plane the 9 loads are unrolled and issued
+// together (clamped addresses for padding positions, masked out of the comparison); the
+// argmax bytes of a channel vector leave in one store.
+template <typename T, int V>
 __global__ void bnpool3_fwd_kernel(PoolG g, const T* __restrict__ y,
                                    const float* __restrict__ scale,
                                    const float* __restrict__ shift, T* __restrict__ out,
@@ -201,53 +257,28 @@ __global__ void bnpool3_fwd_kernel(PoolG g, const T* __restrict__ y,
        t += (int64_t)gridDim.x * blockDim.x) {
     const int c0 = (int)(t % cv) * V;
     int64_t v = t / cv;
-    const int64_t ovox = v;
     const int ow = (int)(v % g.wo); v /= g.wo;
     const int oh = (int)(v % g.ho); v /= g.ho;
     const int od = (int)(v % g.do_);
-    const int64_t nb = v / g.do_;
-    const int z0 = od * g.s - g.p, y0 = oh * g.s - g.p, x0 = ow * g.s - g.p;
-    float sc[V], sh[V], best[V], braw[V];
-    int bi[V];
-#pragma unroll
-    for (int e = 0; e < V; ++e) {
-      sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e];
-      best[e] = -__builtin_inff(); braw[e] = 0.f; bi[e] = -1;
-    }
-    for (int kd = 0; kd < 3; ++kd) {
-      const int z = z0 + kd;
-      if ((unsigned)z >= (unsigned)g.di) continue;
-      float raw[9][V];
-      bool ok[9];
-#pragma unroll
-      for (int w = 0; w < 9; ++w) {
-        const int yy = y0 + w / 3, xx = x0 + w % 3;
-        ok[w] = (unsigned)yy < (unsigned)g.hi && (unsigned)xx < (unsigned)g.wi;
-        const int yc = min(max(yy, 0), g.hi - 1), xc = min(max(xx, 0), g.wi - 1);
-        load_v<T, V>(y + (((nb * g.di + z) * g.hi + yc) * g.wi + xc) * g.c + c0, raw[w]);
-      }
-#pragma unroll
-      for (int w = 0; w < 9; ++w) {
-        if (!ok[w]) continue;
-        const int wi = kd * 9 + w;
-#pragma unroll
-        for (int e = 0; e < V; ++e) {
-          const float val = as_stored<T>(fmaxf(bn_affine(raw[w][e], sc[e], sh[e]), 0.f));
-          if (bi[e] < 0) { bi[e] = wi; braw[e] = raw[w][e]; }
-          if (val > best[e] || val != val) { best[e] = val; bi[e] = wi; braw[e] = raw[w][e]; }
-        }
-      }
-    }
-    store_v<T, V>(out + ovox * g.c + c0, best);
-    store_v<T, V>(ymax + ovox * g.c + c0, braw);
-    uint64_t packed = 0;
-#pragma unroll
-    for (int e = 0; e < V; ++e)
-      packed |= (uint64_t)(uint8_t)(bi[e] | (best[e] > 0.f ? 0x80 : 0)) << (8 * e);
-    if constexpr (V == 8) *reinterpret_cast<uint64_t*>(am + ovox * g.c + c0) = packed;
-    else if constexpr (V == 4) *reinterpret_cast<uint32_t*>(am + ovox * g.c + c0) = (uint32_t)packed;
-    else for (int e = 0; e < V; ++e) am[ovox * g.c + c0 + e] = (uint8_t)(packed >> (8 * e));
+    bnpool3_fwd_one<T, V>(g, y, scale, shift, out, am, ymax, v / g.do_, od, oh, ow, c0);
   }
+}
+
+// Same, one block per output row (blockIdx.y = oh, blockIdx.z = n*do + od) when the
+// channel-vector count is a power of two: the per-thread index math is a shift and a mask
+// instead of five 64-bit divisions (which, at 8 channels per thread, cost more VALU time
+// than the kernel's memory traffic).
+template <typename T, int V>
+__global__ __launch_bounds__(256) void bnpool3_fwd_rows_kernel(
+    PoolG g, int cv_shift, const T* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, T* __restrict__ out, uint8_t* __restrict__ am,
+    T* __restrict__ ymax) {
+  const int oh = blockIdx.y, od = blockIdx.z % g.do_;
+  const int64_t nb = blockIdx.z / g.do_;
+  const int items = g.wo << cv_shift, cmask = (1 << cv_shift) - 1;
+  for (int e = threadIdx.x; e < items; e += 256)
+    bnpool3_fwd_one<T, V>(g, y, scale, shift, out, am, ymax, nb, od, oh, e >> cv_shift,
+                          (e & cmask) * V);
 }
 
 // k = 3, stride 2, pad 1 form of bnpool_bwd_apply_kernel, one thread per 2x2x2 input cell
@@ -255,6 +286,70 @@ __global__ void bnpool3_fwd_kernel(PoolG g, const T* __restrict__ y,
 // cell's 8 inputs share the 8 windows {a, a+1}^3, loaded once (not ~3.4x per input).  All
 // 24 loads of a cell are issued before any use (raw 16-byte registers), so a thread waits
 // for one memory round trip, not eight.
+template <typename T>
+__device__ __forceinline__ void bnpool3s2_bwd_cell(
+    const PoolG& g, const T* __restrict__ gp, const uint8_t* __restrict__ am,
+    const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ coef, T* __restrict__ dy, int64_t nb, int ad, int ah, int aw,
+    int c0) {
+  constexpr int V = Chunk<T>::N;
+  uint64_t a8[8];
+  u32x4 graw[8], yraw[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int qd = q >> 2, qh = (q >> 1) & 1, qw = q & 1;
+    const bool ok = ad + qd < g.do_ && ah + qh < g.ho && aw + qw < g.wo;
+    const int od = min(ad + qd, g.do_ - 1), oh = min(ah + qh, g.ho - 1);
+    const int ow = min(aw + qw, g.wo - 1);
+    const int64_t o = (((nb * g.do_ + od) * g.ho + oh) * g.wo + ow) * g.c + c0;
+    uint64_t w;
+    if constexpr (V == 8) w = *reinterpret_cast<const uint64_t*>(am + o);
+    else w = *reinterpret_cast<const uint32_t*>(am + o);
+    a8[q] = ok ? w : 0;          // 0: no active window (the 0x80 bit is never set)
+    graw[q] = *reinterpret_cast<const u32x4*>(gp + o);
+    const int id = min(2 * ad + qd, g.di - 1), ih = min(2 * ah + qh, g.hi - 1);
+    const int iw = min(2 * aw + qw, g.wi - 1);
+    yraw[q] = *reinterpret_cast<const u32x4*>(y + (((nb * g.di + id) * g.hi + ih) * g.wi + iw) *
+                                                      g.c + c0);
+  }
+  float gv[8][V];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) Chunk<T>::load(reinterpret_cast<const T*>(&graw[q]), gv[q]);
+  float mu[V], is[V], k0[V], k1[V], k2[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const int c = c0 + e;
+    mu[e] = mean[c]; is[e] = invstd[c];
+    k0[e] = coef[c]; k1[e] = coef[g.c + c]; k2[e] = coef[2 * g.c + c];
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int rd = r >> 2, rh = (r >> 1) & 1, rw = r & 1;
+    const int id = 2 * ad + rd, ih = 2 * ah + rh, iw = 2 * aw + rw;
+    float yv[V], acc[V];
+    Chunk<T>::load(reinterpret_cast<const T*>(&yraw[r]), yv);
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int qd = q >> 2, qh = (q >> 1) & 1, qw = q & 1;
+      // an even input (r-bit 0) lies only in window a (q-bit 0); offset inside window
+      // a+q: (i - 2a) + 1 - 2q
+      if ((!rd && qd) || (!rh && qh) || (!rw && qw)) continue;
+      const int wi = 0x80 | (((rd + 1 - 2 * qd) * 3 + (rh + 1 - 2 * qh)) * 3 + (rw + 1 - 2 * qw));
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if ((int)((a8[q] >> (8 * e)) & 0xff) == wi) acc[e] += gv[q][e];
+    }
+    if (id >= g.di || ih >= g.hi || iw >= g.wi) continue;
+    float dv[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+      dv[e] = k0[e] * acc[e] - k1[e] - (yv[e] - mu[e]) * is[e] * k2[e];
+    Chunk<T>::store(dy + (((nb * g.di + id) * g.hi + ih) * g.wi + iw) * g.c + c0, dv);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void bnpool3s2_bwd_apply_kernel(
     PoolG g, const T* __restrict__ gp, const uint8_t* __restrict__ am, const T* __restrict__ y,
@@ -271,63 +366,25 @@ __global__ __launch_bounds__(256) void bnpool3s2_bwd_apply_kernel(
     const int aw = (int)(v % cw); v /= cw;
     const int ah = (int)(v % ch); v /= ch;
     const int ad = (int)(v % cd);
-    const int64_t nb = v / cd;
-    uint64_t a8[8];
-    u32x4 graw[8], yraw[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int qd = q >> 2, qh = (q >> 1) & 1, qw = q & 1;
-      const bool ok = ad + qd < g.do_ && ah + qh < g.ho && aw + qw < g.wo;
-      const int od = min(ad + qd, g.do_ - 1), oh = min(ah + qh, g.ho - 1);
-      const int ow = min(aw + qw, g.wo - 1);
-      const int64_t o = (((nb * g.do_ + od) * g.ho + oh) * g.wo + ow) * g.c + c0;
-      uint64_t w;
-      if constexpr (V == 8) w = *reinterpret_cast<const uint64_t*>(am + o);
-      else w = *reinterpret_cast<const uint32_t*>(am + o);
-      a8[q] = ok ? w : 0;          // 0: no active window (the 0x80 bit is never set)
-      graw[q] = *reinterpret_cast<const u32x4*>(gp + o);
-      const int id = min(2 * ad + qd, g.di - 1), ih = min(2 * ah + qh, g.hi - 1);
-      const int iw = min(2 * aw + qw, g.wi - 1);
-      yraw[q] = *reinterpret_cast<const u32x4*>(y + (((nb * g.di + id) * g.hi + ih) * g.wi + iw) *
-                                                        g.c + c0);
-    }
-    float gv[8][V];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) Chunk<T>::load(reinterpret_cast<const T*>(&graw[q]), gv[q]);
-    float mu[V], is[V], k0[V], k1[V], k2[V];
-#pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const int c = c0 + e;
-      mu[e] = mean[c]; is[e] = invstd[c];
-      k0[e] = coef[c]; k1[e] = coef[g.c + c]; k2[e] = coef[2 * g.c + c];
-    }
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int rd = r >> 2, rh = (r >> 1) & 1, rw = r & 1;
-      const int id = 2 * ad + rd, ih = 2 * ah + rh, iw = 2 * aw + rw;
-      float yv[V], acc[V];
-      Chunk<T>::load(reinterpret_cast<const T*>(&yraw[r]), yv);
-#pragma unroll
-      for (int e = 0; e < V; ++e) acc[e] = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int qd = q >> 2, qh = (q >> 1) & 1, qw = q & 1;
-        // an even input (r-bit 0) lies only in window a (q-bit 0); offset inside window
-        // a+q: (i - 2a) + 1 - 2q
-        if ((!rd && qd) || (!rh && qh) || (!rw && qw)) continue;
-        const int wi = 0x80 | (((rd + 1 - 2 * qd) * 3 + (rh + 1 - 2 * qh)) * 3 + (rw + 1 - 2 * qw));
-#pragma unroll
-        for (int e = 0; e < V; ++e)
-          if ((int)((a8[q] >> (8 * e)) & 0xff) == wi) acc[e] += gv[q][e];
-      }
-      if (id >= g.di || ih >= g.hi || iw >= g.wi) continue;
-      float dv[V];
-#pragma unroll
-      for (int e = 0; e < V; ++e)
-        dv[e] = k0[e] * acc[e] - k1[e] - (yv[e] - mu[e]) * is[e] * k2[e];
-      Chunk<T>::store(dy + (((nb * g.di + id) * g.hi + ih) * g.wi + iw) * g.c + c0, dv);
-    }
+    bnpool3s2_bwd_cell<T>(g, gp, am, y, mean, invstd, coef, dy, v / cd, ad, ah, aw, c0);
   }
+}
+
+// Same, one block per row of cells (blockIdx.y = ah, blockIdx.z = n*cd + ad), power-of-two
+// channel-vector count: shift/mask index math (see bnpool3_fwd_rows_kernel).
+template <typename T>
+__global__ __launch_bounds__(256) void bnpool3s2_bwd_rows_kernel(
+    PoolG g, int cv_shift, const T* __restrict__ gp, const uint8_t* __restrict__ am,
+    const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ coef, T* __restrict__ dy) {
+  constexpr int V = Chunk<T>::N;
+  const int cd = (g.di + 1) >> 1, cw = (g.wi + 1) >> 1;
+  const int ah = blockIdx.y, ad = blockIdx.z % cd;
+  const int64_t nb = blockIdx.z / cd;
+  const int items = cw << cv_shift, cmask = (1 << cv_shift) - 1;
+  for (int e = threadIdx.x; e < items; e += 256)
+    bnpool3s2_bwd_cell<T>(g, gp, am, y, mean, invstd, coef, dy, nb, ad, ah, e >> cv_shift,
+                          (e & cmask) * V);
 }
 
 // Fused backward, dense pass: for every input voxel, g' = sum of the pooled gradients of the
@@ -449,6 +506,12 @@ __global__ void gap_bwd_kernel(int n, int64_t S, int C, const float* __restrict_
   }
 }
 
+// MMAD_POOL_ROWS=0 keeps the grid-stride fused pool kernels (A/B switch)
+bool rows_on() {
+  static const bool v = [] { const char* e = getenv("MMAD_POOL_ROWS"); return !e || atoi(e) != 0; }();
+  return v;
+}
+
 unsigned grid_of(int64_t n) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 256), 256 * 32));
 }
@@ -492,7 +555,13 @@ int bnpool_fwd(const PoolG& g, const void* y, const float* scale, const float* s
                uint8_t* am, void* ymax, hipStream_t st) {
   constexpr int VEC = Chunk<T>::N;
   const int64_t vox = (int64_t)g.n * g.do_ * g.ho * g.wo;
-  if (g.c % VEC == 0 && g.k == 3)
+  const int cv = g.c / VEC;
+  if (g.c % VEC == 0 && g.k == 3 && is_pow2(cv) && rows_on() &&
+      (int64_t)g.n * g.do_ < 65536 && g.ho < 65536)
+    hipLaunchKernelGGL((bnpool3_fwd_rows_kernel<T, VEC>),
+                       dim3(1, (unsigned)g.ho, (unsigned)(g.n * g.do_)), dim3(256), 0, st, g,
+                       ilog2(cv), (const T*)y, scale, shift, (T*)out, am, (T*)ymax);
+  else if (g.c % VEC == 0 && g.k == 3)
     hipLaunchKernelGGL((bnpool3_fwd_kernel<T, VEC>), dim3(grid_of(vox * g.c / VEC)), dim3(256),
                        0, st, g, (const T*)y, scale, shift, (T*)out, am, (T*)ymax);
   else if (g.c % VEC == 0)
@@ -510,7 +579,13 @@ int bnpool_bwd_apply(const PoolG& g, const void* gp, const uint8_t* am, const vo
                      hipStream_t st) {
   constexpr int VEC = Chunk<T>::N;
   const int64_t vox = (int64_t)g.n * g.di * g.hi * g.wi;
-  if (g.c % VEC == 0 && g.k == 3 && g.s == 2 && g.p == 1)
+  const int cv = g.c / VEC, cd = (g.di + 1) >> 1, ch = (g.hi + 1) >> 1;
+  if (g.c % VEC == 0 && g.k == 3 && g.s == 2 && g.p == 1 && is_pow2(cv) && rows_on() &&
+      (int64_t)g.n * cd < 65536 && ch < 65536)
+    hipLaunchKernelGGL((bnpool3s2_bwd_rows_kernel<T>), dim3(1, (unsigned)ch, (unsigned)(g.n * cd)),
+                       dim3(256), 0, st, g, ilog2(cv), (const T*)gp, am, (const T*)y, mean,
+                       invstd, coef, (T*)dy);
+  else if (g.c % VEC == 0 && g.k == 3 && g.s == 2 && g.p == 1)
     hipLaunchKernelGGL((bnpool3s2_bwd_apply_kernel<T>), dim3(grid_of(vox * g.c / VEC / 8 + 1)),
                        dim3(256), 0, st, g, (const T*)gp, am, (const T*)y, mean, invstd, coef,
                        (T*)dy);
