@@ -267,6 +267,70 @@ __global__ void scale_shift_act_kernel(int64_t M, int C, const T* __restrict__ y
   }
 }
 
+// per-channel fp32 parameters of one channel vector: N consecutive floats from a 16-byte
+// aligned offset (N = 4 or 8) as 16-byte loads
+template <int N>
+__device__ __forceinline__ void ld_params(const float* __restrict__ p, float* v) {
+#pragma unroll
+  for (int h = 0; h < N / 4; ++h) {
+    const f32x4 c = *reinterpret_cast<const f32x4*>(p + 4 * h);
+    v[4 * h] = c[0]; v[4 * h + 1] = c[1]; v[4 * h + 2] = c[2]; v[4 * h + 3] = c[3];
+  }
+}
+
+// Fixed-channel form of scale_shift_act_kernel for C / N a power of two dividing 256: the
+// grid stride is a multiple of the chunks per row, so every thread always handles the same
+// channel vector -- its scale/shift (and residual scale/shift) are loaded once, as 16-byte
+// vectors, instead of 2-4 scalar loads per element per chunk (the per-element parameter
+// loads made the old kernel VMEM-issue bound at ~2 TB/s).  Two chunks per trip, loads first.
+template <typename T, int RES>
+__global__ __launch_bounds__(256) void scale_shift_act_fc_kernel(
+    int64_t nchunks, int cpr, const T* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const T* __restrict__ res, const float* __restrict__ rscale,
+    const float* __restrict__ rshift, int relu, T* __restrict__ out) {
+  constexpr int N = Chunk<T>::N;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int c0 = (int)(t0 & (cpr - 1)) * N;
+  float sc[N], sh[N], rs[N], rh[N];
+  ld_params<N>(scale + c0, sc);
+  ld_params<N>(shift + c0, sh);
+  if (RES == 2) {
+    ld_params<N>(rscale + c0, rs);
+    ld_params<N>(rshift + c0, rh);
+  }
+  auto apply = [&](float* v, const float* r) {
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+      float o = bn_affine(v[e], sc[e], sh[e]);
+      if (RES == 1) o += r[e];
+      if (RES == 2) o += r[e] * rs[e] + rh[e];
+      v[e] = relu ? fmaxf(o, 0.f) : o;
+    }
+  };
+  int64_t q = t0;
+  for (; q + stride < nchunks; q += 2 * stride) {
+    float v0[N], v1[N], r0[N], r1[N];
+    Chunk<T>::load(y + q * N, v0);
+    Chunk<T>::load(y + (q + stride) * N, v1);
+    if (RES) {
+      Chunk<T>::load(res + q * N, r0);
+      Chunk<T>::load(res + (q + stride) * N, r1);
+    }
+    apply(v0, r0);
+    apply(v1, r1);
+    Chunk<T>::store(out + q * N, v0);
+    Chunk<T>::store(out + (q + stride) * N, v1);
+  }
+  if (q < nchunks) {
+    float v0[N], r0[N];
+    Chunk<T>::load(y + q * N, v0);
+    if (RES) Chunk<T>::load(res + q * N, r0);
+    apply(v0, r0);
+    Chunk<T>::store(out + q * N, v0);
+  }
+}
+
 template <typename T>
 __global__ void scale_shift_act_scalar_kernel(int64_t M, int C, const T* __restrict__ y,
                                               const float* __restrict__ scale,
@@ -282,6 +346,57 @@ __global__ void scale_shift_act_scalar_kernel(int64_t M, int C, const T* __restr
     float o = bn_affine(Elt<T>::ld(y, i), scale[c], shift[c]);
     if (res) o += rscale ? Elt<T>::ld(res, i) * rscale[c] + rshift[c] : Elt<T>::ld(res, i);
     Elt<T>::st(out, i, relu ? fmaxf(o, 0.f) : o);
+  }
+}
+
+// Fixed-channel form of bn_bwd_apply_kernel (C / V a power of two dividing 256): per-thread
+// channel vector constant, its mean/invstd/coef loaded once as vectors; two chunks a trip.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
+    int64_t nv, int cpr, int C, const T* __restrict__ g, const T* __restrict__ relu_out,
+    const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ coef, T* __restrict__ dy, T* __restrict__ gmask) {
+  constexpr int V = Chunk<T>::N;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int c0 = (int)(t0 & (cpr - 1)) * V;
+  float mu[V], is[V], k0[V], k1[V], k2[V];
+  ld_params<V>(mean + c0, mu);
+  ld_params<V>(invstd + c0, is);
+  ld_params<V>(coef + c0, k0);
+  ld_params<V>(coef + C + c0, k1);
+  ld_params<V>(coef + 2 * C + c0, k2);
+  auto one = [&](int64_t q, const float* gv0, const float* yv, const float* ov) {
+    float gv[V], dv[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      gv[e] = (relu_out && !(ov[e] > 0.f)) ? 0.f : gv0[e];
+      const float xh = (yv[e] - mu[e]) * is[e];
+      dv[e] = k0[e] * gv[e] - k1[e] - xh * k2[e];
+    }
+    Chunk<T>::store(dy + q * V, dv);
+    if (gmask) Chunk<T>::store(gmask + q * V, gv);
+  };
+  int64_t q = t0;
+  for (; q + stride < nv; q += 2 * stride) {
+    float g0[V], g1[V], y0[V], y1[V], o0[V], o1[V];
+    Chunk<T>::load(g + q * V, g0);
+    Chunk<T>::load(g + (q + stride) * V, g1);
+    Chunk<T>::load(y + q * V, y0);
+    Chunk<T>::load(y + (q + stride) * V, y1);
+    if (relu_out) {
+      Chunk<T>::load(relu_out + q * V, o0);
+      Chunk<T>::load(relu_out + (q + stride) * V, o1);
+    }
+    one(q, g0, y0, o0);
+    one(q + stride, g1, y1, o1);
+  }
+  if (q < nv) {
+    float g0[V], y0[V], o0[V];
+    Chunk<T>::load(g + q * V, g0);
+    Chunk<T>::load(y + q * V, y0);
+    if (relu_out) Chunk<T>::load(relu_out + q * V, o0);
+    one(q, g0, y0, o0);
   }
 }
 
@@ -434,7 +549,17 @@ int mmad_scale_shift_act(int dtype, int64_t m, int c, const void* y, const float
 #define SSA(T, R)                                                                          \
   hipLaunchKernelGGL((scale_shift_act_kernel<T, R>), dim3(grid), dim3(256), 0, st, m, c,  \
                      (const T*)y, scale, shift, (const T*)res, rscale, rshift, relu, (T*)out)
-  if (c % epc == 0) {
+#define SSAF(T, R)                                                                         \
+  hipLaunchKernelGGL((scale_shift_act_fc_kernel<T, R>), dim3(grid), dim3(256), 0, st,        \
+                     m * c / epc, c / epc, (const T*)y, scale, shift, (const T*)res, rscale,  \
+                     rshift, relu, (T*)out)
+  if (c % epc == 0 && is_pow2(c / epc) && c / epc <= 256) {
+    if (dtype == MMAD_BF16) {
+      if (rk == 0) SSAF(u16, 0); else if (rk == 1) SSAF(u16, 1); else SSAF(u16, 2);
+    } else {
+      if (rk == 0) SSAF(float, 0); else if (rk == 1) SSAF(float, 1); else SSAF(float, 2);
+    }
+  } else if (c % epc == 0) {
     if (dtype == MMAD_BF16) {
       if (rk == 0) SSA(u16, 0); else if (rk == 1) SSA(u16, 1); else SSA(u16, 2);
     } else {
@@ -450,6 +575,7 @@ int mmad_scale_shift_act(int dtype, int64_t m, int c, const void* y, const float
                        rshift, relu, (float*)out);
   }
 #undef SSA
+#undef SSAF
   return launch_status();
 }
 
@@ -499,6 +625,19 @@ int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* re
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, V>), dim3(ew_grid(m * c / V)), dim3(256), 0, st, \
                      m, c, (const T*)g, (const T*)relu_out, (const T*)y, mean, invstd, coef,  \
                      (T*)dy, (T*)gmask)
+  const int vv = dtype == MMAD_BF16 ? 8 : 4;
+  if (c % vv == 0 && is_pow2(c / vv) && c / vv <= 256) {
+    const int64_t nv = m * c / vv;
+    if (dtype == MMAD_BF16)
+      hipLaunchKernelGGL(bn_bwd_apply_fc_kernel<u16>, dim3(ew_grid(nv)), dim3(256), 0, st, nv,
+                         c / vv, c, (const u16*)g, (const u16*)relu_out, (const u16*)y, mean,
+                         invstd, coef, (u16*)dy, (u16*)gmask);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply_fc_kernel<float>, dim3(ew_grid(nv)), dim3(256), 0, st, nv,
+                         c / vv, c, (const float*)g, (const float*)relu_out, (const float*)y,
+                         mean, invstd, coef, (float*)dy, (float*)gmask);
+    return launch_status();
+  }
   if (dtype == MMAD_BF16) {
     if (c % 8 == 0) APPLY(u16, 8); else APPLY(u16, 1);
   } else {

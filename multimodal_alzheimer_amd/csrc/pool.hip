@@ -198,14 +198,14 @@ __device__ __forceinline__ void bnpool3_fwd_one(const PoolG& g, const T* __restr
                                                 const float* __restrict__ shift,
                                                 T* __restrict__ out, uint8_t* __restrict__ am,
                                                 T* __restrict__ ymax, int64_t nb, int od,
-                                                int oh, int ow, int c0) {
+                                                int oh, int ow, int c0, const float* sc,
+                                                const float* sh) {
   const int64_t ovox = ((nb * g.do_ + od) * g.ho + oh) * g.wo + ow;
   const int z0 = od * g.s - g.p, y0 = oh * g.s - g.p, x0 = ow * g.s - g.p;
-  float sc[V], sh[V], best[V], braw[V];
+  float best[V], braw[V];
   int bi[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) {
-    sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e];
     best[e] = -__builtin_inff(); braw[e] = 0.f; bi[e] = -1;
   }
   for (int kd = 0; kd < 3; ++kd) {
@@ -260,7 +260,10 @@ __global__ void bnpool3_fwd_kernel(PoolG g, const T* __restrict__ y,
     const int ow = (int)(v % g.wo); v /= g.wo;
     const int oh = (int)(v % g.ho); v /= g.ho;
     const int od = (int)(v % g.do_);
-    bnpool3_fwd_one<T, V>(g, y, scale, shift, out, am, ymax, v / g.do_, od, oh, ow, c0);
+    float sc[V], sh[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e]; }
+    bnpool3_fwd_one<T, V>(g, y, scale, shift, out, am, ymax, v / g.do_, od, oh, ow, c0, sc, sh);
   }
 }
 
@@ -276,9 +279,14 @@ __global__ __launch_bounds__(256) void bnpool3_fwd_rows_kernel(
   const int oh = blockIdx.y, od = blockIdx.z % g.do_;
   const int64_t nb = blockIdx.z / g.do_;
   const int items = g.wo << cv_shift, cmask = (1 << cv_shift) - 1;
+  // cv divides 256: this thread's channel vector is the same for every item it visits
+  const int c0 = (threadIdx.x & cmask) * V;
+  float sc[V], sh[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e]; }
   for (int e = threadIdx.x; e < items; e += 256)
-    bnpool3_fwd_one<T, V>(g, y, scale, shift, out, am, ymax, nb, od, oh, e >> cv_shift,
-                          (e & cmask) * V);
+    bnpool3_fwd_one<T, V>(g, y, scale, shift, out, am, ymax, nb, od, oh, e >> cv_shift, c0, sc,
+                          sh);
 }
 
 // k = 3, stride 2, pad 1 form of bnpool_bwd_apply_kernel, one thread per 2x2x2 input cell
@@ -286,12 +294,26 @@ __global__ __launch_bounds__(256) void bnpool3_fwd_rows_kernel(
 // cell's 8 inputs share the 8 windows {a, a+1}^3, loaded once (not ~3.4x per input).  All
 // 24 loads of a cell are issued before any use (raw 16-byte registers), so a thread waits
 // for one memory round trip, not eight.
+template <int V>
+__device__ __forceinline__ void bnbwd_params(int C, int c0, const float* __restrict__ mean,
+                                             const float* __restrict__ invstd,
+                                             const float* __restrict__ coef, float* mu,
+                                             float* is, float* k0, float* k1, float* k2) {
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const int c = c0 + e;
+    mu[e] = mean[c]; is[e] = invstd[c];
+    k0[e] = coef[c]; k1[e] = coef[C + c]; k2[e] = coef[2 * C + c];
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void bnpool3s2_bwd_cell(
     const PoolG& g, const T* __restrict__ gp, const uint8_t* __restrict__ am,
     const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ coef, T* __restrict__ dy, int64_t nb, int ad, int ah, int aw,
-    int c0) {
+    int c0, const float* mu, const float* is, const float* k0, const float* k1,
+    const float* k2) {
   constexpr int V = Chunk<T>::N;
   uint64_t a8[8];
   u32x4 graw[8], yraw[8];
@@ -315,13 +337,6 @@ __device__ __forceinline__ void bnpool3s2_bwd_cell(
   float gv[8][V];
 #pragma unroll
   for (int q = 0; q < 8; ++q) Chunk<T>::load(reinterpret_cast<const T*>(&graw[q]), gv[q]);
-  float mu[V], is[V], k0[V], k1[V], k2[V];
-#pragma unroll
-  for (int e = 0; e < V; ++e) {
-    const int c = c0 + e;
-    mu[e] = mean[c]; is[e] = invstd[c];
-    k0[e] = coef[c]; k1[e] = coef[g.c + c]; k2[e] = coef[2 * g.c + c];
-  }
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const int rd = r >> 2, rh = (r >> 1) & 1, rw = r & 1;
@@ -366,7 +381,10 @@ __global__ __launch_bounds__(256) void bnpool3s2_bwd_apply_kernel(
     const int aw = (int)(v % cw); v /= cw;
     const int ah = (int)(v % ch); v /= ch;
     const int ad = (int)(v % cd);
-    bnpool3s2_bwd_cell<T>(g, gp, am, y, mean, invstd, coef, dy, v / cd, ad, ah, aw, c0);
+    float mu[V], is[V], k0[V], k1[V], k2[V];
+    bnbwd_params<V>(g.c, c0, mean, invstd, coef, mu, is, k0, k1, k2);
+    bnpool3s2_bwd_cell<T>(g, gp, am, y, mean, invstd, coef, dy, v / cd, ad, ah, aw, c0, mu, is,
+                          k0, k1, k2);
   }
 }
 
@@ -382,9 +400,12 @@ __global__ __launch_bounds__(256) void bnpool3s2_bwd_rows_kernel(
   const int ah = blockIdx.y, ad = blockIdx.z % cd;
   const int64_t nb = blockIdx.z / cd;
   const int items = cw << cv_shift, cmask = (1 << cv_shift) - 1;
+  const int c0 = (threadIdx.x & cmask) * V;      // fixed per thread (cv divides 256)
+  float mu[V], is[V], k0[V], k1[V], k2[V];
+  bnbwd_params<V>(g.c, c0, mean, invstd, coef, mu, is, k0, k1, k2);
   for (int e = threadIdx.x; e < items; e += 256)
-    bnpool3s2_bwd_cell<T>(g, gp, am, y, mean, invstd, coef, dy, nb, ad, ah, e >> cv_shift,
-                          (e & cmask) * V);
+    bnpool3s2_bwd_cell<T>(g, gp, am, y, mean, invstd, coef, dy, nb, ad, ah, e >> cv_shift, c0,
+                          mu, is, k0, k1, k2);
 }
 
 // Fused backward, dense pass: for every input voxel, g' = sum of the pooled gradients of the
