@@ -159,6 +159,11 @@ int mmad_bnpool_bwd_apply(int dtype, int n, int c, int di, int hi, int wi, int d
                           const void* y, const float* mean, const float* invstd,
                           const float* coef, void* dy, void* stream);
 int mmad_gap_fwd(int dtype, int n, int64_t s, int c, const void* x, float* y, void* stream);
+/* same, partitioned over voxel slabs so small batches still fill the GPU; ws holds
+ * mmad_gap_fwd_ws_elems(n, s, c) floats of partial sums (summed in a fixed order) */
+int64_t mmad_gap_fwd_ws_elems(int n, int64_t s, int c);
+int mmad_gap_fwd_ws(int dtype, int n, int64_t s, int c, const void* x, float* y, float* ws,
+                    void* stream);
 int mmad_gap_bwd(int dtype, int n, int64_t s, int c, const float* dy, void* dx, void* stream);
 
 /* ---- fusion / classifier MLP head (fp32) ----------------------------------------

@@ -74,6 +74,8 @@ _SIGS = {
     "mmad_bnpool_bwd_reduce": (_i32, [_i32, _i64, _i32] + [_vp] * 7),
     "mmad_bnpool_bwd_apply": (_i32, [_i32] * 12 + [_vp] * 8),
     "mmad_gap_fwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "mmad_gap_fwd_ws_elems": (_i64, [_i32, _i64, _i32]),
+    "mmad_gap_fwd_ws": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp, _vp]),
     "mmad_gap_bwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_linear_fwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp]),
     "mmad_linear_bwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

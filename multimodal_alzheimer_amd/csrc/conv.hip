@@ -718,32 +718,39 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
   }
 }
 
-// Same sum for many slabs: 4 groups of 64 lanes take every 4th slab of 64 consecutive
-// elements (independent load streams instead of one serial chain of `splits` loads per
-// thread -- 128 slabs of a 1x1x1 conv took 32 us as a chain), combined in fixed order.
+// Same sum for many slabs: 4 groups of 64 lanes take every 4th slab of 256 consecutive
+// elements, 16 bytes per lane per load (independent load streams instead of one serial
+// chain of `splits` 4-byte loads per thread -- 128 slabs of a 1x1x1 conv took 32 us as a
+// chain, and 4-byte loads left the slab pass TA-bound at ~2.5 TB/s), combined in fixed
+// order.  total % 4 == 0 (Nd % 8 == 0 is a wgrad precondition).
 __global__ __launch_bounds__(256) void wgrad_reduce_wide_kernel(
     const float* __restrict__ ws, float* __restrict__ dw, int splits, int Nd, int K, int Cs,
     int cs_shift, int taps, int unf_kw, int stride) {
-  __shared__ float red[4][64];
+  __shared__ f32x4 red[4][64];
   const int64_t total = (int64_t)Nd * K;
   const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int64_t idx = (int64_t)blockIdx.x * 64 + e;
-  float s = 0.f;
+  const int64_t idx = ((int64_t)blockIdx.x * 64 + e) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
   if (idx < total) {
 #pragma unroll 4
-    for (int sp = grp * stride; sp < splits; sp += 4 * stride) s += ws[sp * total + idx];
+    for (int sp = grp * stride; sp < splits; sp += 4 * stride)
+      s += *reinterpret_cast<const f32x4*>(ws + sp * total + idx);
   }
   red[grp][e] = s;
   __syncthreads();
   if (grp != 0 || idx >= total) return;
   s = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
-  const int co = (int)(idx / K), k = (int)(idx % K);
-  if (unf_kw > 0) {
-    const int j = k & 7, tkh = k >> 3;
-    if (j < unf_kw) dw[((int64_t)co * taps + tkh) * unf_kw + j] = s;
-  } else {
-    const int tap = k >> cs_shift, ci = k & (Cs - 1);
-    dw[((int64_t)co * Cs + ci) * taps + tap] = s;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t id = idx + q;
+    const int co = (int)(id / K), k = (int)(id % K);
+    if (unf_kw > 0) {
+      const int j = k & 7, tkh = k >> 3;
+      if (j < unf_kw) dw[((int64_t)co * taps + tkh) * unf_kw + j] = s[q];
+    } else {
+      const int tap = k >> cs_shift, ci = k & (Cs - 1);
+      dw[((int64_t)co * Cs + ci) * taps + tap] = s[q];
+    }
   }
 }
 
@@ -764,21 +771,25 @@ __global__ void slab_group_sum_kernel(float* __restrict__ ws, int splits, int64_
 }
 
 // Same sum, for the plain (not unfolded) layout: one block per (co, 64-channel slice);
-// slab reads run along ci (coalesced), the [ci][taps] result goes out through LDS as one
-// contiguous run of the torch tensor.
+// slab reads run along ci, 16 bytes per lane (a wave covers 4 taps x 64 channels), and the
+// [ci][taps] result goes out through LDS as one contiguous run of the torch tensor.
 __global__ __launch_bounds__(256) void wgrad_reduce_t_kernel(const float* __restrict__ ws,
                                                              float* __restrict__ dw, int splits,
                                                              int Nd, int K, int Cs, int taps) {
   __shared__ float tile[64 * 33];
-  const int ct = min(64, Cs), groups = 256 / ct;
+  const int ct = min(64, Cs);                  // channels in this slice (Cs % 16 == 0)
+  const int q4 = ct / 4, tpi = 256 / q4;       // lanes per tap row, taps per block pass
   const int co = blockIdx.y, c0 = blockIdx.x * ct;
-  const int e = threadIdx.x % ct, tg = threadIdx.x / ct;
+  const int e4 = threadIdx.x % q4, tg = threadIdx.x / q4;
   const int64_t total = (int64_t)Nd * K;
-  const float* base = ws + (int64_t)co * K + c0 + e;
-  for (int t = tg; t < taps; t += groups) {
-    float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += base[sp * total + (int64_t)t * Cs];
-    tile[e * (taps + 1) + t] = s;
+  const float* base = ws + (int64_t)co * K + c0 + e4 * 4;
+  for (int t = tg; t < taps; t += tpi) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int sp = 0; sp < splits; ++sp)
+      s += *reinterpret_cast<const f32x4*>(base + sp * total + (int64_t)t * Cs);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tile[(e4 * 4 + q) * (taps + 1) + t] = s[q];
   }
   __syncthreads();
   float* out = dw + ((int64_t)co * Cs + c0) * taps;
@@ -1399,12 +1410,14 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
                       : launch_wgrad<float, 128>(g, sp, x, dy, (float*)workspace, st);
   if (rc) return rc;
   const int64_t total = (int64_t)g.Nd * g.K;
-  if (!unfolded(d) && g.taps <= 32 && sp.splits <= 8)
+  // (the transposing reduce writes whole [ci][taps] runs of dW; scattered 4-byte dW stores
+  // from an element-wise reduce cost ~2x in partial-line writes)
+  if (!unfolded(d) && g.taps > 1 && g.taps <= 32)
     hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)cdiv(g.Cs, 64), (unsigned)g.Nd),
                        dim3(256), 0, st, (const float*)workspace, dw, sp.splits, g.Nd, g.K,
                        g.Cs, g.taps);
   else if (sp.splits >= 8)
-    hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)cdiv(total, 64)), dim3(256), 0,
+    hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
                        st, (const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.cs_shift,
                        g.taps, unfolded(d) ? d->kw : 0, 1);
   else

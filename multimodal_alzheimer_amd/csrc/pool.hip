@@ -484,6 +484,10 @@ __global__ __launch_bounds__(1024) void gap_fwd_kernel(int64_t S, int C, int CB,
                                                       float* __restrict__ y) {
   __shared__ float red[1024 * 8];
   const int n = blockIdx.y;
+  // blockIdx.z > 0 (gridDim.z = P partitions): this block sums voxel slab z of P and
+  // writes raw partial sums to y[(n*P + z)*C + c] (no division); see gap_fold_kernel
+  const int P = gridDim.z, part = blockIdx.z;
+  const int64_t v0 = S * part / P, v1 = S * (part + 1) / P;
   const int cb0 = blockIdx.x * CB;
   const int cw = min(CB, C - cb0);
   const int lpr = cw / V;
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(1024) void gap_fwd_kernel(int64_t S, int C, int CB,
 #pragma unroll
   for (int e = 0; e < V; ++e) s[e] = 0.f;
   if (rl < rpar) {
-    for (int64_t v = rl; v < S; v += rpar) {
+    for (int64_t v = v0 + rl; v < v1; v += rpar) {
       float val[V];
       load_v<T, V>(x + ((int64_t)n * S + v) * C + cb0 + cl * V, val);
 #pragma unroll
@@ -506,8 +510,20 @@ __global__ __launch_bounds__(1024) void gap_fwd_kernel(int64_t S, int C, int CB,
   for (int c = threadIdx.x; c < cw; c += blockDim.x) {
     float acc = 0.f;
     for (int k = 0; k < rpar; ++k) acc += red[k * cw + c];
-    y[(int64_t)n * C + cb0 + c] = acc / (float)S;
+    if (P == 1) y[(int64_t)n * C + cb0 + c] = acc / (float)S;
+    else y[((int64_t)n * P + part) * C + cb0 + c] = acc;
   }
+}
+
+// second level of the partitioned GAP: y[n][c] = (sum over p, in order, of ws[n][p][c]) / S
+__global__ void gap_fold_kernel(int n, int P, int C, int64_t S, const float* __restrict__ ws,
+                                float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n * C) return;
+  const int64_t b = i / C, c = i % C;
+  float acc = 0.f;
+  for (int p = 0; p < P; ++p) acc += ws[(b * P + p) * C + c];
+  y[i] = acc / (float)S;
 }
 
 template <typename T, int V>
@@ -620,9 +636,27 @@ int bnpool_bwd_apply(const PoolG& g, const void* gp, const uint8_t* am, const vo
   return launch_status();
 }
 
+// voxel-slab partitions so a (n, channel-chunk) grid of a few blocks becomes >= 512 blocks
+int gap_parts(int n, int64_t s, int c) {
+  const int64_t blocks = (int64_t)n * cdiv(c, std::min(c, 256));
+  int64_t p = cdiv(512, blocks);
+  p = std::min<int64_t>(p, std::max<int64_t>(1, s / 64));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(p, 1024));
+}
+
 template <typename T>
-int gap_fwd(int n, int64_t s, int c, const void* x, float* y, hipStream_t st) {
+int gap_fwd(int n, int64_t s, int c, const void* x, float* y, hipStream_t st, float* ws = nullptr,
+            int P = 1) {
   constexpr int VEC = Chunk<T>::N;
+  if (ws != nullptr && P > 1 && c % VEC == 0) {
+    const int cb = std::min(c, 256);
+    if (cb % VEC) return MMAD_EUNSUPPORTED;
+    hipLaunchKernelGGL((gap_fwd_kernel<T, VEC>), dim3((unsigned)cdiv(c, cb), (unsigned)n,
+                       (unsigned)P), dim3(1024), 0, st, s, c, cb, (const T*)x, ws);
+    hipLaunchKernelGGL(gap_fold_kernel, dim3((unsigned)cdiv((int64_t)n * c, 256)), dim3(256), 0, st,
+                       n, P, c, s, ws, y);
+    return launch_status();
+  }
   if (c % VEC == 0) {
     const int cb = std::min(c, 256);
     if (cb % VEC) return MMAD_EUNSUPPORTED;
@@ -707,6 +741,21 @@ int mmad_gap_fwd(int dtype, int n, int64_t s, int c, const void* x, float* y, vo
   if (!x || !y) return MMAD_ENULL;
   if (dtype == MMAD_BF16) return gap_fwd<u16>(n, s, c, x, y, as_stream(stream));
   if (dtype == MMAD_F32) return gap_fwd<float>(n, s, c, x, y, as_stream(stream));
+  return MMAD_EBADDTYPE;
+}
+
+int64_t mmad_gap_fwd_ws_elems(int n, int64_t s, int c) {
+  if (n <= 0 || s <= 0 || c <= 0) return -1;
+  return (int64_t)n * gap_parts(n, s, c) * c;
+}
+
+int mmad_gap_fwd_ws(int dtype, int n, int64_t s, int c, const void* x, float* y, float* ws,
+                    void* stream) {
+  if (n <= 0 || s <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!x || !y || !ws) return MMAD_ENULL;
+  const int P = gap_parts(n, s, c);
+  if (dtype == MMAD_BF16) return gap_fwd<u16>(n, s, c, x, y, as_stream(stream), ws, P);
+  if (dtype == MMAD_F32) return gap_fwd<float>(n, s, c, x, y, as_stream(stream), ws, P);
   return MMAD_EBADDTYPE;
 }
 

@@ -482,7 +482,10 @@ class _GapFn(torch.autograd.Function):
         n, c = x.shape[:2]
         s = x.numel() // (n * c)
         y = torch.empty((n, c, 1, 1, 1), dtype=torch.float32, device=x.device)
-        L.call("mmad_gap_fwd", L.dtype_code(x.dtype), n, s, c, L.ptr(x), L.ptr(y), L.stream())
+        ws = torch.empty(L.load().mmad_gap_fwd_ws_elems(n, s, c), dtype=torch.float32,
+                         device=x.device)
+        L.call("mmad_gap_fwd_ws", L.dtype_code(x.dtype), n, s, c, L.ptr(x), L.ptr(y), L.ptr(ws),
+               L.stream())
         ctx.shape = tuple(x.shape)
         ctx.dtype = x.dtype
         return y

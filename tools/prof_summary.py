@@ -84,11 +84,43 @@ def traffic(fetch_dir, write_dir):
                           "scrubbed before each launch (cold)"}
 
 
+def step(d):
+    """Kernels of the last complete step, in launch order, with durations (us)."""
+    rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    # a step ends with the fused Adam launch(es); take the span between the last two
+    ends = [i for i, r in enumerate(rows) if "FusedAdam" in r["Kernel_Name"] or
+            "FusedOptimizerTensorListMetadata" in r["Kernel_Name"]]
+    if len(ends) < 4:
+        sel = rows
+    else:
+        # group consecutive optimizer launches; step = after the 2nd-last group to the last
+        groups, cur = [], [ends[0]]
+        for e in ends[1:]:
+            if e - cur[-1] <= 3:
+                cur.append(e)
+            else:
+                groups.append(cur)
+                cur = [e]
+        groups.append(cur)
+        sel = rows[groups[-2][-1] + 1:groups[-1][-1] + 1]
+    out, tot = [], 0.0
+    for r in sel:
+        us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        tot += us
+        out.append(f"{us:8.1f}  g={r['Grid_Size_X']:>8}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']}  "
+                   f"{short(r['Kernel_Name']).split('(')[0][:90]}")
+    out.append(f"step kernels: {len(sel)}, sum {tot:.1f} us")
+    return "\n".join(out)
+
+
 if __name__ == "__main__":
     mode = sys.argv[1]
     if mode == "stats":
         print(stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 30))
     elif mode == "dominant":
         print(dominant(sys.argv[2], int(sys.argv[3]), *sys.argv[4:5]))
+    elif mode == "step":
+        print(step(sys.argv[2]))
     elif mode == "traffic":
         print(json.dumps(traffic(sys.argv[2], sys.argv[3]), indent=1))
