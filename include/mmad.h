@@ -196,6 +196,24 @@ int mmad_loss_fwd(int b, int c, const double* logits, const int64_t* labels,
                   const double* weight, double gamma, int mode, double* loss,
                   double* dlogits, void* stream);
 
+/* ---- input pipeline normalisation (float64, batched over scans) -------------------
+ * Replaces MultiModalDataset.__getitem__'s per-sample CPU normalisation
+ * (pkg/utils/dataloader.py:213-215 PET, :244-270 MRI per-scan, :272-277 MRI all-scan).
+ * x, mask, out: [nscan][vox] float64 (out may alias x).  ws: mmad_norm_ws_bytes bytes.
+ * min_max: v = nonzero(x*mask); lo/hi = torch.quantile(v, 1-q / q, 'linear') as exact
+ *          order statistics (radix select) -> out = clamp((x-lo)/(hi-lo), 0, 1) * mask;
+ *          q_out (optional, device) receives (lo, hi) per scan.  Bit-exact with the
+ *          reference.  A scan with no nonzero masked voxel: out = NaN (torch raises).
+ * zscore : out = (x - mean(v)) / std(v) * mask, unbiased std.
+ * affine : out = (x - mean) / std over n elements (PET split statistics, all-scan MRI). */
+int64_t mmad_norm_ws_bytes(int nscan, int64_t vox);
+int mmad_mri_minmax_norm(int nscan, int64_t vox, const double* x, const double* mask,
+                         double q, double* out, void* ws, double* q_out, void* stream);
+int mmad_mri_zscore_norm(int nscan, int64_t vox, const double* x, const double* mask,
+                         double* out, void* ws, void* stream);
+int mmad_affine_norm(int64_t n, const double* x, double mean, double stdv, double* out,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -75,6 +75,10 @@ _SIGS = {
     "mmad_bnpool_bwd_apply": (_i32, [_i32] * 12 + [_vp] * 8),
     "mmad_gap_fwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_gap_fwd_ws_elems": (_i64, [_i32, _i64, _i32]),
+    "mmad_norm_ws_bytes": (_i64, [_i32, _i64]),
+    "mmad_mri_minmax_norm": (_i32, [_i32, _i64, _vp, _vp, _f64, _vp, _vp, _vp, _vp]),
+    "mmad_mri_zscore_norm": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_affine_norm": (_i32, [_i64, _vp, _f64, _f64, _vp, _vp]),
     "mmad_gap_fwd_ws": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp, _vp]),
     "mmad_gap_bwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_linear_fwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp]),
