@@ -88,6 +88,20 @@ int64_t mmad_conv3d_stats_rows(const mmad_conv_desc* d, int dtype);
 int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x,
                     const void* w_packed, const float* bias, void* y, float* stats,
                     void* stream);
+/* Eval-mode fused conv + BN (+ residual) + ReLU (BasicBlock / shortcut in .eval(), running
+ * statistics): weights packed with the BN scale folded in (mmad_conv_pack_weight_scaled,
+ * forward layout), `bias` = the folded BN shift (mmad_bn_fold); the epilogue adds `res`
+ * (output-shaped NDHWC, may be NULL) and applies ReLU when `relu` != 0.  Not for the
+ * Cin = 1 stem.  Replaces the eval forward of anat_cnn.py:29-31's backbone blocks. */
+int mmad_conv3d_fwd_ex(const mmad_conv_desc* d, int dtype, const void* x,
+                       const void* w_packed, const float* bias, const void* res, int relu,
+                       void* y, float* stats, void* stream);
+int mmad_conv_pack_weight_scaled(const mmad_conv_desc* d, int dtype, const float* w,
+                                 const float* scale, void* w_packed, int for_dgrad,
+                                 void* stream);
+int mmad_bn_fold(int c, const float* gamma, const float* beta, const float* running_mean,
+                 const float* running_var, float eps, const float* conv_bias, float* scale,
+                 float* bias, void* stream);
 int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy,
                       const void* w_packed_t, void* dx, void* stream);
 int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype); /* bytes */

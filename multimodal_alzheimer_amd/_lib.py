@@ -16,6 +16,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libmmad_hip.so")
 
 F32, BF16, F64 = 0, 1, 2
+EUNSUPPORTED = 1004
 EHIP = 2000
 _HIP_OOM = 2   # hipErrorOutOfMemory
 
@@ -75,6 +76,9 @@ _SIGS = {
     "mmad_bnpool_bwd_apply": (_i32, [_i32] * 12 + [_vp] * 8),
     "mmad_gap_fwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_gap_fwd_ws_elems": (_i64, [_i32, _i64, _i32]),
+    "mmad_conv3d_fwd_ex": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "mmad_conv_pack_weight_scaled": (_i32, [_P, _i32, _vp, _vp, _vp, _i32, _vp]),
+    "mmad_bn_fold": (_i32, [_i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
     "mmad_norm_ws_bytes": (_i64, [_i32, _i64]),
     "mmad_mri_minmax_norm": (_i32, [_i32, _i64, _vp, _vp, _f64, _vp, _vp, _vp, _vp]),
     "mmad_mri_zscore_norm": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp, _vp]),

@@ -210,6 +210,25 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
   if (shift_out) shift_out[c] = bt - (float)mean * gm * is;
 }
 
+// eval-mode BN folded into the preceding conv: scale = gamma / sqrt(var + eps),
+// bias = beta - mean*scale (+ conv_bias*scale); the same arithmetic as bn_finalize_kernel's
+// running-statistics branch, so folded and unfolded eval paths use identical coefficients
+__global__ void bn_fold_kernel(int C, const float* __restrict__ gamma,
+                               const float* __restrict__ beta, const float* __restrict__ mean,
+                               const float* __restrict__ var, float eps,
+                               const float* __restrict__ conv_bias, float* __restrict__ scale,
+                               float* __restrict__ bias) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float is = (float)(1.0 / sqrt((double)var[c] + (double)eps));
+  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  const float sc = gm * is;
+  float sh = bt - mean[c] * gm * is;
+  if (conv_bias) sh += conv_bias[c] * sc;
+  scale[c] = sc;
+  bias[c] = sh;
+}
+
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     int C, int64_t count, int nparts, const float* __restrict__ parts,
     const float* __restrict__ gamma, const float* __restrict__ invstd, int training,
@@ -601,6 +620,17 @@ int mmad_bnpool_bwd_reduce(int dtype, int64_t m, int c, const void* g, const uin
                                  argmax);
   return launch_colsum<float, 3>(m, c, ymax, g, nullptr, mean, invstd, parts, as_stream(stream),
                                  argmax);
+}
+
+int mmad_bn_fold(int c, const float* gamma, const float* beta, const float* running_mean,
+                 const float* running_var, float eps, const float* conv_bias, float* scale,
+                 float* bias, void* stream) {
+  if (c <= 0) return MMAD_EBADSHAPE;
+  if (!running_mean || !running_var || !scale || !bias) return MMAD_ENULL;
+  hipLaunchKernelGGL(bn_fold_kernel, dim3((unsigned)cdiv(c, 256)), dim3(256), 0,
+                     as_stream(stream), c, gamma, beta, running_mean, running_var, eps, conv_bias,
+                     scale, bias);
+  return launch_status();
 }
 
 int mmad_bn_bwd_finalize(int c, int64_t count, int nparts, const float* parts,

@@ -111,6 +111,25 @@ template <> struct Chunk<u16> {
   }
 };
 
+// epilogue of a fused eval-mode conv: 8 bf16 outputs (+ 8 bf16 residuals) (-> ReLU)
+__device__ __forceinline__ u32x4 epi_res_relu(u32x4 v, const u16* res, int relu) {
+  float f[8];
+  Chunk<u16>::load(reinterpret_cast<const u16*>(&v), f);
+  if (res != nullptr) {
+    float r[8];
+    Chunk<u16>::load(res, r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] += r[e];
+  }
+  if (relu) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+  }
+  u32x4 o;
+  Chunk<u16>::store(reinterpret_cast<u16*>(&o), f);
+  return o;
+}
+
 // BN affine (+ReLU) of one value, shared by every kernel that applies a BN so the fused and
 // unfused paths round identically: o = fma(y, scale, shift), relu -> max(o, 0).
 __device__ __forceinline__ float bn_affine(float y, float scale, float shift) {

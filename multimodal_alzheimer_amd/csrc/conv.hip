@@ -47,6 +47,10 @@ struct Geom {
   int Ds, Hs, Ws, Dd, Hd, Wd;
   int KD, KH, KW;
   int sd, sh, sw, pd, ph, pw, dd, dh, dw;
+  // forward epilogue extras (eval-mode fused conv+BN(+residual)+ReLU): residual tensor
+  // shaped like the output (added after bias), ReLU flag
+  const void* res;
+  int relu;
 };
 
 enum { FWD = 0, DGRAD = 1 };
@@ -353,7 +357,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
         const float v = acc[i][j][r] + bv;
         if (lds_out) ctile[row * (CROW / 2) + col] = f2bf(v);
         if (m < Mc && co < g.Nd) {
-          if (!lds_out) Elt<T>::st(dst, dst_row(m) * g.Nd + co, v);
+          if (!lds_out) {
+            const int64_t o = dst_row(m) * g.Nd + co;
+            float w = v;
+            if (MODE == FWD && g.res != nullptr) w += Elt<T>::ld((const T*)g.res, o);
+            if (MODE == FWD && g.relu) w = fmaxf(w, 0.f);
+            Elt<T>::st(dst, o, w);
+          }
           cs[j] += v;
           cq[j] += v * v;
         }
@@ -367,10 +377,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
       const int q = tid + NT * h;
       const int row = q / CPR, c8 = q % CPR;
       const int m = m0 + row, co = n0 + c8 * 8;
-      if (m < Mc && co < g.Nd)
-        *reinterpret_cast<u32x4*>(reinterpret_cast<u16*>(dst) + dst_row(m) * g.Nd + co) =
-            *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) + row * CROW +
-                                            c8 * 16);
+      if (m < Mc && co < g.Nd) {
+        const int64_t o = dst_row(m) * g.Nd + co;
+        u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
+                                                  row * CROW + c8 * 16);
+        if (MODE == FWD && (g.res != nullptr || g.relu))
+          v = epi_res_relu(v, g.res ? reinterpret_cast<const u16*>(g.res) + o : nullptr, g.relu);
+        *reinterpret_cast<u32x4*>(reinterpret_cast<u16*>(dst) + o) = v;
+      }
     }
   }
   if (stats != nullptr) {
@@ -830,16 +844,18 @@ template <typename T>
 __global__ __launch_bounds__(256) void pack_transpose_kernel(const float* __restrict__ w,
                                                              T* __restrict__ wp, int R, int Cc,
                                                              int64_t ob, int jd, int64_t oj1,
-                                                             int oj2, int flip) {
+                                                             int oj2, int flip,
+                                                             const float* __restrict__ scale) {
   __shared__ float tile[64][65];
   const int b = blockIdx.z;
+  const float sb = scale != nullptr ? scale[b] : 1.f;    // per-output-channel (forward layout)
   const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
   const float* src = w + (int64_t)b * R * Cc;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
 #pragma unroll
   for (int r = ty; r < 64; r += 4) {
     const int i = i0 + r, j = j0 + tx;
-    tile[r][tx] = (i < R && j < Cc) ? src[(int64_t)i * Cc + j] : 0.f;
+    tile[r][tx] = (i < R && j < Cc) ? src[(int64_t)i * Cc + j] * sb : 0.f;
   }
   __syncthreads();
 #pragma unroll
@@ -1196,8 +1212,16 @@ int64_t mmad_conv_packed_elems(const mmad_conv_desc* d, int dtype, int for_dgrad
   return (int64_t)g.Nd * g.Kpad;
 }
 
+int mmad_conv_pack_weight_scaled(const mmad_conv_desc* d, int dtype, const float* w,
+                                 const float* scale, void* wp, int for_dgrad, void* stream);
+
 int mmad_conv_pack_weight(const mmad_conv_desc* d, int dtype, const float* w, void* wp,
                           int for_dgrad, void* stream) {
+  return mmad_conv_pack_weight_scaled(d, dtype, w, nullptr, wp, for_dgrad, stream);
+}
+
+int mmad_conv_pack_weight_scaled(const mmad_conv_desc* d, int dtype, const float* w,
+                                 const float* scale, void* wp, int for_dgrad, void* stream) {
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!w || !wp) return MMAD_ENULL;
@@ -1207,6 +1231,7 @@ int mmad_conv_pack_weight(const mmad_conv_desc* d, int dtype, const float* w, vo
   const int mode = for_dgrad ? 1 : (unfolded(d) ? 2 : 0);
   const int flip = for_dgrad && dgrad_as_fwd(d);
   const int64_t total = (int64_t)g.Nd * g.Kpad;
+  if (scale != nullptr && (mode != 0 || g.Kpad != g.K)) return MMAD_EUNSUPPORTED;
   if (mode != 2 && g.Kpad == g.K) {
     // forward: per co, [Ci][taps] -> [taps][Ci]; dgrad: [Co][Ci*taps] -> [Ci][taps][Co]
     const int R = mode == 0 ? d->ci : d->co;
@@ -1217,10 +1242,10 @@ int mmad_conv_pack_weight(const mmad_conv_desc* d, int dtype, const float* w, vo
     dim3 grid((unsigned)cdiv(Cc, 64), (unsigned)cdiv(R, 64), (unsigned)B);
     if (dtype == MMAD_BF16)
       hipLaunchKernelGGL(pack_transpose_kernel<u16>, grid, dim3(256), 0, as_stream(stream), w,
-                         (u16*)wp, R, Cc, ob, jd, oj1, oj2, flip);
+                         (u16*)wp, R, Cc, ob, jd, oj1, oj2, flip, scale);
     else
       hipLaunchKernelGGL(pack_transpose_kernel<float>, grid, dim3(256), 0, as_stream(stream), w,
-                         (float*)wp, R, Cc, ob, jd, oj1, oj2, flip);
+                         (float*)wp, R, Cc, ob, jd, oj1, oj2, flip, scale);
     return launch_status();
   }
   if (dtype == MMAD_BF16)
@@ -1331,6 +1356,27 @@ int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x, const voi
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
   if (!unfolded(d) && use_patch(g, dtype))
     return mmad_patch::fwd(patch_geo(g), x, wp, bias, y, stats, stream);
+  return run_igemm<FWD>(g, dtype, g.M, 1, x, wp, bias, y, stats, as_stream(stream));
+}
+
+int mmad_conv3d_fwd_ex(const mmad_conv_desc* d, int dtype, const void* x, const void* wp,
+                       const float* bias, const void* res, int relu, void* y, float* stats,
+                       void* stream) {
+  if (!desc_ok(d)) return MMAD_EBADSHAPE;
+  if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
+  if (!x || !wp || !y) return MMAD_ENULL;
+  if (res == nullptr && !relu) return mmad_conv3d_fwd(d, dtype, x, wp, bias, y, stats, stream);
+  if (unfolded(d)) return MMAD_EUNSUPPORTED;     // the stem keeps its own epilogue
+  Geom g = fwd_geom(d, dtype);
+  if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
+  g.res = res;
+  g.relu = relu ? 1 : 0;
+  if (use_patch(g, dtype)) {
+    mmad_patch::Geo q = patch_geo(g);
+    q.res = res;
+    q.relu = g.relu;
+    return mmad_patch::fwd(q, x, wp, bias, y, stats, stream);
+  }
   return run_igemm<FWD>(g, dtype, g.M, 1, x, wp, bias, y, stats, as_stream(stream));
 }
 

@@ -12,6 +12,8 @@ struct Geo {
   int nb, Cs, Nd, Kpad;           // input channels, output channels, packed weight row
   int Ds, Hs, Ws, Dd, Hd, Wd;     // source / destination extents
   int KD, KH, KW, pd, ph, pw, dd, dh, dw;
+  const void* res = nullptr;      // eval-mode epilogue: residual (output-shaped) and ReLU
+  int relu = 0;
 };
 // true when the geometry is handled (and the kernel is switched on, MMAD_PATCH)
 bool ok(const Geo& g);

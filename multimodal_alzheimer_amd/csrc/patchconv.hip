@@ -45,6 +45,8 @@ struct PG {
   int PZ, PY, PX, prow8;     // patch extents; patch DMA instructions (8 rows each)
   int ntz, nty, ntx, nbn, taps, nchunk;
   int ring_off;              // LDS byte offset of the weight ring
+  const u16* res;            // eval-mode epilogue extras (see patchconv.h)
+  int relu;
 };
 
 __device__ const u32x4 g_zero16[8] = {};
@@ -234,10 +236,13 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
     const int row = q / CPR, c8 = q % CPR;
     const int co = n0 + c8 * 8;
     int64_t dv;
-    if (dst_vox(row, dv) && co < g.Nd)
-      *reinterpret_cast<u32x4*>(dst + dv * g.Nd + co) =
-          *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) + row * CROW +
-                                          c8 * 16);
+    if (dst_vox(row, dv) && co < g.Nd) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
+                                                row * CROW + c8 * 16);
+      if (g.res != nullptr || g.relu)
+        v = epi_res_relu(v, g.res ? g.res + dv * g.Nd + co : nullptr, g.relu);
+      *reinterpret_cast<u32x4*>(dst + dv * g.Nd + co) = v;
+    }
   }
   if (stats != nullptr) {
     float* red = reinterpret_cast<float*>(smem + TV * CROW);
@@ -300,6 +305,8 @@ PG make_pg(const mmad_patch::Geo& q) {
   g.taps = q.KD * q.KH * q.KW;
   g.nchunk = q.Cs / 64;
   g.ring_off = g.prow8 * 1024;
+  g.res = reinterpret_cast<const u16*>(q.res);
+  g.relu = q.relu;
   return g;
 }
 

@@ -34,6 +34,16 @@ def _conv(cin, cout, k, stride=1, dilation=1):
                       dilation=dilation, bias=False)
 
 
+# Eval-mode (inference, running statistics, no autograd) blocks run each conv+BN(+res)+ReLU
+# as one kernel (volume_ops.conv_bn_act_eval); False forces the training-style ops.
+EVAL_FUSED = True
+
+
+def _eval_fused_ok(block, x):
+    return (EVAL_FUSED and not block.training and not torch.is_grad_enabled() and x.is_cuda
+            and x.dim() == 5)
+
+
 def _conv_bn_act(conv, bn, x, relu=True, res=None, res_conv=None, res_bn=None, res_x=None):
     y, parts = conv.forward_stats(x)
     if res_conv is not None:
@@ -57,11 +67,29 @@ class BasicBlock(nn.Module):
         self.dilation = dilation
 
     def forward(self, x):
+        if _eval_fused_ok(self, x):
+            y = self._eval_fused(x)
+            if y is not None:
+                return y
         h = _conv_bn_act(self.conv1, self.bn1, x)
         if self.downsample is None:
             return _conv_bn_act(self.conv2, self.bn2, h, res=x)
         return _conv_bn_act(self.conv2, self.bn2, h, res_conv=self.downsample[0],
                             res_bn=self.downsample[1], res_x=x)
+
+    def _eval_fused(self, x):
+        """3 (or 2) kernels per block instead of 4-5 conv / BN / add passes: BN folded into
+        the conv weights, residual add + ReLU in the conv epilogue."""
+        h = V.conv_bn_act_eval(x, self.conv1, self.bn1, relu=True)
+        if h is None:
+            return None
+        if self.downsample is None:
+            res = x if x.dtype == h.dtype else None
+        else:
+            res = V.conv_bn_act_eval(x, self.downsample[0], self.downsample[1], relu=False)
+        if res is None:
+            return None
+        return V.conv_bn_act_eval(h, self.conv2, self.bn2, relu=True, res=res)
 
 
 class Bottleneck(nn.Module):
@@ -137,7 +165,7 @@ class ResNet(nn.Module):
         """stem + 4 stages: (N,1,D,H,W) raw volume (f64/f32) -> (N,C,D/8,H/8,W/8) NDHWC."""
         # conv1 -> bn1 -> relu -> maxpool: BN, ReLU and the pool run as one pass over the
         # conv output (volume_ops.batchnorm_relu_maxpool)
-        if self.conv1.weight.is_cuda:
+        if self.conv1.weight.is_cuda and not _eval_fused_ok(self, x):
             V.prepack(self)          # every conv weight repacked in one launch per step
         y, parts = self.conv1.forward_stats(x)
         mp = self.maxpool

@@ -66,6 +66,10 @@ def _desc_tuple(d):
 # geometry appends a (start, end) HIP event pair recorded on the launch stream around it.
 FWD_PROBES = {}
 
+# training-mode BN statistic updates so far (the running buffers are written by our kernels,
+# which torch's tensor version counters do not see); keys the eval-mode folded-weight caches
+_BN_UPDATES = [0]
+
 
 def pack_weight(d, dt_code, weight, cdtype, for_dgrad):
     lib = L.load()
@@ -248,6 +252,66 @@ def conv3d(x, weight, bias=None, stride=(1, 1, 1), padding=(0, 0, 0), dilation=(
                            cdtype, want_stats, packed)
 
 
+def conv_bn_act_eval(x, conv, bn, relu=True, res=None):
+    """Eval-mode conv -> BN (running statistics) [-> + res] [-> ReLU] as ONE kernel: the BN
+    scale is folded into the packed weights and its shift into the conv bias
+    (mmad_bn_fold + mmad_conv_pack_weight_scaled), the residual add and ReLU run in the
+    conv epilogue (mmad_conv3d_fwd_ex).  Inference only (no autograd).  Returns None when
+    the layer is not eligible (Cin = 1 stem, batch-statistics BN, unsupported packing), so
+    the caller falls back to the unfused ops."""
+    if bn.training or bn.running_mean is None or torch.is_grad_enabled():
+        return None
+    cd = conv.compute_dtype
+    if x.shape[1] == 1:
+        return None
+    if x.dtype != cd:
+        x = _cast_raw(x, cd)
+    _check_vol(x, cd)
+    if res is not None:
+        _check_vol(res, cd)
+    lib = L.load()
+    d = conv_desc(tuple(x.shape), tuple(conv.weight.shape), conv._stride3(), conv._pads(),
+                  conv._dilation3())
+    dt = L.dtype_code(cd)
+    # folded weights are cached until a weight / BN tensor changes: in-place optimizer
+    # updates and load_state_dict bump tensor versions; the running statistics are
+    # rewritten by our BN kernels (invisible to torch), counted in _BN_UPDATES
+    key = (cd, conv.weight.data_ptr(), conv.weight._version,
+           None if conv.bias is None else conv.bias._version,
+           None if bn.weight is None else bn.weight._version,
+           None if bn.bias is None else bn.bias._version,
+           bn.running_mean._version, bn.running_var._version, _BN_UPDATES[0])
+    cached = getattr(conv, "_eval_fold", None)
+    if cached is not None and cached[0] == key:
+        wp, bias = cached[1], cached[2]
+        y = _empty_vol(d.n, d.co, d.do_, d.ho, d.wo, cd, x.device)
+        L.call("mmad_conv3d_fwd_ex", d, dt, L.ptr(x), L.ptr(wp), L.ptr(bias), L.ptr(res),
+               int(relu), L.ptr(y), None, L.stream())
+        return y
+    c = d.co
+    scale = torch.empty(c, dtype=torch.float32, device=x.device)
+    bias = torch.empty_like(scale)
+    cb = None if conv.bias is None else conv.bias.detach()
+    L.call("mmad_bn_fold", c, L.ptr(None if bn.weight is None else bn.weight.detach()),
+           L.ptr(None if bn.bias is None else bn.bias.detach()), L.ptr(bn.running_mean),
+           L.ptr(bn.running_var), float(bn.eps), L.ptr(cb), L.ptr(scale), L.ptr(bias),
+           L.stream())
+    n = lib.mmad_conv_packed_elems(d, dt, 0)
+    if n < 0:
+        return None
+    wp = torch.empty(n, dtype=cd, device=x.device)
+    rc = lib.mmad_conv_pack_weight_scaled(d, dt, L.ptr(conv.weight.detach().contiguous()),
+                                          L.ptr(scale), L.ptr(wp), 0, L.stream())
+    if rc == L.EUNSUPPORTED:
+        return None
+    L.check(rc, "mmad_conv_pack_weight_scaled")
+    conv._eval_fold = (key, wp, bias)
+    y = _empty_vol(d.n, d.co, d.do_, d.ho, d.wo, cd, x.device)
+    L.call("mmad_conv3d_fwd_ex", d, dt, L.ptr(x), L.ptr(wp), L.ptr(bias), L.ptr(res), int(relu),
+           L.ptr(y), None, L.stream())
+    return y
+
+
 # ----------------------------------------------------------------------------- batchnorm
 def _rows(t):
     c = t.shape[1]
@@ -280,6 +344,7 @@ def _finalize(y, parts, bn, training):
             parts = folded
         update = training and bn.track_running_stats and bn.running_mean is not None
         if update:
+            _BN_UPDATES[0] += 1
             if bn.momentum is None:
                 raise L.MMADError("BatchNorm momentum=None (cumulative average) unsupported")
         nbt = None

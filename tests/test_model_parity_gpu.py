@@ -179,3 +179,31 @@ def test_two_backbone_fusion_and_three_branch_run():
     o5 = m5.general_step(b, 0, "train")
     o5["loss"].backward()
     assert torch.isfinite(o5["loss"])
+
+
+def test_eval_fused_blocks_match_unfused():
+    """Eval-mode BasicBlocks (BN folded into the conv, residual + ReLU in the epilogue) vs
+    the training-style op sequence on the same trained weights and running statistics."""
+    from multimodal_alzheimer_amd import medicalnet
+    for precision, tol in ((torch.float32, 2e-5), (torch.bfloat16, 3e-2)):
+        torch.manual_seed(3)
+        h = G.anat_hparams(10)
+        m = M.Anat_CNN(h)
+        M.layers.set_compute_dtype(m, precision)
+        m = m.to(DEV)
+        batch = {"mri": torch.rand((2, 32, 32, 32), dtype=torch.float64, device=DEV),
+                 "label": torch.tensor([0, 1], device=DEV)}
+        opt = m.configure_optimizers()
+        for _ in range(3):                       # non-trivial running statistics
+            opt.zero_grad()
+            m.general_step(batch, 0, "train")["loss"].backward()
+            opt.step()
+        m.eval()
+        with torch.no_grad():
+            medicalnet.EVAL_FUSED = True
+            fused = m.general_step(batch, 0, "val")["outputs"].float()
+            medicalnet.EVAL_FUSED = False
+            ref = m.general_step(batch, 0, "val")["outputs"].float()
+            medicalnet.EVAL_FUSED = True
+        err = (fused - ref).abs().max().item()
+        assert err <= tol * max(1.0, ref.abs().max().item()), (precision, err)
