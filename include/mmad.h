@@ -193,6 +193,32 @@ int mmad_concat_cols(int b, int n_in, const float* const* srcs, const int* width
 int mmad_split_cols(int b, int n_out, const float* src, float* const* dsts,
                     const int* widths, void* stream);
 
+/* ---- voxel-level PET-MRI fusion (fusion.hip) ----------------------------------------
+ * mmad_gather_channels: torch.stack((x_pet, x_mri), dim=1).to(float32) of PET_MRI_EF
+ * (pkg/models/fusion_models/early_fusion.py:77-80) written straight into the NDHWC layout
+ * of the Cin = 2 conv (:35), channels padded to cpad = 8 with zeros: source plane c is
+ * srcs[c] + b*batch_stride + v*vox_stride (elements), v over the n*vox voxels; in dtype
+ * f64/f32/bf16 -> out dtype f32/bf16 (f64 -> f32 -> bf16 rounding, as torch).
+ * mmad_pad_rows: dst[r][j] = j < cin ? src[r][j] : 0 for j < cout (pads a conv weight's
+ * Ci -- [Co][Ci*taps] rows -- and cuts the padded weight gradient back).
+ * mmad_concat_channels / mmad_split_channels: torch.cat((a, b), dim=1) of two NDHWC
+ * volumes and its backward ('concatenate' fusion, anat_pet_featuremapfusion.py:112-113).
+ * mmad_max2_fwd / _bwd: torch.max(torch.stack((a, b)), dim=0) ('maxout' fusion, :115-117):
+ * ties and NaN follow torch (ties -> a; NaN propagates); sel[i] = 1 where b was taken; the
+ * gradient goes to the selected operand only.  n % (16 / sizeof(dtype)) == 0.          */
+int mmad_gather_channels(int in_dtype, int nsrc, const void* const* srcs,
+                         int64_t batch_stride, int64_t vox_stride, int n, int64_t vox,
+                         int cpad, int out_dtype, void* dst, void* stream);
+int mmad_pad_rows(int rows, int cin, int cout, const float* src, float* dst, void* stream);
+int mmad_concat_channels(int dtype, int64_t rows, int ca, const void* a, int cb,
+                         const void* b, void* dst, void* stream);
+int mmad_split_channels(int dtype, int64_t rows, int ca, int cb, const void* src, void* a,
+                        void* b, void* stream);
+int mmad_max2_fwd(int dtype, int64_t n, const void* a, const void* b, void* y, uint8_t* sel,
+                  void* stream);
+int mmad_max2_bwd(int dtype, int64_t n, const void* g, const uint8_t* sel, void* ga, void* gb,
+                  void* stream);
+
 /* ---- dtype casts / dropout ------------------------------------------------------ */
 int mmad_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);
 int mmad_dropout_fwd(int dtype, int64_t n, float p, uint64_t seed, const void* x, void* y,

@@ -7,7 +7,8 @@ LightningModule classes (see classifiers.py) and the MedicalNet API (medicalnet.
 """
 from . import _lib, head_ops, layers, medicalnet, preprocess, volume_ops  # noqa: F401
 from .classifiers import (All_Modalities_Fusion, Anat_CNN, Anat_PET_CNN, Base_Model,  # noqa
-                          FocalLoss, PET_CNN_ResNet, PET_MRI_ResNet_Fusion,
+                          FocalLoss, PET_CNN_ResNet, PET_MRI_EF, PET_MRI_FMF,
+                          PET_MRI_ResNet_Fusion,
                           Random_Benchmark_All_CN, Small_PET_CNN, Tabular_MLP)
 
 __version__ = "0.1.0"

@@ -93,6 +93,13 @@ _SIGS = {
     "mmad_dropout_fwd": (_i32, [_i32, _i64, _f32, _u64, _vp, _vp, _vp, _vp]),
     "mmad_dropout_bwd": (_i32, [_i32, _i64, _f32, _vp, _vp, _vp, _vp]),
     "mmad_loss_fwd": (_i32, [_i32, _i32, _vp, _vp, _vp, _f64, _i32, _vp, _vp, _vp]),
+    "mmad_gather_channels": (_i32, [_i32, _i32, _vp, _i64, _i64, _i32, _i64, _i32, _i32, _vp,
+                                    _vp]),
+    "mmad_pad_rows": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp]),
+    "mmad_concat_channels": (_i32, [_i32, _i64, _i32, _vp, _i32, _vp, _vp, _vp]),
+    "mmad_split_channels": (_i32, [_i32, _i64, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "mmad_max2_fwd": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_max2_bwd": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp, _vp]),
 }
 EXPORTS = tuple(_SIGS)
 

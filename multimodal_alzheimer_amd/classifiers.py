@@ -432,6 +432,159 @@ class Anat_PET_CNN(Base_Model):
                                self.hparams)
 
 
+def _small_cnn_stack(hparams, n_in):
+    """n x (Conv3d 'same' (+bias) [BN3d] ReLU MaxPool3d(2) [Dropout]) as built by
+    early_fusion.py:33-43 and anat_pet_featuremapfusion.py:37-58 (same as pet_cnn.py:18-30).
+    Returns (modules, n_in after the stack, n_out of the last conv or None)."""
+    mods, n_out = [], None
+    for n_out, k in zip(hparams["conv_out"], hparams["filter_size"]):
+        mods.append(Lyr.Conv3d(n_in, n_out, k, padding="same"))
+        if hparams.get("batchnorm"):
+            mods.append(Lyr.BatchNorm3d(n_out))
+        mods += [Lyr.ReLU(), Lyr.MaxPool3d(2)]
+        if "dropout_conv_p" in hparams:
+            mods.append(Lyr.Dropout(p=hparams["dropout_conv_p"]))
+        n_in = n_out
+    return mods, n_in, n_out
+
+
+class PET_MRI_EF(Base_Model):
+    """PET-MRI early fusion (pkg/models/fusion_models/early_fusion.py:19-112): the PET and
+    MRI volumes stacked as 2 input channels of one small CNN.
+
+    general_step hands the first conv the two raw f64 volumes as a StackedVolumes (the
+    reference's torch.stack + .to(float32), :77-80, is done inside the conv's gather pass:
+    mmad_gather_channels).  Head (:45-56): GAP, Flatten, [Dropout, Linear(n_in, linear_out),
+    ReLU], Linear(., C) -- with no ``linear_out`` the reference's last Linear takes the loop
+    variable ``n_out`` (the last conv width), reproduced here.  Always weighted CE (:61-62),
+    one Adam group over ``self.model`` without weight decay (:99-106)."""
+
+    def __init__(self, hparams, gpu_id=None):
+        super().__init__(hparams, gpu_id=gpu_id)
+        mods, n_in, n_out = _small_cnn_stack(self.hparams, 2)
+        mods += [Lyr.AdaptiveAvgPool3d(1), nn.Flatten()]
+        if self.hparams.get("linear_out"):
+            n_out = self.hparams["linear_out"]
+            if "dropout_dense_p" in self.hparams:
+                mods.append(Lyr.Dropout(p=self.hparams["dropout_dense_p"]))
+            mods += [Lyr.Linear(n_in, n_out), Lyr.ReLU()]
+        mods.append(Lyr.Linear(n_out, self.hparams["n_classes"]))
+        self.model = nn.Sequential(*mods)
+        self.criterion = Lyr.CrossEntropyLoss(weight=hparams["loss_class_weights"])
+        Lyr.set_compute_dtype(self, Lyr.precision_dtype(hparams))
+
+    def forward(self, x):
+        return self.model(x)
+
+    def general_step(self, batch, batch_idx, mode):
+        from .volume_ops import StackedVolumes
+        x = StackedVolumes([batch["pet1451"], batch["mri"]])
+        y = batch["label"]
+        y_hat = _to_f64(self.forward(x))
+        loss = self.criterion(y_hat, y)
+        if mode != "pred":
+            self.log(mode + "_loss", loss, on_step=True)
+        if mode in ("train", "val"):
+            getattr(self, f"f1_score_{mode}")(y_hat, y)
+            getattr(self, f"f1_score_{mode}_per_class")(y_hat, y)
+        return {"loss": loss, "outputs": y_hat, "labels": y}
+
+    def configure_optimizers(self):
+        opt = torch.optim.Adam(self.model.parameters(), lr=self.hparams["lr"],
+                               fused=self.device.type == "cuda")
+        return _with_scheduler(opt, self.hparams)
+
+
+class Random_Benchmark_All_CN_EF(PET_MRI_EF):
+    """early_fusion.py:113-118 (``Random_Benchmark_All_CN`` there): constant 'all CN'."""
+
+    def forward(self, x):
+        y = super().forward(x)
+        one_hot = torch.zeros_like(y)
+        one_hot[..., 0] = 1
+        return one_hot
+
+
+class PET_MRI_FMF(Base_Model):
+    """PET-MRI feature-map fusion (pkg/models/fusion_models/anat_pet_featuremapfusion.py:20-
+    172): two identical small-CNN branches (``backbone_pet``, ``backbone_mri``), their
+    feature maps fused voxel-wise -- channel concat ('concatenate', mmad_concat_channels)
+    or voxel-wise max ('maxout', mmad_max2_fwd) -- then ``fuse_model``: n_layers_fusion x
+    (Conv3d 'same' [BN3d] ReLU MaxPool3d(2)), GAP, Flatten, [Dropout], Linear(n_out_fusion,
+    64), ReLU, Linear(64, C).  The reference doubles ``n_in_fusion`` after every fusion
+    layer (:78) instead of using n_out_fusion, so only configurations it can run (one
+    fusion layer, as in its search space :69) build here too.  Weighted CE (:94-95); Adam
+    with weight decay l2_reg over all three parts at lr (:135-152)."""
+
+    def __init__(self, hparams, gpu_id=None):
+        super().__init__(hparams, gpu_id=gpu_id)
+        mode = hparams["fusion_mode"]
+        assert mode in ("concatenate", "maxout")
+        self.fusion_mode = mode
+        pet, n_in, _ = _small_cnn_stack(self.hparams, 1)
+        mri, _, _ = _small_cnn_stack(self.hparams, 1)
+        self.backbone_pet = nn.Sequential(*pet)
+        self.backbone_mri = nn.Sequential(*mri)
+        n_in_fusion = 2 * n_in if mode == "concatenate" else n_in
+        fused = []
+        for _ in range(hparams["n_layers_fusion"]):
+            fused.append(Lyr.Conv3d(n_in_fusion, hparams["n_out_fusion"],
+                                    hparams["filter_size_fusion"], padding="same"))
+            if self.hparams.get("batchnorm_fusion"):
+                fused.append(Lyr.BatchNorm3d(hparams["n_out_fusion"]))
+            fused += [Lyr.ReLU(), Lyr.MaxPool3d(2)]
+            n_in_fusion = n_in_fusion * 2
+        fused += [Lyr.AdaptiveAvgPool3d(1), nn.Flatten()]
+        if "dropout_dense_p" in self.hparams:
+            fused.append(Lyr.Dropout(p=self.hparams["dropout_dense_p"]))
+        fused += [Lyr.Linear(hparams["n_out_fusion"], 64), Lyr.ReLU(),
+                  Lyr.Linear(64, self.hparams["n_classes"])]
+        self.fuse_model = nn.Sequential(*fused)
+        self.criterion = Lyr.CrossEntropyLoss(weight=hparams["loss_class_weights"])
+        Lyr.set_compute_dtype(self, Lyr.precision_dtype(hparams))
+
+    def forward(self, x_pet, x_mri):
+        from .volume_ops import cat_channels, maxout
+        out_pet = self.backbone_pet(x_pet)
+        out_mri = self.backbone_mri(x_mri)
+        if self.fusion_mode == "concatenate":
+            fused = cat_channels(out_pet, out_mri)
+        else:
+            fused = maxout(out_pet, out_mri)
+        return self.fuse_model(fused)
+
+    def general_step(self, batch, batch_idx, mode):
+        x_pet = batch["pet1451"].unsqueeze(1)      # raw f64; conv 1 unfolds + casts (:124-127)
+        x_mri = batch["mri"].unsqueeze(1)
+        y = batch["label"]
+        y_hat = _to_f64(self.forward(x_pet=x_pet, x_mri=x_mri))
+        loss = self.criterion(y_hat, y)
+        if mode != "pred":
+            self.log(mode + "_loss", loss, on_step=True)
+        if mode in ("train", "val"):
+            getattr(self, f"f1_score_{mode}")(y_hat, y)
+            getattr(self, f"f1_score_{mode}_per_class")(y_hat, y)
+        return {"loss": loss, "outputs": y_hat, "labels": y}
+
+    def configure_optimizers(self):
+        params = [p for m in (self.backbone_mri, self.backbone_pet, self.fuse_model)
+                  for p in m.parameters()]
+        opt = torch.optim.Adam([{"params": params, "lr": self.hparams["lr"]}],
+                               weight_decay=self.hparams.get("l2_reg", 0) or 0,
+                               fused=self.device.type == "cuda")
+        return _with_scheduler(opt, self.hparams)
+
+
+class Random_Benchmark_All_CN_FMF(PET_MRI_FMF):
+    """anat_pet_featuremapfusion.py:173-178 (``Random_Benchmark_All_CN`` there)."""
+
+    def forward(self, x_pet, x_mri):
+        y = super().forward(x_pet, x_mri)
+        one_hot = torch.zeros_like(y)
+        one_hot[..., 0] = 1
+        return one_hot
+
+
 def _stage1_resnet(cls, hparams, depth, precision):
     h = dict(hparams)
     h.update({"resnet_depth": depth, "linear_out": [], "conv_out": [], "filter_size": [],

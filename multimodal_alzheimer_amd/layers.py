@@ -54,7 +54,9 @@ class Conv3d(nn.Conv3d):
         if self.groups != 1 or self.padding_mode != "zeros":
             raise NotImplementedError("groups != 1 / non-zero padding_mode")
         cd = self.compute_dtype
-        if x.shape[1] != 1 and x.dtype != cd:
+        # raw inputs (Cin = 1, or a channel stack of Cin < 8) are cast by the conv's own
+        # unfold / gather pass
+        if isinstance(x, torch.Tensor) and x.shape[1] % 8 == 0 and x.dtype != cd:
             x = volume_ops.cast(x, cd)
         packed, self._prepacked = self._prepacked, None     # valid for one forward only
         return volume_ops.conv3d(x, self.weight, self.bias, _triple(self.stride), self._pads(),

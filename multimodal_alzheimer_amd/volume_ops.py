@@ -12,6 +12,8 @@ Reference ops replaced (file:line in the reference tree):
   max_pool3d      nn.MaxPool3d         MedicalNet stem; anat_cnn.py:62; pet_cnn.py:26
   global_avg_pool nn.AdaptiveAvgPool3d(1)  anat_cnn.py:66; pet_cnn.py:33
 """
+import ctypes as C
+
 import torch
 
 from . import _lib as L
@@ -153,13 +155,72 @@ def prepack(module, convs=None):
     if not convs:
         return
     cdtype = convs[0].compute_dtype
-    convs = [c for c in convs if c.compute_dtype == cdtype]
+    convs = [c for c in convs if c.compute_dtype == cdtype and
+             (c.weight.shape[1] == 1 or c.weight.shape[1] % 8 == 0)]  # Cin 2..7: padded per call
     with_dgrad = torch.is_grad_enabled()
     plan = getattr(module, "_mmad_pack_plan", None)
     if plan is None or not plan.valid_for(convs, cdtype, with_dgrad):
         plan = PackPlan(convs, cdtype, with_dgrad)
         module._mmad_pack_plan = plan
     plan.run()
+
+
+class StackedVolumes:
+    """``torch.stack(srcs, dim=1)`` of raw single-channel volumes, not materialised.
+
+    PET_MRI_EF stacks the PET and MRI volumes into a 2-channel input
+    (pkg/models/fusion_models/early_fusion.py:77-80); the first conv gathers the planes
+    straight into its channel-padded NDHWC operand (mmad_gather_channels), so the stacked
+    f64 tensor and its f32 copy never exist.  Also accepts one (B, C, D, H, W) tensor with
+    C < 8 (any layout whose D, H, W collapse to one voxel stride)."""
+
+    def __init__(self, srcs):
+        if isinstance(srcs, torch.Tensor):
+            x = srcs
+            n, c, di, hi, wi = x.shape
+            s = x.stride()
+            if not (s[3] == wi * s[4] and s[2] == hi * s[3]):
+                x = x.contiguous()
+                s = x.stride()
+            es = x.element_size()
+            self.ptrs = [x.data_ptr() + ch * s[1] * es for ch in range(c)]
+            self.bstride, self.vstride = s[0], s[4]
+            self._keep = [x]
+        else:
+            srcs = [t.contiguous() for t in srcs]
+            x = srcs[0]
+            if any(t.shape != x.shape or t.dtype != x.dtype or t.device != x.device
+                   for t in srcs):
+                raise L.MMADError("stacked volumes must share shape, dtype and device")
+            if x.dim() != 4:
+                raise L.MMADError("stack sources are (B, D, H, W) volumes")
+            n, di, hi, wi = x.shape
+            c = len(srcs)
+            self.ptrs = [t.data_ptr() for t in srcs]
+            self.bstride, self.vstride = di * hi * wi, 1
+            self._keep = srcs
+        if not 1 <= c <= 8:
+            raise L.MMADError("at most 8 stacked channels")
+        self.shape = torch.Size((n, c, di, hi, wi))
+        self.dtype, self.device = x.dtype, x.device
+
+    def dim(self):
+        return 5
+
+    def gather(self, cdtype):
+        """The padded NDHWC compute-dtype operand: (N, 8, D, H, W) channels_last_3d."""
+        n, c, di, hi, wi = self.shape
+        out = _empty_vol(n, 8, di, hi, wi, cdtype, self.device)
+        srcs = (C.c_void_p * c)(*self.ptrs)
+        L.call("mmad_gather_channels", L.dtype_code(self.dtype), c, srcs, self.bstride,
+               self.vstride, n, di * hi * wi, 8, L.dtype_code(cdtype), L.ptr(out), L.stream())
+        return out
+
+
+def _pad_rows(src, rows, cin, cout, shape):
+    dst = torch.empty(shape, dtype=torch.float32, device=src.device)
+    L.call("mmad_pad_rows", rows, cin, cout, L.ptr(src), L.ptr(dst), L.stream())
+    return dst
 
 
 class _Conv3dFn(torch.autograd.Function):
@@ -172,7 +233,24 @@ class _Conv3dFn(torch.autograd.Function):
         d = conv_desc(tuple(x.shape), tuple(weight.shape), stride, padding, dilation)
         dt = L.dtype_code(cdtype)
         lib = L.load()
-        if d.ci == 1:
+        ctx.ci_real = d.ci
+        wsrc = weight
+        if isinstance(x, StackedVolumes) or (d.ci > 1 and d.ci % 8):
+            # Cin in 2..7 (early fusion): channel-padded operand and weight (fusion.hip);
+            # the zero lanes contribute exact zeros
+            if ctx.needs_input_grad[0]:
+                raise L.MMADError("conv3d: gradient w.r.t. a channel-stacked raw input is "
+                                  "not supported (the input never needs one)")
+            sv = x if isinstance(x, StackedVolumes) else StackedVolumes(x)
+            if sv.shape[1] == 1:
+                raise L.MMADError("a single raw volume goes to conv3d as a (B,1,D,H,W) tensor")
+            taps = d.kd * d.kh * d.kw
+            src = sv.gather(cdtype)
+            wsrc = _pad_rows(weight.detach().contiguous(), d.co, d.ci * taps, 8 * taps,
+                             (d.co, 8, d.kd, d.kh, d.kw))
+            d.ci = 8
+            packed = None
+        elif d.ci == 1:
             if ctx.needs_input_grad[0]:
                 raise L.MMADError("conv3d: gradient w.r.t. a 1-channel raw input volume "
                                   "is not supported (the input never needs one)")
@@ -185,7 +263,7 @@ class _Conv3dFn(torch.autograd.Function):
             src = x
         wp, wpt = packed if packed is not None else (None, None)
         if wp is None:
-            wp = pack_weight(d, dt, weight, cdtype, False)
+            wp = pack_weight(d, dt, wsrc, cdtype, False)
         y = _empty_vol(d.n, d.co, d.do_, d.ho, d.wo, cdtype, x.device)
         stats = None
         if want_stats:
@@ -233,11 +311,16 @@ class _Conv3dFn(torch.autograd.Function):
             lib = L.load()
             ws = torch.empty((lib.mmad_conv3d_wgrad_workspace(d, dt) + 3) // 4,
                              dtype=torch.float32, device=gy.device)
-            dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
+            padded = ctx.ci_real != d.ci
+            dw = torch.empty((d.co, d.ci, d.kd, d.kh, d.kw) if padded else weight.shape,
+                             dtype=torch.float32, device=gy.device)
             db = (torch.empty(d.co, dtype=torch.float32, device=gy.device)
                   if ctx.has_bias else None)
             L.call("mmad_conv3d_wgrad", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db),
                    L.ptr(ws), L.stream())
+            if padded:                     # cut the zero-lane channels back off
+                taps = d.kd * d.kh * d.kw
+                dw = _pad_rows(dw, d.co, d.ci * taps, ctx.ci_real * taps, weight.shape)
             if not ctx.needs_input_grad[1]:
                 dw = None
         return dx, dw, db, None, None, None, None
@@ -572,6 +655,71 @@ class _GapFn(torch.autograd.Function):
 def global_avg_pool(x):
     """AdaptiveAvgPool3d(1): (N,C,D,H,W) NDHWC -> (N,C,1,1,1) float32."""
     return _GapFn.apply(x)
+
+
+# ----------------------------------------------------------------- feature-map fusion
+class _Max2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        _check_vol(a)
+        _check_vol(b, a.dtype)
+        if a.shape != b.shape:
+            raise L.MMADError("maxout fusion needs equal volume shapes")
+        y = torch.empty_like(a)
+        sel = torch.empty(a.numel(), dtype=torch.uint8, device=a.device)
+        L.call("mmad_max2_fwd", L.dtype_code(a.dtype), a.numel(), L.ptr(a), L.ptr(b), L.ptr(y),
+               L.ptr(sel), L.stream())
+        ctx.save_for_backward(sel)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (sel,) = ctx.saved_tensors
+        g = _cl(g)
+        ga, gb = torch.empty_like(g), torch.empty_like(g)
+        L.call("mmad_max2_bwd", L.dtype_code(g.dtype), g.numel(), L.ptr(g), L.ptr(sel),
+               L.ptr(ga), L.ptr(gb), L.stream())
+        return ga, gb
+
+
+def maxout(a, b):
+    """torch.max(torch.stack((a, b), dim=0), dim=0)[0] -- the 'maxout' feature-map fusion
+    (anat_pet_featuremapfusion.py:115-117): ties go to ``a``, NaN propagates."""
+    return _Max2Fn.apply(a, b)
+
+
+class _CatChannelsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        _check_vol(a)
+        _check_vol(b, a.dtype)
+        if a.shape[0] != b.shape[0] or a.shape[2:] != b.shape[2:]:
+            raise L.MMADError("channel concat needs equal batch and spatial extents")
+        n, ca, di, hi, wi = a.shape
+        cb = b.shape[1]
+        y = _empty_vol(n, ca + cb, di, hi, wi, a.dtype, a.device)
+        L.call("mmad_concat_channels", L.dtype_code(a.dtype), n * di * hi * wi, ca, L.ptr(a),
+               cb, L.ptr(b), L.ptr(y), L.stream())
+        ctx.cfg = (ca, cb)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        ca, cb = ctx.cfg
+        g = _cl(g)
+        n, _, di, hi, wi = g.shape
+        ga = _empty_vol(n, ca, di, hi, wi, g.dtype, g.device) if ctx.needs_input_grad[0] else None
+        gb = _empty_vol(n, cb, di, hi, wi, g.dtype, g.device) if ctx.needs_input_grad[1] else None
+        if ga is not None or gb is not None:
+            L.call("mmad_split_channels", L.dtype_code(g.dtype), n * di * hi * wi, ca, cb,
+                   L.ptr(g), L.ptr(ga), L.ptr(gb), L.stream())
+        return ga, gb
+
+
+def cat_channels(a, b):
+    """torch.cat((a, b), dim=1) of two NDHWC volumes -- the 'concatenate' feature-map
+    fusion (anat_pet_featuremapfusion.py:112-113)."""
+    return _CatChannelsFn.apply(a, b)
 
 
 # --------------------------------------------------------------------- elementwise / cast

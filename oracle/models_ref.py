@@ -200,6 +200,107 @@ class ResNetPairFusionRef(nn.Module):
     general_step = AnatPETCNNRef.general_step
 
 
+def _small_cnn_stack(hparams, n_in):
+    """Conv3d 'same' (+bias) [BN3d] ReLU MaxPool3d(2) [Dropout] per conv_out entry:
+    early_fusion.py:33-43, anat_pet_featuremapfusion.py:37-58."""
+    mods = []
+    for n_out, k in zip(hparams["conv_out"], hparams["filter_size"]):
+        mods.append(nn.Conv3d(n_in, n_out, k, padding="same"))
+        if hparams.get("batchnorm"):
+            mods.append(nn.BatchNorm3d(n_out))
+        mods += [nn.ReLU(), nn.MaxPool3d(2)]
+        if "dropout_conv_p" in hparams:
+            mods.append(nn.Dropout(p=hparams["dropout_conv_p"]))
+        n_in = n_out
+    return mods, n_in
+
+
+class EarlyFusionRef(nn.Module):
+    """PET_MRI_EF (pkg/models/fusion_models/early_fusion.py:19-112): stack(pet, mri) as two
+    input channels (:77-80), the small-CNN stack (:33-43), GAP, Flatten, [Dropout, Linear,
+    ReLU] (:49-55), Linear(n_out, C) where n_out is the loop variable when linear_out is
+    falsy (:56), weighted CE (:61-62)."""
+
+    def __init__(self, hparams):
+        super().__init__()
+        self.hparams = dict(hparams)
+        mods, n_in = _small_cnn_stack(hparams, 2)
+        n_out = n_in
+        mods += [nn.AdaptiveAvgPool3d(1), nn.Flatten()]
+        if hparams.get("linear_out"):
+            n_out = hparams["linear_out"]
+            if "dropout_dense_p" in hparams:
+                mods.append(nn.Dropout(p=hparams["dropout_dense_p"]))
+            mods += [nn.Linear(n_in, n_out), nn.ReLU()]
+        mods.append(nn.Linear(n_out, hparams["n_classes"]))
+        self.model = nn.Sequential(*mods)
+        self.criterion = nn.CrossEntropyLoss(weight=hparams["loss_class_weights"])
+
+    def forward(self, x):
+        return self.model(x)
+
+    def inputs(self, batch, dtype=torch.float32):
+        return (torch.stack((batch["pet1451"], batch["mri"]), dim=1).to(dtype=dtype),)
+
+    def general_step(self, batch, batch_idx=0, mode="train"):
+        """early_fusion.py:75-91."""
+        y = batch["label"]
+        y_hat = self(*self.inputs(batch)).to(dtype=torch.double)
+        return {"loss": self.criterion(y_hat, y), "outputs": y_hat, "labels": y}
+
+
+class FeatureMapFusionRef(nn.Module):
+    """PET_MRI_FMF (pkg/models/fusion_models/anat_pet_featuremapfusion.py:20-132): two
+    small-CNN branches (:37-62), fused by channel concat or voxel-wise max (:112-118), then
+    n_layers_fusion x (Conv 'same' [BN] ReLU MaxPool(2)) (:71-78; n_in_fusion doubles per
+    layer, sic), GAP, Flatten, [Dropout], Linear(n_out_fusion, 64), ReLU, Linear(64, C)
+    (:81-92); weighted CE (:94-95)."""
+
+    def __init__(self, hparams):
+        super().__init__()
+        self.hparams = dict(hparams)
+        self.fusion_mode = hparams["fusion_mode"]
+        pet, n_in = _small_cnn_stack(hparams, 1)
+        mri, _ = _small_cnn_stack(hparams, 1)
+        self.backbone_pet = nn.Sequential(*pet)
+        self.backbone_mri = nn.Sequential(*mri)
+        n_in_fusion = 2 * n_in if self.fusion_mode == "concatenate" else n_in
+        fused = []
+        for _ in range(hparams["n_layers_fusion"]):
+            fused.append(nn.Conv3d(n_in_fusion, hparams["n_out_fusion"],
+                                   hparams["filter_size_fusion"], padding="same"))
+            if hparams.get("batchnorm_fusion"):
+                fused.append(nn.BatchNorm3d(hparams["n_out_fusion"]))
+            fused += [nn.ReLU(), nn.MaxPool3d(2)]
+            n_in_fusion = n_in_fusion * 2
+        fused += [nn.AdaptiveAvgPool3d(1), nn.Flatten()]
+        if "dropout_dense_p" in hparams:
+            fused.append(nn.Dropout(p=hparams["dropout_dense_p"]))
+        fused += [nn.Linear(hparams["n_out_fusion"], 64), nn.ReLU(),
+                  nn.Linear(64, hparams["n_classes"])]
+        self.fuse_model = nn.Sequential(*fused)
+        self.criterion = nn.CrossEntropyLoss(weight=hparams["loss_class_weights"])
+
+    def forward(self, x_pet, x_mri):
+        out_pet = self.backbone_pet(x_pet)
+        out_mri = self.backbone_mri(x_mri)
+        if self.fusion_mode == "concatenate":
+            out = torch.cat((out_pet, out_mri), dim=1)
+        else:
+            out, _ = torch.max(torch.stack((out_pet, out_mri), dim=0), dim=0)
+        return self.fuse_model(out)
+
+    def inputs(self, batch, dtype=torch.float32):
+        return (batch["pet1451"].unsqueeze(1).to(dtype=dtype),
+                batch["mri"].unsqueeze(1).to(dtype=dtype))
+
+    def general_step(self, batch, batch_idx=0, mode="train"):
+        """anat_pet_featuremapfusion.py:120-141."""
+        y = batch["label"]
+        y_hat = self(*self.inputs(batch)).to(dtype=torch.double)
+        return {"loss": self.criterion(y_hat, y), "outputs": y_hat, "labels": y}
+
+
 def adam_param_groups(model, hparams):
     """anat_cnn.py:111-136: head lr = lr; backbone lr = lr_pretrained or frozen."""
     groups = []

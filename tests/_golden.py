@@ -34,6 +34,26 @@ def pet_hparams(n_classes=2, **kw):
     return h
 
 
+def ef_hparams(n_classes=2, **kw):
+    """PET_MRI_EF case hparams (mirror of tests/golden/make_golden.py)."""
+    h = {"n_classes": n_classes, "conv_out": [8, 16, 32, 64], "filter_size": [7, 5, 3, 3],
+         "batchnorm": False, "linear_out": 64, "lr": 1e-3, "reduce_factor_lr_schedule": None,
+         "loss_class_weights": torch.tensor(W2 if n_classes == 2 else W3, dtype=torch.double)}
+    h.update(kw)
+    return h
+
+
+def fmf_hparams(mode, n_classes=2, **kw):
+    """PET_MRI_FMF case hparams (mirror of tests/golden/make_golden.py)."""
+    h = {"n_classes": n_classes, "conv_out": [16, 32, 64], "filter_size": [5, 5, 5],
+         "filter_size_fusion": 5, "batchnorm": False, "batchnorm_fusion": False,
+         "fusion_mode": mode, "n_layers_fusion": 1, "n_out_fusion": 64, "lr": 2e-4,
+         "l2_reg": 0, "reduce_factor_lr_schedule": 0.1,
+         "loss_class_weights": torch.tensor(W2 if n_classes == 2 else W3, dtype=torch.double)}
+    h.update(kw)
+    return h
+
+
 def batch_for(shape, n_classes, seed, keys=("mri",)):
     b = {"label": torch.from_numpy(prng.labels(seed + 7, shape[0], n_classes))}
     for i, k in enumerate(keys):
@@ -68,6 +88,15 @@ CASES = {
                       "smallpet", 20, ("pet1451",)),
     "anat_pet_fusion": (lambda: anat_hparams(10, fl_gamma=2), "fusion", 22,
                         ("pet1451", "mri")),
+    "early_fusion": (lambda: ef_hparams(), "ef", 24, ("pet1451", "mri")),
+    "early_fusion_bn3": (lambda: ef_hparams(n_classes=3, batchnorm=True, conv_out=[16, 32, 64],
+                                            filter_size=[5, 5, 3], linear_out=None),
+                         "ef", 26, ("pet1451", "mri")),
+    "fmf_maxout": (lambda: fmf_hparams("maxout"), "fmf", 28, ("pet1451", "mri")),
+    "fmf_concat_bn": (lambda: fmf_hparams("concatenate", n_classes=3, batchnorm=True,
+                                          batchnorm_fusion=True, conv_out=[8, 16, 32],
+                                          filter_size=[7, 5, 3], filter_size_fusion=3,
+                                          n_out_fusion=128), "fmf", 30, ("pet1451", "mri")),
 }
 
 
@@ -85,6 +114,10 @@ def build_oracle(name):
         pet = models_ref.SmallPETCNNRef(pet_hparams())
         mri = models_ref.AnatCNNRef(anat_hparams(10))
         return models_ref.AnatPETCNNRef(h, pet, mri)
+    if kind == "ef":
+        return models_ref.EarlyFusionRef(h)
+    if kind == "fmf":
+        return models_ref.FeatureMapFusionRef(h)
     raise KeyError(kind)
 
 

@@ -294,6 +294,71 @@ def anat_pet_fusion():
     return out
 
 
+def ef_hparams(n_classes=2, **kw):
+    """train_early_fusion.py:236-254 best configuration, dropout keys removed."""
+    h = {"n_classes": n_classes, "conv_out": [8, 16, 32, 64], "filter_size": [7, 5, 3, 3],
+         "batchnorm": False, "linear_out": 64, "lr": 1e-3, "reduce_factor_lr_schedule": None,
+         "loss_class_weights": torch.tensor(W2 if n_classes == 2 else W3, dtype=torch.double)}
+    h.update(kw)
+    return h
+
+
+def fmf_hparams(mode, n_classes=2, **kw):
+    """train_anat_pet_featuremapfusion.py:282-306 best 2-class maxout configuration,
+    dropout keys removed."""
+    h = {"n_classes": n_classes, "conv_out": [16, 32, 64], "filter_size": [5, 5, 5],
+         "filter_size_fusion": 5, "batchnorm": False, "batchnorm_fusion": False,
+         "fusion_mode": mode, "n_layers_fusion": 1, "n_out_fusion": 64, "lr": 2e-4,
+         "l2_reg": 0, "reduce_factor_lr_schedule": 0.1,
+         "loss_class_weights": torch.tensor(W2 if n_classes == 2 else W3, dtype=torch.double)}
+    h.update(kw)
+    return h
+
+
+@case
+def early_fusion():
+    from pkg.models.fusion_models.early_fusion import PET_MRI_EF
+    m = PET_MRI_EF(ef_hparams())
+    load_prng_weights(m, 23)
+    out = {"seed": np.array(23), "shape": np.array([2, 32, 32, 32])}
+    run_case(m, batch_for((2, 32, 32, 32), 2, 24, keys=("pet1451", "mri")), out)
+    return out
+
+
+@case
+def early_fusion_bn3():
+    from pkg.models.fusion_models.early_fusion import PET_MRI_EF
+    m = PET_MRI_EF(ef_hparams(n_classes=3, batchnorm=True, conv_out=[16, 32, 64],
+                              filter_size=[5, 5, 3], linear_out=None))
+    load_prng_weights(m, 25)
+    out = {"seed": np.array(25), "shape": np.array([3, 32, 32, 32])}
+    run_case(m, batch_for((3, 32, 32, 32), 3, 26, keys=("pet1451", "mri")), out)
+    return out
+
+
+@case
+def fmf_maxout():
+    from pkg.models.fusion_models.anat_pet_featuremapfusion import PET_MRI_FMF
+    m = PET_MRI_FMF(fmf_hparams("maxout"))
+    load_prng_weights(m, 27)
+    out = {"seed": np.array(27), "shape": np.array([2, 32, 32, 32])}
+    run_case(m, batch_for((2, 32, 32, 32), 2, 28, keys=("pet1451", "mri")), out)
+    return out
+
+
+@case
+def fmf_concat_bn():
+    from pkg.models.fusion_models.anat_pet_featuremapfusion import PET_MRI_FMF
+    m = PET_MRI_FMF(fmf_hparams("concatenate", n_classes=3, batchnorm=True,
+                                batchnorm_fusion=True, conv_out=[8, 16, 32],
+                                filter_size=[7, 5, 3], filter_size_fusion=3,
+                                n_out_fusion=128))
+    load_prng_weights(m, 29)
+    out = {"seed": np.array(29), "shape": np.array([2, 32, 32, 32])}
+    run_case(m, batch_for((2, 32, 32, 32), 3, 30, keys=("pet1451", "mri")), out)
+    return out
+
+
 def main(names=None):
     install_stubs()
     torch.set_num_threads(min(8, os.cpu_count() or 1))

@@ -325,3 +325,74 @@ def test_library_loaded_is_ours():
     import os
     lib = _lib.load()
     assert os.path.samefile(lib._name, _lib.LIB_PATH)
+
+
+# ------------------------------------------------------------ voxel-level fusion (fusion.hip)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_stacked_input_conv_matches_stack_then_conv(dtype):
+    """early_fusion.py:77-80 + :35: conv over torch.stack((pet, mri), 1).to(float32); the
+    HIP path gathers the two f64 planes into a channel-padded NDHWC operand (odd extents,
+    'same' k=5 with bias) -- forward, weight and bias gradients."""
+    pet, mri = rnd(2, 11, 9, 13, seed=40), rnd(2, 11, 9, 13, seed=41)
+    w = rnd(8, 2, 5, 5, 5, seed=42, scale=0.2).float()
+    b = rnd(8, seed=43, scale=0.1).float()
+    x = torch.stack((pet, mri), 1)
+    xr = x.float().double() if dtype == torch.float32 else x.to(torch.bfloat16).double()
+    wr = w.double().requires_grad_()
+    br = b.double().requires_grad_()
+    ref = F.conv3d(xr, wr if dtype == torch.float32 else wr.to(torch.bfloat16).double(), br,
+                   padding=2)
+    g = rnd(*ref.shape, seed=44)
+    ref.backward(g)
+    wd, bd = w.to(DEV).requires_grad_(), b.to(DEV).requires_grad_()
+    sv = V.StackedVolumes([pet.to(DEV), mri.to(DEV)])
+    y = V.conv3d(sv, wd, bd, padding=(2, 2, 2), cdtype=dtype)
+    y.backward(to_vol(g, dtype))
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    close(y, ref, tol, "fwd")
+    close(wd.grad, wr.grad, tol if dtype == torch.float32 else 3e-2, "dw")
+    close(bd.grad, br.grad, tol if dtype == torch.float32 else 3e-2, "db")
+    # same result from one stacked 5-D NCDHW tensor
+    y2 = V.conv3d(x.to(DEV), wd.detach(), bd.detach(), padding=(2, 2, 2), cdtype=dtype)
+    assert torch.equal(y.detach(), y2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_maxout_ties_nan_and_gradient_routing(dtype):
+    a = rnd(2, 16, 3, 5, 4, seed=45)
+    b = rnd(2, 16, 3, 5, 4, seed=46)
+    b[:, :4] = a[:, :4]                    # exact ties -> first operand (index 0)
+    a[0, 5, 1, 1, 1] = float("nan")
+    b[1, 6, 2, 2, 2] = float("nan")
+    ad, bd = to_vol(a, dtype).requires_grad_(), to_vol(b, dtype).requires_grad_()
+    y = V.maxout(ad, bd)
+    ar, br = ad.detach().cpu().double(), bd.detach().cpu().double()
+    ref, idx = torch.max(torch.stack((ar, br), 0), 0)          # torch's tie / NaN rules
+    assert torch.equal(y.detach().cpu().double().isnan(), ref.isnan())
+    assert torch.equal(y.detach().cpu().double().nan_to_num(), ref.nan_to_num())
+    g = to_vol(rnd(*a.shape, seed=47), dtype)
+    y.backward(g)
+    gq = g.cpu().double()
+    assert torch.equal(ad.grad.cpu().double(), torch.where(idx == 0, gq, 0.0))
+    assert torch.equal(bd.grad.cpu().double(), torch.where(idx == 1, gq, 0.0))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_channel_concat_and_split(dtype):
+    a = to_vol(rnd(2, 16, 3, 4, 5, seed=48), dtype).requires_grad_()
+    b = to_vol(rnd(2, 32, 3, 4, 5, seed=49), dtype).requires_grad_()
+    y = V.cat_channels(a, b)
+    assert torch.equal(y, torch.cat((a.detach(), b.detach()), 1))
+    g = to_vol(rnd(2, 48, 3, 4, 5, seed=50), dtype)
+    y.backward(g)
+    assert torch.equal(a.grad, g[:, :16]) and torch.equal(b.grad, g[:, 16:])
+
+
+def test_pad_rows_roundtrip():
+    w = torch.randn(6, 54, device=DEV)
+    p = torch.empty(6, 216, device=DEV)
+    _lib.call("mmad_pad_rows", 6, 54, 216, _lib.ptr(w), _lib.ptr(p), _lib.stream())
+    assert torch.equal(p[:, :54], w) and not p[:, 54:].any()
+    back = torch.empty_like(w)
+    _lib.call("mmad_pad_rows", 6, 216, 54, _lib.ptr(p), _lib.ptr(back), _lib.stream())
+    assert torch.equal(back, w)

@@ -25,6 +25,10 @@ def build_product(name):
         return M.PET_CNN_ResNet(h)
     if kind == "smallpet":
         return M.Small_PET_CNN(h)
+    if kind == "ef":
+        return M.PET_MRI_EF(h)
+    if kind == "fmf":
+        return M.PET_MRI_FMF(h)
     pet = M.Small_PET_CNN(G.pet_hparams())
     mri = M.Anat_CNN(G.anat_hparams(10))
     return M.Anat_PET_CNN(h, pet_model=pet, mri_model=mri)
@@ -99,7 +103,9 @@ def _f64_oracle_grads(name):
     ref = ref.double()
     batch = G.batch_of(name, g)
     ref.train()
-    if hasattr(ref, "batch_key"):
+    if hasattr(ref, "inputs"):
+        y_hat = ref(*ref.inputs(batch, torch.float64))
+    elif hasattr(ref, "batch_key"):
         y_hat = ref(batch[ref.batch_key].unsqueeze(1).double())
     else:
         y_hat = ref(batch["pet1451"].unsqueeze(1).double(), batch["mri"].unsqueeze(1).double())

@@ -27,6 +27,9 @@ def test_reference_import_paths():
     from pkg.loss_functions.focalloss import FocalLoss
     from pkg.models.base_model import Base_Model
     from pkg.models.fusion_models.anat_pet_fusion import Anat_PET_CNN
+    from pkg.models.fusion_models.anat_pet_featuremapfusion import PET_MRI_FMF
+    from pkg.models.fusion_models.early_fusion import PET_MRI_EF
+    assert PET_MRI_EF is M.PET_MRI_EF and PET_MRI_FMF is M.PET_MRI_FMF
     from pkg.models.mri_models.anat_cnn import Anat_CNN
     from pkg.models.pet_models.pet_cnn import Small_PET_CNN
     from pkg.models.pet_models.pet_resnet_cnn import PET_CNN_ResNet
