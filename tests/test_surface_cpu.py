@@ -84,6 +84,41 @@ def test_fusion_loads_stage1_checkpoints(tmp_path):
     assert list(f2.state_dict()) == list(f.state_dict())
 
 
+def test_stage2_checkpoint_reload_like_stage3(tmp_path):
+    """all_modalities_fusion.py:17-20 reloads the stage-2 fusion model with
+    Anat_PET_CNN.load_from_checkpoint(path_anat_pet, path_pet=..., path_anat=...): the
+    stage-1 checkpoints rebuild the branches, then the stage-2 state_dict (with the
+    model_fuse.* aliases of stage2out / cls2) overwrites every weight."""
+    pet = M.Small_PET_CNN(G.pet_hparams())
+    mri = M.Anat_CNN(G.anat_hparams(10))
+    G.load_prng_weights(pet, 1)
+    G.load_prng_weights(mri, 2)
+    p_pet, p_mri = str(tmp_path / "pet.ckpt"), str(tmp_path / "mri.ckpt")
+    pet.save_checkpoint(p_pet)
+    mri.save_checkpoint(p_mri)
+    f = M.Anat_PET_CNN(G.anat_hparams(10, fl_gamma=2, path_pet=p_pet, path_mri=p_mri))
+    G.load_prng_weights(f, 7)                  # "trained" stage-2 weights differ from stage 1
+    p_f = str(tmp_path / "anat_pet.ckpt")
+    f.save_checkpoint(p_f)
+    keys = list(torch.load(p_f, weights_only=True)["state_dict"])
+    assert "model_fuse.0.weight" in keys and "stage2out.weight" in keys
+    f2 = M.Anat_PET_CNN.load_from_checkpoint(p_f, path_pet=p_pet, path_anat=p_mri)
+    for (k, a), (_, b) in zip(f.state_dict().items(), f2.state_dict().items()):
+        assert torch.equal(a, b), k
+    assert f2.model_fuse[0] is f2.stage2out
+
+
+@pytest.mark.parametrize("name", ["early_fusion_bn3", "fmf_concat_bn"])
+def test_voxel_fusion_checkpoint_roundtrip(tmp_path, name):
+    m = build_product(name)
+    G.load_prng_weights(m, 5)
+    path = str(tmp_path / f"{name}.ckpt")
+    m.save_checkpoint(path)
+    m2 = type(m).load_from_checkpoint(path)
+    for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k
+
+
 def test_frozen_backbone_without_lr_pretrained():
     h = G.anat_hparams(10, lr_pretrained=None)
     m = M.Anat_CNN(h)
