@@ -118,18 +118,25 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: everything else (RCCL's version banner, library
+    # chatter) goes to stderr; the result is written to the saved stdout descriptor
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
+    # MMAD_DP_SELFTEST=1 (under torchrun) runs the RCCL gradient all-reduce path even at N=1
+    dp = world > 1 or os.environ.get("MMAD_DP_SELFTEST") == "1"
+    if dp:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     torch.manual_seed(15 + rank)
     model = M.Anat_CNN(hparams(args.precision)).cuda()
     opt = model.configure_optimizers()
-    reducer = GradAllReduce(model.parameters()) if world > 1 else None
+    reducer = GradAllReduce(model.parameters()) if dp else None
     B, S = args.batch, args.size
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)   # this rank's shard
     batch = {"mri": torch.rand((B, S, S, S), device="cuda", dtype=torch.float64, generator=g),
@@ -187,8 +194,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(S)
     if rank == 0:
-        print(json.dumps(result))
-    if world > 1:
+        sys.stdout.flush()
+        os.write(out_fd, (json.dumps(result) + "\n").encode())
+    if dp:
         dist.destroy_process_group()
 
 

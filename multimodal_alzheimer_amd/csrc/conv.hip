@@ -82,7 +82,12 @@ __device__ __forceinline__ void fill_taps_fwd(const Geom& g, int* tapoff) {
 // ---- implicit GEMM (forward / per-parity-class dgrad) --------------------------------
 // Block = WGM x WGN waves, tile BM voxels x BN channels, NST-deep LDS ring with NST-1 stages
 // of LDS-DMA in flight (asm DMA + counted vmcnt + raw barrier, see wgrad_kernel).
-template <typename T, int BN, int MODE, int BM, int WGM = 2, int WGN = 2, int NST = 2>
+// RBT = K bytes per stage row: 128 (8 x 16-B chunks, XOR swizzle row & 7) or 64 (bf16 only:
+// 4 chunks, swizzle 3 * ((row >> 3) & 1), which keeps every 16-lane ds_read_b128 group on 16
+// distinct bank slots); 64-B rows halve the stage so the same LDS holds twice the stages
+// in flight.
+template <typename T, int BN, int MODE, int BM, int WGM = 2, int WGN = 2, int NST = 2,
+          int RBT = RB>
 __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* __restrict__ src,
                                                        const T* __restrict__ wgt,
                                                        const float* __restrict__ bias,
@@ -90,11 +95,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
                                                        float* __restrict__ stats, int nbm,
                                                        int nbn) {
   constexpr int EPC = 16 / (int)sizeof(T);
-  constexpr int BK = RB / (int)sizeof(T);
+  constexpr int BK = RBT / (int)sizeof(T);
+  static_assert(RBT == 128 || (RBT == 64 && sizeof(T) == 2), "stage row bytes");
+  constexpr int RPI = 1024 / RBT;                        // tile rows per DMA instruction
   constexpr int NW = WGM * WGN, NT = 64 * NW;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;          // per-wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int A_BYTES = BM * RB, B_BYTES = BN * RB, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_BYTES = BM * RBT, B_BYTES = BN * RBT, STAGE = A_BYTES + B_BYTES;
   constexpr int AI = A_BYTES / (1024 * NW), BI = B_BYTES / (1024 * NW);
   static_assert(AI * 1024 * NW == A_BYTES && BI * 1024 * NW == B_BYTES, "tile/wave split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -147,15 +154,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
     Kc = ntap * g.Cs;
   }
 
-  // this lane's A rows: one per DMA instruction, row = (wave*AI + i)*8 + lane/8
-  const int lrow = lane >> 3;
-  const int lchunk = (lane & 7) ^ lrow;          // logical K chunk this lane fetches
+  // this lane's A rows: one per DMA instruction, row = (wave*AI + i)*RPI + lane/(RBT/16)
+  const int lrow = RBT == 128 ? lane >> 3 : lane >> 2;
+  const int lchunk = RBT == 128 ? (lane & 7) ^ lrow              // logical K chunk fetched
+                                : (lane & 3) ^ (3 * ((lrow >> 3) & 1));
   int rz[AI], ry[AI], rx[AI];
   int64_t rbase[AI];
   bool rok[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
-    const int m = m0 + (wave * AI + i) * 8 + lrow;
+    const int m = m0 + (wave * AI + i) * RPI + lrow;
     rok[i] = m < Mc;
     const int mm = rok[i] ? m : 0;
     const int xw = mm % Wc;
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
     const int woff = MODE == FWD ? k : (kok ? (tapidx[ti] << g.cs_shift) + ci : 0);
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
-      const int co = n0 + (wave * BI + i) * 8 + lrow;
+      const int co = n0 + (wave * BI + i) * RPI + lrow;
       const void* p = (co < g.Nd && kok) ? (const void*)(wgt + (int64_t)co * g.Kpad + woff)
                                          : (const void*)g_zero_chunk;
       glds16_asm(p, lds_addr_of(sbase + A_BYTES + (wave * BI + i) * 1024));
@@ -238,7 +246,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
 
   const int wm = wave % WGM, wn = wave / WGM;
   const int lr = lane & 15, lk = lane >> 4;
-  const int sw8 = lr & 7;                          // swizzle of every row this lane reads
+  const int sw8 = RBT == 128 ? lr & 7 : 3 * ((lr >> 3) & 1);   // swizzle of this lane's rows
   // fp32 mode sums K in two levels (fresh partial every FLUSH stages): one f32 MFMA chain
   // over K = 27*512 terms grows the rounding error ~K-fold and flips ReLU masks.
   constexpr int FLUSH = 8;
@@ -249,17 +257,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
     for (int j = 0; j < TN; ++j) acc[i][j] = part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int stage) {
-    const char* a = ring + stage * STAGE + (wm * WTM + lr) * RB;
-    const char* b = ring + stage * STAGE + A_BYTES + (wn * WTN + lr) * RB;
+    const char* a = ring + stage * STAGE + (wm * WTM + lr) * RBT;
+    const char* b = ring + stage * STAGE + A_BYTES + (wn * WTN + lr) * RBT;
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int s = 0; s < BK / 32; ++s) {
         const int off = ((4 * s + lk) ^ sw8) << 4;
         bf16x8 fa[TM], fb[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(a + i * 16 * RB + off);
+        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(a + i * 16 * RBT + off);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(b + j * 16 * RB + off);
+        for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(b + j * 16 * RBT + off);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -272,9 +280,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
         const int off = ((s ^ sw8) << 4) + lk * 4;
         float fa[TM], fb[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const float*>(a + i * 16 * RB + off);
+        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const float*>(a + i * 16 * RBT + off);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const float*>(b + j * 16 * RB + off);
+        for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const float*>(b + j * 16 * RBT + off);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1085,16 +1093,17 @@ bool set_lds(F* kern, size_t lds) {
                                              (int)lds) == hipSuccess;
 }
 
-template <typename T, int BN, int MODE, int BMT, int WGM = 2, int WGN = 2, int NST = 2>
+template <typename T, int BN, int MODE, int BMT, int WGM = 2, int WGN = 2, int NST = 2,
+          int RBT = RB>
 int launch_igemm_bm(const Geom& g, int64_t m_max, int classes, const void* src, const void* w,
                     const float* bias, void* dst, float* stats, hipStream_t st) {
-  const size_t ring = (size_t)NST * (BMT + BN) * RB;
+  const size_t ring = (size_t)NST * (BMT + BN) * RBT;
   const size_t epi = 1024 + (size_t)BMT * (BN * 2 + 16) + (size_t)(WGM - 1) * 2 * BN * 4;
   const size_t lds = TAPB + std::max(ring, epi);
-  static const bool ok = set_lds(igemm_kernel<T, BN, MODE, BMT, WGM, WGN, NST>, lds);
+  static const bool ok = set_lds(igemm_kernel<T, BN, MODE, BMT, WGM, WGN, NST, RBT>, lds);
   if (!ok) return MMAD_EUNSUPPORTED;
   const int nbm = (int)cdiv(m_max, BMT), nbn = (int)cdiv(g.Nd, BN);
-  hipLaunchKernelGGL((igemm_kernel<T, BN, MODE, BMT, WGM, WGN, NST>),
+  hipLaunchKernelGGL((igemm_kernel<T, BN, MODE, BMT, WGM, WGN, NST, RBT>),
                      dim3((unsigned)(nbm * nbn), (unsigned)classes), dim3(64 * WGM * WGN), lds,
                      st, g, (const T*)src, (const T*)w, bias, (T*)dst, stats, nbm, nbn);
   return launch_status();
@@ -1112,6 +1121,8 @@ int big_cfg_for(const Geom& g, int dtype, int64_t m_max, int classes) {
   if (cfg == 0)   // default: 256 x 256 tiles (8 waves) when they give every CU a block
     return g.Nd % 256 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 256) >= 256 ? 2 : 0;
   if (cfg == 4) return g.Nd % 128 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 128) >= 256 ? 4 : 0;
+  if (cfg == 5 || cfg == 6)
+    return g.Nd % 256 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 256) >= 256 ? cfg : 0;
   return g.Nd % 256 == 0 && cdiv(m_max, 128) * classes * (g.Nd / 256) >= 256 ? cfg : 0;
 }
 // MMAD_STEM=0 routes the MedicalNet stem through the generic implicit GEMM (A/B switch)
@@ -1122,7 +1133,7 @@ bool stem_kernel_on() {
 // rows per M tile of a forward launch (= rows of the BN partial-sum buffer per tile)
 int fwd_tile_rows(const Geom& g, int dtype) {
   const int cfg = big_cfg_for(g, dtype, g.M, 1);
-  if (cfg == 2 || cfg == 4) return 256;
+  if (cfg == 2 || cfg == 4 || cfg == 5 || cfg == 6) return 256;
   if (cfg) return 128;
   return igemm_bm(g.M, g);
 }
@@ -1145,6 +1156,12 @@ int run_igemm_t(const Geom& g, int64_t m_max, int classes, const void* src, cons
       if (cfg == 4)   // 256 x 128 tile, 8 waves (4 x 2), 2-deep ring
         return launch_igemm_bm<T, 128, MODE, 256, 4, 2, 2>(g, m_max, classes, src, w, bias,
                                                           dst, stats, st);
+      if (cfg == 5)   // 256 x 256 tile, 64-B stage rows, 4-deep ring (3 stages in flight)
+        return launch_igemm_bm<T, 256, MODE, 256, 2, 4, 4, 64>(g, m_max, classes, src, w, bias,
+                                                              dst, stats, st);
+      if (cfg == 6)   // 256 x 256 tile, 64-B stage rows, 3-deep ring
+        return launch_igemm_bm<T, 256, MODE, 256, 2, 4, 3, 64>(g, m_max, classes, src, w, bias,
+                                                              dst, stats, st);
     }
   }
   const bool small = igemm_bm(m_max * classes, g) == 64;

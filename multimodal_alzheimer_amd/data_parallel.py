@@ -66,8 +66,23 @@ class GradAllReduce:
             self._launch(bi)
 
     def _launch(self, bi):
-        flat = torch.cat([p.grad.reshape(-1) for p in self.buckets[bi]])
-        work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        grads = [p.grad for p in self.buckets[bi]]
+        if grads[0].is_cuda:
+            # conv weight gradients are produced on volume_ops' side stream (the backward
+            # pass joins it only at its end): gather and reduce there, after the main
+            # stream's gradients (BN, head) too, so the collective overlaps the rest of
+            # the backward without waiting for it
+            from .volume_ops import grad_stream
+            main = torch.cuda.current_stream()
+            side = grad_stream(grads[0].device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                flat = torch.cat([g.reshape(-1) for g in grads])
+                work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group,
+                                       async_op=True)
+        else:
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._inflight[bi] = (flat, work)
 
     def finish(self):
@@ -79,6 +94,9 @@ class GradAllReduce:
                     if p.grad is None:
                         p.grad = torch.zeros_like(p)
                 self._launch(bi)
+        if self.params and self.params[0].is_cuda:
+            from .volume_ops import grad_stream
+            torch.cuda.current_stream().wait_stream(grad_stream(self.params[0].device))
         for bi, (flat, work) in sorted(self._inflight.items()):
             work.wait()
             flat.div_(self.world)

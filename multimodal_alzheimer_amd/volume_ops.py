@@ -13,6 +13,7 @@ Reference ops replaced (file:line in the reference tree):
   global_avg_pool nn.AdaptiveAvgPool3d(1)  anat_cnn.py:66; pet_cnn.py:33
 """
 import ctypes as C
+import os
 
 import torch
 
@@ -71,6 +72,40 @@ FWD_PROBES = {}
 # training-mode BN statistic updates so far (the running buffers are written by our kernels,
 # which torch's tensor version counters do not see); keys the eval-mode folded-weight caches
 _BN_UPDATES = [0]
+
+# Weight gradients run on a second HIP stream: nothing downstream in the backward pass needs
+# dW, so each conv's wgrad (+ split-K reduce) overlaps the dgrad -> BN-backward chain that
+# is the backward's critical path, filling the machine during its small launches.  The
+# main stream joins the side stream once, at the end of the backward pass (an autograd
+# engine callback), before anything (optimizer, gradient all-reduce) reads a dW.
+# Measured 2 % SLOWER on the ResNet-10 step (1564 vs 1598 vol/s, MI355X): the side-stream
+# wgrad blocks take CUs from the one-block-per-CU dgrad tiles on the critical path.  So it
+# is off unless MMAD_WGRAD_STREAM=1 (A/B switch); the gradient all-reduce still uses the
+# side stream (data_parallel.GradAllReduce).
+WGRAD_STREAM = os.environ.get("MMAD_WGRAD_STREAM", "0") == "1"
+_SIDE = {}
+_JOIN_PENDING = set()
+
+
+def grad_stream(device):
+    """The side stream weight gradients are produced on (one per device)."""
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+def _queue_join(main, side):
+    key = (main.cuda_stream, side.cuda_stream)
+    if key in _JOIN_PENDING:
+        return
+    _JOIN_PENDING.add(key)
+
+    def join():
+        _JOIN_PENDING.discard(key)
+        main.wait_stream(side)
+
+    torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
 def pack_weight(d, dt_code, weight, cdtype, for_dgrad):
@@ -308,22 +343,38 @@ class _Conv3dFn(torch.autograd.Function):
             dx = _empty_vol(d.n, d.ci, d.di, d.hi, d.wi, cdtype, gy.device)
             L.call("mmad_conv3d_dgrad", d, dt, L.ptr(gy), L.ptr(wpt), L.ptr(dx), L.stream())
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            lib = L.load()
-            ws = torch.empty((lib.mmad_conv3d_wgrad_workspace(d, dt) + 3) // 4,
-                             dtype=torch.float32, device=gy.device)
-            padded = ctx.ci_real != d.ci
-            dw = torch.empty((d.co, d.ci, d.kd, d.kh, d.kw) if padded else weight.shape,
-                             dtype=torch.float32, device=gy.device)
-            db = (torch.empty(d.co, dtype=torch.float32, device=gy.device)
-                  if ctx.has_bias else None)
-            L.call("mmad_conv3d_wgrad", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db),
-                   L.ptr(ws), L.stream())
-            if padded:                     # cut the zero-lane channels back off
-                taps = d.kd * d.kh * d.kw
-                dw = _pad_rows(dw, d.co, d.ci * taps, ctx.ci_real * taps, weight.shape)
+            main = torch.cuda.current_stream()
+            side = grad_stream(gy.device) if WGRAD_STREAM else main
+            if side is not main:
+                side.wait_stream(main)          # gy (and src) complete
+            with torch.cuda.stream(side):
+                dw, db = _wgrad(ctx, d, dt, src, gy, weight)
+            if side is not main:
+                # memory first used on the side stream stays reserved until it is done
+                for t in (src, gy, dw, db):
+                    if t is not None:
+                        t.record_stream(side)
+                _queue_join(main, side)
             if not ctx.needs_input_grad[1]:
                 dw = None
         return dx, dw, db, None, None, None, None
+
+
+def _wgrad(ctx, d, dt, src, gy, weight):
+    """dW (torch layout, fp32) and the bias gradient of one conv, on the current stream."""
+    lib = L.load()
+    ws = torch.empty((lib.mmad_conv3d_wgrad_workspace(d, dt) + 3) // 4, dtype=torch.float32,
+                     device=gy.device)
+    padded = ctx.ci_real != d.ci
+    dw = torch.empty((d.co, d.ci, d.kd, d.kh, d.kw) if padded else weight.shape,
+                     dtype=torch.float32, device=gy.device)
+    db = torch.empty(d.co, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+    L.call("mmad_conv3d_wgrad", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db), L.ptr(ws),
+           L.stream())
+    if padded:                             # cut the zero-lane channels back off
+        taps = d.kd * d.kh * d.kw
+        dw = _pad_rows(dw, d.co, d.ci * taps, ctx.ci_real * taps, weight.shape)
+    return dw, db
 
 
 def conv3d(x, weight, bias=None, stride=(1, 1, 1), padding=(0, 0, 0), dilation=(1, 1, 1),
