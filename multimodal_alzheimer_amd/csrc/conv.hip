@@ -463,7 +463,8 @@ template <typename T, int BMW, int WBK, int NST, int WBNT = WBN, int WGM = 2, in
 __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* __restrict__ src,
                                                        const T* __restrict__ dy,
                                                        float* __restrict__ ws, int m_per_split,
-                                                       uint32_t src_bytes, uint32_t dy_bytes) {
+                                                       uint32_t src_bytes, uint32_t dy_bytes,
+                                                       int xcd_remap) {
   constexpr int EPC = 16 / (int)sizeof(T);
   constexpr int NW = WGM * WGN;
   constexpr int AROWB = BMW * (int)sizeof(T), BROWB = WBNT * (int)sizeof(T);
@@ -480,8 +481,23 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int k0 = blockIdx.x * WBNT, co0 = blockIdx.y * BMW;
-  const int mbeg = blockIdx.z * m_per_split;
+  // XCD-aware block order: the hardware deals workgroups round-robin over the 8 XCDs, so
+  // in launch order the k-tiles of one m-split (which read the same dY rows and shifted
+  // views of the same X rows) would land on 8 different L2s.  Each XCD instead walks a
+  // contiguous range of (k-tile, co-tile, split) tiles, k fastest.
+  int bxk = blockIdx.x, byc = blockIdx.y, bzs = blockIdx.z;
+  if (xcd_remap) {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int nwg = nx * ny * gridDim.z;
+    const int bid = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+    const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    bxk = tile % nx;
+    byc = (tile / nx) % ny;
+    bzs = tile / (nx * ny);
+  }
+  const int k0 = bxk * WBNT, co0 = byc * BMW;
+  const int mbeg = bzs * m_per_split;
   const int mend = min(g.M, mbeg + m_per_split);
   fill_taps_fwd(g, tapoff);
   __syncthreads();
@@ -705,7 +721,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
     }
   }
   flush();
-  float* out = ws + (int64_t)blockIdx.z * g.Nd * g.K;
+  float* out = ws + (int64_t)bzs * g.Nd * g.K;
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -1180,6 +1196,12 @@ int run_igemm(const Geom& g, int dtype, int64_t m_max, int classes, const void* 
   return run_igemm_t<float, MODE>(g, m_max, classes, src, w, bias, dst, stats, st);
 }
 
+// MMAD_WGRAD_XCD=0 keeps launch-order block placement (A/B switch)
+int wgrad_xcd() {
+  static const int v = [] { const char* e = getenv("MMAD_WGRAD_XCD"); return e ? atoi(e) : 1; }();
+  return v;
+}
+
 template <typename T, int BMW, int WBK, int NST, int WBNT, int WGM, int WGN, bool XFIX>
 int launch_wgrad_x(const Geom& g, const WSplit& sp, const void* x, const void* dy, float* ws,
                    hipStream_t st) {
@@ -1191,7 +1213,7 @@ int launch_wgrad_x(const Geom& g, const WSplit& sp, const void* x, const void* d
   dim3 grid((unsigned)cdiv(g.K, WBNT), (unsigned)cdiv(g.Nd, BMW), (unsigned)sp.splits);
   hipLaunchKernelGGL((wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX>), grid,
                      dim3(64 * WGM * WGN), lds, st, g, (const T*)x, (const T*)dy, ws,
-                     sp.m_per_split, xb, yb);
+                     sp.m_per_split, xb, yb, wgrad_xcd());
   return launch_status();
 }
 
