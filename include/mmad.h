@@ -236,6 +236,16 @@ int mmad_loss_fwd(int b, int c, const double* logits, const int64_t* labels,
                   const double* weight, double gamma, int mode, double* loss,
                   double* dlogits, void* stream);
 
+/* ---- test-set bootstrap (Base_Model.bootstrap_metric, pkg/models/base_model.py:219-239) --
+ * For each of ndraw drawings d (idx[d][0..n) = the drawing's sample indices, as drawn by
+ * torch.randint(0, n, (n,)) in the reference loop): f1[d] = torchmetrics-0.10 macro F1 and
+ * mcc[d] = multiclass Matthews correlation of argmax(logits[idx]) vs labels[idx], f32.
+ * c <= 16.  mmad_mean_std: out = (mean, unbiased std) of v in f64.                      */
+int mmad_bootstrap_cls_metrics(int n, int c, const double* logits, const int64_t* labels,
+                               int ndraw, const int64_t* idx, float* f1, float* mcc,
+                               void* stream);
+int mmad_mean_std(int n, const float* v, double* out, void* stream);
+
 /* ---- input pipeline normalisation (float64, batched over scans) -------------------
  * Replaces MultiModalDataset.__getitem__'s per-sample CPU normalisation
  * (pkg/utils/dataloader.py:213-215 PET, :244-270 MRI per-scan, :272-277 MRI all-scan).

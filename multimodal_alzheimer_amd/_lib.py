@@ -100,6 +100,8 @@ _SIGS = {
     "mmad_split_channels": (_i32, [_i32, _i64, _i32, _i32, _vp, _vp, _vp, _vp]),
     "mmad_max2_fwd": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "mmad_max2_bwd": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_bootstrap_cls_metrics": (_i32, [_i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "mmad_mean_std": (_i32, [_i32, _vp, _vp, _vp]),
 }
 EXPORTS = tuple(_SIGS)
 

@@ -155,7 +155,20 @@ class Base_Model(LightningModule, ABC):
         self.log_dict(d)
 
     def bootstrap_metric(self, metric, y_hat, y_labels, n_drawings=1000):
-        """base_model.py:219-239: mean and 1.96*std over n_drawings resamples."""
+        """base_model.py:219-239: mean and 1.96*std over n_drawings resamples.
+
+        Macro F1 / MCC metrics on device tensors run all drawings in one launch
+        (mmad_bootstrap_cls_metrics, one block per drawing).  The drawings' indices come
+        from the same global torch RNG calls as the reference loop (one (n_drawings, n)
+        randint = n_drawings successive (n,) draws, element for element), so the sampled
+        sets are identical.  Other metric objects keep the reference's loop."""
+        kind = _bootstrap_kind(metric)
+        if kind is not None and y_hat.is_cuda and y_hat.dim() == 2:
+            n = len(y_hat)
+            idx = torch.randint(0, n, (n_drawings, n))
+            f1, mcc = head_ops.bootstrap_cls_metrics(y_hat, y_labels, idx)
+            ms = head_ops.mean_std(f1 if kind == "f1" else mcc).cpu()
+            return ms[0].float(), (1.96 * ms[1]).float()
         metric.to(self.device)
         vals = torch.zeros(n_drawings)
         n = len(y_hat)
@@ -165,6 +178,17 @@ class Base_Model(LightningModule, ABC):
             vals[i] = metric.compute()
             metric.reset()
         return torch.mean(vals), 1.96 * torch.std(vals)
+
+
+def _bootstrap_kind(metric):
+    """'f1' for a macro MulticlassF1Score, 'mcc' for MulticlassMatthewsCorrCoef, else None
+    (torchmetrics classes or the lightning_compat stand-ins)."""
+    name = type(metric).__name__
+    if name == "MulticlassF1Score" and getattr(metric, "average", "macro") == "macro":
+        return "f1"
+    if name == "MulticlassMatthewsCorrCoef":
+        return "mcc"
+    return None
 
 
 # ---------------------------------------------------------------------------- heads

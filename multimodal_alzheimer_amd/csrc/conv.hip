@@ -120,7 +120,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
   // dst lattice: the whole output grid (FWD) or one stride-parity class of dX (DGRAD)
   int pz = 0, py = 0, px = 0, Dc = g.Dd, Hc = g.Hd, Wc = g.Wd, Mc = g.M;
   if (MODE == DGRAD) {
-    const int cls = blockIdx.y;
+    // classes dispatch in blockIdx.y order; the all-odd class (index sd*sh*sw - 1) has the
+    // most taps (2^3 for a stride-2 3^3 conv vs 1 for all-even), so run it first: the light
+    // classes then fill the tail instead of the heavy ones extending it
+    const int cls = (int)gridDim.y - 1 - (int)blockIdx.y;
     px = cls % g.sw; py = (cls / g.sw) % g.sh; pz = cls / (g.sw * g.sh);
     Dc = (g.Dd - pz + g.sd - 1) / g.sd;
     Hc = (g.Hd - py + g.sh - 1) / g.sh;

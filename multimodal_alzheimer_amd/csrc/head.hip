@@ -205,6 +205,78 @@ __global__ __launch_bounds__(256) void loss_kernel(int B, int C, const double* _
   }
 }
 
+// Bootstrap of the test-set classification metrics (pkg/models/base_model.py:219-239):
+// one block per drawing; the drawing's confusion matrix is counted in LDS (integer adds, so
+// the result does not depend on their order), then thread 0 evaluates torchmetrics-0.10
+// macro F1 (classes with tp + fp + fn = 0 left out of the mean) and multiclass MCC (0 when
+// a marginal is degenerate) in f64 and rounds to f32, as metric.compute() returns f32.
+// pred = argmax of the f64 logits row, first index on ties (torch.argmax).
+constexpr int BOOT_MAXC = 16;
+__global__ __launch_bounds__(256) void bootstrap_kernel(int n, int C, const double* __restrict__ x,
+                                                        const int64_t* __restrict__ y,
+                                                        const int64_t* __restrict__ idx,
+                                                        float* __restrict__ f1,
+                                                        float* __restrict__ mcc) {
+  __shared__ int cm[BOOT_MAXC * BOOT_MAXC];
+  const int d = blockIdx.x;
+  for (int i = threadIdx.x; i < C * C; i += blockDim.x) cm[i] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int64_t s = idx[(int64_t)d * n + i];
+    const double* row = x + s * C;
+    int p = 0;
+    double best = row[0];
+    for (int c = 1; c < C; ++c)
+      if (row[c] > best || (row[c] != row[c] && best == best)) { best = row[c]; p = c; }
+    const int64_t t = y[s];
+    if (t >= 0 && t < C) atomicAdd(&cm[t * C + p], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double f1sum = 0.0;
+    int used = 0;
+    double s = 0.0, tr = 0.0, tp_sum = 0.0, pp = 0.0, tt = 0.0;
+    for (int c = 0; c < C; ++c) {
+      double tk = 0.0, pk = 0.0;
+      for (int j = 0; j < C; ++j) { tk += cm[c * C + j]; pk += cm[j * C + c]; }
+      const double tp = cm[c * C + c], fp = pk - tp, fn = tk - tp;
+      if (tp + fp + fn > 0) { f1sum += 2.0 * tp / (2.0 * tp + fp + fn); ++used; }
+      s += tk; tr += tp; tp_sum += tk * pk; pp += pk * pk; tt += tk * tk;
+    }
+    f1[d] = (float)(used ? f1sum / used : 0.0);
+    const double cov_tp = tr * s - tp_sum, cov_pp = s * s - pp, cov_tt = s * s - tt;
+    mcc[d] = (float)(cov_pp * cov_tt == 0.0 ? 0.0 : cov_tp / sqrt(cov_tt * cov_pp));
+  }
+}
+
+// out = (mean, unbiased std) of v[0..n) in f64, fixed-order block reduction
+__global__ __launch_bounds__(256) void mean_std_kernel(int n, const float* __restrict__ v,
+                                                       double* __restrict__ out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += v[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0;
+    for (int k = 0; k < (int)blockDim.x; ++k) a += red[k];
+    red[0] = a / n;
+  }
+  __syncthreads();
+  const double mu = red[0];
+  __syncthreads();
+  double q = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) q += (v[i] - mu) * (v[i] - mu);
+  red[threadIdx.x] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0;
+    for (int k = 0; k < (int)blockDim.x; ++k) a += red[k];
+    out[0] = mu;
+    out[1] = n > 1 ? sqrt(a / (n - 1)) : __builtin_nan("");
+  }
+}
+
 unsigned grid_n(int64_t n, int block = 256) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, block), 256 * 16));
 }
@@ -331,6 +403,23 @@ int mmad_loss_fwd(int b, int c, const double* logits, const int64_t* labels, con
   if (!logits || !labels || !loss || !dlogits) return MMAD_ENULL;
   hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, as_stream(stream), b, c, logits, labels,
                      weight, gamma, mode, loss, dlogits, (int*)nullptr);
+  return launch_status();
+}
+
+int mmad_bootstrap_cls_metrics(int n, int c, const double* logits, const int64_t* labels,
+                               int ndraw, const int64_t* idx, float* f1, float* mcc,
+                               void* stream) {
+  if (n <= 0 || c <= 0 || c > BOOT_MAXC || ndraw <= 0) return MMAD_EBADSHAPE;
+  if (!logits || !labels || !idx || !f1 || !mcc) return MMAD_ENULL;
+  hipLaunchKernelGGL(bootstrap_kernel, dim3((unsigned)ndraw), dim3(256), 0, as_stream(stream), n,
+                     c, logits, labels, idx, f1, mcc);
+  return launch_status();
+}
+
+int mmad_mean_std(int n, const float* v, double* out, void* stream) {
+  if (n <= 0) return MMAD_EBADSHAPE;
+  if (!v || !out) return MMAD_ENULL;
+  hipLaunchKernelGGL(mean_std_kernel, dim3(1), dim3(256), 0, as_stream(stream), n, v, out);
   return launch_status();
 }
 

@@ -175,3 +175,29 @@ def focal_loss(logits, target, gamma):
         n, c = logits.shape[:2]
         logits = logits.reshape(n, c, -1).transpose(1, 2).reshape(-1, c)
     return _LossFn.apply(logits, target.reshape(-1), None, float(gamma), 1)
+
+
+def bootstrap_cls_metrics(logits, labels, idx):
+    """Per-drawing (macro F1, MCC) of argmax(logits[idx[d]]) vs labels[idx[d]] for every
+    drawing d (Base_Model.bootstrap_metric, base_model.py:219-239), one block per drawing.
+    Returns two float32 device tensors of length idx.shape[0]."""
+    L.require_device(logits, labels)
+    x = logits.detach()
+    if x.dtype != torch.float64:
+        x = cast(x, torch.float64)
+    x = x.contiguous()
+    y = labels.contiguous().to(torch.int64)
+    ix = idx.to(device=x.device, dtype=torch.int64).contiguous()
+    nd, n = ix.shape
+    f1 = torch.empty(nd, dtype=torch.float32, device=x.device)
+    mcc = torch.empty_like(f1)
+    L.call("mmad_bootstrap_cls_metrics", n, x.shape[1], L.ptr(x), L.ptr(y), nd, L.ptr(ix),
+           L.ptr(f1), L.ptr(mcc), L.stream())
+    return f1, mcc
+
+
+def mean_std(v):
+    """(mean, unbiased std) of a float32 device vector, f64 accumulation."""
+    out = torch.empty(2, dtype=torch.float64, device=v.device)
+    L.call("mmad_mean_std", v.numel(), L.ptr(v.contiguous()), L.ptr(out), L.stream())
+    return out

@@ -213,3 +213,26 @@ def test_eval_fused_blocks_match_unfused():
             medicalnet.EVAL_FUSED = True
         err = (fused - ref).abs().max().item()
         assert err <= tol * max(1.0, ref.abs().max().item()), (precision, err)
+
+
+@pytest.mark.parametrize("n,c", [(37, 2), (120, 3), (7, 3)])
+def test_bootstrap_metrics_on_device_match_reference_loop(n, c):
+    """Base_Model.bootstrap_metric (base_model.py:219-239) on device vs the oracle's
+    restatement of the reference loop, same global RNG state: the drawn index sets are
+    identical, so mean and CI agree to f32 rounding (ties in the logits included)."""
+    from multimodal_alzheimer_amd.lightning_compat import (MulticlassF1Score,
+                                                          MulticlassMatthewsCorrCoef)
+    from oracle import metrics_ref
+    g = torch.Generator().manual_seed(n)
+    y_hat = torch.randn(n, c, generator=g, dtype=torch.float64).round(decimals=1)
+    y_hat[: n // 4] = torch.relu(y_hat[: n // 4]) * 0       # all-zero rows: argmax ties
+    y = torch.randint(0, c, (n,), generator=g)
+    m = M.Anat_CNN(G.anat_hparams(10, n_classes=c)).to(DEV)
+    for kind, metric in (("f1", MulticlassF1Score(num_classes=c, average="macro")),
+                         ("mcc", MulticlassMatthewsCorrCoef(num_classes=c))):
+        torch.manual_seed(123)
+        mean_ref, ci_ref, _ = metrics_ref.bootstrap(kind, y_hat, y, 1000)
+        torch.manual_seed(123)
+        mean, ci = m.bootstrap_metric(metric, y_hat.to(DEV), y.to(DEV), 1000)
+        assert abs(mean.item() - mean_ref.item()) <= 2e-6, (kind, mean, mean_ref)
+        assert abs(ci.item() - ci_ref.item()) <= 2e-6 * max(1.0, ci_ref.item()), (kind, ci, ci_ref)

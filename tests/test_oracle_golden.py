@@ -79,3 +79,21 @@ def test_tie_argmax_first_index():
     g = G.load("losses")
     assert (torch.from_numpy(g["tie_logits"]).argmax(1).numpy() == g["tie_argmax"]).all()
     assert list(g["tie_argmax"]) == [0, 0, 1, 0]
+
+
+@pytest.mark.parametrize("seed,n,c", [(0, 37, 2), (1, 64, 3), (2, 5, 3)])
+def test_bootstrap_metric_oracle_vs_sklearn(seed, n, c):
+    """The bootstrap metrics restated from torchmetrics 0.10's definitions agree with
+    scikit-learn's independent implementations on every drawing."""
+    from sklearn.metrics import f1_score, matthews_corrcoef
+    from oracle import metrics_ref
+    g = torch.Generator().manual_seed(seed)
+    y_hat = torch.randn(n, c, generator=g, dtype=torch.float64)
+    y = torch.randint(0, c, (n,), generator=g)
+    pred = y_hat.argmax(1)
+    for d in range(20):
+        m = torch.randint(0, n, (n,), generator=g)
+        cm = metrics_ref.confusion(pred[m].numpy(), y[m].numpy(), c)
+        assert abs(metrics_ref.macro_f1(cm) -
+                   f1_score(y[m].numpy(), pred[m].numpy(), average="macro")) < 1e-12
+        assert abs(metrics_ref.mcc(cm) - matthews_corrcoef(y[m].numpy(), pred[m].numpy())) < 1e-12
