@@ -36,6 +36,9 @@ class GradAllReduce:
     def __init__(self, params, bucket_mb=32.0, group=None):
         self.group = group
         self.world = dist.get_world_size(group)
+        # RCCL averages in the collective itself (ncclAvg); gloo has no AVG: sum, then scale
+        self._avg = dist.get_backend(group) == "nccl"
+        self._op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
         self.params = [p for p in params if p.requires_grad]
         cap = int(bucket_mb * (1 << 20))
         self.buckets = []
@@ -52,6 +55,18 @@ class GradAllReduce:
         for bi, b in enumerate(self.buckets):
             for p in b:
                 self._owner[p] = bi
+        # Persistent flat buffer per bucket; each parameter's slice is offered to the conv
+        # backward as its weight-gradient destination (``p._mmad_grad_view``), so the big
+        # conv gradients are produced in place: no gather before the collective and no
+        # copy back after it.  Gradients produced elsewhere (BN, head) are copied in/out.
+        self.flats = []
+        for b in self.buckets:
+            flat = torch.empty(sum(p.numel() for p in b), dtype=b[0].dtype, device=b[0].device)
+            off = 0
+            for p in b:
+                p._mmad_grad_view = flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            self.flats.append(flat)
         self._hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
         self.reset()
 
@@ -65,29 +80,37 @@ class GradAllReduce:
         if self._pending[bi] == 0:
             self._launch(bi)
 
+    def _foreign(self, bi):
+        """(grads, views) of the bucket's parameters whose .grad is not their slice."""
+        pairs = [(p.grad, p._mmad_grad_view) for p in self.buckets[bi]
+                 if p.grad.data_ptr() != p._mmad_grad_view.data_ptr()]
+        return [g for g, _ in pairs], [v for _, v in pairs]
+
     def _launch(self, bi):
-        grads = [p.grad for p in self.buckets[bi]]
-        if grads[0].is_cuda:
-            # conv weight gradients are produced on volume_ops' side stream (the backward
+        flat = self.flats[bi]
+        grads, views = self._foreign(bi)
+        if flat.is_cuda:
+            # conv weight gradients may come from volume_ops' side stream (the backward
             # pass joins it only at its end): gather and reduce there, after the main
             # stream's gradients (BN, head) too, so the collective overlaps the rest of
             # the backward without waiting for it
             from .volume_ops import grad_stream
             main = torch.cuda.current_stream()
-            side = grad_stream(grads[0].device)
+            side = grad_stream(flat.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                flat = torch.cat([g.reshape(-1) for g in grads])
-                work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group,
-                                       async_op=True)
+                if grads:
+                    torch._foreach_copy_(views, grads)
+                work = dist.all_reduce(flat, op=self._op, group=self.group, async_op=True)
         else:
-            flat = torch.cat([g.reshape(-1) for g in grads])
-            work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        self._inflight[bi] = (flat, work)
+            if grads:
+                torch._foreach_copy_(views, grads)
+            work = dist.all_reduce(flat, op=self._op, group=self.group, async_op=True)
+        self._inflight[bi] = work
 
     def finish(self):
         """Wait for every bucket (launching any whose grads never all arrived), then
-        write grad = mean over ranks back into each parameter."""
+        make every parameter's grad the mean over ranks."""
         for bi, b in enumerate(self.buckets):
             if bi not in self._inflight:
                 for p in b:
@@ -97,14 +120,14 @@ class GradAllReduce:
         if self.params and self.params[0].is_cuda:
             from .volume_ops import grad_stream
             torch.cuda.current_stream().wait_stream(grad_stream(self.params[0].device))
-        for bi, (flat, work) in sorted(self._inflight.items()):
+        for bi, work in sorted(self._inflight.items()):
             work.wait()
-            flat.div_(self.world)
-            off = 0
-            for p in self.buckets[bi]:
-                n = p.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
-                off += n
+            if not self._avg:
+                self.flats[bi].div_(self.world)
+            grads, views = self._foreign(bi)
+            if grads:
+                # one multi-tensor launch per bucket, not one copy kernel per parameter
+                torch._foreach_copy_(grads, views)
         self.reset()
 
     def remove(self):

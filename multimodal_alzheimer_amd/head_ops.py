@@ -11,7 +11,7 @@ import ctypes as C
 import torch
 
 from . import _lib as L
-from .volume_ops import cast
+from .volume_ops import cast, grad_slot
 
 
 class _LinearFn(torch.autograd.Function):
@@ -31,6 +31,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight, y if relu else None)
         ctx.has_bias = bias is not None
         ctx.relu = relu
+        ctx.params = (weight, bias)        # gradient-slot lookup (volume_ops.grad_slot)
         return y
 
     @staticmethod
@@ -50,9 +51,9 @@ class _LinearFn(torch.autograd.Function):
             dx = torch.empty_like(x)
         need_w = ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2])
         if need_w:
-            dw = torch.empty(weight.shape, dtype=torch.float32, device=g.device)
+            dw = grad_slot(ctx.params[0], tuple(weight.shape), g.device)
             if ctx.has_bias:
-                db = torch.empty(n_out, dtype=torch.float32, device=g.device)
+                db = grad_slot(ctx.params[1], (n_out,), g.device)
         L.call("mmad_linear_bwd", b, n_in, n_out, L.ptr(x), L.ptr(weight.detach()), L.ptr(g),
                L.ptr(dx), L.ptr(dw), L.ptr(db), L.stream())
         return dx, (dw if ctx.needs_input_grad[1] else None), db, None

@@ -108,6 +108,17 @@ def _queue_join(main, side):
     torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
+def grad_slot(param, shape, device):
+    """Destination for a parameter's gradient: a fresh alias of its data-parallel bucket
+    slice (``_mmad_grad_view``, set by data_parallel.GradAllReduce) while the parameter has
+    no gradient yet -- autograd then adopts it as ``.grad`` and the all-reduce needs no
+    gather -- else a new fp32 tensor."""
+    slot = getattr(param, "_mmad_grad_view", None) if param is not None else None
+    if slot is not None and param.grad is None and tuple(slot.shape) == tuple(shape):
+        return slot.view(slot.shape)
+    return torch.empty(shape, dtype=torch.float32, device=device)
+
+
 def pack_weight(d, dt_code, weight, cdtype, for_dgrad):
     lib = L.load()
     n = lib.mmad_conv_packed_elems(d, dt_code, int(for_dgrad))
@@ -315,6 +326,7 @@ class _Conv3dFn(torch.autograd.Function):
             e1.record()
             probe.append((e0, e1))
         ctx.save_for_backward(src, weight)
+        ctx.wparam = weight                # the Parameter itself (gradient slot lookup)
         ctx.wpt = wpt                      # prepacked dgrad layout (or None: pack in bwd)
         ctx.set_materialize_grads(False)   # the stats output never gets a gradient
         ctx.desc = _desc_tuple(d)
@@ -348,7 +360,7 @@ class _Conv3dFn(torch.autograd.Function):
             if side is not main:
                 side.wait_stream(main)          # gy (and src) complete
             with torch.cuda.stream(side):
-                dw, db = _wgrad(ctx, d, dt, src, gy, weight)
+                dw, db = _wgrad(ctx, d, dt, src, gy, weight, ctx.wparam)
             if side is not main:
                 # memory first used on the side stream stays reserved until it is done
                 for t in (src, gy, dw, db):
@@ -360,14 +372,22 @@ class _Conv3dFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
-def _wgrad(ctx, d, dt, src, gy, weight):
-    """dW (torch layout, fp32) and the bias gradient of one conv, on the current stream."""
+def _wgrad(ctx, d, dt, src, gy, weight, wparam=None):
+    """dW (torch layout, fp32) and the bias gradient of one conv, on the current stream.
+    When the weight parameter carries a gradient slot (``_mmad_grad_view``: its slice of
+    a data-parallel bucket, data_parallel.GradAllReduce) and has no gradient yet, dW is
+    written straight into it; autograd then adopts that tensor as ``.grad`` as-is."""
     lib = L.load()
     ws = torch.empty((lib.mmad_conv3d_wgrad_workspace(d, dt) + 3) // 4, dtype=torch.float32,
                      device=gy.device)
     padded = ctx.ci_real != d.ci
-    dw = torch.empty((d.co, d.ci, d.kd, d.kh, d.kw) if padded else weight.shape,
-                     dtype=torch.float32, device=gy.device)
+    slot = getattr(wparam, "_mmad_grad_view", None) if wparam is not None else None
+    if slot is not None and not padded and wparam.grad is None and \
+            slot.shape == weight.shape and slot.dtype == torch.float32:
+        dw = slot.view(slot.shape)     # a fresh alias: autograd adopts it only if unshared
+    else:
+        dw = torch.empty((d.co, d.ci, d.kd, d.kh, d.kw) if padded else weight.shape,
+                         dtype=torch.float32, device=gy.device)
     db = torch.empty(d.co, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
     L.call("mmad_conv3d_wgrad", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db), L.ptr(ws),
            L.stream())
@@ -498,7 +518,8 @@ def _finalize(y, parts, bn, training):
     return mean, invstd, scale, shift, use_batch
 
 
-def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask):
+def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask,
+                 params=(None, None)):
     m, c = _rows(y)
     dev = y.device
     dt = L.dtype_code(y.dtype)
@@ -506,8 +527,8 @@ def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask):
     parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
     L.call("mmad_bn_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y), L.ptr(mean),
            L.ptr(invstd), L.ptr(parts), L.stream())
-    dgamma = torch.empty(c, dtype=torch.float32, device=dev)
-    dbeta = torch.empty_like(dgamma)
+    dgamma = grad_slot(params[0], (c,), dev)
+    dbeta = grad_slot(params[1], (c,), dev)
     coef = torch.empty(3 * c, dtype=torch.float32, device=dev)
     L.call("mmad_bn_bwd_finalize", c, m, nparts, L.ptr(parts), L.ptr(gamma), L.ptr(invstd),
            int(batch_stats), L.ptr(dgamma), L.ptr(dbeta), L.ptr(coef), L.stream())
@@ -538,6 +559,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.save_for_backward(y, out if relu else None, mean, invstd, gamma,
                               res if rbn is not None else None, rmean, rinvstd, rgamma)
         ctx.cfg = (relu, batch, rbatch, res is not None, rbn is not None)
+        ctx.params = ((gamma, beta), (rgamma, rbeta))   # gradient-slot lookup (grad_slot)
         return out
 
     @staticmethod
@@ -549,11 +571,12 @@ class _BNActFn(torch.autograd.Function):
             g = cast(g, y.dtype)
         gam = None if gamma is None else gamma.detach()
         dy, dgamma, dbeta, gmask = _bn_backward(g, out, y, mean, invstd, gam, batch,
-                                                has_res and not has_rbn)
+                                                has_res and not has_rbn, ctx.params[0])
         dres = drg = drb = None
         if has_rbn:
             rg = None if rgamma is None else rgamma.detach()
-            dres, drg, drb, _ = _bn_backward(g, out, rres, rmean, rinvstd, rg, rbatch, False)
+            dres, drg, drb, _ = _bn_backward(g, out, rres, rmean, rinvstd, rg, rbatch, False,
+                                             ctx.params[1])
         elif has_res:
             dres = gmask
         return (dy, None, dgamma if ctx.needs_input_grad[2] else None,
@@ -600,6 +623,7 @@ class _BNReluPoolFn(torch.autograd.Function):
                L.ptr(y), L.ptr(scale), L.ptr(shift), L.ptr(out), L.ptr(am), L.ptr(ymax),
                L.stream())
         ctx.save_for_backward(y, am, ymax, mean, invstd, gamma)
+        ctx.params = (gamma, beta)
         ctx.geo = (n, c, di, hi, wi, do, ho, wo, k, s, p)
         ctx.batch = batch
         return out
@@ -618,8 +642,8 @@ class _BNReluPoolFn(torch.autograd.Function):
         parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
         L.call("mmad_bnpool_bwd_reduce", dt, mp, c, L.ptr(g), L.ptr(am), L.ptr(ymax),
                L.ptr(mean), L.ptr(invstd), L.ptr(parts), L.stream())
-        dgamma = torch.empty(c, dtype=torch.float32, device=dev)
-        dbeta = torch.empty_like(dgamma)
+        dgamma = grad_slot(ctx.params[0], (c,), dev)
+        dbeta = grad_slot(ctx.params[1], (c,), dev)
         coef = torch.empty(3 * c, dtype=torch.float32, device=dev)
         gam = None if gamma is None else gamma.detach()
         L.call("mmad_bn_bwd_finalize", c, n * di * hi * wi, nparts, L.ptr(parts), L.ptr(gam),

@@ -236,3 +236,37 @@ def test_bootstrap_metrics_on_device_match_reference_loop(n, c):
         mean, ci = m.bootstrap_metric(metric, y_hat.to(DEV), y.to(DEV), 1000)
         assert abs(mean.item() - mean_ref.item()) <= 2e-6, (kind, mean, mean_ref)
         assert abs(ci.item() - ci_ref.item()) <= 2e-6 * max(1.0, ci_ref.item()), (kind, ci, ci_ref)
+
+
+def test_grad_allreduce_rccl_bucket_views_single_rank():
+    """GradAllReduce over RCCL (world 1, so the mean is the local gradient): conv weight
+    gradients written straight into the bucket slices, BN / head gradients copied in and
+    out; two steps with set_to_none=True and one accumulating step (set_to_none=False)
+    all equal the plain single-process gradients."""
+    import torch.distributed as dist
+    from multimodal_alzheimer_amd.data_parallel import GradAllReduce
+    batch = {k: v.to(DEV) for k, v in G.batch_for((2, 32, 32, 32), 2, 41).items()}
+    ref = M.Anat_CNN(G.anat_hparams(10, linear_out=[32]))
+    G.load_prng_weights(ref, 40)
+    ref = ref.to(DEV)
+    mdl = M.Anat_CNN(G.anat_hparams(10, linear_out=[32]))
+    mdl.load_state_dict(ref.state_dict())
+    mdl = mdl.to(DEV)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29561", rank=0, world_size=1,
+                            device_id=torch.device(DEV, torch.cuda.current_device()))
+    try:
+        red = GradAllReduce(mdl.parameters(), bucket_mb=8.0)
+        assert len(red.buckets) > 1
+        for step, none in enumerate((True, True, False)):
+            for m in (ref, mdl):
+                m.zero_grad(set_to_none=none)
+                m.general_step(batch, 0, "train")["loss"].backward()
+            red.finish()
+            torch.cuda.synchronize()
+            conv = mdl.model.layer4[0].conv2.weight
+            if none:
+                assert conv.grad.data_ptr() == conv._mmad_grad_view.data_ptr(), step
+            for (k, a), (_, b) in zip(ref.named_parameters(), mdl.named_parameters()):
+                assert torch.allclose(a.grad, b.grad, rtol=1e-5, atol=1e-7), (step, k)
+    finally:
+        dist.destroy_process_group()
