@@ -117,7 +117,16 @@ def main():
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--workload", default="mri", choices=["mri", "fusion", "three"],
+                    help="mri: BASELINE config 2 (the metric); fusion: config 3/4, PET+MRI "
+                         "ResNet-10 x2 + MLP head, focal loss, pairs/sec; three: config 5, "
+                         "MRI ResNet-34 + PET ResNet-18 + tabular MLP at 160^3, triples/sec")
     args = ap.parse_args()
+    if args.workload != "mri":
+        args.no_roofline = True         # the probe times config 2's dominant kernel
+        args.no_cpu_baseline = True
+        if args.workload == "three" and args.size == 128:
+            args.size = 160
     # stdout carries exactly one JSON line: everything else (RCCL's version banner, library
     # chatter) goes to stderr; the result is written to the saved stdout descriptor
     sys.stdout.flush()
@@ -134,7 +143,13 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     torch.manual_seed(15 + rank)
-    model = M.Anat_CNN(hparams(args.precision)).cuda()
+    if args.workload == "mri":
+        model = M.Anat_CNN(hparams(args.precision)).cuda()
+    elif args.workload == "fusion":
+        model = M.PET_MRI_ResNet_Fusion(dict(hparams(args.precision), fl_gamma=2)).cuda()
+    else:
+        model = M.All_Modalities_Fusion(dict(hparams(args.precision), fl_gamma=2,
+                                             resnet_depth_mri=34, resnet_depth_pet=18)).cuda()
     opt = model.configure_optimizers()
     # 4 MiB buckets: layer4's big weights still go in early (each its own bucket, launched
     # while backward continues), and the bucket launched last -- stem + layer1, ready only
@@ -144,6 +159,11 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)   # this rank's shard
     batch = {"mri": torch.rand((B, S, S, S), device="cuda", dtype=torch.float64, generator=g),
              "label": torch.randint(0, 2, (B,), device="cuda", generator=g)}
+    if args.workload != "mri":            # z-scored PET (dataloader.py:213-215)
+        batch["pet1451"] = torch.randn((B, S, S, S), device="cuda", dtype=torch.float64,
+                                       generator=g)
+    if args.workload == "three":          # 9 tabular features (dataloader.py:306)
+        batch["tabular"] = torch.rand((B, 9), device="cuda", dtype=torch.float64, generator=g)
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -187,7 +207,19 @@ def main():
                    "global_batch": B * world, "volume": [1, S, S, S],
                    "parallelism": f"dp{world}"},
     }
-    if S in FLOP_PER_VOL:
+    if args.workload != "mri":
+        unit = "pairs/sec" if args.workload == "fusion" else "triples/sec"
+        desc = ("BASELINE config 3/4: PET+MRI ResNet-10 x2 late fusion + MLP head"
+                if args.workload == "fusion" else
+                "BASELINE config 5: MRI ResNet-34 + PET ResNet-18 + tabular MLP")
+        result.update({
+            "metric": f"{unit} fwd+bwd, {desc} @{S}^3 bf16 (secondary workload)",
+            "unit": unit,
+            "config": {"workload": f"{desc}, 2x1x{S}^3 (+9 tabular), batch {B}/GPU, focal "
+                                   f"loss gamma 2, Adam, fwd+bwd+step",
+                       "global_batch": B * world, "volume": [1, S, S, S],
+                       "parallelism": f"dp{world}"}})
+    elif S in FLOP_PER_VOL:
         per_gpu = value / world
         result["step_mfma_frac"] = per_gpu * FLOP_PER_VOL[S] / (
             PEAK_BF16 if cdtype == torch.bfloat16 else PEAK_F32)
