@@ -25,6 +25,10 @@ constexpr int CO = 64;            // output channels
 constexpr int YT = 2;             // output rows per block
 constexpr int XW = 64;            // output columns per row (max)
 constexpr int ROWB = XW * 16;     // one unfolded input row in LDS (1 KiB)
+// wgrad ring rows are padded by 64 B: its transposing U reads put lanes two taps (= two
+// rows) apart in one 32-lane group, and 1088-byte rows move those onto the other 16 banks
+// (at 1024 B every such pair was a 2-way conflict)
+constexpr int ROWB_W = ROWB + 64;
 constexpr int CROW = CO * 2 + 16; // C tile row (bf16, padded)
 
 __device__ const u32x4 g_zero_kb[64] = {};   // 1 KiB of zeros: DMA source for padding rows
@@ -282,7 +286,7 @@ __global__ __launch_bounds__(512) void stem_wgrad_kernel(StemG g, const u16* __r
     const void* p = ok ? (const void*)(U + ((((int64_t)nb * g.di + zi) * g.hi + yi) * g.wo +
                                             lane) * 8)
                        : (const void*)(g_zero_kb + lane);
-    glds16_asm(p, lds_addr_of(ring + (slot * YIN + t) * ROWB));
+    glds16_asm(p, lds_addr_of(ring + (slot * YIN + t) * ROWB_W));
   };
   // dY tile of z-step oz: 128 rows (voxel m = yl*64 + x) of 64 channels; one DMA
   // instruction = 8 rows; lane chunk swizzled so the transposing reads are conflict-free
@@ -333,7 +337,7 @@ __global__ __launch_bounds__(512) void stem_wgrad_kernel(StemG g, const u16* __r
 #pragma unroll
   for (int j = 0; j < 7; ++j) {
     const int t = min(2 * (7 * wk + j) + (p >> 1), KD * KH - 1);
-    b_off[j] = ((t / KH) << 20) | ((t % KH) * ROWB + (p & 1) * 8);
+    b_off[j] = ((t / KH) << 20) | ((t % KH) * ROWB_W + (p & 1) * 8);
   }
 
 #pragma unroll 1
@@ -363,7 +367,7 @@ __global__ __launch_bounds__(512) void stem_wgrad_kernel(StemG g, const u16* __r
       for (int j = 0; j < 7; ++j) {                // U: k tile j
         int slot = sbase + (b_off[j] >> 20);
         slot -= slot >= g.rz ? g.rz : 0;
-        const char* rowp = ring + (slot * YIN + yl * SH) * ROWB + (b_off[j] & 0xfffff);
+        const char* rowp = ring + (slot * YIN + yl * SH) * ROWB_W + (b_off[j] & 0xfffff);
         bf16x4 vlo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)(rowp + x0 * 16));
         bf16x4 vhi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)(rowp + x1 * 16));
         fb[j] = __builtin_shufflevector(vlo, vhi, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -400,7 +404,10 @@ bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds) {
   g.sd = d->sd; g.sh = d->sh; g.pd = d->pd; g.ph = d->ph;
   const int ntap = d->kd * d->kh;
   g.kpad = (int)cdiv(ntap * 8, 64) * 64;        // as mmad_conv_pack_weight (mode 2)
-  g.wrow = g.kpad * 2 + 16;
+  // weight row stride: (wrow / 16) % 16 == 10 makes the B-fragment reads (16 rows x 4 tap
+  // groups per 16-lane ds_read_b128 group) hit 16 distinct 16-byte bank slots; the former
+  // +16-byte pad (57 slots: % 16 == 9) put up to 8 lanes of a group on one slot
+  g.wrow = g.kpad * 2 + 16 * (int)(((10 - (g.kpad * 2 / 16)) % 16 + 16) % 16);
   g.rz = d->kd + g.sd;                           // planes of this and the next z-step
   g.yin = (YT - 1) * g.sh + d->kh;
   g.nks = (int)cdiv(ntap, 4);
@@ -451,7 +458,7 @@ int wgrad(const mmad_conv_desc* d, const void* x_unf, const void* dy, float* ws,
   size_t lds;
   if (!geom_for(d, g, blocks, lds)) return MMAD_EUNSUPPORTED;
   // LDS: U plane ring, then two dY tiles
-  g.ring_off = g.rz * g.yin * ROWB;
+  g.ring_off = g.rz * g.yin * ROWB_W;
   const size_t wl = (size_t)g.ring_off + 2 * YT * XW * CO * 2;
   static const bool ok = hipFuncSetAttribute((const void*)stem_wgrad_kernel<7, 7, 2, 2>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
