@@ -29,7 +29,8 @@ sys.path.insert(0, REPO)
 
 import multimodal_alzheimer_amd as M  # noqa: E402
 from multimodal_alzheimer_amd import _lib, volume_ops  # noqa: E402
-from multimodal_alzheimer_amd.data_parallel import GradAllReduce  # noqa: E402
+from multimodal_alzheimer_amd.data_parallel import (GradAllReduce,  # noqa: E402
+                                                    broadcast_module_state)
 
 W2 = [0.20314960629921264, 0.7968503937007874]
 FLOP_PER_VOL = {128: 424.7e9}            # fwd+bwd ResNet-10 @128^3
@@ -154,7 +155,10 @@ def main():
     # 4 MiB buckets: layer4's big weights still go in early (each its own bucket, launched
     # while backward continues), and the bucket launched last -- stem + layer1, ready only
     # when backward ends, so its all-reduce is not hidden -- stays ~1 MB instead of ~15 MB
-    reducer = GradAllReduce(model.parameters(), bucket_mb=4.0) if dp else None
+    reducer = None
+    if dp:
+        broadcast_module_state(model)          # identical replicas, as DDP
+        reducer = GradAllReduce(model.parameters(), bucket_mb=4.0)
     B, S = args.batch, args.size
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)   # this rank's shard
     batch = {"mri": torch.rand((B, S, S, S), device="cuda", dtype=torch.float64, generator=g),

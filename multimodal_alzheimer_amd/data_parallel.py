@@ -32,6 +32,14 @@ def shard_indices(n_samples, rank, world, epoch=0, shuffle=True, seed=15):
     return order[rank:total:world]
 
 
+def broadcast_module_state(module, src=0, group=None):
+    """Every rank starts from rank ``src``'s parameters and buffers (BN running statistics,
+    num_batches_tracked), as DDP does at construction."""
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src=src, group=group)
+
+
 class GradAllReduce:
     def __init__(self, params, bucket_mb=32.0, group=None):
         self.group = group

@@ -11,7 +11,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 import torch.nn as nn
 
-from multimodal_alzheimer_amd.data_parallel import GradAllReduce, shard_indices
+from multimodal_alzheimer_amd.data_parallel import (GradAllReduce, broadcast_module_state,
+                                                    shard_indices)
 
 
 def _model():
@@ -66,3 +67,26 @@ def test_shard_indices_cover(n, world):
     assert len(flat) == -(-n // world) * world
     assert shard_indices(n, 0, world, epoch=3) == shards[0]
     assert shard_indices(n, 0, world, epoch=4) != shards[0] or n < 3
+
+
+def _bcast_worker(rank, world, init_file, out_file):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank,
+                            world_size=world)
+    torch.manual_seed(100 + rank)                      # deliberately different replicas
+    m = nn.Sequential(nn.Linear(4, 8), nn.BatchNorm1d(8))
+    m[1].running_mean.fill_(float(rank))
+    broadcast_module_state(m)
+    torch.save({k: v.clone() for k, v in m.state_dict().items()}, f"{out_file}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_broadcast_module_state_makes_replicas_identical():
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_bcast_worker, args=(world, os.path.join(td, "init"), os.path.join(td, "sd")),
+                 nprocs=world, join=True)
+        sds = [torch.load(os.path.join(td, f"sd.{r}"), weights_only=True) for r in range(world)]
+    for k in sds[0]:
+        assert torch.equal(sds[0][k], sds[1][k]), k
+    assert torch.equal(sds[1]["1.running_mean"], torch.zeros(8))
