@@ -141,6 +141,15 @@ int mmad_bn_bwd_finalize(int c, int64_t count, int nparts, const float* parts,
 int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* relu_out,
                       const void* y, const float* mean, const float* invstd,
                       const float* coef, void* dy, void* gmask_out, void* stream);
+/* BN + ReLU without residual (bn1 of every BasicBlock): the same two passes with the ReLU
+ * mask recomputed from y as fma(y, scale, shift) > 0 (the forward's affine, so the mask
+ * equals out > 0) instead of read from the ReLU output -- one tensor fewer per pass. */
+int mmad_bn_relu_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* y,
+                            const float* mean, const float* invstd, const float* scale,
+                            const float* shift, float* parts, void* stream);
+int mmad_bn_relu_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* y,
+                           const float* mean, const float* invstd, const float* scale,
+                           const float* shift, const float* coef, void* dy, void* stream);
 int mmad_relu_fwd(int dtype, int64_t n, const void* x, void* y, void* stream);
 int mmad_relu_bwd(int dtype, int64_t n, const void* g, const void* out, void* dx, void* stream);
 int mmad_add(int dtype, int64_t n, const void* a, const void* b, void* out, void* stream);

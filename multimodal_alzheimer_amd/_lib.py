@@ -102,6 +102,8 @@ _SIGS = {
     "mmad_max2_bwd": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "mmad_bootstrap_cls_metrics": (_i32, [_i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "mmad_mean_std": (_i32, [_i32, _vp, _vp, _vp]),
+    "mmad_bn_relu_bwd_reduce": (_i32, [_i32, _i64, _i32] + [_vp] * 8),
+    "mmad_bn_relu_bwd_apply": (_i32, [_i32, _i64, _i32] + [_vp] * 9),
 }
 EXPORTS = tuple(_SIGS)
 

@@ -40,7 +40,9 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ invstd,
                                                      float* __restrict__ parts,
-                                                     const uint8_t* __restrict__ act) {
+                                                     const uint8_t* __restrict__ act,
+                                                     const float* __restrict__ msc,
+                                                     const float* __restrict__ msh) {
   __shared__ float red[2][2048];
   const int tid = threadIdx.x;
   const int lpr = C / V;
@@ -52,21 +54,30 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
 #pragma unroll
   for (int e = 0; e < V; ++e) { s[e] = 0.f; q[e] = 0.f; }
   if (rl < rpar) {
-    float mu[V], is[V];
-    if (MODE == 1 || MODE == 3) {
+    float mu[V], is[V], sc[V], sh[V];
+    if (MODE == 1 || MODE == 3 || MODE == 4) {
 #pragma unroll
       for (int e = 0; e < V; ++e) { mu[e] = mean[cl * V + e]; is[e] = invstd[cl * V + e]; }
+    }
+    if (MODE == 4) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) { sc[e] = msc[cl * V + e]; sh[e] = msh[cl * V + e]; }
     }
     for (int64_t r = r0 + rl; r < r1; r += rpar) {
       const int64_t i = r * C + cl * V;
       float yv[V];
       if constexpr (V == Chunk<T>::N) Chunk<T>::load(y + i, yv);
       else for (int e = 0; e < V; ++e) yv[e] = Elt<T>::ld(y, i + e);
-      if (MODE == 1 || MODE == 3) {
+      if (MODE == 1 || MODE == 3 || MODE == 4) {
         float gv[V], ov[V];
         if constexpr (V == Chunk<T>::N) Chunk<T>::load(g + i, gv);
         else for (int e = 0; e < V; ++e) gv[e] = Elt<T>::ld(g, i + e);
-        if (MODE == 3) {
+        if (MODE == 4) {
+          // ReLU mask of a BN+ReLU without residual, recomputed from its input y with the
+          // forward's own affine (bn_affine): out > 0 <=> fma(y, scale, shift) > 0
+#pragma unroll
+          for (int e = 0; e < V; ++e) gv[e] = bn_affine(yv[e], sc[e], sh[e]) > 0.f ? gv[e] : 0.f;
+        } else if (MODE == 3) {
 #pragma unroll
           for (int e = 0; e < V; ++e) gv[e] = (act[i + e] & 0x80) ? gv[e] : 0.f;
         } else if (relu_out != nullptr) {
@@ -119,16 +130,19 @@ __global__ void parts_fold_kernel(int C, int nparts, int group, const float* __r
 template <typename T, int MODE>
 int launch_colsum(int64_t M, int C, const void* y, const void* g, const void* ro,
                   const float* mean, const float* invstd, float* parts, hipStream_t st,
-                  const uint8_t* act = nullptr) {
+                  const uint8_t* act = nullptr, const float* msc = nullptr,
+                  const float* msh = nullptr) {
   const PartPlan pp = part_plan(M);
   constexpr int VEC = Chunk<T>::N;
   dim3 grid((unsigned)pp.nparts);
   if (C % VEC == 0 && C / VEC <= 256) {
     hipLaunchKernelGGL((colsum_kernel<T, MODE, VEC>), grid, dim3(256), 0, st, M, C, pp.rpp,
-                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act);
+                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act, msc,
+                       msh);
   } else if (C <= 256) {
     hipLaunchKernelGGL((colsum_kernel<T, MODE, 1>), grid, dim3(256), 0, st, M, C, pp.rpp,
-                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act);
+                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act, msc,
+                       msh);
   } else {
     return MMAD_EUNSUPPORTED;
   }
@@ -370,11 +384,12 @@ __global__ void scale_shift_act_scalar_kernel(int64_t M, int C, const T* __restr
 
 // Fixed-channel form of bn_bwd_apply_kernel (C / V a power of two dividing 256): per-thread
 // channel vector constant, its mean/invstd/coef loaded once as vectors; two chunks a trip.
-template <typename T>
+template <typename T, bool MASKY = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
     int64_t nv, int cpr, int C, const T* __restrict__ g, const T* __restrict__ relu_out,
     const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
-    const float* __restrict__ coef, T* __restrict__ dy, T* __restrict__ gmask) {
+    const float* __restrict__ coef, T* __restrict__ dy, T* __restrict__ gmask,
+    const float* __restrict__ msc = nullptr, const float* __restrict__ msh = nullptr) {
   constexpr int V = Chunk<T>::N;
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -385,11 +400,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
   ld_params<V>(coef + c0, k0);
   ld_params<V>(coef + C + c0, k1);
   ld_params<V>(coef + 2 * C + c0, k2);
+  float sc[V], sh[V];
+  if constexpr (MASKY) {
+    ld_params<V>(msc + c0, sc);
+    ld_params<V>(msh + c0, sh);
+  }
   auto one = [&](int64_t q, const float* gv0, const float* yv, const float* ov) {
     float gv[V], dv[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      gv[e] = (relu_out && !(ov[e] > 0.f)) ? 0.f : gv0[e];
+      if constexpr (MASKY) gv[e] = bn_affine(yv[e], sc[e], sh[e]) > 0.f ? gv0[e] : 0.f;
+      else gv[e] = (relu_out && !(ov[e] > 0.f)) ? 0.f : gv0[e];
       const float xh = (yv[e] - mu[e]) * is[e];
       dv[e] = k0[e] * gv[e] - k1[e] - xh * k2[e];
     }
@@ -607,6 +628,43 @@ int mmad_bn_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* r
   if (dtype == MMAD_BF16)
     return launch_colsum<u16, 1>(m, c, y, g, relu_out, mean, invstd, parts, as_stream(stream));
   return launch_colsum<float, 1>(m, c, y, g, relu_out, mean, invstd, parts, as_stream(stream));
+}
+
+// BN + ReLU (no residual) backward with the ReLU mask recomputed from y: the same partial
+// sums / input gradient as mmad_bn_bwd_reduce / _apply with relu_out, without reading it
+int mmad_bn_relu_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* y,
+                            const float* mean, const float* invstd, const float* scale,
+                            const float* shift, float* parts, void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!g || !y || !mean || !invstd || !scale || !shift || !parts) return MMAD_ENULL;
+  if (dtype == MMAD_BF16)
+    return launch_colsum<u16, 4>(m, c, y, g, nullptr, mean, invstd, parts, as_stream(stream),
+                                 nullptr, scale, shift);
+  return launch_colsum<float, 4>(m, c, y, g, nullptr, mean, invstd, parts, as_stream(stream),
+                                 nullptr, scale, shift);
+}
+
+int mmad_bn_relu_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* y,
+                           const float* mean, const float* invstd, const float* scale,
+                           const float* shift, const float* coef, void* dy, void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!g || !y || !mean || !invstd || !scale || !shift || !coef || !dy) return MMAD_ENULL;
+  const int vv = dtype == MMAD_BF16 ? 8 : 4;
+  if (!(c % vv == 0 && is_pow2(c / vv) && c / vv <= 256)) return MMAD_EUNSUPPORTED;
+  const int64_t nv = m * c / vv;
+  hipStream_t st = as_stream(stream);
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_fc_kernel<u16, true>), dim3(ew_grid(nv)), dim3(256), 0, st,
+                       nv, c / vv, c, (const u16*)g, (const u16*)nullptr, (const u16*)y, mean,
+                       invstd, coef, (u16*)dy, (u16*)nullptr, scale, shift);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_fc_kernel<float, true>), dim3(ew_grid(nv)), dim3(256), 0,
+                       st, nv, c / vv, c, (const float*)g, (const float*)nullptr,
+                       (const float*)y, mean, invstd, coef, (float*)dy, (float*)nullptr, scale,
+                       shift);
+  return launch_status();
 }
 
 int mmad_bnpool_bwd_reduce(int dtype, int64_t m, int c, const void* g, const uint8_t* argmax,

@@ -518,15 +518,30 @@ def _finalize(y, parts, bn, training):
     return mean, invstd, scale, shift, use_batch
 
 
+def _mask_from_y_ok(y):
+    """the fixed-channel apply kernel (and so the y-mask variant) covers this layout"""
+    c = y.shape[1]
+    v = 8 if y.dtype == torch.bfloat16 else 4
+    return c % v == 0 and (c // v) & (c // v - 1) == 0 and c // v <= 256
+
+
 def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask,
-                 params=(None, None)):
+                 params=(None, None), mask_affine=None):
+    """BN (+ReLU) backward.  ``mask_affine`` = (scale, shift) of a BN+ReLU without residual:
+    the ReLU mask is then recomputed from y (mmad_bn_relu_bwd_*) instead of read from
+    ``relu_out``."""
     m, c = _rows(y)
     dev = y.device
     dt = L.dtype_code(y.dtype)
     nparts = L.load().mmad_bn_bwd_parts(m, c)
     parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
-    L.call("mmad_bn_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y), L.ptr(mean),
-           L.ptr(invstd), L.ptr(parts), L.stream())
+    if mask_affine is not None:
+        sc, sh = mask_affine
+        L.call("mmad_bn_relu_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(y), L.ptr(mean),
+               L.ptr(invstd), L.ptr(sc), L.ptr(sh), L.ptr(parts), L.stream())
+    else:
+        L.call("mmad_bn_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y),
+               L.ptr(mean), L.ptr(invstd), L.ptr(parts), L.stream())
     dgamma = grad_slot(params[0], (c,), dev)
     dbeta = grad_slot(params[1], (c,), dev)
     coef = torch.empty(3 * c, dtype=torch.float32, device=dev)
@@ -534,8 +549,13 @@ def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask,
            int(batch_stats), L.ptr(dgamma), L.ptr(dbeta), L.ptr(coef), L.stream())
     dy = torch.empty_like(y)
     gmask = torch.empty_like(y) if want_gmask else None
-    L.call("mmad_bn_bwd_apply", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y), L.ptr(mean),
-           L.ptr(invstd), L.ptr(coef), L.ptr(dy), L.ptr(gmask), L.stream())
+    if mask_affine is not None:
+        L.call("mmad_bn_relu_bwd_apply", dt, m, c, L.ptr(g), L.ptr(y), L.ptr(mean),
+               L.ptr(invstd), L.ptr(mask_affine[0]), L.ptr(mask_affine[1]), L.ptr(coef),
+               L.ptr(dy), L.stream())
+    else:
+        L.call("mmad_bn_bwd_apply", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y),
+               L.ptr(mean), L.ptr(invstd), L.ptr(coef), L.ptr(dy), L.ptr(gmask), L.stream())
     return dy, dgamma, dbeta, gmask
 
 
@@ -556,8 +576,10 @@ class _BNActFn(torch.autograd.Function):
         L.call("mmad_scale_shift_act", L.dtype_code(y.dtype), m, c, L.ptr(y), L.ptr(scale),
                L.ptr(shift), L.ptr(res), L.ptr(rscale), L.ptr(rshift), int(relu), L.ptr(out),
                L.stream())
-        ctx.save_for_backward(y, out if relu else None, mean, invstd, gamma,
+        masky = relu and res is None and y.dim() == 5 and _mask_from_y_ok(y)
+        ctx.save_for_backward(y, out if relu and not masky else None, mean, invstd, gamma,
                               res if rbn is not None else None, rmean, rinvstd, rgamma)
+        ctx.mask_affine = (scale, shift) if masky else None
         ctx.cfg = (relu, batch, rbatch, res is not None, rbn is not None)
         ctx.params = ((gamma, beta), (rgamma, rbeta))   # gradient-slot lookup (grad_slot)
         return out
@@ -571,7 +593,8 @@ class _BNActFn(torch.autograd.Function):
             g = cast(g, y.dtype)
         gam = None if gamma is None else gamma.detach()
         dy, dgamma, dbeta, gmask = _bn_backward(g, out, y, mean, invstd, gam, batch,
-                                                has_res and not has_rbn, ctx.params[0])
+                                                has_res and not has_rbn, ctx.params[0],
+                                                ctx.mask_affine)
         dres = drg = drb = None
         if has_rbn:
             rg = None if rgamma is None else rgamma.detach()
