@@ -169,12 +169,21 @@ def main():
     if args.workload == "three":          # 9 tabular features (dataloader.py:306)
         batch["tabular"] = torch.rand((B, 9), device="cuda", dtype=torch.float64, generator=g)
 
-    def step():
+    dp_events = []                          # (start, end) around each timed finish()
+
+    def step(timed=False):
         opt.zero_grad(set_to_none=True)
         out = model.general_step(batch, 0, "train")
         out["loss"].backward()
         if reducer is not None:
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             reducer.finish()
+            if timed:
+                e1.record()
+                dp_events.append((e0, e1))
         opt.step()
 
     for _ in range(args.warmup):
@@ -187,7 +196,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(timed=True)
     torch.cuda.synchronize()
     volume_ops.FWD_PROBES.clear()
     if world > 1:
@@ -228,6 +237,12 @@ def main():
         result["step_mfma_frac"] = per_gpu * FLOP_PER_VOL[S] / (
             PEAK_BF16 if cdtype == torch.bfloat16 else PEAK_F32)
         result["hbm_roofline_frac_m2"] = per_gpu * M2_BYTES_PER_VOL / PEAK_HBM
+    if reducer is not None and dp_events:
+        # main-stream time from the end of backward to averaged gradients: the part of the
+        # all-reduce that backward did not hide (plus the copies of non-slot gradients)
+        result["dp"] = {"buckets_mb": [round(f.numel() * 4 / 2 ** 20, 2) for f in reducer.flats],
+                        "exposed_allreduce_ms": sum(a.elapsed_time(b) for a, b in dp_events)
+                        / len(dp_events), "backend": "rccl"}
     if rank == 0 and not args.no_roofline:
         result["roofline"] = dominant_kernel_roofline(events, B, S, cdtype)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
