@@ -37,7 +37,8 @@ struct StemG {
   int n, di, hi, wo, do_, ho;
   int sd, sh, pd, ph;
   int kpad, wrow;                 // packed weight row (elements), LDS weight row (bytes)
-  int rz, yin, nks;               // ring planes, rows per plane, K-steps of 32
+  int rz, yin, nks;               // ring planes (wgrad), rows per plane, K-steps of 32
+  int rzf;                        // forward ring planes: KD + 2*SD (two z-steps ahead)
   int nyb, nzc, zsteps;           // y-pairs, z-chunks, z-steps per block
   int ring_off, c_off, red_off;   // LDS offsets (bytes)
 };
@@ -51,7 +52,6 @@ __global__ __launch_bounds__(320) void stem_fwd_kernel(StemG g, const u16* __res
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* wimg = smem;
   char* ring = smem + g.ring_off;
-  char* ctile = smem + g.c_off;
   float* red = reinterpret_cast<float*>(smem + g.red_off);
   constexpr int NTAP = KD * KH, NKS = (NTAP + 3) / 4;   // K-steps of 4 taps (32)
   constexpr int NTHR = 320;                               // 4 compute waves + 1 loader
@@ -98,15 +98,17 @@ __global__ __launch_bounds__(320) void stem_fwd_kernel(StemG g, const u16* __res
 #pragma unroll
     for (int f = 0; f < RSTEP; ++f) {
       const int kd = KD - SD + f / YIN;
-      load_row(ozn * SD - g.pd + kd, (ozn * SD + kd) % g.rz, f % YIN);
+      load_row(ozn * SD - g.pd + kd, (ozn * SD + kd) % g.rzf, f % YIN);
     }
   };
   if (loader) {
-    // prologue: all KD planes of the first z-step
+    // prologue: all KD planes of the first z-step, then the next step's SD new planes (the
+    // ring holds KD + 2*SD planes, so the loader always runs two z-steps ahead)
 #pragma unroll 1
     for (int kd = 0; kd < KD; ++kd)
 #pragma unroll 1
-      for (int t = 0; t < YIN; ++t) load_row(oz0 * SD - g.pd + kd, (oz0 * SD + kd) % g.rz, t);
+      for (int t = 0; t < YIN; ++t) load_row(oz0 * SD - g.pd + kd, (oz0 * SD + kd) % g.rzf, t);
+    if (oz0 + 1 < oz1) load_step(oz0 + 1);
   }
 
   const int yl = (wave >> 1) & 1, xh = wave & 1;  // compute wave: output row yl, cols xh*32..
@@ -137,19 +139,20 @@ __global__ __launch_bounds__(320) void stem_fwd_kernel(StemG g, const u16* __res
 
 #pragma unroll 1
   for (int oz = oz0; oz < oz1; ++oz) {
-    // planes of oz landed; every wave done with step oz-1 (including its C-tile reads)
+    // planes of oz landed (step oz+1's RSTEP DMAs may still fly); every wave done with the
+    // fragment reads of step oz-1, so its planes' slots are free for step oz+2
     if (loader) {
-      wait_vm_lgkm0<0>();
+      if (oz + 1 < oz1) wait_vm_lgkm0<RSTEP>();
+      else wait_vm_lgkm0<0>();
     } else {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     raw_barrier();
     if (loader) {
-      if (oz + 1 < oz1) load_step(oz + 1);      // next z-step's planes land during this one
-      raw_barrier();                            // matches the compute waves' C-tile barrier
+      if (oz + 2 < oz1) load_step(oz + 2);      // lands during steps oz and oz+1
       continue;
     }
-    const int sbase = (oz * SD) % g.rz;
+    const int sbase = (oz * SD) % g.rzf;
     f32x4 acc[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -158,7 +161,7 @@ __global__ __launch_bounds__(320) void stem_fwd_kernel(StemG g, const u16* __res
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
       int slot = sbase + a_kd[s];
-      slot -= slot >= g.rz ? g.rz : 0;
+      slot -= slot >= g.rzf ? g.rzf : 0;
       const char* arow = ring + (slot * YIN + yl * SH + a_kh[s]) * ROWB + (xh * 32 + lr) * 16;
       bf16x8 fa[2], fb[4];
 #pragma unroll
@@ -176,7 +179,10 @@ __global__ __launch_bounds__(320) void stem_fwd_kernel(StemG g, const u16* __res
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
 
-    // epilogue: 8-byte runs into the LDS C tile, then whole 16-byte lines to the output
+    // epilogue straight from the accumulators: each lane owns 4 consecutive channels of
+    // one voxel (8-byte stores; the 4 j-stores of a voxel fill its 128-byte line in L2), no
+    // LDS C tile and no second barrier per z-step
+    u16* yrow = y + (((int64_t)nb * g.do_ + oz) * g.ho + oy) * g.wo * CO;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int x = xh * 32 + i * 16 + lr;
@@ -195,21 +201,8 @@ __global__ __launch_bounds__(320) void stem_fwd_kernel(StemG g, const u16* __res
         uint2 pk;
         pk.x = pack_bf16x2(v[0], v[1]);
         pk.y = pack_bf16x2(v[2], v[3]);
-        *reinterpret_cast<uint2*>(ctile + (yl * XW + x) * CROW + (j * 16 + lk * 4) * 2) = pk;
+        if (ok) *reinterpret_cast<uint2*>(yrow + (int64_t)x * CO + j * 16 + lk * 4) = pk;
       }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    raw_barrier();
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {                // 128 rows x 8 chunks, 256 compute threads
-      const int q = tid + 256 * h;
-      const int row = q >> 3, c8 = q & 7;
-      const int ry = row >> 6, x = row & 63;
-      const int yy = yb * YT + ry;
-      if (x < g.wo && yy < g.ho)
-        *reinterpret_cast<u32x4*>(y + ((((int64_t)nb * g.do_ + oz) * g.ho + yy) * g.wo + x) * CO +
-                                  c8 * 8) =
-            *reinterpret_cast<const u32x4*>(ctile + row * CROW + c8 * 16);
     }
   }
 
@@ -409,6 +402,7 @@ bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds) {
   // +16-byte pad (57 slots: % 16 == 9) put up to 8 lanes of a group on one slot
   g.wrow = g.kpad * 2 + 16 * (int)(((10 - (g.kpad * 2 / 16)) % 16 + 16) % 16);
   g.rz = d->kd + g.sd;                           // planes of this and the next z-step
+  g.rzf = d->kd + 2 * g.sd;                      // forward: and the one after
   g.yin = (YT - 1) * g.sh + d->kh;
   g.nks = (int)cdiv(ntap, 4);
   if (g.nks > 16 || g.kpad < g.nks * 32) return false;
@@ -418,8 +412,8 @@ bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds) {
   g.zsteps = (int)cdiv(g.do_, g.nzc);
   g.nzc = (int)cdiv(g.do_, g.zsteps);
   g.ring_off = CO * g.wrow;
-  g.c_off = g.ring_off + g.rz * g.yin * ROWB;
-  g.red_off = g.c_off + YT * XW * CROW;
+  g.c_off = g.ring_off + g.rzf * g.yin * ROWB;   // (no C tile: the epilogue stores directly)
+  g.red_off = g.c_off;
   lds = (size_t)g.red_off + 4 * 2 * CO * sizeof(float);
   blocks = (int)(base * g.nzc);
   return lds <= 160 * 1024 && base * g.nzc < (int64_t(1) << 31);
