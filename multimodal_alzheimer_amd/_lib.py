@@ -13,7 +13,8 @@ import os
 import torch
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libmmad_hip.so")
+# MMAD_LIB_PATH: an alternative build of the same library (A/B experiments, tools/)
+LIB_PATH = os.environ.get("MMAD_LIB_PATH") or os.path.join(_PKG, "libmmad_hip.so")
 
 F32, BF16, F64 = 0, 1, 2
 EUNSUPPORTED = 1004

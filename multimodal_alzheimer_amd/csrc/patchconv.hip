@@ -8,14 +8,14 @@
 // Why a second conv kernel: the implicit GEMM (conv.hip) stages the A operand row by row,
 // so every input voxel is fetched from L2 into LDS once per tap (27x) and, with only 64
 // output channels to amortise it over, the 64-channel layers ran L2->LDS-bound at ~500
-// TFLOP/s.  Here a block owns a 4 x 8 x 8 box of output voxels (256 GEMM rows) x 64/128
-// output channels, DMAs the input box plus its halo (the "patch": 6 x 10 x 10 voxels x 64
-// channels = 75 KiB for a 3^3 conv) into LDS ONCE, and builds each tap's A fragments from
-// it by address offset: 2.3 fetches per input voxel instead of 27.  Per tap only the
+// TFLOP/s.  Here a block owns a TZ x 8 x 8 box of output voxels (TZ = 2: 128 GEMM rows) x
+// 64 output channels, DMAs the input box plus its halo (the "patch": 4 x 10 x 10 voxels x
+// 64 channels = 50 KiB for a 3^3 conv) into LDS ONCE, and builds each tap's A fragments
+// from it by address offset: ~3 fetches per input voxel instead of 27.  Per tap only the
 // weights (64 x 64 bf16, 8 KiB) stream through a 3-deep LDS ring by LDS-DMA.  The tap
 // loop is compiled for the 3x3x3 dilation-1 stencil, so all tap offsets are constants.
 //
-//  * 4 waves of 64 x 64 wave tiles (16 MFMA 16x16x32 per K-half), each fragment read once
+//  * 4 waves of (TV/4) x 64 wave tiles (MFMA 16x16x32), each fragment read once
 //    per wave with ds_read_b128; wider layers run one block per 64-channel N slice;
 //  * patch rows are 128-byte voxel slices; 16-byte chunks XOR-swizzled by (patch x & 7),
 //    which makes every fragment read of every tap conflict-free (rows of a fragment are
@@ -34,7 +34,14 @@
 
 namespace {
 
-constexpr int TZ = 4, TY = 8, TX = 8, TV = TZ * TY * TX;   // output voxels per tile
+// 2 x 8 x 8 output boxes: the patch (4 x 10 x 10 voxels x 128 B = 50 KB) plus the weight
+// ring fit twice in the 160 KB LDS, so two blocks share a CU and one's per-tap barrier no
+// longer idles the MFMA pipes; measured against 4 x 8 x 8 boxes (one block per CU, twice
+// the tap reuse): layer1 fwd 90 -> 77 us, dgrad 85 -> 80 us, layer2.conv2 fwd 43 -> 37 us
+#ifndef MMAD_PATCH_TZ
+#define MMAD_PATCH_TZ 2
+#endif
+constexpr int TZ = MMAD_PATCH_TZ, TY = 8, TX = 8, TV = TZ * TY * TX;   // output voxels per tile
 constexpr int RB = 128;                                    // bytes per patch row / K slice
 constexpr int NST = 3;                                     // weight ring depth
 constexpr int LDS_MAX = 160 * 1024;
