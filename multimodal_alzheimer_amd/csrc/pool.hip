@@ -294,29 +294,67 @@ __global__ __launch_bounds__(256) void bnpool3_fwd_rows_kernel(
 // cell's 8 inputs share the 8 windows {a, a+1}^3, loaded once (not ~3.4x per input).  All
 // 24 loads of a cell are issued before any use (raw 16-byte registers), so a thread waits
 // for one memory round trip, not eight.
+// Per-thread BN-backward constants of channels c0..c0+V-1:
+// dy = k0 * g' - k1 - (y - mu) * kt, with kt = invstd * coef2
 template <int V>
 __device__ __forceinline__ void bnbwd_params(int C, int c0, const float* __restrict__ mean,
                                              const float* __restrict__ invstd,
                                              const float* __restrict__ coef, float* mu,
-                                             float* is, float* k0, float* k1, float* k2) {
+                                             float* k0, float* k1, float* kt) {
 #pragma unroll
   for (int e = 0; e < V; ++e) {
     const int c = c0 + e;
-    mu[e] = mean[c]; is[e] = invstd[c];
-    k0[e] = coef[c]; k1[e] = coef[C + c]; k2[e] = coef[2 * C + c];
+    mu[e] = mean[c];
+    k0[e] = coef[c]; k1[e] = coef[C + c]; kt[e] = invstd[c] * coef[2 * C + c];
   }
 }
 
-template <typename T>
+// V elements of T held packed in 32-bit words (V * sizeof(T) = 8 or 16 bytes)
+template <typename T, int V>
+struct Packed {
+  static constexpr int W = V * (int)sizeof(T) / 4;
+  uint32_t w[W];
+  __device__ __forceinline__ void load(const T* p) {
+    if constexpr (W == 4) {
+      const u32x4 c = *reinterpret_cast<const u32x4*>(p);
+      w[0] = c[0]; w[1] = c[1]; w[2] = c[2]; w[3] = c[3];
+    } else {
+      const uint2 c = *reinterpret_cast<const uint2*>(p);
+      w[0] = c.x; w[1] = c.y;
+    }
+  }
+  __device__ __forceinline__ float get(int e) const {
+    if constexpr (sizeof(T) == 4) return __uint_as_float(w[e]);
+    else return __uint_as_float((e & 1) ? (w[e >> 1] & 0xffff0000u) : (w[e >> 1] << 16));
+  }
+};
+
+template <typename T, int V>
+__device__ __forceinline__ void store_packed(T* p, const float* v) {
+  if constexpr (sizeof(T) == 4 && V == 4) {
+    f32x4 c; c[0] = v[0]; c[1] = v[1]; c[2] = v[2]; c[3] = v[3];
+    *reinterpret_cast<f32x4*>(p) = c;
+  } else if constexpr (V == 8) {
+    u32x4 c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+    *reinterpret_cast<u32x4*>(p) = c;
+  } else {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
+}
+
+// V = 4 channels per thread in both dtypes (8-byte bf16 / 16-byte fp32 accesses): the 8
+// windows' argmax bytes, pooled gradients and the cell's 8 inputs stay packed, so the cell
+// fits in ~100 VGPRs (4+ waves per SIMD; 8 bf16 channels per thread needed 247)
+template <typename T, int V>
 __device__ __forceinline__ void bnpool3s2_bwd_cell(
     const PoolG& g, const T* __restrict__ gp, const uint8_t* __restrict__ am,
-    const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
-    const float* __restrict__ coef, T* __restrict__ dy, int64_t nb, int ad, int ah, int aw,
-    int c0, const float* mu, const float* is, const float* k0, const float* k1,
-    const float* k2) {
-  constexpr int V = Chunk<T>::N;
-  uint64_t a8[8];
-  u32x4 graw[8], yraw[8];
+    const T* __restrict__ y, T* __restrict__ dy, int64_t nb, int ad, int ah, int aw, int c0,
+    const float* mu, const float* k0, const float* k1, const float* kt) {
+  static_assert(V == 4, "argmax bytes are read as one 32-bit word");
+  uint32_t a4[8];
+  Packed<T, V> graw[8], yraw[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int qd = q >> 2, qh = (q >> 1) & 1, qw = q & 1;
@@ -324,25 +362,18 @@ __device__ __forceinline__ void bnpool3s2_bwd_cell(
     const int od = min(ad + qd, g.do_ - 1), oh = min(ah + qh, g.ho - 1);
     const int ow = min(aw + qw, g.wo - 1);
     const int64_t o = (((nb * g.do_ + od) * g.ho + oh) * g.wo + ow) * g.c + c0;
-    uint64_t w;
-    if constexpr (V == 8) w = *reinterpret_cast<const uint64_t*>(am + o);
-    else w = *reinterpret_cast<const uint32_t*>(am + o);
-    a8[q] = ok ? w : 0;          // 0: no active window (the 0x80 bit is never set)
-    graw[q] = *reinterpret_cast<const u32x4*>(gp + o);
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(am + o);
+    a4[q] = ok ? w : 0;          // 0: no active window (the 0x80 bit is never set)
+    graw[q].load(gp + o);
     const int id = min(2 * ad + qd, g.di - 1), ih = min(2 * ah + qh, g.hi - 1);
     const int iw = min(2 * aw + qw, g.wi - 1);
-    yraw[q] = *reinterpret_cast<const u32x4*>(y + (((nb * g.di + id) * g.hi + ih) * g.wi + iw) *
-                                                      g.c + c0);
+    yraw[q].load(y + (((nb * g.di + id) * g.hi + ih) * g.wi + iw) * g.c + c0);
   }
-  float gv[8][V];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) Chunk<T>::load(reinterpret_cast<const T*>(&graw[q]), gv[q]);
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const int rd = r >> 2, rh = (r >> 1) & 1, rw = r & 1;
     const int id = 2 * ad + rd, ih = 2 * ah + rh, iw = 2 * aw + rw;
-    float yv[V], acc[V];
-    Chunk<T>::load(reinterpret_cast<const T*>(&yraw[r]), yv);
+    float acc[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) acc[e] = 0.f;
 #pragma unroll
@@ -351,26 +382,24 @@ __device__ __forceinline__ void bnpool3s2_bwd_cell(
       // an even input (r-bit 0) lies only in window a (q-bit 0); offset inside window
       // a+q: (i - 2a) + 1 - 2q
       if ((!rd && qd) || (!rh && qh) || (!rw && qw)) continue;
-      const int wi = 0x80 | (((rd + 1 - 2 * qd) * 3 + (rh + 1 - 2 * qh)) * 3 + (rw + 1 - 2 * qw));
+      const uint32_t wi = 0x80 | (((rd + 1 - 2 * qd) * 3 + (rh + 1 - 2 * qh)) * 3 + (rw + 1 - 2 * qw));
 #pragma unroll
       for (int e = 0; e < V; ++e)
-        if ((int)((a8[q] >> (8 * e)) & 0xff) == wi) acc[e] += gv[q][e];
+        if (((a4[q] >> (8 * e)) & 0xff) == wi) acc[e] += graw[q].get(e);
     }
     if (id >= g.di || ih >= g.hi || iw >= g.wi) continue;
     float dv[V];
 #pragma unroll
-    for (int e = 0; e < V; ++e)
-      dv[e] = k0[e] * acc[e] - k1[e] - (yv[e] - mu[e]) * is[e] * k2[e];
-    Chunk<T>::store(dy + (((nb * g.di + id) * g.hi + ih) * g.wi + iw) * g.c + c0, dv);
+    for (int e = 0; e < V; ++e) dv[e] = k0[e] * acc[e] - k1[e] - (yraw[r].get(e) - mu[e]) * kt[e];
+    store_packed<T, V>(dy + (((nb * g.di + id) * g.hi + ih) * g.wi + iw) * g.c + c0, dv);
   }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(256) void bnpool3s2_bwd_apply_kernel(
     PoolG g, const T* __restrict__ gp, const uint8_t* __restrict__ am, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ coef, T* __restrict__ dy) {
-  constexpr int V = Chunk<T>::N;
   const int cv = g.c / V;
   const int cd = (g.di + 1) >> 1, ch = (g.hi + 1) >> 1, cw = (g.wi + 1) >> 1;
   const int64_t total = (int64_t)g.n * cd * ch * cw * cv;
@@ -381,31 +410,28 @@ __global__ __launch_bounds__(256) void bnpool3s2_bwd_apply_kernel(
     const int aw = (int)(v % cw); v /= cw;
     const int ah = (int)(v % ch); v /= ch;
     const int ad = (int)(v % cd);
-    float mu[V], is[V], k0[V], k1[V], k2[V];
-    bnbwd_params<V>(g.c, c0, mean, invstd, coef, mu, is, k0, k1, k2);
-    bnpool3s2_bwd_cell<T>(g, gp, am, y, mean, invstd, coef, dy, v / cd, ad, ah, aw, c0, mu, is,
-                          k0, k1, k2);
+    float mu[V], k0[V], k1[V], kt[V];
+    bnbwd_params<V>(g.c, c0, mean, invstd, coef, mu, k0, k1, kt);
+    bnpool3s2_bwd_cell<T, V>(g, gp, am, y, dy, v / cd, ad, ah, aw, c0, mu, k0, k1, kt);
   }
 }
 
 // Same, one block per row of cells (blockIdx.y = ah, blockIdx.z = n*cd + ad), power-of-two
 // channel-vector count: shift/mask index math (see bnpool3_fwd_rows_kernel).
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(256) void bnpool3s2_bwd_rows_kernel(
     PoolG g, int cv_shift, const T* __restrict__ gp, const uint8_t* __restrict__ am,
     const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ coef, T* __restrict__ dy) {
-  constexpr int V = Chunk<T>::N;
   const int cd = (g.di + 1) >> 1, cw = (g.wi + 1) >> 1;
   const int ah = blockIdx.y, ad = blockIdx.z % cd;
   const int64_t nb = blockIdx.z / cd;
   const int items = cw << cv_shift, cmask = (1 << cv_shift) - 1;
   const int c0 = (threadIdx.x & cmask) * V;      // fixed per thread (cv divides 256)
-  float mu[V], is[V], k0[V], k1[V], k2[V];
-  bnbwd_params<V>(g.c, c0, mean, invstd, coef, mu, is, k0, k1, k2);
+  float mu[V], k0[V], k1[V], kt[V];
+  bnbwd_params<V>(g.c, c0, mean, invstd, coef, mu, k0, k1, kt);
   for (int e = threadIdx.x; e < items; e += 256)
-    bnpool3s2_bwd_cell<T>(g, gp, am, y, mean, invstd, coef, dy, nb, ad, ah, e >> cv_shift, c0,
-                          mu, is, k0, k1, k2);
+    bnpool3s2_bwd_cell<T, V>(g, gp, am, y, dy, nb, ad, ah, e >> cv_shift, c0, mu, k0, k1, kt);
 }
 
 // Fused backward, dense pass: for every input voxel, g' = sum of the pooled gradients of the
@@ -617,13 +643,14 @@ int bnpool_bwd_apply(const PoolG& g, const void* gp, const uint8_t* am, const vo
   constexpr int VEC = Chunk<T>::N;
   const int64_t vox = (int64_t)g.n * g.di * g.hi * g.wi;
   const int cv = g.c / VEC, cd = (g.di + 1) >> 1, ch = (g.hi + 1) >> 1;
-  if (g.c % VEC == 0 && g.k == 3 && g.s == 2 && g.p == 1 && is_pow2(cv) && rows_on() &&
-      (int64_t)g.n * cd < 65536 && ch < 65536)
-    hipLaunchKernelGGL((bnpool3s2_bwd_rows_kernel<T>), dim3(1, (unsigned)ch, (unsigned)(g.n * cd)),
-                       dim3(256), 0, st, g, ilog2(cv), (const T*)gp, am, (const T*)y, mean,
-                       invstd, coef, (T*)dy);
-  else if (g.c % VEC == 0 && g.k == 3 && g.s == 2 && g.p == 1)
-    hipLaunchKernelGGL((bnpool3s2_bwd_apply_kernel<T>), dim3(grid_of(vox * g.c / VEC / 8 + 1)),
+  const int cv4 = g.c / 4;    // the k3 s2 cell kernels take 4 channels per thread
+  if (g.c % 4 == 0 && g.k == 3 && g.s == 2 && g.p == 1 && is_pow2(cv4) && cv4 <= 256 &&
+      rows_on() && (int64_t)g.n * cd < 65536 && ch < 65536)
+    hipLaunchKernelGGL((bnpool3s2_bwd_rows_kernel<T, 4>),
+                       dim3(1, (unsigned)ch, (unsigned)(g.n * cd)), dim3(256), 0, st, g,
+                       ilog2(cv4), (const T*)gp, am, (const T*)y, mean, invstd, coef, (T*)dy);
+  else if (g.c % 4 == 0 && g.k == 3 && g.s == 2 && g.p == 1)
+    hipLaunchKernelGGL((bnpool3s2_bwd_apply_kernel<T, 4>), dim3(grid_of(vox * g.c / 4 / 8 + 1)),
                        dim3(256), 0, st, g, (const T*)gp, am, (const T*)y, mean, invstd, coef,
                        (T*)dy);
   else if (g.c % VEC == 0)
