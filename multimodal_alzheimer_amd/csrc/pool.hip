@@ -267,6 +267,72 @@ __global__ void bnpool3_fwd_kernel(PoolG g, const T* __restrict__ y,
   }
 }
 
+// bf16 form of bnpool3_fwd_one for 8 channels, on packed words: per pair of channels one
+// packed FMA, one RNE pack to bf16 and one packed 16-bit max for the ReLU (bf16 bits of a
+// non-negative value order like integers), then each channel's candidate is the 32-bit key
+// (bf16 bits << 16 | 31 - window index), so "larger value, else earlier position" is one
+// unsigned compare.  The old per-channel float compare / index / raw bookkeeping cost ~11
+// VALU ops per loaded element and made the kernel VALU-bound; this is ~7.  Padded window
+// positions load their clamped in-window neighbour and carry that neighbour's index, so
+// they tie with it and never win.  NaN: relu(NaN) stays NaN (as torch) and wins the window.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void bnpool3_fwd_one_bf16(const PoolG& g, const u16* __restrict__ y,
+                                                     u16* __restrict__ out,
+                                                     uint8_t* __restrict__ am,
+                                                     u16* __restrict__ ymax, int64_t nb, int od,
+                                                     int oh, int ow, int c0, const f32x2* sc2,
+                                                     const f32x2* sh2) {
+  const int64_t ovox = ((nb * g.do_ + od) * g.ho + oh) * g.wo + ow;
+  const int z0 = od * g.s - g.p, y0 = oh * g.s - g.p, x0 = ow * g.s - g.p;
+  uint32_t key[8], rb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { key[e] = 0; rb[e] = 0; }
+  for (int kd = 0; kd < 3; ++kd) {
+    const int z = z0 + kd;
+    if ((unsigned)z >= (unsigned)g.di) continue;     // block-uniform (od is per block)
+    u32x4 raw[9];
+    uint32_t tag[9];
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+      const int yc = min(max(y0 + w / 3, 0), g.hi - 1), xc = min(max(x0 + w % 3, 0), g.wi - 1);
+      tag[w] = 31 - (kd * 9 + (yc - y0) * 3 + (xc - x0));
+      raw[w] = *reinterpret_cast<const u32x4*>(y + (((nb * g.di + z) * g.hi + yc) * g.wi + xc) *
+                                                       g.c + c0);
+    }
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const uint32_t word = raw[w][p];
+        const f32x2 a = {__uint_as_float(word << 16), __uint_as_float(word & 0xffff0000u)};
+        const f32x2 s = __builtin_elementwise_fma(a, sc2[p], sh2[p]);
+        const s16x2 v = __builtin_elementwise_max(
+            __builtin_bit_cast(s16x2, __builtin_convertvector(s, bf16x2)), (s16x2){0, 0});
+        const uint32_t pk = __builtin_bit_cast(uint32_t, v);
+        const uint32_t k0 = (pk << 16) | tag[w], k1 = (pk & 0xffff0000u) | tag[w];
+        if (k0 > key[2 * p]) { key[2 * p] = k0; rb[2 * p] = word; }
+        if (k1 > key[2 * p + 1]) { key[2 * p + 1] = k1; rb[2 * p + 1] = word; }
+      }
+    }
+  }
+  u32x4 o, r;
+  uint64_t packed = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    o[p] = (key[2 * p] >> 16) | (key[2 * p + 1] & 0xffff0000u);
+    r[p] = (rb[2 * p] & 0xffffu) | (rb[2 * p + 1] & 0xffff0000u);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t vb = key[e] >> 16;            // bf16 bits, sign clear
+    const bool pos = vb != 0 && vb <= 0x7f80u;   // > 0 and not NaN: ReLU passed it
+    packed |= (uint64_t)((31 - (key[e] & 31)) | (pos ? 0x80 : 0)) << (8 * e);
+  }
+  *reinterpret_cast<u32x4*>(out + ovox * g.c + c0) = o;
+  *reinterpret_cast<u32x4*>(ymax + ovox * g.c + c0) = r;
+  *reinterpret_cast<uint64_t*>(am + ovox * g.c + c0) = packed;
+}
+
 // Same, one block per output row (blockIdx.y = oh, blockIdx.z = n*do + od) when the
 // channel-vector count is a power of two: the per-thread index math is a shift and a mask
 // instead of five 64-bit divisions (which, at 8 channels per thread, cost more VALU time
@@ -281,12 +347,23 @@ __global__ __launch_bounds__(256) void bnpool3_fwd_rows_kernel(
   const int items = g.wo << cv_shift, cmask = (1 << cv_shift) - 1;
   // cv divides 256: this thread's channel vector is the same for every item it visits
   const int c0 = (threadIdx.x & cmask) * V;
-  float sc[V], sh[V];
+  if constexpr (sizeof(T) == 2 && V == 8) {
+    f32x2 sc2[4], sh2[4];
 #pragma unroll
-  for (int e = 0; e < V; ++e) { sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e]; }
-  for (int e = threadIdx.x; e < items; e += 256)
-    bnpool3_fwd_one<T, V>(g, y, scale, shift, out, am, ymax, nb, od, oh, e >> cv_shift, c0, sc,
-                          sh);
+    for (int p = 0; p < 4; ++p) {
+      sc2[p] = (f32x2){scale[c0 + 2 * p], scale[c0 + 2 * p + 1]};
+      sh2[p] = (f32x2){shift[c0 + 2 * p], shift[c0 + 2 * p + 1]};
+    }
+    for (int e = threadIdx.x; e < items; e += 256)
+      bnpool3_fwd_one_bf16(g, y, out, am, ymax, nb, od, oh, e >> cv_shift, c0, sc2, sh2);
+  } else {
+    float sc[V], sh[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e]; }
+    for (int e = threadIdx.x; e < items; e += 256)
+      bnpool3_fwd_one<T, V>(g, y, scale, shift, out, am, ymax, nb, od, oh, e >> cv_shift, c0, sc,
+                            sh);
+  }
 }
 
 // k = 3, stride 2, pad 1 form of bnpool_bwd_apply_kernel, one thread per 2x2x2 input cell
@@ -642,8 +719,8 @@ int bnpool_bwd_apply(const PoolG& g, const void* gp, const uint8_t* am, const vo
                      hipStream_t st) {
   constexpr int VEC = Chunk<T>::N;
   const int64_t vox = (int64_t)g.n * g.di * g.hi * g.wi;
-  const int cv = g.c / VEC, cd = (g.di + 1) >> 1, ch = (g.hi + 1) >> 1;
-  const int cv4 = g.c / 4;    // the k3 s2 cell kernels take 4 channels per thread
+  const int cd = (g.di + 1) >> 1, ch = (g.hi + 1) >> 1;
+  const int cv4 = g.c / 4;   // the k3 s2 cell kernels take 4 channels per thread
   if (g.c % 4 == 0 && g.k == 3 && g.s == 2 && g.p == 1 && is_pow2(cv4) && cv4 <= 256 &&
       rows_on() && (int64_t)g.n * cd < 65536 && ch < 65536)
     hipLaunchKernelGGL((bnpool3s2_bwd_rows_kernel<T, 4>),
