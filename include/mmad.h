@@ -72,7 +72,9 @@ int mmad_conv_pack_weight(const mmad_conv_desc* d, int dtype, const float* w,
 typedef struct mmad_pack_job {
   const float* w;
   void* w_packed;
-  int32_t rows, cols, batch, jdiv, ostride_j2, tiles_x, tiles_y, pad_;
+  /* source row i of batch entry b is row i % rdiv of packed block b * rows / rdiv + i / rdiv
+   * (forward jobs fold every output channel into one rows = co * ci matrix)            */
+  int32_t rows, cols, batch, jdiv, ostride_j2, tiles_x, tiles_y, pad_, rdiv;
   int64_t ostride_b, ostride_j1, tile0;
 } mmad_pack_job;
 int mmad_conv_pack_job(const mmad_conv_desc* d, int dtype, int for_dgrad, const float* w,

@@ -34,7 +34,7 @@ class PackJob(C.Structure):
     """mirror of mmad_pack_job (include/mmad.h)"""
     _fields_ = ([("w", C.c_void_p), ("w_packed", C.c_void_p)] +
                 [(n, C.c_int32) for n in ("rows", "cols", "batch", "jdiv", "ostride_j2",
-                                          "tiles_x", "tiles_y", "pad_")] +
+                                          "tiles_x", "tiles_y", "pad_", "rdiv")] +
                 [(n, C.c_int64) for n in ("ostride_b", "ostride_j1", "tile0")])
 
 

@@ -895,11 +895,14 @@ __global__ __launch_bounds__(256) void pack_transpose_kernel(const float* __rest
   }
 }
 
-// Batched form: blockIdx.x walks the concatenated tile ranges of all jobs.
+// Batched form: blockIdx.x walks the concatenated tile ranges of all jobs.  A tile is
+// 64 x 64 (rows x cols), or 128 x 32 when cols <= 32 (the 27-tap forward jobs: 84 % of a
+// tile's lanes carry data instead of 42 %); source reads run along cols, packed stores
+// along rows, both through a padded LDS tile.
 template <typename T>
 __global__ __launch_bounds__(256) void pack_batch_kernel(const mmad_pack_job* __restrict__ jobs,
                                                          int njobs) {
-  __shared__ float tile[64][65];
+  __shared__ float tile[128 * 33 > 64 * 65 ? 128 * 33 : 64 * 65];
   // job lookup: last job with tile0 <= blockIdx.x (jobs sorted by tile0)
   int lo = 0, hi = njobs - 1;
   const int64_t bid = blockIdx.x;
@@ -913,24 +916,28 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const mmad_pack_job* __
   t /= jb.tiles_x;
   const int by = (int)(t % jb.tiles_y);
   const int b = (int)(t / jb.tiles_y);
-  const int R = jb.rows, Cc = jb.cols, jd = jb.jdiv, oj2 = jb.ostride_j2;
-  const int i0 = by * 64, j0 = bx * 64;
+  const int R = jb.rows, Cc = jb.cols, jd = jb.jdiv, oj2 = jb.ostride_j2, rdiv = jb.rdiv;
+  const bool narrow = Cc <= 32;                       // job-uniform
+  const int TR = narrow ? 128 : 64, TC = narrow ? 32 : 64, LD = TC + 1;
+  const int i0 = by * TR, j0 = bx * TC;
   const float* src = jb.w + (int64_t)b * R * Cc;
   T* wp = reinterpret_cast<T*>(jb.w_packed);
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-#pragma unroll
-  for (int r = ty; r < 64; r += 4) {
-    const int i = i0 + r, j = j0 + tx;
-    tile[r][tx] = (i < R && j < Cc) ? src[(int64_t)i * Cc + j] : 0.f;
+  const int cl = threadIdx.x & (TC - 1), rl = threadIdx.x / TC, rstep = 256 / TC;
+  for (int r = rl; r < TR; r += rstep) {
+    const int i = i0 + r, j = j0 + cl;
+    tile[r * LD + cl] = (i < R && j < Cc) ? src[(int64_t)i * Cc + j] : 0.f;
   }
   __syncthreads();
-#pragma unroll
-  for (int c = ty; c < 64; c += 4) {
-    const int j = j0 + c, i = i0 + tx;
-    if (i < R && j < Cc)
-      Elt<T>::st(wp, (int64_t)b * jb.ostride_b + (int64_t)(j / jd) * jb.ostride_j1 +
-                         (int64_t)(jb.pad_ ? jd - 1 - j % jd : j % jd) * oj2 + i,
-                 tile[tx][c]);
+  const int rw = threadIdx.x & (TR - 1), cw = threadIdx.x / TR, cstep = 256 / TR;
+  const int i = i0 + rw;
+  if (i >= R) return;
+  const int64_t obase = (int64_t)(b * (R / rdiv) + i / rdiv) * jb.ostride_b + i % rdiv;
+  for (int c = cw; c < TC; c += cstep) {
+    const int j = j0 + c;
+    if (j < Cc)
+      Elt<T>::st(wp, obase + (int64_t)(j / jd) * jb.ostride_j1 +
+                         (int64_t)(jb.pad_ ? jd - 1 - j % jd : j % jd) * oj2,
+                 tile[rw * LD + c]);
   }
 }
 
@@ -1313,15 +1320,19 @@ int mmad_conv_pack_job(const mmad_conv_desc* d, int dtype, int for_dgrad, const 
   mmad_pack_job j{};
   j.w = w;
   j.w_packed = wp;
-  j.rows = fw ? d->ci : d->co;
+  // forward: [co][ci][tap] -> [co][tap][ci] with all co in one (co*ci) x taps matrix
+  // (row i -> block i / ci, offset i % ci); dgrad: one co x (ci*taps) matrix
+  j.rows = fw ? d->co * d->ci : d->co;
+  j.rdiv = fw ? d->ci : d->co;
   j.cols = fw ? g.taps : d->ci * g.taps;
-  j.batch = fw ? d->co : 1;
+  j.batch = 1;
   j.jdiv = g.taps;
   j.ostride_j2 = fw ? d->ci : d->co;
   j.ostride_b = fw ? g.Kpad : 0;
   j.ostride_j1 = fw ? 0 : g.Kpad;
-  j.tiles_x = (int)cdiv(j.cols, 64);
-  j.tiles_y = (int)cdiv(j.rows, 64);
+  const bool narrow = j.cols <= 32;      // pack_batch_kernel's 128 x 32 tile
+  j.tiles_x = (int)cdiv(j.cols, narrow ? 32 : 64);
+  j.tiles_y = (int)cdiv(j.rows, narrow ? 128 : 64);
   j.pad_ = for_dgrad && dgrad_as_fwd(d);       // reversed tap order (see dgrad_as_fwd)
   j.tile0 = tile0;
   *job = j;
