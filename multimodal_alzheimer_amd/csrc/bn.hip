@@ -150,7 +150,8 @@ int launch_colsum(int64_t M, int C, const void* y, const void* g, const void* ro
 }
 
 // f64 sum of the partial rows; block = FC channels x 64 part-lanes (1024 threads), loads
-// unrolled 4 deep, then a fixed-shape LDS tree over the part-lanes (deterministic).
+// unrolled 8 deep (16 in flight per thread: the finalize kernels are load-latency bound),
+// then a fixed-shape LDS tree over the part-lanes (deterministic).
 constexpr int FC = 16;
 __device__ __forceinline__ void sum_parts(int c, int C, int nparts, const float* parts,
                                           double* sm, double& S, double& Q) {
@@ -158,15 +159,16 @@ __device__ __forceinline__ void sum_parts(int c, int C, int nparts, const float*
   double s = 0.0, q = 0.0;
   if (c < C) {
     int p = py;
-    for (; p + 192 < nparts; p += 256) {
-      float a[4], b[4];
+    constexpr int U = 8;
+    for (; p + 64 * (U - 1) < nparts; p += 64 * U) {
+      float a[U], b[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         a[u] = parts[((int64_t)(p + 64 * u) * 2) * C + c];
         b[u] = parts[((int64_t)(p + 64 * u) * 2 + 1) * C + c];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) { s += a[u]; q += b[u]; }
+      for (int u = 0; u < U; ++u) { s += a[u]; q += b[u]; }
     }
     for (; p < nparts; p += 64) {
       s += parts[((int64_t)p * 2) * C + c];

@@ -965,6 +965,38 @@ __global__ void unfold_w_kernel(const TI* __restrict__ x, TO* __restrict__ xu, i
   }
 }
 
+// Same, UNF_RB input rows per block staged through LDS (Wi <= UNF_MAXW): the rows are one
+// contiguous span, read with one coalesced load per element instead of one strided load
+// per (output, tap); the taps then come from LDS.
+constexpr int UNF_RB = 8, UNF_MAXW = 256;
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void unfold_w_rows_kernel(const TI* __restrict__ x,
+                                                            TO* __restrict__ xu, int64_t rows,
+                                                            int Wi, int Wo, int KW, int sw,
+                                                            int pw, int dw) {
+  __shared__ float row[UNF_RB * UNF_MAXW];
+  const int64_t r0 = (int64_t)blockIdx.x * UNF_RB;
+  const int nr = (int)min((int64_t)UNF_RB, rows - r0);
+  for (int k = threadIdx.x; k < nr * Wi; k += 256) row[k] = (float)x[r0 * Wi + k];
+  __syncthreads();
+  for (int k = threadIdx.x; k < nr * Wo; k += 256) {
+    const int r = k / Wo, xo = k - r * Wo;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int xi = xo * sw - pw + j * dw;
+      v[j] = (j < KW && xi >= 0 && xi < Wi) ? row[r * Wi + xi] : 0.f;
+    }
+    const int64_t idx = r0 * Wo + k;
+    if constexpr (sizeof(TO) == 2) {
+      Chunk<u16>::store(reinterpret_cast<u16*>(xu) + idx * 8, v);
+    } else {
+      Chunk<float>::store(reinterpret_cast<float*>(xu) + idx * 8, v);
+      Chunk<float>::store(reinterpret_cast<float*>(xu) + idx * 8 + 4, v + 4);
+    }
+  }
+}
+
 // ---- host-side geometry ---------------------------------------------------------------
 // packed-weight row stride granule: one 128-byte K slice (a stage row)
 int bk_of(int dtype) { return dtype == MMAD_BF16 ? 64 : 32; }
@@ -1371,9 +1403,17 @@ int mmad_conv_unfold_input(const mmad_conv_desc* d, int in_dtype, const void* x,
   const int64_t rows = (int64_t)d->n * d->di * d->hi;
   const unsigned grid = grid_for(rows * d->wo);
   hipStream_t st = as_stream(stream);
-#define UNF(TI, TO)                                                                    \
-  hipLaunchKernelGGL((unfold_w_kernel<TI, TO>), dim3(grid), dim3(256), 0, st, (const TI*)x, \
-                     (TO*)xu, rows, d->wi, d->wo, d->kw, d->sw, d->pw, d->dw)
+  const bool staged = d->wi <= UNF_MAXW && rows / UNF_RB < INT32_MAX;
+  const unsigned sgrid = (unsigned)cdiv(rows, UNF_RB);
+#define UNF(TI, TO)                                                                         \
+  do {                                                                                      \
+    if (staged)                                                                             \
+      hipLaunchKernelGGL((unfold_w_rows_kernel<TI, TO>), dim3(sgrid), dim3(256), 0, st,     \
+                         (const TI*)x, (TO*)xu, rows, d->wi, d->wo, d->kw, d->sw, d->pw, d->dw); \
+    else                                                                                    \
+      hipLaunchKernelGGL((unfold_w_kernel<TI, TO>), dim3(grid), dim3(256), 0, st,           \
+                         (const TI*)x, (TO*)xu, rows, d->wi, d->wo, d->kw, d->sw, d->pw, d->dw); \
+  } while (0)
   if (dtype == MMAD_BF16) {
     if (in_dtype == MMAD_F64) UNF(double, u16);
     else if (in_dtype == MMAD_F32) UNF(float, u16);
