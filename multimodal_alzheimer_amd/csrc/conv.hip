@@ -1491,6 +1491,15 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
   // the largest parity class (0,0,0) sizes the grid
   const int64_t mmax = (int64_t)d->n * cdiv(d->di, d->sd) * cdiv(d->hi, d->sh) * cdiv(d->wi, d->sw);
+  if (g.taps == 1 && d->pd == 0 && d->ph == 0 && d->pw == 0) {
+    // strided 1^3 conv (shortcut B): only the all-even class has a tap, so dX is one fill
+    // plus that class's GEMM (the 7 empty classes as igemm launches cost ~3x more)
+    const int64_t bytes = (int64_t)d->n * d->di * d->hi * d->wi * d->ci *
+                          (dtype == MMAD_BF16 ? 2 : 4);
+    const int rc = hip_status(hipMemsetAsync(dx, 0, (size_t)bytes, as_stream(stream)));
+    if (rc) return rc;
+    return run_igemm<DGRAD>(g, dtype, mmax, 1, dy, wpt, nullptr, dx, nullptr, as_stream(stream));
+  }
   return run_igemm<DGRAD>(g, dtype, mmax, d->sd * d->sh * d->sw, dy, wpt, nullptr, dx, nullptr,
                           as_stream(stream));
 }

@@ -400,8 +400,9 @@ def test_pad_rows_roundtrip():
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_batched_weight_pack_equals_per_call_pack(dtype):
-    """PackPlan (one launch for every conv: 64x64 LDS-tile jobs for the dgrad layout,
-    row-wise jobs for the forward layout) == mmad_conv_pack_weight per conv, bit for bit."""
+    """PackPlan (one launch for every conv: 64x64 LDS-tile jobs for the dgrad layout, one
+    (co*ci) x taps job per forward layout, 128x32 tiles when taps <= 32) ==
+    mmad_conv_pack_weight per conv, bit for bit."""
     from multimodal_alzheimer_amd import layers as Lyr
     specs = [(64, 64, 3, 1, 1, 1), (64, 128, 3, 2, 1, 1), (128, 256, 3, 1, 2, 2),
              (64, 128, 1, 2, 0, 1), (256, 512, 1, 1, 0, 1), (32, 64, 5, 1, 2, 1)]
@@ -426,3 +427,28 @@ def test_batched_weight_pack_equals_per_call_pack(dtype):
         if wpt is not None:
             assert torch.equal(wpt.view(iv), V.pack_weight(d, code, c.weight, dtype, True).view(iv))
     assert batched >= 5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,k,s,p", [((2, 1, 5, 6, 22), 7, 2, 3), ((1, 1, 3, 4, 131), 7, 2, 3),
+                                         ((1, 1, 2, 3, 300), 5, 1, 2)],
+                         ids=["w22", "w131_rows_ragged", "w300_unstaged"])
+def test_unfold_input_f64(shape, k, s, p, dtype):
+    """W-unfold of an f64 volume for the Cin = 1 convs (LDS-staged rows for W <= 256, the
+    per-output form above): out[row][wo][j] = x[row][wo*s - p + j] (0 outside / j >= k),
+    f64 -> fp32 -> dtype, exactly."""
+    x = rnd(*shape, seed=90).to(DEV)
+    d = V.conv_desc(shape, (8, 1, k, k, k), (s, s, s), (p, p, p), (1, 1, 1))
+    out = torch.empty(_lib.load().mmad_conv_unfolded_elems(d), dtype=dtype, device=DEV)
+    _lib.call("mmad_conv_unfold_input", d, _lib.dtype_code(torch.float64), _lib.ptr(x),
+              _lib.dtype_code(dtype), _lib.ptr(out), _lib.stream())
+    torch.cuda.synchronize()
+    n, _, di, hi, wi = shape
+    wo = d.wo
+    rows = x.reshape(-1, wi).float().cpu()
+    ref = torch.zeros(rows.shape[0], wo, 8)
+    for j in range(k):
+        xi = torch.arange(wo) * s - p + j
+        ok = (xi >= 0) & (xi < wi)
+        ref[:, ok, j] = rows[:, xi[ok]]
+    assert torch.equal(out.view(rows.shape[0], wo, 8).cpu(), ref.to(dtype))
