@@ -63,15 +63,9 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
 #pragma unroll
       for (int e = 0; e < V; ++e) { sc[e] = msc[cl * V + e]; sh[e] = msh[cl * V + e]; }
     }
-    for (int64_t r = r0 + rl; r < r1; r += rpar) {
-      const int64_t i = r * C + cl * V;
-      float yv[V];
-      if constexpr (V == Chunk<T>::N) Chunk<T>::load(y + i, yv);
-      else for (int e = 0; e < V; ++e) yv[e] = Elt<T>::ld(y, i + e);
+    // one row's contribution, from its y / g / relu_out values
+    auto accum = [&](int64_t i, float* yv, float* gv, const float* ov) {
       if (MODE == 1 || MODE == 3 || MODE == 4) {
-        float gv[V], ov[V];
-        if constexpr (V == Chunk<T>::N) Chunk<T>::load(g + i, gv);
-        else for (int e = 0; e < V; ++e) gv[e] = Elt<T>::ld(g, i + e);
         if (MODE == 4) {
           // ReLU mask of a BN+ReLU without residual, recomputed from its input y with the
           // forward's own affine (bn_affine): out > 0 <=> fma(y, scale, shift) > 0
@@ -81,8 +75,6 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
 #pragma unroll
           for (int e = 0; e < V; ++e) gv[e] = (act[i + e] & 0x80) ? gv[e] : 0.f;
         } else if (relu_out != nullptr) {
-          if constexpr (V == Chunk<T>::N) Chunk<T>::load(relu_out + i, ov);
-          else for (int e = 0; e < V; ++e) ov[e] = Elt<T>::ld(relu_out, i + e);
 #pragma unroll
           for (int e = 0; e < V; ++e) gv[e] = ov[e] > 0.f ? gv[e] : 0.f;
         }
@@ -98,6 +90,50 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
           if (MODE == 0) q[e] += yv[e] * yv[e];
         }
       }
+    };
+    constexpr bool NEED_G = MODE == 1 || MODE == 3 || MODE == 4;
+    int64_t r = r0 + rl;
+    if constexpr (V == Chunk<T>::N) {
+      // 4 rows' 16-byte loads issued before any is used (the loop is load-latency bound:
+      // 512-1024 blocks of 4 waves keep too few bytes in flight with one row at a time);
+      // rows are still added in the same order
+      constexpr int U = 4;
+      for (; r + (U - 1) * rpar < r1; r += U * rpar) {
+        u32x4 yr[U], gr[U], orr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t i = (r + u * rpar) * C + cl * V;
+          yr[u] = *reinterpret_cast<const u32x4*>(y + i);
+          if (NEED_G) gr[u] = *reinterpret_cast<const u32x4*>(g + i);
+          if (MODE == 1 && relu_out != nullptr)
+            orr[u] = *reinterpret_cast<const u32x4*>(relu_out + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t i = (r + u * rpar) * C + cl * V;
+          float yv[V], gv[V], ov[V];
+          Chunk<T>::load(reinterpret_cast<const T*>(&yr[u]), yv);
+          if (NEED_G) Chunk<T>::load(reinterpret_cast<const T*>(&gr[u]), gv);
+          if (MODE == 1 && relu_out != nullptr)
+            Chunk<T>::load(reinterpret_cast<const T*>(&orr[u]), ov);
+          accum(i, yv, gv, ov);
+        }
+      }
+    }
+    for (; r < r1; r += rpar) {
+      const int64_t i = r * C + cl * V;
+      float yv[V], gv[V], ov[V];
+      if constexpr (V == Chunk<T>::N) Chunk<T>::load(y + i, yv);
+      else for (int e = 0; e < V; ++e) yv[e] = Elt<T>::ld(y, i + e);
+      if (NEED_G) {
+        if constexpr (V == Chunk<T>::N) Chunk<T>::load(g + i, gv);
+        else for (int e = 0; e < V; ++e) gv[e] = Elt<T>::ld(g, i + e);
+        if (MODE == 1 && relu_out != nullptr) {
+          if constexpr (V == Chunk<T>::N) Chunk<T>::load(relu_out + i, ov);
+          else for (int e = 0; e < V; ++e) ov[e] = Elt<T>::ld(relu_out, i + e);
+        }
+      }
+      accum(i, yv, gv, ov);
     }
 #pragma unroll
     for (int e = 0; e < V; ++e) {
