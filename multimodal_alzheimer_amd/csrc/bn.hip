@@ -158,6 +158,7 @@ __global__ void parts_fold_kernel(int C, int nparts, int group, const float* __r
   for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
     float s = 0.f;
     const int p1 = min(nparts, (o + 1) * group);
+#pragma unroll 8
     for (int p = o * group; p < p1; ++p) s += in[(int64_t)p * 2 * C + c];
     out[(int64_t)o * 2 * C + c] = s;
   }

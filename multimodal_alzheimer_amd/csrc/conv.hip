@@ -806,6 +806,7 @@ __global__ void slab_group_sum_kernel(float* __restrict__ ws, int splits, int64_
     const int64_t idx = t % total;
     float s = 0.f;
     const int s1 = min(splits, (gi + 1) * G);
+#pragma unroll 16
     for (int sp = gi * G; sp < s1; ++sp) s += ws[sp * total + idx];
     ws[(int64_t)gi * G * total + idx] = s;
   }
