@@ -29,6 +29,7 @@ sys.path.insert(0, REPO)
 
 import multimodal_alzheimer_amd as M  # noqa: E402
 from multimodal_alzheimer_amd import _lib, volume_ops  # noqa: E402
+from multimodal_alzheimer_amd.graph_step import GraphedTrainStep  # noqa: E402
 from multimodal_alzheimer_amd.data_parallel import (GradAllReduce,  # noqa: E402
                                                     broadcast_module_state)
 
@@ -118,6 +119,9 @@ def main():
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as one captured HIP graph (graph_step.GraphedTrainStep;"
+                         " N=1 only, no dominant-kernel probe)")
     ap.add_argument("--workload", default="mri", choices=["mri", "fusion", "three"],
                     help="mri: BASELINE config 2 (the metric); fusion: config 3/4, PET+MRI "
                          "ResNet-10 x2 + MLP head, focal loss, pairs/sec; three: config 5, "
@@ -186,8 +190,18 @@ def main():
                 dp_events.append((e0, e1))
         opt.step()
 
-    for _ in range(args.warmup):
-        step()
+    if args.graph:
+        if dp:
+            raise SystemExit("--graph does not combine with the RCCL all-reduce path")
+        args.no_roofline = True          # the per-launch event probe is not captured
+        gstep = GraphedTrainStep(model, opt, batch, warmup=max(1, args.warmup))
+        gstep()
+
+        def step(timed=False):
+            gstep()
+    else:
+        for _ in range(args.warmup):
+            step()
     if world > 1:
         dist.barrier()
     events = []
@@ -237,6 +251,8 @@ def main():
         result["step_mfma_frac"] = per_gpu * FLOP_PER_VOL[S] / (
             PEAK_BF16 if cdtype == torch.bfloat16 else PEAK_F32)
         result["hbm_roofline_frac_m2"] = per_gpu * M2_BYTES_PER_VOL / PEAK_HBM
+    if args.graph:
+        result["config"]["step_launch"] = "hip graph replay"
     if reducer is not None and dp_events:
         # main-stream time from the end of backward to averaged gradients: the part of the
         # all-reduce that backward did not hide (plus the copies of non-slot gradients)
