@@ -14,6 +14,8 @@ only exchange per step is the gradient all-reduce:
 
 Backend "nccl" is RCCL on ROCm; "gloo" runs the same code on CPU for the tests.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -38,6 +40,19 @@ def broadcast_module_state(module, src=0, group=None):
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, src=src, group=group)
+
+
+# MMAD_DP_GRAD_SLOTS=0: conv weight gradients go to fresh tensors and are copied into the
+# buckets like the BN / head gradients (A/B switch for the in-place bucket slots)
+_GRAD_SLOTS = os.environ.get("MMAD_DP_GRAD_SLOTS", "1") != "0"
+
+
+_SLICE_ALIGN = 256   # bytes
+
+
+def _aligned(numel, elsize):
+    step = max(1, _SLICE_ALIGN // elsize)
+    return -(-numel // step) * step
 
 
 class GradAllReduce:
@@ -67,13 +82,23 @@ class GradAllReduce:
         # backward as its weight-gradient destination (``p._mmad_grad_view``), so the big
         # conv gradients are produced in place: no gather before the collective and no
         # copy back after it.  Gradients produced elsewhere (BN, head) are copied in/out.
+        # Every slice starts on a 256-byte boundary: an odd-sized tensor (the head's 2-float
+        # bias) must not shift the slices behind it, or torch's fused Adam sees one
+        # unaligned gradient and drops to its scalar path for all of them (measured 118 vs
+        # 64 us per step on MI355X), and the collective runs on unaligned rows.  The pad
+        # lanes are zeros and stay zeros (sum / mean of zeros).
         self.flats = []
+        self._views = {}
         for b in self.buckets:
-            flat = torch.empty(sum(p.numel() for p in b), dtype=b[0].dtype, device=b[0].device)
-            off = 0
+            offs, off = [], 0
             for p in b:
-                p._mmad_grad_view = flat[off:off + p.numel()].view_as(p)
-                off += p.numel()
+                offs.append(off)
+                off += _aligned(p.numel(), p.element_size())
+            flat = torch.zeros(off, dtype=b[0].dtype, device=b[0].device)
+            for p, o in zip(b, offs):
+                self._views[p] = flat[o:o + p.numel()].view_as(p)
+                if _GRAD_SLOTS:
+                    p._mmad_grad_view = self._views[p]
             self.flats.append(flat)
         self._hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
         self.reset()
@@ -90,8 +115,8 @@ class GradAllReduce:
 
     def _foreign(self, bi):
         """(grads, views) of the bucket's parameters whose .grad is not their slice."""
-        pairs = [(p.grad, p._mmad_grad_view) for p in self.buckets[bi]
-                 if p.grad.data_ptr() != p._mmad_grad_view.data_ptr()]
+        pairs = [(p.grad, self._views[p]) for p in self.buckets[bi]
+                 if p.grad.data_ptr() != self._views[p].data_ptr()]
         return [g for g, _ in pairs], [v for _, v in pairs]
 
     def _launch(self, bi):

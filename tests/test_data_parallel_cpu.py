@@ -90,3 +90,24 @@ def test_broadcast_module_state_makes_replicas_identical():
     for k in sds[0]:
         assert torch.equal(sds[0][k], sds[1][k]), k
     assert torch.equal(sds[1]["1.running_mean"], torch.zeros(8))
+
+
+def test_bucket_slices_are_256_byte_aligned():
+    """Odd-sized parameters (a 2-float bias) must not misalign the slices after them: torch's
+    fused Adam takes its scalar path when any gradient is unaligned (data_parallel.py)."""
+    with tempfile.TemporaryDirectory() as d:
+        dist.init_process_group("gloo", init_method=f"file://{d}/init", rank=0, world_size=1)
+        try:
+            m = nn.Sequential(nn.Linear(7, 2), nn.Linear(2, 3), nn.Linear(3, 64))
+            red = GradAllReduce(m.parameters(), bucket_mb=1.0)
+            for bi, b in enumerate(red.buckets):
+                base = red.flats[bi].data_ptr()   # device allocations are >= 256-B aligned
+                for p in b:
+                    v = red._views[p]
+                    assert (v.data_ptr() - base) % 256 == 0
+                    assert v.shape == p.shape
+            for flat in red.flats:
+                assert not flat.any()       # pad lanes start (and stay) zero
+            red.remove()
+        finally:
+            dist.destroy_process_group()
