@@ -78,35 +78,68 @@ def dominant_kernel_roofline(events, batch, size, dtype):
             "flop_per_launch": flops, "avg_launch_ms": sec * 1e3, "launches": len(events)}
 
 
-def cpu_baseline(size, seconds_budget=20.0):
-    """CPU oracle (torch fp32 restatement of the reference path) fwd+bwd+Adam, B=1."""
+def host_cores():
+    """CPU cores this process may run on: the affinity mask, capped by a cgroup CPU quota
+    (the GPU box's share is a quota; os.cpu_count() there reports the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(size, budgets=((1, 10.0), (8, 16.0))):
+    """CPU oracle (torch fp32 restatement of the reference path, verified against the real
+    reference code in tests/golden) fwd+bwd+Adam on all host cores this process may use, at
+    batch 1 and at the bench's batch 8; ``value`` is the batch-8 rate."""
     from oracle import models_ref
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cores()
     torch.set_num_threads(threads)
     h = hparams("32")
     m = models_ref.AnatCNNRef(h)
     opt = torch.optim.Adam(models_ref.adam_param_groups(m, h), weight_decay=0)
-    g = torch.Generator().manual_seed(15)
-    batch = {"mri": torch.rand((1, size, size, size), generator=g, dtype=torch.float64),
-             "label": torch.tensor([1])}
+    rates, samples = {}, []
+    for b, budget in budgets:
+        g = torch.Generator().manual_seed(15)
+        batch = {"mri": torch.rand((b, size, size, size), generator=g, dtype=torch.float64),
+                 "label": torch.randint(0, 2, (b,), generator=g)}
 
-    def step():
-        opt.zero_grad(set_to_none=True)
-        m.general_step(batch, 0, "train")["loss"].backward()
-        opt.step()
+        def step():
+            opt.zero_grad(set_to_none=True)
+            m.general_step(batch, 0, "train")["loss"].backward()
+            opt.step()
 
-    step()
-    t0 = time.perf_counter()
-    n = 0
-    while True:
         step()
-        n += 1
-        el = time.perf_counter() - t0
-        if el > seconds_budget or n >= 30:
-            break
-    return {"value": n / el, "unit": "volumes/sec", "cores": threads, "kind": "port",
-            "sample": f"{n} fwd+bwd+Adam steps of the torch-CPU oracle ResNet-10, 1x{size}^3, "
-                      f"batch 1, fp32, {threads} threads ({el:.1f} s)"}
+        t0 = time.perf_counter()
+        n = 0
+        while True:
+            step()
+            n += 1
+            el = time.perf_counter() - t0
+            if el > budget or n >= 30:
+                break
+        rates[b] = n * b / el
+        samples.append(f"batch {b}: {n} steps in {el:.1f} s")
+    return {"value": rates[8], "unit": "volumes/sec", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "machine_cpus": os.cpu_count(),
+            "value_batch1": rates[1],
+            "sample": f"torch-CPU oracle ResNet-10 fwd+bwd+Adam, 1x{size}^3, fp32, {threads} "
+                      f"threads ({'; '.join(samples)})"}
 
 
 def main():

@@ -234,6 +234,10 @@ int mmad_max2_bwd(int dtype, int64_t n, const void* g, const uint8_t* sel, void*
 int mmad_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);
 int mmad_dropout_fwd(int dtype, int64_t n, float p, uint64_t seed, const void* x, void* y,
                      uint8_t* keep, void* stream);
+/* as mmad_dropout_fwd with the seed read from device memory when the kernel runs
+ * (pet_cnn.py:27-29, :38-39 under HIP-graph replay: each replay draws a fresh mask) */
+int mmad_dropout_fwd_dev(int dtype, int64_t n, float p, const uint64_t* seed, const void* x,
+                         void* y, uint8_t* keep, void* stream);
 int mmad_dropout_bwd(int dtype, int64_t n, float p, const void* g, const uint8_t* keep,
                      void* dx, void* stream);
 

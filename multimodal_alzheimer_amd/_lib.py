@@ -92,6 +92,7 @@ _SIGS = {
     "mmad_split_cols": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp]),
     "mmad_cast": (_i32, [_i32, _i32, _i64, _vp, _vp, _vp]),
     "mmad_dropout_fwd": (_i32, [_i32, _i64, _f32, _u64, _vp, _vp, _vp, _vp]),
+    "mmad_dropout_fwd_dev": (_i32, [_i32, _i64, _f32, _vp, _vp, _vp, _vp, _vp]),
     "mmad_dropout_bwd": (_i32, [_i32, _i64, _f32, _vp, _vp, _vp, _vp]),
     "mmad_loss_fwd": (_i32, [_i32, _i32, _vp, _vp, _vp, _f64, _i32, _vp, _vp, _vp]),
     "mmad_gather_channels": (_i32, [_i32, _i32, _vp, _i64, _i64, _i32, _i64, _i32, _i32, _vp,

@@ -263,10 +263,79 @@ def _merge_groups(groups):
     return out
 
 
+class MergedAdam(torch.optim.Adam):
+    """torch.optim.Adam built from the reference's param-group list (one group per tensor,
+    anat_cnn.py:112-126, anat_pet_fusion.py:94-114) that RUNS on the merged groups
+    (``_merge_groups``: one fused multi-tensor launch per learning rate) but SPEAKS the
+    reference's layout in ``state_dict()`` / ``load_state_dict()``: a checkpoint's
+    ``optimizer_states`` written by the reference resumes here and ours resumes in the
+    reference (Lightning calls exactly these two methods for ``ckpt_path=`` resumes).
+
+    ``load_state_dict`` accepts either layout: the reference's per-tensor groups (mapped into
+    the merged groups; tensors of one merged group share every hyperparameter, the lr
+    included, because they were merged on it and a scheduler scales them alike) or the
+    merged layout torch's own ``Adam.state_dict`` of this object would have produced."""
+
+    def __init__(self, groups, **kw):
+        self._ref_groups = []
+        for grp in groups:
+            ps = grp["params"]
+            ps = [ps] if isinstance(ps, torch.Tensor) else list(ps)
+            self._ref_groups.append(ps)
+        super().__init__(_merge_groups(groups), **kw)
+
+    def _merged_index(self):
+        order = [p for g in self.param_groups for p in g["params"]]
+        gidx = [gi for gi, g in enumerate(self.param_groups) for _ in g["params"]]
+        return {id(p): i for i, p in enumerate(order)}, gidx
+
+    def state_dict(self):
+        sd = super().state_dict()
+        if len(self._ref_groups) == len(self.param_groups):
+            return sd                      # nothing was merged: the layouts coincide
+        idx, gidx = self._merged_index()
+        state, groups, j = {}, [], 0
+        for ps in self._ref_groups:
+            ids = []
+            for p in ps:
+                i = idx[id(p)]
+                if i in sd["state"]:
+                    state[j] = sd["state"][i]
+                ids.append(j)
+                j += 1
+            g = {k: v for k, v in sd["param_groups"][gidx[idx[id(ps[0])]]].items()
+                 if k != "params"}
+            g["params"] = ids
+            groups.append(g)
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, state_dict):
+        saved = state_dict["param_groups"]
+        per_tensor = (len(self._ref_groups) != len(self.param_groups) and
+                      len(saved) == len(self._ref_groups) and
+                      all(len(g["params"]) == len(ps) for g, ps in zip(saved, self._ref_groups)))
+        if per_tensor:
+            idx, gidx = self._merged_index()
+            state, first = {}, {}
+            for g, ps in zip(saved, self._ref_groups):
+                for j, p in zip(g["params"], ps):
+                    i = idx[id(p)]
+                    first.setdefault(gidx[i], g)
+                    if j in state_dict["state"]:
+                        state[i] = state_dict["state"][j]
+            groups, base = [], 0
+            for gi, g in enumerate(self.param_groups):
+                src = {k: v for k, v in first[gi].items() if k != "params"}
+                src["params"] = list(range(base, base + len(g["params"])))
+                base += len(g["params"])
+                groups.append(src)
+            state_dict = {"state": state, "param_groups": groups}
+        super().load_state_dict(state_dict)
+
+
 def _adam(groups, hparams, device):
     fused = device.type == "cuda"
-    groups = _merge_groups(groups)
-    return torch.optim.Adam(groups, weight_decay=hparams.get("l2_reg", 0) or 0, fused=fused)
+    return MergedAdam(groups, weight_decay=hparams.get("l2_reg", 0) or 0, fused=fused)
 
 
 def _with_scheduler(opt, hparams):

@@ -30,8 +30,10 @@ PartPlan part_plan(int64_t M) {
 //   MODE 2: y                  (conv bias gradient)
 //   MODE 3: as MODE 1 with the mask from bit 7 of act[] (fused BN+ReLU+max-pool backward,
 //           rows = pooled outputs, y = the pre-BN value at each window's argmax)
-// V channels per thread (16-byte vectors when C % VEC == 0), C / V lanes per row and
-// 256 / (C / V) rows in flight per block; one LDS pass folds the row lanes.
+// V channels per thread (16-byte vectors when C % VEC == 0), CC / V lanes per row and
+// 256 / (CC / V) rows in flight per block; one LDS pass folds the row lanes.  Wide rows
+// (C / V > 256, e.g. ResNet-50's 2048 channels) are split over gridDim.y channel slabs of
+// CC = C / gridDim.y channels each.
 template <typename T, int MODE, int V>
 __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t rpp,
                                                      const T* __restrict__ y,
@@ -45,7 +47,9 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
                                                      const float* __restrict__ msh) {
   __shared__ float red[2][2048];
   const int tid = threadIdx.x;
-  const int lpr = C / V;
+  const int CC = C / (int)gridDim.y;           // this block's channel slab
+  const int cb = (int)blockIdx.y * CC;
+  const int lpr = CC / V;
   const int rpar = 256 / lpr;
   const int cl = tid % lpr, rl = tid / lpr;
   const int64_t r0 = (int64_t)blockIdx.x * rpp;
@@ -57,11 +61,11 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
     float mu[V], is[V], sc[V], sh[V];
     if (MODE == 1 || MODE == 3 || MODE == 4) {
 #pragma unroll
-      for (int e = 0; e < V; ++e) { mu[e] = mean[cl * V + e]; is[e] = invstd[cl * V + e]; }
+      for (int e = 0; e < V; ++e) { mu[e] = mean[cb + cl * V + e]; is[e] = invstd[cb + cl * V + e]; }
     }
     if (MODE == 4) {
 #pragma unroll
-      for (int e = 0; e < V; ++e) { sc[e] = msc[cl * V + e]; sh[e] = msh[cl * V + e]; }
+      for (int e = 0; e < V; ++e) { sc[e] = msc[cb + cl * V + e]; sh[e] = msh[cb + cl * V + e]; }
     }
     // one row's contribution, from its y / g / relu_out values
     auto accum = [&](int64_t i, float* yv, float* gv, const float* ov) {
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
         u32x4 yr[U], gr[U], orr[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int64_t i = (r + u * rpar) * C + cl * V;
+          const int64_t i = (r + u * rpar) * C + cb + cl * V;
           yr[u] = *reinterpret_cast<const u32x4*>(y + i);
           if (NEED_G) gr[u] = *reinterpret_cast<const u32x4*>(g + i);
           if (MODE == 1 && relu_out != nullptr)
@@ -110,7 +114,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int64_t i = (r + u * rpar) * C + cl * V;
+          const int64_t i = (r + u * rpar) * C + cb + cl * V;
           float yv[V], gv[V], ov[V];
           Chunk<T>::load(reinterpret_cast<const T*>(&yr[u]), yv);
           if (NEED_G) Chunk<T>::load(reinterpret_cast<const T*>(&gr[u]), gv);
@@ -121,7 +125,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
       }
     }
     for (; r < r1; r += rpar) {
-      const int64_t i = r * C + cl * V;
+      const int64_t i = r * C + cb + cl * V;
       float yv[V], gv[V], ov[V];
       if constexpr (V == Chunk<T>::N) Chunk<T>::load(y + i, yv);
       else for (int e = 0; e < V; ++e) yv[e] = Elt<T>::ld(y, i + e);
@@ -137,16 +141,16 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
     }
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      red[0][rl * C + cl * V + e] = s[e];
-      red[1][rl * C + cl * V + e] = q[e];
+      red[0][rl * CC + cl * V + e] = s[e];
+      red[1][rl * CC + cl * V + e] = q[e];
     }
   }
   __syncthreads();
-  for (int c = tid; c < C; c += 256) {
+  for (int c = tid; c < CC; c += 256) {
     float ss = 0.f, qq = 0.f;
-    for (int k = 0; k < rpar; ++k) { ss += red[0][k * C + c]; qq += red[1][k * C + c]; }
-    parts[((int64_t)blockIdx.x * 2) * C + c] = ss;
-    parts[((int64_t)blockIdx.x * 2 + 1) * C + c] = qq;
+    for (int k = 0; k < rpar; ++k) { ss += red[0][k * CC + c]; qq += red[1][k * CC + c]; }
+    parts[((int64_t)blockIdx.x * 2) * C + cb + c] = ss;
+    parts[((int64_t)blockIdx.x * 2 + 1) * C + cb + c] = qq;
   }
 }
 
@@ -172,7 +176,11 @@ int launch_colsum(int64_t M, int C, const void* y, const void* g, const void* ro
   const PartPlan pp = part_plan(M);
   constexpr int VEC = Chunk<T>::N;
   dim3 grid((unsigned)pp.nparts);
-  if (C % VEC == 0 && C / VEC <= 256) {
+  // channel slabs for wide rows: the smallest power-of-two split whose slab fits one block
+  int slabs = 1;
+  while (C % (slabs * 2 * VEC) == 0 && C / (slabs * VEC) > 256) slabs *= 2;
+  if (C % (slabs * VEC) == 0 && C / (slabs * VEC) <= 256) {
+    grid.y = (unsigned)slabs;
     hipLaunchKernelGGL((colsum_kernel<T, MODE, VEC>), grid, dim3(256), 0, st, M, C, pp.rpp,
                        (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act, msc,
                        msh);

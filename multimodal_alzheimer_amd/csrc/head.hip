@@ -112,9 +112,13 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 }
 
 template <typename T>
-__global__ void dropout_fwd_kernel(int64_t n, float p, uint64_t seed, const T* __restrict__ x,
+__global__ void dropout_fwd_kernel(int64_t n, float p, uint64_t seed,
+                                   const uint64_t* __restrict__ seed_dev, const T* __restrict__ x,
                                    T* __restrict__ y, uint8_t* __restrict__ keep) {
   const float sc = 1.f / (1.f - p);
+  // a device-resident seed (drawn on the stream by the caller) keeps the mask fresh under
+  // HIP-graph replay, where a host scalar would be frozen into the captured arguments
+  if (seed_dev) seed = *seed_dev;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const float u = (float)(mix64(seed * 0xD1342543DE82EF95ull + (uint64_t)i) >> 40) * 0x1p-24f;
@@ -367,19 +371,31 @@ int mmad_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, vo
   return launch_status();
 }
 
-int mmad_dropout_fwd(int dtype, int64_t n, float p, uint64_t seed, const void* x, void* y,
-                     uint8_t* keep, void* stream) {
+static int dropout_fwd_launch(int dtype, int64_t n, float p, uint64_t seed,
+                              const uint64_t* seed_dev, const void* x, void* y, uint8_t* keep,
+                              void* stream) {
   if (n <= 0 || !(p >= 0.f && p < 1.f)) return MMAD_EBADSHAPE;
   if (!x || !y || !keep) return MMAD_ENULL;
   if (dtype == MMAD_BF16)
     hipLaunchKernelGGL(dropout_fwd_kernel<u16>, dim3(grid_n(n)), dim3(256), 0, as_stream(stream),
-                       n, p, seed, (const u16*)x, (u16*)y, keep);
+                       n, p, seed, seed_dev, (const u16*)x, (u16*)y, keep);
   else if (dtype == MMAD_F32)
     hipLaunchKernelGGL(dropout_fwd_kernel<float>, dim3(grid_n(n)), dim3(256), 0,
-                       as_stream(stream), n, p, seed, (const float*)x, (float*)y, keep);
+                       as_stream(stream), n, p, seed, seed_dev, (const float*)x, (float*)y, keep);
   else
     return MMAD_EBADDTYPE;
   return launch_status();
+}
+
+int mmad_dropout_fwd(int dtype, int64_t n, float p, uint64_t seed, const void* x, void* y,
+                     uint8_t* keep, void* stream) {
+  return dropout_fwd_launch(dtype, n, p, seed, nullptr, x, y, keep, stream);
+}
+
+int mmad_dropout_fwd_dev(int dtype, int64_t n, float p, const uint64_t* seed, const void* x,
+                         void* y, uint8_t* keep, void* stream) {
+  if (!seed) return MMAD_ENULL;
+  return dropout_fwd_launch(dtype, n, p, 0, seed, x, y, keep, stream);
 }
 
 int mmad_dropout_bwd(int dtype, int64_t n, float p, const void* g, const uint8_t* keep, void* dx,

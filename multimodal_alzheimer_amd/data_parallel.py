@@ -10,7 +10,14 @@ only exchange per step is the gradient all-reduce:
 * ``GradAllReduce`` -- gradient buckets (~32 MiB, reverse registration order so the
   last layers' gradients, ready first in backward, go first) all-reduced asynchronously
   from post-accumulate-grad hooks while backward continues; ``finish()`` waits, averages
-  and writes the reduced gradients back.  BN statistics stay per replica (as DDP).
+  and writes the reduced gradients back.
+
+BN batch statistics are per replica (each rank normalises its own shard, as DDP without
+SyncBatchNorm).  The running statistics: DDP's default ``broadcast_buffers=True`` copies
+rank 0's buffers to every rank before each forward; ``broadcast_module_state(model,
+buffers_only=True)`` once per step does the same here (bench.py does not call it: ranks'
+running statistics then drift apart, which changes nothing in training mode and only
+matters for evaluating on a rank other than 0).
 
 Backend "nccl" is RCCL on ROCm; "gloo" runs the same code on CPU for the tests.
 """
@@ -34,11 +41,14 @@ def shard_indices(n_samples, rank, world, epoch=0, shuffle=True, seed=15):
     return order[rank:total:world]
 
 
-def broadcast_module_state(module, src=0, group=None):
-    """Every rank starts from rank ``src``'s parameters and buffers (BN running statistics,
-    num_batches_tracked), as DDP does at construction."""
+def broadcast_module_state(module, src=0, group=None, buffers_only=False):
+    """Every rank takes rank ``src``'s parameters and buffers (BN running statistics,
+    num_batches_tracked), as DDP does at construction; ``buffers_only`` re-syncs just the
+    buffers, as DDP's ``broadcast_buffers=True`` does before every forward."""
+    ts = list(module.buffers()) if buffers_only else \
+        list(module.parameters()) + list(module.buffers())
     with torch.no_grad():
-        for t in list(module.parameters()) + list(module.buffers()):
+        for t in ts:
             dist.broadcast(t.data, src=src, group=group)
 
 

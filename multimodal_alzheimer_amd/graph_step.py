@@ -13,16 +13,33 @@ the step, the optimizer made capturable (set here), gradients produced inside th
 (``zero_grad(set_to_none=True)`` before capture).  Warm-up iterations run eagerly on a side
 stream first, as torch requires, so the model takes ``warmup`` optimizer steps before the
 first replay.  Not combined with the RCCL gradient all-reduce (data_parallel) here.
+
+What a replay changes without running Python is made visible to the host-side state that
+depends on it:
+* each group's ``lr`` becomes a 0-d device tensor before capture, so the captured fused Adam
+  reads it at replay time and an LR scheduler (``ReduceLROnPlateau`` from
+  ``configure_optimizers``, anat_cnn.py:129-134) that updates it in place
+  (``param_group['lr'].fill_``) takes effect on the next replay;
+* the eval-mode folded-weight cache (``volume_ops.conv_bn_act_eval``) is keyed on tensor
+  versions and a BN-update counter, which a replay bumps neither of: every replay advances
+  ``volume_ops._BN_UPDATES`` so the next evaluation refolds;
+* dropout draws its seed on the device (``head_ops.dropout``), so every replay gets a
+  fresh mask.
 """
 import torch
+
+from . import volume_ops
 
 
 class GraphedTrainStep:
     def __init__(self, model, optimizer, batch, warmup=3):
         self.model, self.optimizer = model, optimizer
         self.static = {k: v.clone() if torch.is_tensor(v) else v for k, v in batch.items()}
+        dev = next(model.parameters()).device
         for g in optimizer.param_groups:
             g["capturable"] = True
+            if not torch.is_tensor(g["lr"]):
+                g["lr"] = torch.tensor(float(g["lr"]), dtype=torch.float32, device=dev)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -50,4 +67,5 @@ class GraphedTrainStep:
                 if torch.is_tensor(v):
                     self.static[k].copy_(v, non_blocking=True)
         self.graph.replay()
+        volume_ops._BN_UPDATES[0] += 1     # weights / running stats changed on the device
         return self.out

@@ -98,7 +98,7 @@ def concat_features(*xs):
 
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, p, seed):
+    def forward(ctx, x, p):
         L.require_device(x)
         dense = x.is_contiguous() or (x.dim() == 5 and
                                       x.is_contiguous(memory_format=torch.channels_last_3d))
@@ -106,8 +106,13 @@ class _DropoutFn(torch.autograd.Function):
             x = x.contiguous()
         y = torch.empty_like(x)
         keep = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
-        L.call("mmad_dropout_fwd", L.dtype_code(x.dtype), x.numel(), float(p), seed, L.ptr(x),
-               L.ptr(y), L.ptr(keep), L.stream())
+        # the seed is drawn on the device from torch's CUDA generator and read by the kernel
+        # when it runs: reproducible under torch.manual_seed, never synchronises, and graph
+        # safe (a captured draw advances the generator's Philox offset on every replay, so a
+        # replayed step gets a fresh mask instead of the one baked in at capture)
+        seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, device=x.device)
+        L.call("mmad_dropout_fwd_dev", L.dtype_code(x.dtype), x.numel(), float(p), L.ptr(seed),
+               L.ptr(x), L.ptr(y), L.ptr(keep), L.stream())
         ctx.save_for_backward(keep)
         ctx.p = p
         ctx.like = y
@@ -121,7 +126,7 @@ class _DropoutFn(torch.autograd.Function):
         dx = torch.empty_like(g)
         L.call("mmad_dropout_bwd", L.dtype_code(g.dtype), g.numel(), float(ctx.p), L.ptr(g),
                L.ptr(keep), L.ptr(dx), L.stream())
-        return dx, None, None
+        return dx, None
 
 
 def dropout(x, p, training):
@@ -129,10 +134,7 @@ def dropout(x, p, training):
         return x
     if p >= 1.0:
         raise L.MMADError("dropout p must be < 1")
-    # host-side seed from torch's CPU generator: reproducible under torch.manual_seed and
-    # never synchronises the device
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-    return _DropoutFn.apply(x, float(p), seed)
+    return _DropoutFn.apply(x, float(p))
 
 
 class _LossFn(torch.autograd.Function):

@@ -76,6 +76,12 @@ CASES = {
     "anat_r10_64": (lambda: anat_hparams(10), "anat", 13, ("mri",)),
     "anat_r10_32_live": (lambda: anat_hparams(10), "anat", 32, ("mri",)),
     "anat_r10_64_live": (lambda: anat_hparams(10), "anat", 33, ("mri",)),
+    "anat_r10_mni": (lambda: anat_hparams(10), "anat", 1035, ("mri",)),
+    "anat_r50": (lambda: anat_hparams(50), "anat", 36, ("mri",)),
+    "anat_conv_out": (lambda: anat_hparams(10, n_classes=3, batchnorm_begin=True,
+                                           conv_out=[32], filter_size=[3],
+                                           batchnorm_conv=True, linear_out=[16]),
+                      "anat", 37, ("mri",)),
     "anat_r18_head": (lambda: anat_hparams(18, n_classes=3, batchnorm_begin=True,
                                            batchnorm_dense=True, linear_out=[64, 32],
                                            fl_gamma=2), "anat", 14, ("mri",)),
@@ -126,3 +132,33 @@ def batch_of(name, g):
     shape = tuple(int(v) for v in g["shape"])
     n_classes = g["train_logits"].shape[1]
     return batch_for(shape, n_classes, bseed, keys)
+
+
+def fusion_via_stage1_checkpoints(tmp_dir):
+    """The reference's stage chain (anat_pet_fusion.py:17-32): stage-1 Small_PET_CNN and
+    Anat_CNN saved as PL checkpoints, the fusion built from the two paths.  Weights are the
+    golden `anat_pet_fusion` case's: the backbone tensors travel through the checkpoints,
+    the stage-2 head is loaded afterwards.  Returns (fusion model, golden state dict)."""
+    import multimodal_alzheimer_amd as M
+    g = load("anat_pet_fusion")
+    h = CASES["anat_pet_fusion"][0]()
+    fus0 = M.Anat_PET_CNN(h, pet_model=M.Small_PET_CNN(pet_hparams()),
+                          mri_model=M.Anat_CNN(anat_hparams(10)))
+    load_prng_weights(fus0, int(g["seed"]))
+    sd = fus0.state_dict()
+    pet, mri = M.Small_PET_CNN(pet_hparams()), M.Anat_CNN(anat_hparams(10))
+    with torch.no_grad():
+        for prefix, mdl, sub in (("model_pet.", pet, "model."), ("model_mri.", mri, "")):
+            own = mdl.state_dict()
+            for k, v in sd.items():
+                if k.startswith(prefix):
+                    own[sub + k[len(prefix):]].copy_(v)
+    p_pet, p_mri = os.path.join(tmp_dir, "pet.ckpt"), os.path.join(tmp_dir, "mri.ckpt")
+    pet.save_checkpoint(p_pet)
+    mri.save_checkpoint(p_mri)
+    fus = M.Anat_PET_CNN(h, path_pet=p_pet, path_anat=p_mri)
+    head = {k: v for k, v in sd.items() if not k.startswith(("model_pet.", "model_mri."))}
+    missing, unexpected = fus.load_state_dict(head, strict=False)
+    assert not unexpected
+    assert all(k.startswith(("model_pet.", "model_mri.")) for k in missing)
+    return fus, sd

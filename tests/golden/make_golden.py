@@ -188,12 +188,14 @@ def losses():
 
 
 def _anat(depth, size, bsz, seed, **kw):
+    """size: an int (cubic volume) or a (D, H, W) tuple."""
     from pkg.models.mri_models.anat_cnn import Anat_CNN
     torch.manual_seed(0)
     m = Anat_CNN(anat_hparams(depth, **kw))
     load_prng_weights(m, seed)
-    out = {"seed": np.array(seed), "shape": np.array([bsz, size, size, size])}
-    run_case(m, batch_for((bsz, size, size, size), m.hparams["n_classes"], seed + 1), out)
+    dhw = (size,) * 3 if isinstance(size, int) else tuple(size)
+    out = {"seed": np.array(seed), "shape": np.array((bsz,) + dhw)}
+    run_case(m, batch_for((bsz,) + dhw, m.hparams["n_classes"], seed + 1), out)
     return out
 
 
@@ -226,6 +228,29 @@ def anat_r10_32_live():
 @case
 def anat_r10_64_live():                      # BASELINE config 1 with live gradients
     return _anat_live(10, 64, 2, 32)
+
+
+@case
+def anat_r10_mni():
+    """The reference's real input geometry: MNI 2 mm volumes, 91 x 109 x 91
+    (pkg/utils/dataloader.py:228-229 nib get_fdata; stride-8 output 12 x 14 x 12,
+    pkg/utils/outdated/inspect_model.py:105)."""
+    return _anat_live(10, (91, 109, 91), 2, 34)
+
+
+@case
+def anat_r50():
+    """ResNet-50 (Bottleneck 1^3 -> 3^3 -> 1^3, 2048 features; anat_cnn.py:42-43)."""
+    return _anat_live(50, 32, 2, 35)
+
+
+@case
+def anat_conv_out():
+    """conv_seg with a conv_out block (anat_cnn.py:52-63): BN3d(512) -> Conv3d(512, 32, 3,
+    'same') -> BN3d(32) -> ReLU -> MaxPool3d(2) -> GAP -> Linear(32, 16) -> ReLU ->
+    Linear(16, 3) -> ReLU, at 64^3 (8^3 after the backbone, 4^3 after the pool)."""
+    return _anat_live(10, 64, 2, 36, n_classes=3, batchnorm_begin=True, conv_out=[32],
+                      filter_size=[3], batchnorm_conv=True, linear_out=[16])
 
 
 @case

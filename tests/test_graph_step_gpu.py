@@ -33,6 +33,9 @@ def test_graph_replay_equals_eager_steps(precision):
     warm, steps = 2, 3
 
     opt_a = a.configure_optimizers()
+    for grp in opt_a.param_groups:             # as GraphedTrainStep configures it: the
+        grp["capturable"] = True               # captured Adam reads lr from the device
+        grp["lr"] = torch.tensor(float(grp["lr"]), device="cuda")
     for _ in range(warm):                      # GraphedTrainStep's eager warm-up steps
         opt_a.zero_grad(set_to_none=True)
         a.general_step(batches[0], 0, "train")["loss"].backward()
@@ -55,3 +58,88 @@ def test_graph_replay_equals_eager_steps(precision):
     for (na, pa), (nb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
         assert na == nb
         assert torch.equal(pa, pb), na
+
+
+def _batch(seed, n=2, s=32):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return {"mri": torch.rand((n, s, s, s), device="cuda", dtype=torch.float64, generator=g),
+            "label": torch.randint(0, 2, (n,), device="cuda", generator=g)}
+
+
+def _eval_fused_vs_unfused(m, batch):
+    from multimodal_alzheimer_amd import medicalnet
+    m.eval()
+    with torch.no_grad():
+        medicalnet.EVAL_FUSED = True
+        fused = m.general_step(batch, 0, "val")["outputs"].clone()
+        medicalnet.EVAL_FUSED = False
+        ref = m.general_step(batch, 0, "val")["outputs"].clone()
+        medicalnet.EVAL_FUSED = True
+    m.train()
+    return fused, ref
+
+
+def test_graph_replays_then_eval_refolds_weights():
+    """train (graph replays) -> eval -> more replays -> eval: the eval-mode folded-weight
+    cache must see the weights and running statistics the replays changed on the device
+    (a replay runs no Python, so no tensor version moves)."""
+    torch.manual_seed(5)
+    m = M.Anat_CNN(_hparams("32")).cuda()
+    opt = m.configure_optimizers()
+    batch = _batch(6)
+    gs = GraphedTrainStep(m, opt, batch, warmup=1)
+    outs = []
+    for _ in range(2):
+        for _ in range(2):
+            gs()
+        fused, ref = _eval_fused_vs_unfused(m, batch)
+        assert (fused - ref).abs().max().item() <= 2e-5 * max(1.0, ref.abs().max().item())
+        outs.append(ref)
+    assert not torch.equal(outs[0], outs[1]), "weights did not change between evaluations"
+
+
+def test_graph_replay_draws_fresh_dropout_masks():
+    """head_ops.dropout inside a captured graph: every replay draws a new mask (device-side
+    seed), keep rate ~ 1 - p, kept values scaled by 1 / (1 - p)."""
+    from multimodal_alzheimer_amd import head_ops
+    p = 0.4
+    x = torch.rand(1 << 16, device="cuda") + 0.5
+    head_ops.dropout(x, p, True)                    # warm up outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = head_ops.dropout(x, p, True)
+    masks = []
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        keep = y != 0
+        masks.append(keep.clone())
+        assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+        assert torch.allclose(y[keep], x[keep] / (1 - p), rtol=1e-6)
+    assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
+
+
+def test_graph_replay_follows_lr_scheduler():
+    """ReduceLROnPlateau (configure_optimizers with reduce_factor_lr_schedule) updates the
+    device-resident lr in place; the next replay uses it: at lr ~1e-33 Adam moves nothing."""
+    torch.manual_seed(7)
+    h = dict(_hparams("32"), reduce_factor_lr_schedule=1e-30)
+    m = M.Anat_CNN(h).cuda()
+    cfg = m.configure_optimizers()
+    opt, sched = cfg["optimizer"], cfg["lr_scheduler"]
+    sched.patience = 0
+    gs = GraphedTrainStep(m, opt, _batch(8), warmup=1)
+    gs()
+    before = {k: v.detach().clone() for k, v in m.named_parameters()}
+    gs()
+    moved = [k for k, v in m.named_parameters() if not torch.equal(v, before[k])]
+    assert moved, "a replay at the configured lr must update the weights"
+    sched.step(1.0)
+    sched.step(2.0)                                # no improvement -> lr *= 1e-30
+    assert all(float(g["lr"]) < 1e-30 for g in opt.param_groups)
+    before = {k: v.detach().clone() for k, v in m.named_parameters()}
+    gs()
+    torch.cuda.synchronize()
+    for k, v in m.named_parameters():
+        assert torch.equal(v, before[k]), k

@@ -452,3 +452,32 @@ def test_unfold_input_f64(shape, k, s, p, dtype):
         ok = (xi >= 0) & (xi < wi)
         ref[:, ok, j] = rows[:, xi[ok]]
     assert torch.equal(out.view(rows.shape[0], wo, 8).cpu(), ref.to(dtype))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("p", [0.2, 0.5])
+def test_dropout_keep_rate_scaling_routing(dtype, p):
+    """nn.Dropout(p) semantics (pet_cnn.py:27-29, :38-39): train mode zeroes ~p of the
+    elements and scales the rest by 1/(1-p); backward routes the gradient through the same
+    mask with the same scale; eval mode is the identity; two calls draw different masks."""
+    n = 1 << 18
+    x = (torch.rand(n, device=DEV) + 0.5).to(dtype).requires_grad_(True)
+    y = head_ops.dropout(x, p, True)
+    keep = y.detach() != 0
+    rate = keep.float().mean().item()
+    assert abs(rate - (1 - p)) < 4 * ((p * (1 - p) / n) ** 0.5) + 1e-3
+    sc = 1.0 / (1.0 - p)
+    exp = (x.detach().float() * sc).to(dtype)
+    assert torch.equal(y.detach()[keep], exp[keep])
+    g = (torch.rand(n, device=DEV) - 0.5).to(dtype)
+    y.backward(g)
+    assert torch.equal(x.grad[~keep], torch.zeros_like(x.grad[~keep]))
+    assert torch.equal(x.grad[keep], (g.float() * sc).to(dtype)[keep])
+    y2 = head_ops.dropout(x.detach(), p, True)
+    assert not torch.equal(y2 != 0, keep)
+    assert head_ops.dropout(x.detach(), p, False) is not None
+    assert torch.equal(head_ops.dropout(x.detach(), p, False), x.detach())
+    # 5-D channels-last volumes keep their layout
+    v = to_vol(rnd(2, 8, 3, 4, 5, seed=91), dtype)
+    yv = head_ops.dropout(v, p, True)
+    assert yv.is_contiguous(memory_format=CL)

@@ -1,0 +1,116 @@
+"""Optimizer state in the reference's checkpoint layout (CPU, no kernel launches).
+
+The reference builds one Adam param group per tensor (anat_cnn.py:111-128,
+anat_pet_fusion.py:94-117); the product runs Adam on groups merged per learning rate
+(classifiers.MergedAdam) but its state_dict() / load_state_dict() speak the per-tensor
+layout, so Lightning's ``optimizer_states`` resume in either direction."""
+import copy
+
+import torch
+
+import multimodal_alzheimer_amd as M
+from oracle import models_ref
+from tests import _golden as G
+
+
+def _fake_grads(params, seed):
+    g = torch.Generator().manual_seed(seed)
+    for p in params:
+        if p.requires_grad:
+            p.grad = torch.randn(p.shape, generator=g) * 1e-2
+
+
+def _ref_groups_anat(model, h):
+    return models_ref.adam_param_groups(model, h)
+
+
+def _assert_state_equal(a, b):
+    assert len(a["param_groups"]) == len(b["param_groups"])
+    for ga, gb in zip(a["param_groups"], b["param_groups"]):
+        assert ga["params"] == gb["params"]
+        for k in ("lr", "betas", "eps", "weight_decay", "amsgrad"):
+            assert float(torch.as_tensor(ga[k]).sum()) == float(torch.as_tensor(gb[k]).sum()), k
+    assert sorted(a["state"]) == sorted(b["state"])
+    for k in a["state"]:
+        for f in ("step", "exp_avg", "exp_avg_sq"):
+            assert torch.equal(torch.as_tensor(a["state"][k][f]).float(),
+                               torch.as_tensor(b["state"][k][f]).float()), (k, f)
+
+
+def test_merged_adam_speaks_reference_layout_anat():
+    h = G.anat_hparams(10, linear_out=[32])
+    m = M.Anat_CNN(h)
+    G.load_prng_weights(m, 3)
+    ref = copy.deepcopy(m)
+    opt = m.configure_optimizers()
+    assert len(opt.param_groups) == 2                        # merged: lr and lr_pretrained
+    ref_opt = torch.optim.Adam(_ref_groups_anat(ref, h), weight_decay=h["l2_reg"])
+    assert len(ref_opt.param_groups) == len(list(ref.model.parameters()))
+    for step in range(2):
+        _fake_grads(m.parameters(), 10 + step)
+        _fake_grads(ref.parameters(), 10 + step)
+        opt.step()
+        ref_opt.step()
+    for (k, a), (_, b) in zip(m.state_dict().items(), ref.state_dict().items()):
+        assert torch.equal(a, b), k                           # Adam is element-wise
+    _assert_state_equal(opt.state_dict(), ref_opt.state_dict())
+
+    # reference checkpoint -> product (resume), then one more identical step
+    m2 = copy.deepcopy(ref)
+    m2.__class__ = M.Anat_CNN
+    opt2 = M.Anat_CNN.configure_optimizers(m2)
+    opt2.load_state_dict(copy.deepcopy(ref_opt.state_dict()))   # as through a file
+    _fake_grads(m2.parameters(), 20)
+    _fake_grads(ref.parameters(), 20)
+    opt2.step()
+    ref_opt.step()
+    for (k, a), (_, b) in zip(m2.state_dict().items(), ref.state_dict().items()):
+        assert torch.equal(a, b), k
+    # product checkpoint -> reference
+    ref3 = copy.deepcopy(m2)
+    ref3_opt = torch.optim.Adam(_ref_groups_anat(ref3, h), weight_decay=h["l2_reg"])
+    ref3_opt.load_state_dict(copy.deepcopy(opt2.state_dict()))
+    _assert_state_equal(ref3_opt.state_dict(), ref_opt.state_dict())
+    # and the merged layout still loads into the merged optimizer
+    opt2.load_state_dict(torch.optim.Adam.state_dict(opt2))
+
+
+def test_merged_adam_reference_layout_fusion_and_scheduler():
+    """Anat_PET_CNN: model_fuse (+ its stage2out / cls2 aliases), reduce_dim_mri, then the
+    stage-1 backbones at lr_pretrained (anat_pet_fusion.py:94-114); a reduced lr survives
+    the round trip."""
+    h = G.anat_hparams(10, fl_gamma=2, reduce_factor_lr_schedule=0.5)
+    pet = M.Small_PET_CNN(G.pet_hparams())
+    mri = M.Anat_CNN(G.anat_hparams(10))
+    m = M.Anat_PET_CNN(h, pet_model=pet, mri_model=mri)
+    cfg = m.configure_optimizers()
+    opt = cfg["optimizer"]
+    ref_groups = [{"params": p, "lr": h["lr"]} for p in m.model_fuse.parameters()]
+    ref_groups += [{"params": p, "lr": h["lr"]} for p in m.reduce_dim_mri.parameters()]
+    ref_groups += [{"params": p, "lr": h["lr_pretrained"]} for p in m.model_pet.parameters()]
+    ref_groups += [{"params": p, "lr": h["lr_pretrained"]} for p in m.model_mri.parameters()]
+    sd = opt.state_dict()
+    assert len(sd["param_groups"]) == len(ref_groups)
+    _fake_grads(m.parameters(), 5)
+    opt.step()
+    for g in opt.param_groups:
+        g["lr"] *= 0.5
+    sd = opt.state_dict()
+    ref_opt = torch.optim.Adam(ref_groups, weight_decay=h["l2_reg"])
+    ref_opt.load_state_dict(copy.deepcopy(sd))
+    lrs = [g["lr"] for g in ref_opt.param_groups]
+    assert lrs[0] == h["lr"] * 0.5 and lrs[-1] == h["lr_pretrained"] * 0.5
+    opt.load_state_dict(copy.deepcopy(ref_opt.state_dict()))
+    assert sorted(g["lr"] for g in opt.param_groups) == sorted({h["lr"] * 0.5,
+                                                                h["lr_pretrained"] * 0.5})
+
+
+def test_stage1_checkpoints_feed_fusion(tmp_path):
+    """Stage 1 -> stage 2 through PL-format checkpoint files: the fusion model built from the
+    two paths holds exactly the golden case's tensors (the GPU twin runs it against the
+    golden logits)."""
+    fus, sd = G.fusion_via_stage1_checkpoints(str(tmp_path))
+    got = fus.state_dict()
+    assert list(got) == list(sd)
+    for k, v in sd.items():
+        assert torch.equal(got[k], v), k
