@@ -200,6 +200,61 @@ class ResNetPairFusionRef(nn.Module):
     general_step = AnatPETCNNRef.general_step
 
 
+class TabularMLPRef(nn.Module):
+    """BUILD EXTENSION (config 5): 9 tabular features (pkg/utils/dataloader.py:306) ->
+    Linear(9,64) -> ReLU -> Linear(64,64) -> ReLU."""
+
+    def __init__(self, n_features=9, width=64):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(n_features, width), nn.ReLU(),
+                                 nn.Linear(width, width), nn.ReLU())
+
+    def forward(self, x):
+        return self.net(x.reshape(x.shape[0], -1))
+
+
+class AllModalitiesRef(nn.Module):
+    """BUILD EXTENSION (BASELINE config 5): the stage-3 head of All_Modalities_Fusion
+    (all_modalities_fusion.py:50-79: three 64-d stage-2 features -> cat 192 ->
+    Linear(192,64) -> ReLU -> Linear(64,C)) over an MRI ResNet, a PET ResNet (both cut to
+    conv_seg[:2] and reduced 512 -> 64 + ReLU as reduce_dim_mri, anat_pet_fusion.py:49) and
+    the tabular MLP that replaces the TabPFN branch.  Concat order pet, mri, tabular (the
+    build extension's own; the reference concatenates its three stage-2 pair models'
+    outputs, all_modalities_fusion.py:74-77, two of which embed TabPFN)."""
+
+    def __init__(self, hparams, mri_stage1, pet_stage1):
+        super().__init__()
+        self.hparams = dict(hparams)
+        self.model_mri = mri_stage1
+        self.model_mri.model.conv_seg = self.model_mri.model.conv_seg[:2]
+        self.model_pet = pet_stage1
+        self.model_pet.model.conv_seg = self.model_pet.model.conv_seg[:2]
+        self.model_tabular = TabularMLPRef(hparams.get("n_tabular_features", 9))
+        self.relu = nn.ReLU()
+        self.reduce_dim_mri = nn.Sequential(nn.Linear(512, 64), self.relu)
+        self.reduce_dim_pet = nn.Sequential(nn.Linear(512, 64), self.relu)
+        self.stage3out = nn.Linear(64 * 3, 64)
+        self.cls3 = nn.Linear(64, hparams["n_classes"])
+        self.model_fuse = nn.Sequential(self.stage3out, self.relu, self.cls3)
+        self.criterion = make_criterion(hparams)
+
+    def forward(self, x_pet, x_mri, x_tab):
+        bs = x_mri.shape[0]
+        out_mri = self.reduce_dim_mri(self.model_mri(x_mri).view(bs, -1))
+        out_pet = self.reduce_dim_pet(self.model_pet(x_pet).view(bs, -1))
+        out_tab = self.model_tabular(x_tab)
+        return self.model_fuse(torch.cat((out_pet, out_mri, out_tab), dim=1))
+
+    def inputs(self, batch, dtype=torch.float32):
+        return (batch["pet1451"].unsqueeze(1).to(dtype), batch["mri"].unsqueeze(1).to(dtype),
+                batch["tabular"].unsqueeze(1).to(dtype))
+
+    def general_step(self, batch, batch_idx=0, mode="train"):
+        y_hat = self(*self.inputs(batch)).to(dtype=torch.double)
+        return {"loss": self.criterion(y_hat, batch["label"]), "outputs": y_hat,
+                "labels": batch["label"]}
+
+
 def _small_cnn_stack(hparams, n_in):
     """Conv3d 'same' (+bias) [BN3d] ReLU MaxPool3d(2) [Dropout] per conv_out entry:
     early_fusion.py:33-43, anat_pet_featuremapfusion.py:37-58."""

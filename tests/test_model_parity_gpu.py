@@ -108,18 +108,24 @@ def test_model_matches_reference(name):
             ref32 = g[key]
             exact = f64[pname][: ref32.size]
             ours = params[pname].grad.detach().double().cpu().numpy().ravel()[: ref32.size]
-            _assert_f64_bar(key, ours, ref32, exact, gscale)
+            _assert_f64_bar(key, ours, ref32, exact, gscale, params[pname].shape[0])
 
 
-def _assert_f64_bar(key, ours, ref32, exact, gscale):
+def _assert_f64_bar(key, ours, ref32, exact, gscale, rows=None):
     """ours within max(4x the reference-fp32 error, 1e-2 of the tensor's max) of the f64
-    evaluation, for every element but at most one: a single ReLU mask flip (a pre-activation
-    within fp32 rounding of 0 -- tools/diag_maskflip.py finds channel 503 of
-    layer4.1.bn2 at |x| = 2.9e-5 in anat_r50's 50-layer forward) moves exactly one bias
-    gradient by that element's own gradient, which the reference's fp32 path can do just
-    as well; that element must still stay within 25 % of the tensor's max."""
+    evaluation, except in at most one output channel (row ``rows`` of the tensor seen as
+    [rows][-1]; default: one element): a single ReLU mask flip -- a pre-activation within
+    fp32 rounding of 0 (tools/diag_maskflip.py finds channel 503 of layer4.1.bn2 at
+    |x| = 2.9e-5 in anat_r50's 50-layer forward) -- routes that voxel's gradient
+    differently, which moves that channel's BN gradients and its conv filter's gradient
+    (dW[c] = sum dY[v, c] X[v + tap]) and nothing else measurably (the flipped activation is
+    ~0 on either side, so the next layer's dW barely sees it).  The reference's own fp32 path
+    can flip just as well; that channel must still stay within 25 % of the tensor's max."""
     e_ref = np.abs(ref32 - exact).max()
-    err = np.sort(np.abs(ours - exact))[::-1]
+    n = exact.size
+    rows = n if rows is None or n % rows else rows
+    err = np.abs(ours - exact).reshape(rows, -1).max(axis=1)
+    err = np.sort(err)[::-1]
     bound = max(4 * e_ref, 1e-2 * np.abs(exact).max()) + 1e-6 * gscale
     second = err[1] if err.size > 1 else 0.0
     assert second <= bound and err[0] <= max(bound, 0.25 * np.abs(exact).max()), \
@@ -167,7 +173,7 @@ def test_fp32_gradient_error_no_worse_than_reference_cpu(name):
         ours = params[pname].grad.detach().double().cpu().numpy().ravel()[: ref32.size]
         e_ref = np.abs(ref32 - exact).max()
         e_ours = np.abs(ours - exact).max()
-        _assert_f64_bar(pname, ours, ref32, exact, gscale)
+        _assert_f64_bar(pname, ours, ref32, exact, gscale, params[pname].shape[0])
         worst = max(worst, e_ours / (e_ref + 1e-6 * gscale))
     assert worst > 0
 

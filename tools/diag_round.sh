@@ -1,2 +1,4 @@
-timeout -k 10 300 python -u -m pytest tests/test_fullsize_gpu.py -k step -x -q -s --timeout 200 > gpurun_out/diag_cos.txt 2>&1
-grep "^cos\|passed\|failed" gpurun_out/diag_cos.txt
+timeout -k 10 500 python -u -m pytest tests/test_fusion_configs_gpu.py -x -v --timeout 300 --timeout-method thread > gpurun_out/fusion_tests.txt 2>&1
+rc=$?
+grep -E "PASS|FAIL|^E " gpurun_out/fusion_tests.txt | head -30
+exit $rc
