@@ -1094,6 +1094,11 @@ bool use_patch(const Geom& g, int dtype) {
   return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
          mmad_patch::ok(patch_geo(g));
 }
+// the residue-class kernel (latticeconv.hip) for dilated stride-1 bf16 convs on 4d^3 grids
+bool use_lattice(const Geom& g, int dtype) {
+  return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
+         mmad_lattice::ok(patch_geo(g));
+}
 
 int bn_of(const Geom& g) { return g.Nd <= 64 ? 64 : 128; }
 
@@ -1435,6 +1440,7 @@ int64_t mmad_conv3d_stats_rows(const mmad_conv_desc* d, int dtype) {
   if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on())
     return mmad_stem::fwd_stats_rows(d);
   const Geom g = fwd_geom(d, dtype);
+  if (!unfolded(d) && use_lattice(g, dtype)) return mmad_lattice::tiles(patch_geo(g));
   if (!unfolded(d) && use_patch(g, dtype)) return mmad_patch::tiles(patch_geo(g));
   return cdiv(g.M, fwd_tile_rows(g, dtype));
 }
@@ -1448,6 +1454,8 @@ int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x, const voi
     return mmad_stem::fwd(d, x, wp, bias, y, stats, stream);
   const Geom g = fwd_geom(d, dtype);
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
+  if (!unfolded(d) && use_lattice(g, dtype))
+    return mmad_lattice::fwd(patch_geo(g), x, wp, bias, y, stats, stream);
   if (!unfolded(d) && use_patch(g, dtype))
     return mmad_patch::fwd(patch_geo(g), x, wp, bias, y, stats, stream);
   return run_igemm<FWD>(g, dtype, g.M, 1, x, wp, bias, y, stats, as_stream(stream));
@@ -1465,6 +1473,12 @@ int mmad_conv3d_fwd_ex(const mmad_conv_desc* d, int dtype, const void* x, const 
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
   g.res = res;
   g.relu = relu ? 1 : 0;
+  if (use_lattice(g, dtype)) {
+    mmad_patch::Geo q = patch_geo(g);
+    q.res = res;
+    q.relu = g.relu;
+    return mmad_lattice::fwd(q, x, wp, bias, y, stats, stream);
+  }
   if (use_patch(g, dtype)) {
     mmad_patch::Geo q = patch_geo(g);
     q.res = res;
@@ -1483,6 +1497,8 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
   if (dgrad_as_fwd(d)) {
     const Geom gf = dgrad_fwd_geom(d, dtype);
     if (!geom_ok(gf, dtype)) return MMAD_EUNSUPPORTED;
+    if (use_lattice(gf, dtype))
+      return mmad_lattice::fwd(patch_geo(gf), dy, wpt, nullptr, dx, nullptr, stream);
     if (use_patch(gf, dtype))
       return mmad_patch::fwd(patch_geo(gf), dy, wpt, nullptr, dx, nullptr, stream);
     return run_igemm<FWD>(gf, dtype, gf.M, 1, dy, wpt, nullptr, dx, nullptr,

@@ -22,3 +22,12 @@ int64_t tiles(const Geo& g);
 int fwd(const Geo& g, const void* src, const void* wp, const float* bias, void* dst,
         float* stats, void* stream);
 }  // namespace mmad_patch
+
+// Residue-class conv for dilated 3^3 convs on a 4d^3 grid (latticeconv.hip): same geometry
+// record, packed weights and partial-sum layout as the patch kernel.
+namespace mmad_lattice {
+bool ok(const mmad_patch::Geo& g);
+int64_t tiles(const mmad_patch::Geo& g);
+int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,
+        float* stats, void* stream);
+}  // namespace mmad_lattice
