@@ -32,6 +32,7 @@
 //    residual + ReLU (eval-mode fused BN), bf16 tile transposed through LDS into 16-byte
 //    channel-vector stores; tiles walk the XCDs in contiguous ranges (the 4 channel tiles
 //    and neighbouring planes of one sub group share an L2).
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -352,6 +353,282 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   }
 }
 
+
+// ---- weight gradient on the residue-class lattice ----------------------------------------
+// dW[co][tap][ci] = sum over output voxels v of dY[v][co] * X[v + tap][ci], v walked as
+// (sub group, plane tz, position, 32 subs): a K step of 32 voxels is 32 subs at ONE output
+// position, so a tap's X rows for that step are the 32 subs at one shifted position of one
+// input plane -- or, when the shift leaves the 4^3 sub-lattice, the zero padding, read from
+// a 2 KiB zero block (uniform address select, no branch: those MFMAs add zeros).
+//  * block = 64 output channels x 32 input channels x all 27 taps over a split of the sub
+//    groups; 8 waves = 2 (16-channel ci halves) x 4 tap groups of 7 (6); per wave 4 x 7
+//    accumulator tiles;
+//  * X input planes (32 subs x 16 positions x 32 channels = 32 KiB) stream through a 4-slot
+//    ring, each loaded once per sub group (the tile of output plane tz reads planes
+//    tz-1..tz+1; plane o+2 of the stream is issued when output plane o starts);
+//  * dY (2 positions x 32 subs x 64 channels = 8 KiB per stage) through a 3-slot ring;
+//  * both operands are m-major images read with transposing ds_read_b64_tr_b16 fragment
+//    reads (as conv.hip's wgrad_kernel); fp32 partial slabs [split][co][tap*Cs + ci] are
+//    summed and transposed by conv.hip's wgrad_reduce_t_kernel.
+constexpr int WXROW = 64;                 // X rows: 32 ci x 2 B
+constexpr int WYROW = 128;                // dY rows: 64 co x 2 B
+constexpr int WPLANE = PL * WXROW;        // 32 KiB
+constexpr int WXSLOTS = 4;
+constexpr int WYST = 2 * NS * WYROW;      // 8 KiB: 2 positions per stage
+constexpr int WYSLOTS = 3;
+constexpr int WZERO_OFF = WXSLOTS * WPLANE;
+constexpr int WY_OFF = WZERO_OFF + NS * WXROW;
+constexpr int WLDS = WY_OFF + WYSLOTS * WYST;
+
+// 16-byte chunk swizzles of bf16 m-major rows for the transposing fragment reads (a read
+// covers rows {0-3, 8-11} (+4) x two chunks): 64-B rows (4 chunks) move rows 8-15 to the
+// other 32-B half; 128-B rows as conv.hip's wgrad_kernel.  Both stay inside the row.
+__device__ __forceinline__ int wsz64(int r) { return 2 * ((r >> 3) & 1); }
+__device__ __forceinline__ int wsz128(int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); }
+
+// transposed fragment (8 consecutive K rows of one 16-column group) from an m-major image
+template <int ROWB>
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int r0, int col) {
+  const int ch = col >> 3, hb = (col & 7) * 2;
+  const int r1 = r0 + 4;
+  const int s0 = ROWB == 64 ? wsz64(r0) : wsz128(r0);
+  const int s1 = ROWB == 64 ? wsz64(r1) : wsz128(r1);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (LDS_AS bf16x4*)(img + r0 * ROWB + ((ch ^ s0) << 4) + hb));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (LDS_AS bf16x4*)(img + r1 * ROWB + ((ch ^ s1) << 4) + hb));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+struct LWG {
+  int nb, Cs, Nd, d, K;
+  int groups_per_split;
+};
+
+__global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* __restrict__ src,
+                                                             const u16* __restrict__ dy,
+                                                             float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware order: the co tiles of one (ci chunk, split) read the same X planes
+  const int nci = g.Cs / KC, nco = g.Nd / 64;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int cot = tile % nco;
+  const int t2 = tile / nco;
+  const int cit = t2 % nci, split = t2 / nci;
+  const int co0 = cot * 64, ci0 = cit * KC;
+  const int d = g.d, E = S * d;
+  const int gpn = d * d * d / NS;
+  const int g0 = split * g.groups_per_split;
+  const int nplane_out = g.groups_per_split * S;    // output planes of this block
+  const int nstage = nplane_out * 8;                // 2 positions per stage
+  const int64_t plane_vox = (int64_t)d * E * E;
+
+  // zero block (the padding rows)
+  for (int i = tid; i < NS * WXROW / 16; i += NTHR)
+    *reinterpret_cast<u32x4*>(smem + WZERO_OFF + i * 16) = u32x4{0u, 0u, 0u, 0u};
+
+  // sub s of group gi -> voxel of (plane z, position ty, tx) = a group-uniform part
+  // (scalar, recomputed per stage / plane) + a per-lane sub part (constant: a group holds
+  // 32 consecutive classes, so for d = 4 or 8 the sub's class digits never carry into the
+  // group's, and the lane part is the same in every group)
+  auto grp_vox = [&](int gi, int z, int ty, int tx) -> int64_t {
+    const int n = gi / gpn, q = (gi % gpn) * NS;
+    const int rz = q / (d * d), ry = (q / d) % d, rx = q % d;
+    return (((int64_t)n * E + rz + d * z) * E + ry + d * ty) * E + rx + d * tx;
+  };
+  auto sub_part = [&](int s) -> int64_t {
+    const int q = s;                                 // classes 0..31 of a 32-aligned group
+    const int rz = q / (d * d), ry = (q / d) % d, rx = q % d;
+    return ((int64_t)rz * E + ry) * E + rx;
+  };
+  // X stream entry e = (group g0 + e / 4, plane e % 4) into slot e % 4: 4 instructions per
+  // wave of 16 rows x 64 B (row = pos * 32 + sub)
+  const int xrow_l = lane >> 2;
+  int64_t xlane[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int row = (wave * 4 + k) * 16 + xrow_l;
+    const int pos = row / NS, sb = row % NS;
+    const int chunk = (lane & 3) ^ wsz64(row);
+    xlane[k] = (sub_part(sb) + (int64_t)d * (pos / S) * E + d * (pos % S)) * g.Cs + ci0 +
+               chunk * 8;
+  }
+  auto issue_x = [&](int e) {
+    const int gi = g0 + e / S, pz = e % S;
+    char* slot = smem + (e % WXSLOTS) * WPLANE;
+    const u16* base = src + grp_vox(gi, pz, 0, 0) * g.Cs;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      glds16_asm(base + xlane[k], lds_addr_of(slot + (wave * 4 + k) * 1024));
+  };
+  // dY stage s = (output plane s / 8, positions 2*(s%8), +1): one instruction per wave of
+  // 8 rows x 128 B (row = q * 32 + sub; position 2m + q = (ty, tx) = (m / 2, 2 (m % 2) + q))
+  const int yrow = wave * 8 + (lane >> 3);
+  const int ychunk = (lane & 7) ^ wsz128(yrow);
+  const int64_t ylane = (sub_part(yrow % NS) + (int64_t)d * (yrow / NS)) * g.Nd + co0 +
+                        ychunk * 8;
+
+
+  const int cf = wave & 1, tg = wave >> 1;          // ci half, tap group
+  const int t0 = tg * 7, nt = tg == 3 ? 6 : 7;
+  const int lk = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int rsel = 8 * lk + q4;                     // this lane's K rows r, r + 4 of a step
+  f32x4 acc[4][7];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Fragment addressing, hoisted out of the K loop.  Per lane: the byte offsets of its two
+  // transposed 8-byte reads (rows rsel and rsel + 4) in a dY image (4 channel groups, two
+  // positions) and in an X position block.  Per wave (scalar): each of its taps' offset in
+  // the X ring relative to (plane tz, position) and the positions / planes where that tap
+  // is inside the sub-lattice.  X entry e sits in slot e % 4 and a sub group's planes are
+  // entries 4g..4g+3, so plane z of the current group is slot z.
+  auto tr_off = [&](int rowb, int r, int col, int sw) -> uint32_t {
+    return (uint32_t)(r * rowb + ((((col >> 3) ^ sw)) << 4) + (col & 7) * 2);
+  };
+  uint32_t ya_lo[2][4], ya_hi[2][4];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r0 = q * NS + rsel, col = i * 16 + 4 * p4;
+      ya_lo[q][i] = tr_off(WYROW, r0, col, wsz128(r0));
+      ya_hi[q][i] = tr_off(WYROW, r0 + 4, col, wsz128(r0 + 4));
+    }
+  const uint32_t xb_lo = tr_off(WXROW, rsel, cf * 16 + 4 * p4, wsz64(rsel));
+  const uint32_t xb_hi = tr_off(WXROW, rsel + 4, cf * 16 + 4 * p4, wsz64(rsel + 4));
+  int dk[7];
+  uint32_t pmask[7], zmask[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int t = min(t0 + k, 26);
+    const int kz = t / 9 - 1, ky = (t / 3) % 3 - 1, kx = t % 3 - 1;
+    dk[k] = kz * WPLANE + (ky * S + kx) * NS * WXROW;
+    uint32_t pm = 0, zm = 0;
+    for (int pq = 0; pq < S * S; ++pq) {
+      const int sy = pq / S + ky, sx = pq % S + kx;
+      if ((unsigned)sy < (unsigned)S && (unsigned)sx < (unsigned)S) pm |= 1u << pq;
+    }
+    for (int z = 0; z < S; ++z)
+      if ((unsigned)(z + kz) < (unsigned)S) zm |= 1u << z;
+    pmask[k] = k < nt ? (uint32_t)__builtin_amdgcn_readfirstlane(pm) : 0u;
+    zmask[k] = (uint32_t)__builtin_amdgcn_readfirstlane(zm);
+    dk[k] = __builtin_amdgcn_readfirstlane(dk[k]);
+  }
+  auto tr8 = [](const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p);
+  };
+  // one K step = output position POS (compile time) of the current plane: fragment reads
+  // (MFMAs separately); vm[k] = the positions where tap k is inside the sub-lattice on this
+  // plane (0 for the padding planes and for a wave's unused 7th tap slot)
+  struct WFr { bf16x8 a[4], b[7]; };
+  uint32_t vm[7];
+  int pbase = 0;                                    // plane tz's X offset in the ring
+  auto kread = [&](const char* yimg, auto qc, auto posc, WFr& f) {
+    constexpr int Q = decltype(qc)::value, POS = decltype(posc)::value;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      f.a[i] = __builtin_shufflevector(tr8(yimg + ya_lo[Q][i]), tr8(yimg + ya_hi[Q][i]),
+                                       0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const bool ok = (vm[k] >> POS) & 1u;
+      const char* img = smem + (ok ? pbase + POS * NS * WXROW + dk[k] : WZERO_OFF);
+      f.b[k] = __builtin_shufflevector(tr8(img + xb_lo), tr8(img + xb_hi), 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  };
+  // MFMAs of a K step; a tap outside the sub-lattice (its reads came from the zero block)
+  // is skipped by a uniform branch -- the reads stay unconditional so the LDS counter
+  // waits before each MFMA group remain exact
+  auto kmma = [&](const WFr& f, auto posc) {
+    constexpr int POS = decltype(posc)::value;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+#ifndef LAT_WG_DENSE
+      if ((vm[k] >> POS) & 1u)
+#endif
+      {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[k], acc[i][k], 0, 0, 0);
+      }
+    }
+  };
+
+  // dY of stage (plane o, pair m) into ring slot sl
+  auto issue_y_at = [&](int64_t plane_vox0, int m, int sl) {
+    const u16* base = dy + (plane_vox0 + (int64_t)d * (m / 2) * E + 2 * d * (m % 2)) * g.Nd;
+    glds16_asm(base + ylane, lds_addr_of(smem + WY_OFF + sl * WYST + wave * 1024));
+  };
+  auto plane_y0 = [&](int o) -> int64_t { return grp_vox(g0 + o / S, o % S, 0, 0); };
+
+  // prologue: X entries 0 and 1, dY stages 0 and 1
+  issue_x(0);
+  issue_x(1);
+  issue_y_at(plane_y0(0), 0, 0);
+  issue_y_at(plane_y0(0), 1, 1);
+  for (int o = 0; o < nplane_out; ++o) {
+    const int tz = o % S;
+    const bool xnow = o + 2 < nplane_out;           // X plane o + 2 issued at stage 0
+    pbase = tz * WPLANE;
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+      vm[k] = ((zmask[k] >> tz) & 1u) ? pmask[k] : 0u;
+    const int64_t y_here = plane_y0(o);
+    const int64_t y_next = o + 1 < nplane_out ? plane_y0(o + 1) : y_here;
+    const int sl0 = (o * 8) % WYSLOTS;
+    auto stage = [&](auto mc) {
+      constexpr int M = decltype(mc)::value;
+      const int sl = (sl0 + M) % WYSLOTS;
+      // dY of this stage landed (issued two stages ago); younger: the next stage's dY and,
+      // at stages 1 and 2, the X plane issued at stage 0 right after stage 2's dY
+      const bool last = o + 1 == nplane_out && M == 7;
+      if ((M == 1 || M == 2) && xnow) wait_vm_lgkm0<5>();
+      else if (last) wait_vm_lgkm0<0>();
+      else wait_vm_lgkm0<1>();
+      raw_barrier();
+      if (M < 6) issue_y_at(y_here, M + 2, (sl + 2) % WYSLOTS);
+      else if (o + 1 < nplane_out) issue_y_at(y_next, M - 6, (sl + 2) % WYSLOTS);
+      if (M == 0 && xnow) issue_x(o + 2);
+      const char* yimg = smem + WY_OFF + sl * WYST;
+      WFr f0, f1;
+      kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, f0);
+      kread(yimg, std::integral_constant<int, 1>{}, std::integral_constant<int, 2 * M + 1>{}, f1);
+      kmma(f0, std::integral_constant<int, 2 * M>{});
+      kmma(f1, std::integral_constant<int, 2 * M + 1>{});
+    };
+    stage(std::integral_constant<int, 0>{});
+    stage(std::integral_constant<int, 1>{});
+    stage(std::integral_constant<int, 2>{});
+    stage(std::integral_constant<int, 3>{});
+    stage(std::integral_constant<int, 4>{});
+    stage(std::integral_constant<int, 5>{});
+    stage(std::integral_constant<int, 6>{});
+    stage(std::integral_constant<int, 7>{});
+  }
+
+  // partial slab [split][co][tap * Cs + ci]
+  float* out = ws + (int64_t)split * g.Nd * g.K;
+  const int lr = lane & 15;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    if (k < nt) {
+      const int kcol = (t0 + k) * g.Cs + ci0 + cf * 16 + lr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          out[(int64_t)(co0 + i * 16 + lk * 4 + r) * g.K + kcol] = acc[i][k][r];
+    }
+  }
+}
+
 int lattice_mode() {
   static const int v = [] { const char* e = getenv("MMAD_LATTICE"); return e ? atoi(e) : 1; }();
   return v;
@@ -374,12 +651,68 @@ bool ok(const mmad_patch::Geo& q) {
   if (q.Cs % KC || q.Nd % BNL || q.Kpad != 27 * q.Cs) return false;
   // one 512-thread block per CU: below 256 tiles the row-gather implicit GEMM (more, smaller
   // blocks) is as fast (layer4.0.conv1 dgrad, 128 tiles: 237 vs 232 us)
-  if (lattice_mode() == 1 && tiles(q) * (q.Nd / BNL) < 256) return false;
+  if (lattice_mode() == 1 && mmad_lattice::tiles(q) * (q.Nd / BNL) < 256) return false;
   return (int64_t)q.nb * E * E * E * q.Cs < (int64_t(1) << 40);
 }
 
 int64_t tiles(const mmad_patch::Geo& q) {
   return (int64_t)q.nb * q.dd * q.dd * q.dd / NS * S;
+}
+
+
+int wgrad_splits(const mmad_patch::Geo& q) {
+  const int64_t tiles = (int64_t)(q.Cs / KC) * (q.Nd / 64);
+  const int ngroups = q.nb * q.dd * q.dd * q.dd / NS;
+  int sp = 1;
+  while (tiles * sp < 256 && ngroups % (sp * 2) == 0) sp *= 2;
+  return sp;
+}
+
+// MMAD_LATTICE_WGRAD=0 routes layer4's wgrad back to the row-gather wgrad_kernel (A/B).
+// At 2 waves per SIMD the per-stage fragment reads and barrier are not hidden, so this
+// kernel is only ~2 % ahead of wgrad_kernel (4 blocks of 4 waves per CU) in the step:
+// 4.25-4.30 vs 4.32 ms (MI355X, batch 8, interleaved A/B); l4c2 380 + 20 us (isolated)
+int lattice_wgrad_mode() {
+  static const int v = [] {
+    const char* e = getenv("MMAD_LATTICE_WGRAD");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+bool wgrad_ok(const mmad_patch::Geo& q) {
+  if (lattice_mode() <= 0 || lattice_wgrad_mode() <= 0) return false;
+  const int d = q.dd;
+  if (q.KD != 3 || q.KH != 3 || q.KW != 3 || q.dh != d || q.dw != d || d < 2) return false;
+  if (q.pd != d || q.ph != d || q.pw != d) return false;
+  const int E = S * d;
+  if (q.Ds != E || q.Hs != E || q.Ws != E || q.Dd != E || q.Hd != E || q.Wd != E) return false;
+  if ((d * d * d) % NS || q.Cs % KC || q.Nd % 64 || (d != 4 && d != 8)) return false;
+  const int64_t tiles = (int64_t)(q.Cs / KC) * (q.Nd / 64) * wgrad_splits(q);
+  if (lattice_mode() == 1 && tiles < 256) return false;
+  return (int64_t)q.nb * E * E * E * std::max(q.Cs, q.Nd) < (int64_t(1) << 40);
+}
+
+int64_t wgrad_workspace(const mmad_patch::Geo& q) {
+  return (int64_t)wgrad_splits(q) * q.Nd * 27 * q.Cs * 4;
+}
+
+int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, int* splits,
+          void* stream) {
+  if (!wgrad_ok(q)) return MMAD_EUNSUPPORTED;
+  static const bool attr = hipFuncSetAttribute((const void*)lattice_wgrad_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               WLDS) == hipSuccess;
+  if (!attr) return MMAD_EUNSUPPORTED;
+  const int sp = wgrad_splits(q);
+  LWG g{};
+  g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.d = q.dd; g.K = 27 * q.Cs;
+  g.groups_per_split = q.nb * q.dd * q.dd * q.dd / NS / sp;
+  const int64_t nblk = (int64_t)(q.Cs / KC) * (q.Nd / 64) * sp;
+  hipLaunchKernelGGL(lattice_wgrad_kernel, dim3((unsigned)nblk), dim3(NTHR), WLDS,
+                     as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  *splits = sp;
+  return launch_status();
 }
 
 int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias,

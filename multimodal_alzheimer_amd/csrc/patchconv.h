@@ -30,4 +30,10 @@ bool ok(const mmad_patch::Geo& g);
 int64_t tiles(const mmad_patch::Geo& g);
 int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,
         float* stats, void* stream);
+// weight gradient: fp32 partial slabs [splits][Nd][27 * Cs] into ws (wgrad_workspace bytes),
+// *splits set; the caller sums / transposes them into the torch layout
+bool wgrad_ok(const mmad_patch::Geo& g);
+int64_t wgrad_workspace(const mmad_patch::Geo& g);
+int wgrad(const mmad_patch::Geo& g, const void* x, const void* dy, float* ws, int* splits,
+          void* stream);
 }  // namespace mmad_lattice

@@ -4,7 +4,7 @@ import collections
 import re
 import sys
 
-RULES = [("igemm", "igemm fwd/dgrad"), ("patch_conv", "patch conv"), ("wgrad_kernel", "wgrad"),
+RULES = [("igemm", "igemm fwd/dgrad"), ("lattice", "lattice conv"), ("patch_conv", "patch conv"), ("wgrad_kernel", "wgrad"),
          ("reduce", "wgrad reduce"), ("slab", "wgrad reduce"), ("stem_fwd", "stem fwd"),
          ("stem_wgrad", "stem wgrad"), ("bnpool", "bnpool fused"), ("scale_shift", "bn apply"),
          ("colsum", "bn bwd reduce"), ("bn_bwd_apply", "bn bwd apply"),
