@@ -1099,6 +1099,10 @@ bool use_lattice(const Geom& g, int dtype) {
   return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
          mmad_lattice::ok(patch_geo(g));
 }
+bool use_lattice8(const Geom& g, int dtype) {
+  return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
+         mmad_lattice8::ok(patch_geo(g));
+}
 bool use_lattice_wgrad(const Geom& g, int dtype) {
   return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
          mmad_lattice::wgrad_ok(patch_geo(g));
@@ -1445,6 +1449,7 @@ int64_t mmad_conv3d_stats_rows(const mmad_conv_desc* d, int dtype) {
     return mmad_stem::fwd_stats_rows(d);
   const Geom g = fwd_geom(d, dtype);
   if (!unfolded(d) && use_lattice(g, dtype)) return mmad_lattice::tiles(patch_geo(g));
+  if (!unfolded(d) && use_lattice8(g, dtype)) return mmad_lattice8::tiles(patch_geo(g));
   if (!unfolded(d) && use_patch(g, dtype)) return mmad_patch::tiles(patch_geo(g));
   return cdiv(g.M, fwd_tile_rows(g, dtype));
 }
@@ -1460,6 +1465,8 @@ int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x, const voi
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
   if (!unfolded(d) && use_lattice(g, dtype))
     return mmad_lattice::fwd(patch_geo(g), x, wp, bias, y, stats, stream);
+  if (!unfolded(d) && use_lattice8(g, dtype))
+    return mmad_lattice8::fwd(patch_geo(g), x, wp, bias, y, stats, stream);
   if (!unfolded(d) && use_patch(g, dtype))
     return mmad_patch::fwd(patch_geo(g), x, wp, bias, y, stats, stream);
   return run_igemm<FWD>(g, dtype, g.M, 1, x, wp, bias, y, stats, as_stream(stream));
@@ -1477,11 +1484,12 @@ int mmad_conv3d_fwd_ex(const mmad_conv_desc* d, int dtype, const void* x, const 
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
   g.res = res;
   g.relu = relu ? 1 : 0;
-  if (use_lattice(g, dtype)) {
+  if (use_lattice(g, dtype) || use_lattice8(g, dtype)) {
     mmad_patch::Geo q = patch_geo(g);
     q.res = res;
     q.relu = g.relu;
-    return mmad_lattice::fwd(q, x, wp, bias, y, stats, stream);
+    return use_lattice(g, dtype) ? mmad_lattice::fwd(q, x, wp, bias, y, stats, stream)
+                                 : mmad_lattice8::fwd(q, x, wp, bias, y, stats, stream);
   }
   if (use_patch(g, dtype)) {
     mmad_patch::Geo q = patch_geo(g);
@@ -1503,6 +1511,8 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
     if (!geom_ok(gf, dtype)) return MMAD_EUNSUPPORTED;
     if (use_lattice(gf, dtype))
       return mmad_lattice::fwd(patch_geo(gf), dy, wpt, nullptr, dx, nullptr, stream);
+    if (use_lattice8(gf, dtype))
+      return mmad_lattice8::fwd(patch_geo(gf), dy, wpt, nullptr, dx, nullptr, stream);
     if (use_patch(gf, dtype))
       return mmad_patch::fwd(patch_geo(gf), dy, wpt, nullptr, dx, nullptr, stream);
     return run_igemm<FWD>(gf, dtype, gf.M, 1, dy, wpt, nullptr, dx, nullptr,

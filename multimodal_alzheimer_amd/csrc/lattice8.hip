@@ -1,0 +1,384 @@
+// Residue-class convolution for MedicalNet's layer3 convs (3x3x3, dilation 2, padding 2,
+// stride 1; 128/256 channels on the 16^3 grid of a 128^3 input, reached from
+// pkg/models/mri_models/anat_cnn.py:29-31), forward and -- over reversed taps -- input
+// gradient, gfx950 bf16.
+//
+// The dilation-2 conv on a 16^3 grid is 8 independent dense 3^3 convs (padding 1), one per
+// residue class (rz, ry, rx) in {0,1}^3, each on an 8^3 sub-lattice (latticeconv.hip does
+// the same for layer4's 4^3 sub-lattices).  Here a tile is one sample's 8 classes over one
+// whole z-plane of the sub-lattice: 64 positions x 8 classes = 512 GEMM rows
+// (position-major), so the tile needs no y/x halo -- a y or x shift that leaves the plane
+// is padding -- and only the three input planes tz-1..tz+1 (32 input channels each chunk,
+// 96 KiB) sit in LDS as the patch.  Per tap only the weights stream (64 output channels x
+// 32 input channels = 4 KiB; 3 taps = one stage; 3-slot ring, two stages in flight).
+//  * a 16-row MFMA fragment is 2 x-neighbouring positions x 8 classes: a y shift out of
+//    the plane drops the whole fragment (compile-time per wave row, skipped); an x shift
+//    out of the plane drops half the lanes, which then read a zero row (one select);
+//  * 8 waves = 4 x 2 wave tiles of 128 rows (two y rows of the plane) x 32 channels;
+//  * the loop walks (chunk, kz, ky) stages with kx = -1, 0, 1 inside, the next tap's
+//    fragment reads in flight during each tap's MFMAs; patch planes for the next chunk are
+//    reloaded as soon as the current chunk's last stage on them has run;
+//  * epilogue as the implicit GEMM: bias, BN partial sums (one row per tile), optional
+//    residual + ReLU, bf16 tile transposed through LDS into 16-byte channel stores.
+#include <cstdlib>
+#include <type_traits>
+
+#include "common.h"
+#include "patchconv.h"
+
+namespace {
+
+constexpr int S8 = 8;                      // sub-lattice extent
+constexpr int NC = 8;                      // classes (d^3, d = 2)
+constexpr int PL8 = S8 * S8 * NC;          // rows per plane (512)
+constexpr int RB8 = 64;                    // bytes per row (32 channels)
+constexpr int KC8 = RB8 / 2;
+constexpr int PLANE8 = PL8 * RB8;          // 32 KiB
+constexpr int BN8 = 64;                    // output channels per tile
+constexpr int BTAP8 = BN8 * RB8;           // 4 KiB
+constexpr int TPS8 = 3;
+constexpr int BSLOT8 = TPS8 * BTAP8;       // 12 KiB
+constexpr int NSL8 = 3;
+constexpr int RING8 = 3 * PLANE8;
+constexpr int ZERO8 = RING8 + NSL8 * BSLOT8;
+constexpr int MAIN8 = ZERO8 + RB8;
+constexpr int CROW8 = BN8 * 2 + 16;
+constexpr int EPI8 = PL8 * CROW8 + 3 * 2 * BN8 * 4;
+constexpr int LDS8 = MAIN8 > EPI8 ? MAIN8 : EPI8;
+constexpr int NT8 = 512;
+
+struct L8 {
+  int nb, Cs, Nd, Kpad, nbn, nchunk;
+  const u16* res;
+  int relu;
+};
+
+__device__ __forceinline__ int swz8(int row) { return 3 * ((row >> 3) & 1); }
+
+struct Fr8 {
+  bf16x8 b[2];
+  bf16x8 a[8];
+};
+
+// fragment f of wave row WM: plane row ty = 2*WM + (f >> 2), x pair j = f & 3
+template <int WM, int KY>
+__device__ constexpr bool row_ok(int f) {
+  return 2 * WM + (f >> 2) + KY >= 0 && 2 * WM + (f >> 2) + KY < S8;
+}
+
+// ao: this lane's row offset + chunk for an even (index 0) / odd (1) x shift; zlane: the
+// lane's zero-row address; lhi: lane is the fragment's second x position
+template <int WM, int KY, int KX>
+__device__ __forceinline__ void read8(const char* bsl, const char* pl, const uint32_t (&ao)[2],
+                                      const char* zp, bool lhi, Fr8& f) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    f.b[j] = *reinterpret_cast<const bf16x8*>(bsl + (KX + 1) * BTAP8 + j * 16 * RB8);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if (row_ok<WM, KY>(q)) {
+      constexpr int dummy = 0;
+      const int ty = 2 * WM + (q >> 2) + KY + dummy, x0 = 2 * (q & 3) + KX;
+      const int base = (ty * S8 + x0) * NC * RB8;       // may be -8 rows: lanes redirected
+      const char* p = pl + base + ao[KX & 1];
+      if (KX == -1 && (q & 3) == 0) p = lhi ? p : zp;
+      if (KX == 1 && (q & 3) == 3) p = lhi ? zp : p;
+      f.a[q] = *reinterpret_cast<const bf16x8*>(p);
+    }
+  }
+}
+
+template <int WM, int KY>
+__device__ __forceinline__ void mma8(f32x4 (&acc)[8][2], const Fr8& f) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if (row_ok<WM, KY>(q)) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[q], f.b[j], acc[q][j], 0, 0, 0);
+    }
+}
+
+template <int WM, int KY>
+__device__ __forceinline__ void stage8(f32x4 (&acc)[8][2], const char* bsl, const char* pl,
+                                       const uint32_t (&ao)[2], const char* zp, bool lhi) {
+  Fr8 f0, f1;
+  read8<WM, KY, -1>(bsl, pl, ao, zp, lhi, f0);
+  read8<WM, KY, 0>(bsl, pl, ao, zp, lhi, f1);
+  mma8<WM, KY>(acc, f0);
+  read8<WM, KY, 1>(bsl, pl, ao, zp, lhi, f0);
+  mma8<WM, KY>(acc, f1);
+  mma8<WM, KY>(acc, f0);
+}
+
+__global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __restrict__ src,
+                                                            const u16* __restrict__ wgt,
+                                                            const float* __restrict__ bias,
+                                                            u16* __restrict__ dst,
+                                                            float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem + RING8;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int nt = tile % g.nbn;
+  const int t2 = tile / g.nbn;
+  const int tz = t2 % S8, n = t2 / S8;
+  const int n0 = nt * BN8;
+  constexpr int E = 2 * S8;                          // 16
+
+  if (tid < RB8 / 16)
+    *reinterpret_cast<u32x4*>(smem + ZERO8 + tid * 16) = u32x4{0u, 0u, 0u, 0u};
+
+  // ---- patch DMA: plane slot p <- plane tz - 1 + p, chunk cc; 4 instructions per wave of
+  // 16 rows x 64 B (row = pos * 8 + class)
+  const int lrow = lane >> 2;
+  int64_t pvox[4];
+  int pch[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int row = (wave * 4 + k) * 16 + lrow;
+    const int pos = row >> 3, c = row & 7;
+    const int ty = pos >> 3, tx = pos & 7;
+    pvox[k] = (((int64_t)n * E + (c >> 2)) * E + ((c >> 1) & 1) + 2 * ty) * E + (c & 1) + 2 * tx;
+    pch[k] = (lane & 3) ^ swz8(row);
+  }
+  auto issue_plane = [&](int p, int cc) {
+    const int64_t zoff = (int64_t)2 * (tz - 1 + p) * E * E;
+    char* pb = smem + p * PLANE8;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      glds16_asm(src + (pvox[k] + zoff) * g.Cs + cc * KC8 + pch[k] * 8,
+                 lds_addr_of(pb + (wave * 4 + k) * 1024));
+  };
+  // ---- weight DMA: 3 taps x 64 rows x 64 B = 12 instructions; wave w issues q = w and
+  // (waves 0-3) q = w + 8; instruction q = tap q / 4, rows (q % 4) * 16 ..
+  const int nbi = wave < 4 ? 2 : 1;
+  const u16* wq[2];
+  int wslot_off[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int q = wave + 8 * h;
+    const int row = (q % 4) * 16 + lrow;
+    wq[h] = wgt + (int64_t)(n0 + row) * g.Kpad + ((lane & 3) ^ swz8(row)) * 8 + (q / 4) * g.Cs;
+    wslot_off[h] = (q / 4) * BTAP8 + (q % 4) * 1024;
+  }
+  auto issue_b = [&](int cc, int t, int sl) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (h < nbi)
+        glds16_asm(wq[h] + t * g.Cs + cc * KC8, lds_addr_of(ring + sl * BSLOT8 + wslot_off[h]));
+  };
+
+  const int kz0 = tz == 0 ? 0 : -1, kz1 = tz == S8 - 1 ? 0 : 1;
+  const int nkz = kz1 - kz0 + 1;
+  const int nspc = nkz * 3;
+  const int nstage = g.nchunk * nspc;
+  auto stage_w = [&](int s, int& cc, int& t) {
+    cc = s / nspc;
+    const int r = s - cc * nspc;
+    t = (kz0 + r / 3 + 1) * 9 + (r % 3) * 3;        // first tap (kx = -1) of the stage
+  };
+  auto plane_due = [&](int s, int& p, int& cc) -> bool {
+    if (s < 1) return false;
+    const int c = (s - 1) / nspc, r = (s - 1) - c * nspc;
+    if (r % 3 != 2 || c + 1 >= g.nchunk) return false;
+    p = kz0 + r / 3 + 1;
+    cc = c + 1;
+    return true;
+  };
+
+  const int wm = wave & 3, wn = wave >> 2;
+  const int lr = lane & 15, lk = lane >> 4;
+  const bool lhi = (lr >> 3) != 0;
+  uint32_t ao[2];
+  ao[0] = lr * RB8 + ((lk ^ swz8(lr)) << 4);
+  ao[1] = lr * RB8 + ((lk ^ (3 - swz8(lr))) << 4);   // rows shifted by 8: the other swizzle
+  const char* zp = smem + ZERO8 + (lk << 4);
+  const uint32_t b_lane = (wn * 32 + lr) * RB8 + ((lk ^ swz8(lr)) << 4);
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: chunk-0 planes, weights of stages 0 and 1
+  for (int p = 0; p < 3; ++p)
+    if (p - 1 >= kz0 && p - 1 <= kz1) issue_plane(p, 0);
+  for (int s = 0; s < 2 && s < nstage; ++s) {
+    int cc, t;
+    stage_w(s, cc, t);
+    issue_b(cc, t, s);
+  }
+  int pl_at[2] = {0, 0};                            // plane instructions issued at s-1, s-2
+  auto one_stage = [&](int s) {
+    // B(s) landed; younger: B(s+1) and any plane issued after B(s) (stages s-1, s-2)
+    const int younger = (s + 1 < nstage ? nbi : 0) + pl_at[0] + pl_at[1];
+    switch (younger) {
+      case 0: wait_vm_lgkm0<0>(); break;
+      case 1: wait_vm_lgkm0<1>(); break;
+      case 2: wait_vm_lgkm0<2>(); break;
+      case 4: wait_vm_lgkm0<4>(); break;
+      case 5: wait_vm_lgkm0<5>(); break;
+      default: wait_vm_lgkm0<6>(); break;
+    }
+    raw_barrier();
+    pl_at[1] = pl_at[0];
+    pl_at[0] = 0;
+    if (s + 2 < nstage) {
+      int cc, t;
+      stage_w(s + 2, cc, t);
+      issue_b(cc, t, (s + 2) % NSL8);
+    }
+    int p, pc;
+    if (plane_due(s, p, pc)) {
+      issue_plane(p, pc);
+      pl_at[0] = 4;
+    }
+  };
+  auto run = [&](auto wmc) {
+    constexpr int WM = decltype(wmc)::value;
+    const int ngrp = nstage / 3;
+    for (int g2 = 0; g2 < ngrp; ++g2) {
+      const int kz = kz0 + g2 % nkz;
+      const char* pl = smem + (kz + 1) * PLANE8;
+      const int s0 = g2 * 3;
+      one_stage(s0);
+      stage8<WM, -1>(acc, ring + (s0 % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
+      one_stage(s0 + 1);
+      stage8<WM, 0>(acc, ring + ((s0 + 1) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
+      one_stage(s0 + 2);
+      stage8<WM, 1>(acc, ring + ((s0 + 2) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
+    }
+  };
+  switch (wm) {
+    case 0: run(std::integral_constant<int, 0>{}); break;
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    default: run(std::integral_constant<int, 3>{}); break;
+  }
+  __syncthreads();                                  // patch / ring reused by the epilogue
+
+  // ---- epilogue: acc[q][j][e] is tile row (ty*8 + 2*(q&3))*8 + lk*4 + e with
+  // ty = 2*wm + (q >> 2), column wn*32 + j*16 + lr
+  auto dst_vox = [&](int row) -> int64_t {
+    const int pos = row >> 3, c = row & 7;
+    const int ty = pos >> 3, tx = pos & 7;
+    return (((int64_t)n * E + (c >> 2) + 2 * tz) * E + ((c >> 1) & 1) + 2 * ty) * E + (c & 1) +
+           2 * tx;
+  };
+  u16* ctile = reinterpret_cast<u16*>(smem);
+  float cs[2], cq[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    cs[j] = 0.f;
+    cq[j] = 0.f;
+    const int col = wn * 32 + j * 16 + lr;
+    const float bv = bias != nullptr ? bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int ty = 2 * wm + (q >> 2);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = (ty * S8 + 2 * (q & 3)) * NC + lk * 4 + e;
+        const float v = acc[q][j][e] + bv;
+        ctile[row * (CROW8 / 2) + col] = f2bf(v);
+        cs[j] += v;
+        cq[j] += v * v;
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN8 / 8;
+#pragma unroll
+  for (int hh = 0; hh < PL8 * CPR / NT8; ++hh) {
+    const int qd = tid + NT8 * hh;
+    const int row = qd / CPR, c8 = qd % CPR;
+    const int64_t o = dst_vox(row) * g.Nd + n0 + c8 * 8;
+    u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
+                                              row * CROW8 + c8 * 16);
+    if (g.res != nullptr || g.relu) v = epi_res_relu(v, g.res ? g.res + o : nullptr, g.relu);
+    *reinterpret_cast<u32x4*>(dst + o) = v;
+  }
+  if (stats != nullptr) {
+    float* red = reinterpret_cast<float*>(smem + PL8 * CROW8);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      cs[j] += __shfl_xor(cs[j], 16, 64);
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 16, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+    }
+    if (wm > 0 && lk == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wn * 32 + j * 16 + lr;
+        red[(wm - 1) * 2 * BN8 + col] = cs[j];
+        red[(wm - 1) * 2 * BN8 + BN8 + col] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && lk == 0) {
+      const int mt = n * S8 + tz;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wn * 32 + j * 16 + lr;
+        float ss = cs[j], qs = cq[j];
+        for (int w = 1; w < 4; ++w) {              // fixed order: deterministic
+          ss += red[(w - 1) * 2 * BN8 + col];
+          qs += red[(w - 1) * 2 * BN8 + BN8 + col];
+        }
+        stats[((int64_t)mt * 2) * g.Nd + n0 + col] = ss;
+        stats[((int64_t)mt * 2 + 1) * g.Nd + n0 + col] = qs;
+      }
+    }
+  }
+}
+
+int lattice8_mode() {
+  static const int v = [] { const char* e = getenv("MMAD_LATTICE8"); return e ? atoi(e) : 1; }();
+  return v;
+}
+
+}  // namespace
+
+namespace mmad_lattice8 {
+
+bool ok(const mmad_patch::Geo& q) {
+  if (lattice8_mode() <= 0) return false;
+  if (q.KD != 3 || q.KH != 3 || q.KW != 3) return false;
+  if (q.dd != 2 || q.dh != 2 || q.dw != 2 || q.pd != 2 || q.ph != 2 || q.pw != 2) return false;
+  constexpr int E = 2 * S8;
+  if (q.Ds != E || q.Hs != E || q.Ws != E || q.Dd != E || q.Hd != E || q.Wd != E) return false;
+  if (q.Cs % KC8 || q.Nd % BN8 || q.Kpad != 27 * q.Cs) return false;
+  // one 512-thread block per CU: with fewer than 256 tiles (layer3.0.conv1 dgrad, 128
+  // output channels: 99 vs 92 us) the row-gather GEMM's more, smaller blocks win
+  if (lattice8_mode() == 1 && (int64_t)q.nb * S8 * (q.Nd / BN8) < 256) return false;
+  return (int64_t)q.nb * E * E * E * q.Cs < (int64_t(1) << 40);
+}
+
+int64_t tiles(const mmad_patch::Geo& q) { return (int64_t)q.nb * S8; }
+
+int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias,
+        void* dst, float* stats, void* stream) {
+  if (!mmad_lattice8::ok(q)) return MMAD_EUNSUPPORTED;
+  static const bool attr = hipFuncSetAttribute((const void*)lattice8_conv_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               LDS8) == hipSuccess;
+  if (!attr) return MMAD_EUNSUPPORTED;
+  L8 g{};
+  g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.Kpad = q.Kpad;
+  g.nbn = q.Nd / BN8;
+  g.nchunk = q.Cs / KC8;
+  g.res = reinterpret_cast<const u16*>(q.res);
+  g.relu = q.relu;
+  const int64_t nblk = (int64_t)q.nb * S8 * g.nbn;
+  hipLaunchKernelGGL(lattice8_conv_kernel, dim3((unsigned)nblk), dim3(NT8), LDS8,
+                     as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
+                     stats);
+  return launch_status();
+}
+
+}  // namespace mmad_lattice8

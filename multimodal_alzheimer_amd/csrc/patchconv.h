@@ -37,3 +37,11 @@ int64_t wgrad_workspace(const mmad_patch::Geo& g);
 int wgrad(const mmad_patch::Geo& g, const void* x, const void* dy, float* ws, int* splits,
           void* stream);
 }  // namespace mmad_lattice
+
+// Residue-class conv for dilation-2 3^3 convs on a 16^3 grid (lattice8.hip, layer3).
+namespace mmad_lattice8 {
+bool ok(const mmad_patch::Geo& g);
+int64_t tiles(const mmad_patch::Geo& g);
+int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,
+        float* stats, void* stream);
+}  // namespace mmad_lattice8

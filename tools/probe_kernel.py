@@ -18,6 +18,7 @@ LAYERS = {
     "stem": (1, 64, 128, 7, 2, 3, 1),
     "l1c": (64, 64, 32, 3, 1, 1, 1),
     "l2c1": (64, 128, 32, 3, 2, 1, 1),
+    "l3c1": (128, 256, 16, 3, 1, 2, 2),
     "l3c2": (256, 256, 16, 3, 1, 2, 2),
     "l4c1": (256, 512, 16, 3, 1, 4, 4),
     "l4c2": (512, 512, 16, 3, 1, 4, 4),
