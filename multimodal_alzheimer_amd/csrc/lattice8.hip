@@ -55,8 +55,9 @@ struct L8 {
 
 __device__ __forceinline__ int swz8(int row) { return 3 * ((row >> 3) & 1); }
 
+template <int TN>
 struct Fr8 {
-  bf16x8 b[2];
+  bf16x8 b[TN];
   bf16x8 a[8];
 };
 
@@ -68,11 +69,11 @@ __device__ constexpr bool row_ok(int f) {
 
 // ao: this lane's row offset + chunk for an even (index 0) / odd (1) x shift; zlane: the
 // lane's zero-row address; lhi: lane is the fragment's second x position
-template <int WM, int KY, int KX>
+template <int TN, int WM, int KY, int KX>
 __device__ __forceinline__ void read8(const char* bsl, const char* pl, const uint32_t (&ao)[2],
-                                      const char* zp, bool lhi, Fr8& f) {
+                                      const char* zp, bool lhi, Fr8<TN>& f) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < TN; ++j)
     f.b[j] = *reinterpret_cast<const bf16x8*>(bsl + (KX + 1) * BTAP8 + j * 16 * RB8);
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -88,29 +89,32 @@ __device__ __forceinline__ void read8(const char* bsl, const char* pl, const uin
   }
 }
 
-template <int WM, int KY>
-__device__ __forceinline__ void mma8(f32x4 (&acc)[8][2], const Fr8& f) {
+template <int TN, int WM, int KY>
+__device__ __forceinline__ void mma8(f32x4 (&acc)[8][TN], const Fr8<TN>& f) {
 #pragma unroll
   for (int q = 0; q < 8; ++q)
     if (row_ok<WM, KY>(q)) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < TN; ++j)
         acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[q], f.b[j], acc[q][j], 0, 0, 0);
     }
 }
 
-template <int WM, int KY>
-__device__ __forceinline__ void stage8(f32x4 (&acc)[8][2], const char* bsl, const char* pl,
+template <int TN, int WM, int KY>
+__device__ __forceinline__ void stage8(f32x4 (&acc)[8][TN], const char* bsl, const char* pl,
                                        const uint32_t (&ao)[2], const char* zp, bool lhi) {
-  Fr8 f0, f1;
-  read8<WM, KY, -1>(bsl, pl, ao, zp, lhi, f0);
-  read8<WM, KY, 0>(bsl, pl, ao, zp, lhi, f1);
-  mma8<WM, KY>(acc, f0);
-  read8<WM, KY, 1>(bsl, pl, ao, zp, lhi, f0);
-  mma8<WM, KY>(acc, f1);
-  mma8<WM, KY>(acc, f0);
+  Fr8<TN> f0, f1;
+  read8<TN, WM, KY, -1>(bsl, pl, ao, zp, lhi, f0);
+  read8<TN, WM, KY, 0>(bsl, pl, ao, zp, lhi, f1);
+  mma8<TN, WM, KY>(acc, f0);
+  read8<TN, WM, KY, 1>(bsl, pl, ao, zp, lhi, f0);
+  mma8<TN, WM, KY>(acc, f1);
+  mma8<TN, WM, KY>(acc, f0);
 }
 
+// TN = 16-column MFMA tiles per wave: 2 (64-channel tiles) or 1 (32 channels, for layers
+// whose 64-channel tiling leaves CUs idle)
+template <int TN>
 __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __restrict__ src,
                                                             const u16* __restrict__ wgt,
                                                             const float* __restrict__ bias,
@@ -126,7 +130,8 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   const int nt = tile % g.nbn;
   const int t2 = tile / g.nbn;
   const int tz = t2 % S8, n = t2 / S8;
-  const int n0 = nt * BN8;
+  constexpr int BW = 16 * TN * 2;                  // output channels of this tile
+  const int n0 = nt * BW;
   constexpr int E = 2 * S8;                          // 16
 
   if (tid < RB8 / 16)
@@ -153,22 +158,24 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
       glds16_asm(src + (pvox[k] + zoff) * g.Cs + cc * KC8 + pch[k] * 8,
                  lds_addr_of(pb + (wave * 4 + k) * 1024));
   };
-  // ---- weight DMA: 3 taps x 64 rows x 64 B = 12 instructions; wave w issues q = w and
-  // (waves 0-3) q = w + 8; instruction q = tap q / 4, rows (q % 4) * 16 ..
-  const int nbi = wave < 4 ? 2 : 1;
+  // ---- weight DMA: 3 taps x BW rows x 64 B = 6*TN instructions; wave w issues q = w
+  // and q = w + 8 (while < 6*TN); instruction q = tap q / (2TN), rows (q % 2TN) * 16 ..
+  constexpr int NQ = 3 * 2 * TN;
+  const int nbi = (wave < NQ ? 1 : 0) + (wave + 8 < NQ ? 1 : 0);
   const u16* wq[2];
   int wslot_off[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int q = wave + 8 * h;
-    const int row = (q % 4) * 16 + lrow;
-    wq[h] = wgt + (int64_t)(n0 + row) * g.Kpad + ((lane & 3) ^ swz8(row)) * 8 + (q / 4) * g.Cs;
-    wslot_off[h] = (q / 4) * BTAP8 + (q % 4) * 1024;
+    const int q = min(wave + 8 * h, NQ - 1);
+    const int row = (q % (2 * TN)) * 16 + lrow;
+    wq[h] = wgt + (int64_t)(n0 + row) * g.Kpad + ((lane & 3) ^ swz8(row)) * 8 +
+            (q / (2 * TN)) * g.Cs;
+    wslot_off[h] = (q / (2 * TN)) * BTAP8 + (q % (2 * TN)) * 1024;
   }
   auto issue_b = [&](int cc, int t, int sl) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
-      if (h < nbi)
+      if (wave + 8 * h < NQ)
         glds16_asm(wq[h] + t * g.Cs + cc * KC8, lds_addr_of(ring + sl * BSLOT8 + wslot_off[h]));
   };
 
@@ -197,12 +204,12 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   ao[0] = lr * RB8 + ((lk ^ swz8(lr)) << 4);
   ao[1] = lr * RB8 + ((lk ^ (3 - swz8(lr))) << 4);   // rows shifted by 8: the other swizzle
   const char* zp = smem + ZERO8 + (lk << 4);
-  const uint32_t b_lane = (wn * 32 + lr) * RB8 + ((lk ^ swz8(lr)) << 4);
-  f32x4 acc[8][2];
+  const uint32_t b_lane = (wn * 16 * TN + lr) * RB8 + ((lk ^ swz8(lr)) << 4);
+  f32x4 acc[8][TN];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: chunk-0 planes, weights of stages 0 and 1
   for (int p = 0; p < 3; ++p)
@@ -246,11 +253,11 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
       const char* pl = smem + (kz + 1) * PLANE8;
       const int s0 = g2 * 3;
       one_stage(s0);
-      stage8<WM, -1>(acc, ring + (s0 % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
+      stage8<TN, WM, -1>(acc, ring + (s0 % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
       one_stage(s0 + 1);
-      stage8<WM, 0>(acc, ring + ((s0 + 1) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
+      stage8<TN, WM, 0>(acc, ring + ((s0 + 1) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
       one_stage(s0 + 2);
-      stage8<WM, 1>(acc, ring + ((s0 + 2) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
+      stage8<TN, WM, 1>(acc, ring + ((s0 + 2) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
     }
   };
   switch (wm) {
@@ -270,12 +277,12 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
            2 * tx;
   };
   u16* ctile = reinterpret_cast<u16*>(smem);
-  float cs[2], cq[2];
+  float cs[TN], cq[TN];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < TN; ++j) {
     cs[j] = 0.f;
     cq[j] = 0.f;
-    const int col = wn * 32 + j * 16 + lr;
+    const int col = wn * 16 * TN + j * 16 + lr;
     const float bv = bias != nullptr ? bias[n0 + col] : 0.f;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -291,7 +298,7 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
     }
   }
   __syncthreads();
-  constexpr int CPR = BN8 / 8;
+  constexpr int CPR = BW / 8;
 #pragma unroll
   for (int hh = 0; hh < PL8 * CPR / NT8; ++hh) {
     const int qd = tid + NT8 * hh;
@@ -305,7 +312,7 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   if (stats != nullptr) {
     float* red = reinterpret_cast<float*>(smem + PL8 * CROW8);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < TN; ++j) {
       cs[j] += __shfl_xor(cs[j], 16, 64);
       cs[j] += __shfl_xor(cs[j], 32, 64);
       cq[j] += __shfl_xor(cq[j], 16, 64);
@@ -313,22 +320,22 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
     }
     if (wm > 0 && lk == 0) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = wn * 32 + j * 16 + lr;
-        red[(wm - 1) * 2 * BN8 + col] = cs[j];
-        red[(wm - 1) * 2 * BN8 + BN8 + col] = cq[j];
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * 16 * TN + j * 16 + lr;
+        red[(wm - 1) * 2 * BW + col] = cs[j];
+        red[(wm - 1) * 2 * BW + BW + col] = cq[j];
       }
     }
     __syncthreads();
     if (wm == 0 && lk == 0) {
       const int mt = n * S8 + tz;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = wn * 32 + j * 16 + lr;
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * 16 * TN + j * 16 + lr;
         float ss = cs[j], qs = cq[j];
         for (int w = 1; w < 4; ++w) {              // fixed order: deterministic
-          ss += red[(w - 1) * 2 * BN8 + col];
-          qs += red[(w - 1) * 2 * BN8 + BN8 + col];
+          ss += red[(w - 1) * 2 * BW + col];
+          qs += red[(w - 1) * 2 * BW + BW + col];
         }
         stats[((int64_t)mt * 2) * g.Nd + n0 + col] = ss;
         stats[((int64_t)mt * 2 + 1) * g.Nd + n0 + col] = qs;
@@ -352,10 +359,10 @@ bool ok(const mmad_patch::Geo& q) {
   if (q.dd != 2 || q.dh != 2 || q.dw != 2 || q.pd != 2 || q.ph != 2 || q.pw != 2) return false;
   constexpr int E = 2 * S8;
   if (q.Ds != E || q.Hs != E || q.Ws != E || q.Dd != E || q.Hd != E || q.Wd != E) return false;
-  if (q.Cs % KC8 || q.Nd % BN8 || q.Kpad != 27 * q.Cs) return false;
-  // one 512-thread block per CU: with fewer than 256 tiles (layer3.0.conv1 dgrad, 128
-  // output channels: 99 vs 92 us) the row-gather GEMM's more, smaller blocks win
-  if (lattice8_mode() == 1 && (int64_t)q.nb * S8 * (q.Nd / BN8) < 256) return false;
+  if (q.Cs % KC8 || q.Nd % 32 || q.Kpad != 27 * q.Cs) return false;
+  // one 512-thread block per CU: with too few tiles even at 32 channels the row-gather
+  // GEMM's more, smaller blocks win
+  if (lattice8_mode() == 1 && (int64_t)q.nb * S8 * (q.Nd / 32) < 256) return false;
   return (int64_t)q.nb * E * E * E * q.Cs < (int64_t(1) << 40);
 }
 
@@ -364,20 +371,29 @@ int64_t tiles(const mmad_patch::Geo& q) { return (int64_t)q.nb * S8; }
 int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias,
         void* dst, float* stats, void* stream) {
   if (!mmad_lattice8::ok(q)) return MMAD_EUNSUPPORTED;
-  static const bool attr = hipFuncSetAttribute((const void*)lattice8_conv_kernel,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               LDS8) == hipSuccess;
+  static const bool attr =
+      hipFuncSetAttribute((const void*)lattice8_conv_kernel<2>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) == hipSuccess &&
+      hipFuncSetAttribute((const void*)lattice8_conv_kernel<1>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) == hipSuccess;
   if (!attr) return MMAD_EUNSUPPORTED;
+  // 64-channel tiles when they give every CU a block, else 32
+  const bool wide = q.Nd % BN8 == 0 && (int64_t)q.nb * S8 * (q.Nd / BN8) >= 256;
   L8 g{};
   g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.Kpad = q.Kpad;
-  g.nbn = q.Nd / BN8;
+  g.nbn = q.Nd / (wide ? BN8 : 32);
   g.nchunk = q.Cs / KC8;
   g.res = reinterpret_cast<const u16*>(q.res);
   g.relu = q.relu;
   const int64_t nblk = (int64_t)q.nb * S8 * g.nbn;
-  hipLaunchKernelGGL(lattice8_conv_kernel, dim3((unsigned)nblk), dim3(NT8), LDS8,
-                     as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                     stats);
+  if (wide)
+    hipLaunchKernelGGL(lattice8_conv_kernel<2>, dim3((unsigned)nblk), dim3(NT8), LDS8,
+                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
+                       stats);
+  else
+    hipLaunchKernelGGL(lattice8_conv_kernel<1>, dim3((unsigned)nblk), dim3(NT8), LDS8,
+                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
+                       stats);
   return launch_status();
 }
 

@@ -68,8 +68,9 @@ struct LG {
 
 __device__ __forceinline__ int swz(int row) { return 3 * ((row >> 3) & 1); }
 
+template <int TN>
 struct Frags {
-  bf16x8 b[4];
+  bf16x8 b[TN];
   bf16x8 a[4][2];
 };
 
@@ -79,10 +80,10 @@ __device__ constexpr bool tap_ok(int i) {
   return i + KY >= 0 && i + KY < S && ((i + WM) & 3) + KX >= 0 && ((i + WM) & 3) + KX < S;
 }
 
-template <int WM, int KY, int KX>
-__device__ __forceinline__ void read_tap(const char* bsl, const char* apl, Frags& f) {
+template <int TN, int WM, int KY, int KX>
+__device__ __forceinline__ void read_tap(const char* bsl, const char* apl, Frags<TN>& f) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < TN; ++j)
     f.b[j] = *reinterpret_cast<const bf16x8*>(bsl + (KX + 1) * BTAP + j * 16 * RBL);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -96,15 +97,15 @@ __device__ __forceinline__ void read_tap(const char* bsl, const char* apl, Frags
   }
 }
 
-template <int WM, int KY, int KX>
-__device__ __forceinline__ void mma_tap(f32x4 (&acc)[8][4], const Frags& f) {
+template <int TN, int WM, int KY, int KX>
+__device__ __forceinline__ void mma_tap(f32x4 (&acc)[8][TN], const Frags<TN>& f) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (tap_ok<WM, KY, KX>(i)) {
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < TN; ++j) {
 #ifndef LAT_NO_MFMA
           acc[i * 2 + h][j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i][h], f.b[j], acc[i * 2 + h][j], 0, 0, 0);
@@ -114,17 +115,20 @@ __device__ __forceinline__ void mma_tap(f32x4 (&acc)[8][4], const Frags& f) {
   }
 }
 
-template <int WM, int KY>
-__device__ __forceinline__ void stage_body(f32x4 (&acc)[8][4], const char* bsl, const char* apl) {
-  Frags f0, f1;
-  read_tap<WM, KY, -1>(bsl, apl, f0);
-  read_tap<WM, KY, 0>(bsl, apl, f1);
-  mma_tap<WM, KY, -1>(acc, f0);
-  read_tap<WM, KY, 1>(bsl, apl, f0);
-  mma_tap<WM, KY, 0>(acc, f1);
-  mma_tap<WM, KY, 1>(acc, f0);
+template <int TN, int WM, int KY>
+__device__ __forceinline__ void stage_body(f32x4 (&acc)[8][TN], const char* bsl, const char* apl) {
+  Frags<TN> f0, f1;
+  read_tap<TN, WM, KY, -1>(bsl, apl, f0);
+  read_tap<TN, WM, KY, 0>(bsl, apl, f1);
+  mma_tap<TN, WM, KY, -1>(acc, f0);
+  read_tap<TN, WM, KY, 1>(bsl, apl, f0);
+  mma_tap<TN, WM, KY, 0>(acc, f1);
+  mma_tap<TN, WM, KY, 1>(acc, f0);
 }
 
+// TN = 16-column MFMA tiles per wave: 4 (128-channel tiles) or 2 (64-channel tiles, for
+// layers whose 128-channel tiling leaves CUs idle)
+template <int TN>
 __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __restrict__ src,
                                                             const u16* __restrict__ wgt,
                                                             const float* __restrict__ bias,
@@ -143,7 +147,8 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   const int d = g.d, E = S * d;                     // grid extent per dimension
   const int gpn = d * d * d / NS;                   // sub groups per sample
   const int n = gid / gpn, q0 = (gid % gpn) * NS;   // sample, first class of the group
-  const int n0 = nt * BNL;
+  constexpr int BW = 32 * TN;                      // output channels of this tile
+  const int n0 = nt * BW;
   const int64_t plane_vox = (int64_t)d * E * E;     // voxel step between planes tz, tz+1
 
   // ---- patch DMA: plane slot p <- absolute plane tz - 1 + p of chunk cc (32 rows per
@@ -172,13 +177,23 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   };
   // ---- weight DMA: stage (chunk cc, first tap t) into ring slot sl: 3 consecutive taps
   // (one kx row), 16 rows per wave per tap
-  const int brow = wave * 16 + lrow;
-  const u16* wrow = wgt + (int64_t)(n0 + brow) * g.Kpad + (((lane & 3) ^ swz(brow)) * 8);
+  // 2*TN instructions of 16 rows per tap, 6*TN per stage: wave w issues q = w + 8h
+  constexpr int NQ = TPS * 2 * TN;
+  const u16* wq[3];
+  int wq_off[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int q = min(wave + 8 * h, NQ - 1);
+    const int tk = q / (2 * TN), rb = q % (2 * TN);
+    const int row = rb * 16 + lrow;
+    wq[h] = wgt + (int64_t)(n0 + row) * g.Kpad + (((lane & 3) ^ swz(row)) * 8) + tk * g.Cs;
+    wq_off[h] = tk * BTAP + rb * 1024;
+  }
   auto issue_b = [&](int cc, int t, int sl) {
 #pragma unroll
-    for (int k = 0; k < TPS; ++k)
-      glds16_asm(wrow + (t + k) * g.Cs + cc * KC,
-                 lds_addr_of(ring + sl * BSLOT + k * BTAP + wave * 1024));
+    for (int h = 0; h < 3; ++h)
+      if (wave + 8 * h < NQ)
+        glds16_asm(wq[h] + t * g.Cs + cc * KC, lds_addr_of(ring + sl * BSLOT + wq_off[h]));
   };
 
   // stage list: chunk-major, then the valid kz planes, then ky; a stage runs kx = -1, 0, 1
@@ -205,12 +220,12 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   const int wm = wave & 3, wn = wave >> 2;
   const int lr = lane & 15, lk = lane >> 4;
   const uint32_t a_lane = lr * RBL + ((lk ^ swz(lr)) << 4);
-  const uint32_t b_lane = (wn * 64 + lr) * RBL + ((lk ^ swz(lr)) << 4);
-  f32x4 acc[8][4];
+  const uint32_t b_lane = (wn * 16 * TN + lr) * RBL + ((lk ^ swz(lr)) << 4);
+  f32x4 acc[8][TN];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto stage_w = [&](int s, int& cc, int& t) {       // packed-weight tap of stage s, kx = -1
     int kz, ky;
@@ -259,11 +274,11 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
       const char* apl = smem + (kz + 1) * PLANE + a_lane;
       const int s0 = g2 * 3;
       one_stage(s0);
-      stage_body<WM, -1>(acc, ring + (s0 % NSTL) * BSLOT + b_lane, apl);
+      stage_body<TN, WM, -1>(acc, ring + (s0 % NSTL) * BSLOT + b_lane, apl);
       one_stage(s0 + 1);
-      stage_body<WM, 0>(acc, ring + ((s0 + 1) % NSTL) * BSLOT + b_lane, apl);
+      stage_body<TN, WM, 0>(acc, ring + ((s0 + 1) % NSTL) * BSLOT + b_lane, apl);
       one_stage(s0 + 2);
-      stage_body<WM, 1>(acc, ring + ((s0 + 2) % NSTL) * BSLOT + b_lane, apl);
+      stage_body<TN, WM, 1>(acc, ring + ((s0 + 2) % NSTL) * BSLOT + b_lane, apl);
     }
   };
   switch (wm) {
@@ -284,12 +299,12 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
     return (((int64_t)n * E + rz + d * tz) * E + ry + d * ty) * E + rx + d * tx;
   };
   u16* ctile = reinterpret_cast<u16*>(smem);
-  float cs[4], cq[4];
+  float cs[TN], cq[TN];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < TN; ++j) {
     cs[j] = 0.f;
     cq[j] = 0.f;
-    const int col = wn * 64 + j * 16 + lr;
+    const int col = wn * 16 * TN + j * 16 + lr;
     const float bv = bias != nullptr ? bias[n0 + col] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -307,7 +322,7 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
     }
   }
   __syncthreads();
-  constexpr int CPR = BNL / 8;
+  constexpr int CPR = BW / 8;
 #pragma unroll
   for (int hh = 0; hh < PL * CPR / NTHR; ++hh) {
     const int qd = tid + NTHR * hh;
@@ -321,7 +336,7 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   if (stats != nullptr) {
     float* red = reinterpret_cast<float*>(smem + PL * CROW);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < TN; ++j) {
       cs[j] += __shfl_xor(cs[j], 16, 64);
       cs[j] += __shfl_xor(cs[j], 32, 64);
       cq[j] += __shfl_xor(cq[j], 16, 64);
@@ -329,22 +344,22 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
     }
     if (wm > 0 && lk == 0) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = wn * 64 + j * 16 + lr;
-        red[(wm - 1) * 2 * BNL + col] = cs[j];
-        red[(wm - 1) * 2 * BNL + BNL + col] = cq[j];
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * 16 * TN + j * 16 + lr;
+        red[(wm - 1) * 2 * BW + col] = cs[j];
+        red[(wm - 1) * 2 * BW + BW + col] = cq[j];
       }
     }
     __syncthreads();
     if (wm == 0 && lk == 0) {
       const int mt = gid * S + tz;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = wn * 64 + j * 16 + lr;
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * 16 * TN + j * 16 + lr;
         float ss = cs[j], qs = cq[j];
         for (int w = 1; w < 4; ++w) {              // fixed order: deterministic
-          ss += red[(w - 1) * 2 * BNL + col];
-          qs += red[(w - 1) * 2 * BNL + BNL + col];
+          ss += red[(w - 1) * 2 * BW + col];
+          qs += red[(w - 1) * 2 * BW + BW + col];
         }
         stats[((int64_t)mt * 2) * g.Nd + n0 + col] = ss;
         stats[((int64_t)mt * 2 + 1) * g.Nd + n0 + col] = qs;
@@ -648,10 +663,10 @@ bool ok(const mmad_patch::Geo& q) {
   const int E = S * d;
   if (q.Ds != E || q.Hs != E || q.Ws != E || q.Dd != E || q.Hd != E || q.Wd != E) return false;
   if ((d * d * d) % NS) return false;
-  if (q.Cs % KC || q.Nd % BNL || q.Kpad != 27 * q.Cs) return false;
-  // one 512-thread block per CU: below 256 tiles the row-gather implicit GEMM (more, smaller
-  // blocks) is as fast (layer4.0.conv1 dgrad, 128 tiles: 237 vs 232 us)
-  if (lattice_mode() == 1 && mmad_lattice::tiles(q) * (q.Nd / BNL) < 256) return false;
+  if (q.Cs % KC || q.Nd % 64 || q.Kpad != 27 * q.Cs) return false;
+  // one 512-thread block per CU: tiles too few for the CUs even at 64 channels leave the
+  // row-gather implicit GEMM (more, smaller blocks) ahead
+  if (lattice_mode() == 1 && mmad_lattice::tiles(q) * (q.Nd / 64) < 256) return false;
   return (int64_t)q.nb * E * E * E * q.Cs < (int64_t(1) << 40);
 }
 
@@ -718,21 +733,30 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
 int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias,
         void* dst, float* stats, void* stream) {
   if (!mmad_lattice::ok(q)) return MMAD_EUNSUPPORTED;
-  static const bool attr = hipFuncSetAttribute((const void*)lattice_conv_kernel,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               LDS_BYTES) == hipSuccess;
+  static const bool attr =
+      hipFuncSetAttribute((const void*)lattice_conv_kernel<4>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
+      hipFuncSetAttribute((const void*)lattice_conv_kernel<2>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   if (!attr) return MMAD_EUNSUPPORTED;
+  // 128-channel tiles (4 MFMA columns per wave) when they give every CU a block, else 64
+  const bool wide = q.Nd % BNL == 0 && mmad_lattice::tiles(q) * (q.Nd / BNL) >= 256;
   LG g{};
   g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.Kpad = q.Kpad; g.d = q.dd;
   g.ngroups = q.nb * q.dd * q.dd * q.dd / NS;
-  g.nbn = q.Nd / BNL;
+  g.nbn = q.Nd / (wide ? BNL : 64);
   g.nchunk = q.Cs / KC;
   g.res = reinterpret_cast<const u16*>(q.res);
   g.relu = q.relu;
   const int64_t nblk = (int64_t)g.ngroups * S * g.nbn;
-  hipLaunchKernelGGL(lattice_conv_kernel, dim3((unsigned)nblk), dim3(NTHR), LDS_BYTES,
-                     as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                     stats);
+  if (wide)
+    hipLaunchKernelGGL(lattice_conv_kernel<4>, dim3((unsigned)nblk), dim3(NTHR), LDS_BYTES,
+                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
+                       stats);
+  else
+    hipLaunchKernelGGL(lattice_conv_kernel<2>, dim3((unsigned)nblk), dim3(NTHR), LDS_BYTES,
+                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
+                       stats);
   return launch_status();
 }
 

@@ -22,3 +22,7 @@ timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv \
   -- python3 tools/probe_dominant.py > $OUT/pmc_write.log 2>&1
 echo "pmc ok"
+python3 tools/prof_summary.py traffic $OUT/pmc_fetch $OUT/pmc_write > $OUT/traffic.json
+python3 tools/prof_summary.py stats $OUT/prof 40 > $OUT/stats.txt
+python3 tools/prof_summary.py step $OUT/prof > $OUT/step.txt
+echo "summaries ok"

@@ -64,7 +64,8 @@ def dominant(d, grid_x, name="igemm_kernel<unsigned short, 256, 0, 256"):
 def counter(d, name):
     rows = list(csv.DictReader(open(f"{d}/run_counter_collection.csv")))
     vals = [float(r["Counter_Value"]) for r in rows
-            if "igemm_kernel" in r["Kernel_Name"] and r["Counter_Name"] == name]
+            if ("igemm_kernel" in r["Kernel_Name"] or "lattice_conv_kernel" in r["Kernel_Name"])
+            and r["Counter_Name"] == name]
     return vals
 
 
@@ -74,7 +75,7 @@ def traffic(fetch_dir, write_dir):
     # rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB
     fb = statistics.median(f) * 1024 * 2
     wb = statistics.median(w) * 1024
-    return {"kernel": "igemm_kernel layer4.0.conv2 fwd (bf16, 8x512x16^3, 3^3 dil 4)",
+    return {"kernel": "lattice_conv_kernel layer4.0.conv2 fwd (bf16, 8x512x16^3, 3^3 dil 4)",
             "launches": [len(f), len(w)],
             "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
             "hbm_bytes_per_launch": fb + wb,
