@@ -238,6 +238,275 @@ __global__ __launch_bounds__(320) void stem_fwd_kernel(StemG g, const u16* __res
   }
 }
 
+// ---- forward, y-quad form ------------------------------------------------------------------
+// Two compute waves per SIMD and no loader wave: a block owns FOUR output rows x all 64
+// columns x 64 channels and walks its z range; wave w computes row w & 3, channels
+// 32 (w >> 2) .. +32.  Each wave keeps its 32 x 416 weight slice in registers (26 B
+// fragments), so the only LDS reads are the input rows (4 per 8 MFMAs), and the epilogue of
+// z-step oz-1 (bias, BN partial sums, bf16 stores) is spread over the MFMAs of z-step oz
+// (two accumulator sets).  (One wave per row with all 64 channels needs 208 VGPRs of
+// weights: the compiler then serialises every input read behind its MFMAs.)  The ring holds KD + 2*SD planes of 13 rows; every
+// wave issues the same number of plane DMAs (padding ones into a dummy row) and output
+// stores (buffer stores whose masked lanes fall outside the resource and are dropped) per
+// z-step, so one counted vmcnt wait covers "this step's planes have landed".
+constexpr int YQ = 4;                      // output rows per block (one per wave)
+constexpr int YINQ = (YQ - 1) * 2 + 7;     // input rows per plane
+constexpr int RZQ = 7 + 2 * 2;             // ring planes
+constexpr int PLQ = YINQ * ROWB;           // one plane in LDS
+constexpr int NKSQ = 13;                   // K-steps of 4 taps
+constexpr int NWQ = 8;                     // waves
+constexpr int DMAQ = 4;                    // plane-row DMAs per wave per z-step: 26 = 2x4 + 6x3
+constexpr int PROQ = 12;                   // prologue DMAs per wave (91 rows)
+constexpr int STQ = 4;                     // output stores (16 B) per wave per z-step
+constexpr uint32_t OOBQ = 0x40000000u;     // masked-lane store offset (past any resource)
+constexpr size_t LDSQ = (size_t)RZQ * PLQ + ROWB + 4 * 2 * CO * sizeof(float);
+
+template <bool BIAS>
+__global__ __launch_bounds__(512) void stem_fwdq_kernel(StemG g, const u16* __restrict__ U,
+                                                        const u16* __restrict__ wp,
+                                                        const float* __restrict__ bias,
+                                                        u16* __restrict__ y,
+                                                        float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem;
+  float* red = reinterpret_cast<float*>(smem + RZQ * PLQ + ROWB);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwg = gridDim.x, bid0 = blockIdx.x;
+  const int xcd = bid0 & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid0 >> 3);
+  const int zc = bid % g.nzc;
+  const int yb = (bid / g.nzc) % g.nyb;
+  const int nb = bid / (g.nzc * g.nyb);
+  const int oz0 = zc * g.zsteps;
+  const int oz1 = min(g.do_, oz0 + g.zsteps);
+  const int ybase = yb * YQ * 2 - g.ph;
+
+  // Padding rows read past the end of a buffer resource over this sample's U
+  // (the range check returns zeros without touching memory: a shared zero buffer would put
+  // every block's padding reads on one L2 channel)
+  const __amdgpu_buffer_rsrc_t rsu = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(U + (int64_t)nb * g.di * g.hi * g.wo * 8), 0,
+      (int)__builtin_amdgcn_readfirstlane(g.di * g.hi * g.wo * 16), 0x00020000);
+  auto load_row = [&](int zi, int slot, int t) __attribute__((always_inline)) {
+    const int yi = ybase + t;
+    bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi && lane < g.wo;
+#ifdef STEMQ_NO_DMA
+    ok = false;                                   // (experiment: no input traffic)
+#endif
+    const uint32_t voff = ok ? (uint32_t)(((zi * g.hi + yi) * g.wo + lane) * 16) : OOBQ;
+    buf_lds16_asm(voff, rsu, lds_addr_of(smem) + (uint32_t)(slot * PLQ + t * ROWB));
+  };
+  // the 2 new planes of z-step ozn: 26 rows over the 8 waves (waves 0-1: 4, others 3)
+  auto load_step = [&](int ozn) __attribute__((always_inline)) {
+    if (ozn >= oz1) return;
+#pragma unroll
+    for (int h = 0; h < DMAQ; ++h) {
+      const int f = wave + NWQ * h;
+      const int kd = 5 + f / YINQ;
+      if (f < 2 * YINQ) load_row(ozn * 2 - g.pd + kd, (ozn * 2 + kd) % RZQ, f % YINQ);
+    }
+  };
+  const size_t plane_out = (size_t)g.ho * g.wo * CO * 2;      // bytes of one output z-plane
+  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(y + (int64_t)nb * g.do_ * g.ho * g.wo * CO), 0,
+      (int)__builtin_amdgcn_readfirstlane((int)(plane_out * g.do_)), 0x00020000);
+  auto dummy_stores = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int e = 0; e < STQ; ++e)
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rsy, 2 * OOBQ + e * 16, 0, 0);
+  };
+  // vm ops this wave issues after the DMAs of step oz: the STQ stores of step oz-2's loop,
+  // step oz+1's DMAs (if that step exists), the STQ stores of step oz-1's loop.  The
+  // prologue mimics that sequence with dropped stores.
+  const int ndma = wave < 2 ? 4 : 3;
+  auto wait_planes = [&](int oz) __attribute__((always_inline)) {
+    if (oz + 1 >= oz1) wait_vm_lgkm0<2 * STQ>();
+    else if (ndma == 4) wait_vm_lgkm0<2 * STQ + 4>();
+    else wait_vm_lgkm0<2 * STQ + 3>();
+  };
+
+  // prologue: the 7 planes of the first z-step, then the next step's 2
+#pragma unroll 1
+  for (int h = 0; h < PROQ; ++h) {
+    const int f = wave + NWQ * h, kd = f / YINQ;
+    if (f < 7 * YINQ) load_row(oz0 * 2 - g.pd + kd, (oz0 * 2 + kd) % RZQ, f % YINQ);
+  }
+  dummy_stores();
+  load_step(oz0 + 1);
+  dummy_stores();
+
+  const int lr = lane & 15, lk = lane >> 4;
+  const int yl = wave & 3, ch = wave >> 2;
+  // weights: this wave's fragments for all 13 K-steps and its 2 channel tiles (104 VGPRs).
+  // Row m of tile j is channel ch*32 + (m >> 2)*8 + j*4 + (m & 3), so a lane's 4 + 4 results
+  // are 8 consecutive channels (one 16-byte store per voxel)
+  auto chan = [&](int j, int m) { return ch * 32 + (m >> 2) * 8 + j * 4 + (m & 3); };
+  bf16x8 fb[NKSQ][2];
+#pragma unroll
+  for (int s = 0; s < NKSQ; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      fb[s][j] = *reinterpret_cast<const bf16x8*>(wp + (int64_t)chan(j, lr) * g.kpad + 32 * s +
+                                                  8 * lk);
+  // A row of this lane at K-step s: tap t = 4s + lk = 7 kd + kh; kd is the step's first plane
+  // (4s / 7) or the next one, kh = (4s % 7) + lk - (next ? 7 : 0).  The last step's taps
+  // 48..51 all read tap 48 (weights past tap 49 are zero; a wrapped read could hit a plane
+  // still in flight or never written)
+  const uint32_t lane_a = (uint32_t)((yl * 2 + lk) * ROWB + lr * 16);
+  const uint32_t lane_l = (uint32_t)((yl * 2 + 6) * ROWB + lr * 16);
+  float bv[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = BIAS ? bias[chan(j, lk * 4 + r)] : 0.f;
+  const int oy = yb * YQ + yl;
+  const bool yok = oy < g.ho;
+  uint32_t so[4];
+  bool xok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int x = i * 16 + lr;
+    xok[i] = x < g.wo;
+    so[i] = yok && xok[i] ? (uint32_t)(((oy * g.wo + x) * CO + ch * 32 + lk * 8) * 2) : OOBQ;
+  }
+  float cs[2][4], cq[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { cs[j][r] = 0.f; cq[j][r] = 0.f; }
+
+  // epilogue of voxel group i of the previous step's accumulators (both channel tiles).
+  // Without bias the partial sums need no masking: the first step's P is zero, columns
+  // x >= wo read zero input rows, and a wave whose row is past ho never writes its sums.
+  // (Branch-free: a uniform branch here would split the MFMA schedule into small blocks.)
+  auto epi = [&](f32x4 (&P)[4][2], int i, bool live, uint32_t soff) __attribute__((always_inline)) {
+    float v[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[j][r] = P[i][j][r] + bv[j][r];
+        const float vs = BIAS ? (live && xok[i] ? v[j][r] : 0.f) : v[j][r];
+        cs[j][r] += vs;
+        cq[j][r] = fmaf(vs, vs, cq[j][r]);
+      }
+    const u32x4 pk{pack_bf16x2(v[0][0], v[0][1]), pack_bf16x2(v[0][2], v[0][3]),
+                   pack_bf16x2(v[1][0], v[1][1]), pack_bf16x2(v[1][2], v[1][3])};
+#ifdef STEMQ_NO_STORE
+    soff = OOBQ;                                  // (experiment: every store dropped)
+#endif
+    // (offset folded into the VGPR, soffset a literal 0: for a >8-byte MUBUF store with an
+    // SGPR soffset the compiler inserts no wait state before the data registers are
+    // rewritten, and on gfx950 the last lanes of the store then read the new values)
+    __builtin_amdgcn_raw_buffer_store_b128(pk, rsy, so[i] + soff, 0, 0);
+  };
+
+  // z-step oz into C while the epilogue of step oz-1 (P) drains
+  auto zstep = [&](f32x4 (&C)[4][2], f32x4 (&P)[4][2], int oz) __attribute__((always_inline)) {
+    wait_planes(oz);                               // planes of oz landed (all waves' ...)
+    raw_barrier();                                 // ... and step oz-1's reads are done
+    load_step(oz + 2);
+    const bool plive = oz > oz0;
+    const uint32_t psoff = plive ? (uint32_t)((oz - 1) * plane_out) : OOBQ;
+    const int sb = (oz * 2) % RZQ;
+    auto pbk = [&](int k) __attribute__((always_inline)) {
+      const int sl = sb + k;
+      return (uint32_t)((sl >= RZQ ? sl - RZQ : sl) * PLQ);
+    };
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) C[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // input fragments of K-step s (4 x 16 voxels), read one K-step ahead of their MFMAs
+    auto read_a = [&](int s, bf16x8 (&fa)[4]) __attribute__((always_inline)) {
+      const int kl = (4 * s) / 7, c = 7 * (kl + 1) - 4 * s;   // lanes lk >= c: next plane
+      uint32_t aoff;
+      if (s == NKSQ - 1) {
+        aoff = pbk(6) + lane_l;
+      } else if (c >= 4) {
+        aoff = pbk(kl) + lane_a + (uint32_t)((4 * s) % 7) * ROWB;
+      } else {
+        const uint32_t lo = pbk(kl) + (uint32_t)((4 * s) % 7) * ROWB;
+        const uint32_t hi = pbk(kl + 1) + (uint32_t)((4 * s) % 7) * ROWB - 7 * ROWB;
+        aoff = (lk >= c ? hi : lo) + lane_a;
+      }
+      const char* ap = ring + aoff;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ap + i * 256);
+    };
+    bf16x8 fa[2][4];
+    read_a(0, fa[0]);
+#pragma unroll
+    for (int s = 0; s < NKSQ; ++s) {
+      if (s + 1 < NKSQ) read_a(s + 1, fa[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#ifdef STEMQ_NO_MFMA
+      if (s == 0)                                 // (experiment: one K-step of MFMAs)
+#endif
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          C[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][j], fa[s & 1][i], C[i][j], 0,
+                                                            0, 0);
+      if (s >= 2 && s < 10 && (s & 1) == 0) epi(P, (s - 2) >> 1, plive, psoff);
+      // scheduling fence: the next step's reads stay ahead of this step's MFMAs (left
+      // alone, the scheduler serialises every read behind the MFMAs that consume it)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  f32x4 acc0[4][2], acc1[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int oz = oz0;
+#pragma unroll 1
+  for (; oz + 1 < oz1; oz += 2) {
+    zstep(acc0, acc1, oz);
+    zstep(acc1, acc0, oz + 1);
+  }
+  // the last step's epilogue (a plain tail: nothing waits on these stores)
+  if (oz < oz1) {
+    zstep(acc0, acc1, oz);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) epi(acc0, i, true, (uint32_t)(oz * plane_out));
+  } else if (oz > oz0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) epi(acc1, i, true, (uint32_t)((oz - 1) * plane_out));
+  }
+  wait_vm_lgkm0<0>();                              // (dummy DMAs into LDS before exit)
+
+  if (stats != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          cs[j][r] += __shfl_xor(cs[j][r], o, 64);
+          cq[j][r] += __shfl_xor(cq[j][r], o, 64);
+        }
+        if (lr == 0) {
+          red[(yl * 2) * CO + chan(j, lk * 4 + r)] = yok ? cs[j][r] : 0.f;
+          red[(yl * 2 + 1) * CO + chan(j, lk * 4 + r)] = yok ? cq[j][r] : 0.f;
+        }
+      }
+    __syncthreads();
+    if (tid < CO) {
+      float ss = 0.f, sq = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        ss += red[(w * 2) * CO + tid];
+        sq += red[(w * 2 + 1) * CO + tid];
+      }
+      stats[((int64_t)bid * 2) * CO + tid] = ss;
+      stats[((int64_t)bid * 2 + 1) * CO + tid] = sq;
+    }
+  }
+}
+
 // ---- stem weight gradient ----------------------------------------------------------------
 // dW[co][k] = sum over output voxels m of dY[m][co] * U(m, k), k = (kd*7 + kh)*8 + kw.
 // Same block walk as the forward (n, y-pair, z range; the U planes in an LDS ring), plus
@@ -388,7 +657,16 @@ __global__ __launch_bounds__(512) void stem_wgrad_kernel(StemG g, const u16* __r
     }
 }
 
-bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds) {
+// MMAD_STEM_QUAD=0 keeps the y-pair forward kernel (A/B switch)
+bool quad_on() {
+  static const bool on = [] {
+    const char* e = getenv("MMAD_STEM_QUAD");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
+bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds, bool quad = false) {
   if (d->ci != 1 || d->co != CO || d->kd != 7 || d->kh != 7 || d->kw > 8) return false;
   if (d->sd != 2 || d->sh != 2) return false;     // the instantiated form (MedicalNet)
   if (d->dd != 1 || d->dh != 1 || d->dw != 1 || d->wo > XW || d->wo < 1) return false;
@@ -403,10 +681,15 @@ bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds) {
   g.wrow = g.kpad * 2 + 16 * (int)(((10 - (g.kpad * 2 / 16)) % 16 + 16) % 16);
   g.rz = d->kd + g.sd;                           // planes of this and the next z-step
   g.rzf = d->kd + 2 * g.sd;                      // forward: and the one after
-  g.yin = (YT - 1) * g.sh + d->kh;
+  const int yt = quad ? YQ : YT;
+  g.yin = (yt - 1) * g.sh + d->kh;
   g.nks = (int)cdiv(ntap, 4);
   if (g.nks > 16 || g.kpad < g.nks * 32) return false;
-  g.nyb = (int)cdiv(g.ho, YT);
+  if (quad && ((int64_t)g.ho * g.wo * CO * 2 * g.do_ >= (int64_t(1) << 30) ||
+               (int64_t)g.di * g.hi * g.wo * 16 >= (int64_t(1) << 30) || g.rzf != RZQ ||
+               g.yin != YINQ || g.nks != NKSQ))
+    return false;
+  g.nyb = (int)cdiv(g.ho, yt);
   const int64_t base = (int64_t)g.n * g.nyb;
   g.nzc = (int)std::max<int64_t>(1, std::min<int64_t>(g.do_, cdiv(256, base)));
   g.zsteps = (int)cdiv(g.do_, g.nzc);
@@ -414,7 +697,7 @@ bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds) {
   g.ring_off = CO * g.wrow;
   g.c_off = g.ring_off + g.rzf * g.yin * ROWB;   // (no C tile: the epilogue stores directly)
   g.red_off = g.c_off;
-  lds = (size_t)g.red_off + 4 * 2 * CO * sizeof(float);
+  lds = quad ? LDSQ : (size_t)g.red_off + 4 * 2 * CO * sizeof(float);
   blocks = (int)(base * g.nzc);
   return lds <= 160 * 1024 && base * g.nzc < (int64_t(1) << 31);
 }
@@ -434,7 +717,8 @@ int64_t fwd_stats_rows(const mmad_conv_desc* d) {
   StemG g;
   int blocks;
   size_t lds;
-  if (!geom_for(d, g, blocks, lds)) return -1;
+  if (!(quad_on() && geom_for(d, g, blocks, lds, true)) && !geom_for(d, g, blocks, lds))
+    return -1;
   return blocks;                                 // one BN partial row per block
 }
 
@@ -468,6 +752,23 @@ int fwd(const mmad_conv_desc* d, const void* x_unf, const void* w_packed, const 
   StemG g;
   int blocks;
   size_t lds;
+  if (quad_on() && geom_for(d, g, blocks, lds, true)) {
+    static const bool okq =
+        hipFuncSetAttribute((const void*)stem_fwdq_kernel<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, LDSQ) == hipSuccess &&
+        hipFuncSetAttribute((const void*)stem_fwdq_kernel<true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, LDSQ) == hipSuccess;
+    if (!okq) return MMAD_EUNSUPPORTED;
+    if (bias != nullptr)
+      hipLaunchKernelGGL(stem_fwdq_kernel<true>, dim3((unsigned)blocks), dim3(512), LDSQ,
+                         as_stream(stream), g, (const u16*)x_unf, (const u16*)w_packed, bias,
+                         (u16*)y, stats);
+    else
+      hipLaunchKernelGGL(stem_fwdq_kernel<false>, dim3((unsigned)blocks), dim3(512), LDSQ,
+                         as_stream(stream), g, (const u16*)x_unf, (const u16*)w_packed, bias,
+                         (u16*)y, stats);
+    return launch_status();
+  }
   if (!geom_for(d, g, blocks, lds)) return MMAD_EUNSUPPORTED;
   static const bool ok = hipFuncSetAttribute((const void*)stem_fwd_kernel<7, 7, 2, 2>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
