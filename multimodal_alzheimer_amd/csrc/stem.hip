@@ -657,6 +657,189 @@ __global__ __launch_bounds__(512) void stem_wgrad_kernel(StemG g, const u16* __r
     }
 }
 
+// Same walk and output as stem_wgrad_kernel with the per-step address arithmetic hoisted:
+// every DMA of a wave has a fixed lane offset into a per-sample buffer resource that only
+// moves by a constant per z-step (padding rows fall past the resource and read zeros, so no
+// shared zero buffer and no per-row range checks), and every LDS fragment read is a
+// per-z-step base register plus an immediate.  The next K-step's fragments are read ahead
+// of the current MFMAs (fenced, so the scheduler keeps them there).
+template <int KD, int KH, int SD, int SH>
+__global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const u16* __restrict__ U,
+                                                          const u16* __restrict__ dy,
+                                                          float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int YIN = (YT - 1) * SH + KH, RSTEP = SD * YIN;
+  constexpr int DYB = YT * XW * CO * 2;
+  constexpr int NH = (RSTEP + 16 + 7) / 8;          // DMA slots per wave per step
+  constexpr uint32_t OOB = 0x80000000u;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwg = gridDim.x, bid0 = blockIdx.x;
+  const int xcd = bid0 & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid0 >> 3);
+  const int zc = bid % g.nzc;
+  const int yb = (bid / g.nzc) % g.nyb;
+  const int nb = bid / (g.nzc * g.nyb);
+  const int oz0 = zc * g.zsteps;
+  const int oz1 = min(g.do_, oz0 + g.zsteps);
+  const int ybase = yb * YT * SH - g.ph;
+  const uint32_t ring_l = lds_addr_of(smem), dyr_l = ring_l + (uint32_t)g.ring_off;
+
+  const __amdgpu_buffer_rsrc_t rsu = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(U + (int64_t)nb * g.di * g.hi * g.wo * 8), 0,
+      (int)__builtin_amdgcn_readfirstlane(g.di * g.hi * g.wo * 16), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(dy + (int64_t)nb * g.do_ * g.ho * g.wo * CO), 0,
+      (int)__builtin_amdgcn_readfirstlane(g.do_ * g.ho * g.wo * CO * 2), 0x00020000);
+  const uint32_t ustep = (uint32_t)(SD * g.hi * g.wo * 16), dstep = (uint32_t)(g.ho * g.wo * CO * 2);
+
+  // this wave's DMA slots h: f = wave + 8h; U rows of the step's SD new planes (f < RSTEP),
+  // then the 16 dY pieces (8 rows x 128 B each, chunk-swizzled for the transposing reads)
+  uint32_t voff[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int f = wave + 8 * h;
+    voff[h] = OOB;
+    if (f < RSTEP) {
+      const int kd = KD - SD + f / YIN, yi = ybase + f % YIN;
+      if ((unsigned)yi < (unsigned)g.hi && lane < g.wo)
+        voff[h] = (uint32_t)((((kd - g.pd) * g.hi + yi) * g.wo + lane) * 16);
+    } else if (f < RSTEP + 16) {
+      const int row = (f - RSTEP) * 8 + (lane >> 3);
+      const int x = row & 63, yy = yb * YT + (row >> 6);
+      const int ch = (lane & 7) ^ dswz(row);
+      if (x < g.wo && yy < g.ho) voff[h] = (uint32_t)(((yy * g.wo + x) * CO + ch * 8) * 2);
+    }
+  }
+  auto load_step = [&](int ozn) __attribute__((always_inline)) {
+    int sbn = (ozn * SD) % g.rz;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int f = wave + 8 * h;
+      if (f < RSTEP) {
+        int slot = sbn + KD - SD + f / YIN;
+        slot -= slot >= g.rz ? g.rz : 0;
+        buf_lds16_asm(voff[h] + (uint32_t)ozn * ustep, rsu,
+                      ring_l + (uint32_t)((slot * YIN + f % YIN) * ROWB_W));
+      } else if (f < RSTEP + 16) {
+        buf_lds16_asm(voff[h] + (uint32_t)ozn * dstep, rsd,
+                      dyr_l + (uint32_t)((ozn & 1) * DYB + (f - RSTEP) * 1024));
+      }
+    }
+  };
+  if (oz0 < oz1) {
+    // prologue: the first step's KD - SD older planes (generic addressing, once)
+#pragma unroll 1
+    for (int f = wave; f < (KD - SD) * YIN; f += 8) {
+      const int kd = f / YIN, zi = oz0 * SD - g.pd + kd, yi = ybase + f % YIN;
+      const bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi &&
+                      lane < g.wo;
+      buf_lds16_asm(ok ? (uint32_t)(((zi * g.hi + yi) * g.wo + lane) * 16) : OOB, rsu,
+                    ring_l + (uint32_t)((((oz0 * SD + kd) % g.rz) * YIN + f % YIN) * ROWB_W));
+    }
+    load_step(oz0);
+  }
+
+  // compute wave w: channels [32*(w&1), +32), k columns [112*(w>>1), +112) = 14 taps
+  const int q = (lane & 15) >> 2, p = lane & 3, lk = lane >> 4;
+  const int wc = wave & 1, wk = wave >> 1;
+  // U fragment of k-tile j: tap t_j = 2*(7 wk + j) + (p >> 1) = 7 kd_j + kh_j; the lane's
+  // row offset in its plane (kh_j row, kw half, voxel x = 8 lk + q of the K-step's 32)
+  int kdj[7];
+  uint32_t rowj[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int t = min(2 * (7 * wk + j) + (p >> 1), KD * KH - 1);
+    kdj[j] = t / KH;
+    rowj[j] = (uint32_t)((t % KH) * ROWB_W + (p & 1) * 8 + (8 * lk + q) * 16);
+  }
+  // dY^T fragment of co tile i: rows r0 = 32 ks + 8 lk + q (and r0 + 4), swizzled chunk
+  uint32_t dlo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int col = wc * 32 + i * 16 + 4 * p, r0 = 8 * lk + q;
+    dlo[i] = (uint32_t)(r0 * 128 + (((col >> 3) ^ dswz(r0)) << 4) + (col & 7) * 2);
+  }
+  f32x4 acc[2][7];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 1
+  for (int oz = oz0; oz < oz1; ++oz) {
+    wait_vm_lgkm0<0>();                            // this wave's DMAs for oz landed
+    raw_barrier();                                 // ... and everyone's; step oz-1 done
+#ifndef STEMW_NO_DMA
+    if (oz + 1 < oz1) load_step(oz + 1);          // lands while the MFMAs of oz run
+#endif
+    const int sbase = (oz * SD) % g.rz;
+    const char* dyt = smem + g.ring_off + (oz & 1) * DYB;
+    const char* pl[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      int slot = sbase + kdj[j];
+      slot -= slot >= g.rz ? g.rz : 0;
+      pl[j] = smem + slot * YIN * ROWB_W + rowj[j];
+    }
+    auto rd = [&](const char* a) __attribute__((always_inline)) {
+      return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)a);
+    };
+    auto read_k = [&](int ks, bf16x8 (&fa)[2], bf16x8 (&fb)[7]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const char* a = dyt + dlo[i] + ks * 32 * 128;
+        fa[i] = __builtin_shufflevector(rd(a), rd(a + 4 * 128), 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        const char* b = pl[j] + (ks >> 1) * SH * ROWB_W + (ks & 1) * 32 * 16;
+        fb[j] = __builtin_shufflevector(rd(b), rd(b + 4 * 16), 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    };
+    bf16x8 fa[2][2], fb[2][7];
+    read_k(0, fa[0], fb[0]);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks + 1 < 4) read_k(ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#ifdef STEMW_NO_MFMA
+      if (ks == 0)                                // (experiment: one K-step of MFMAs)
+#endif
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 7; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks & 1][i], fb[ks & 1][j],
+                                                              acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // this block's partial slab: ws[bid][co][k], k < 392
+  float* out = ws + (int64_t)bid * CO * WK;
+  const int lr = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int k = wk * WKW + j * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = wc * 32 + i * 16 + lk * 4 + r;
+        if (k < WK) out[(int64_t)co * WK + k] = acc[i][j][r];
+      }
+    }
+}
+
+// MMAD_STEM_WG2=0 keeps the first stem weight-gradient kernel (A/B switch)
+bool wg2_on() {
+  static const bool on = [] {
+    const char* e = getenv("MMAD_STEM_WG2");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
 // MMAD_STEM_QUAD=0 keeps the y-pair forward kernel (A/B switch)
 bool quad_on() {
   static const bool on = [] {
@@ -740,10 +923,20 @@ int wgrad(const mmad_conv_desc* d, const void* x_unf, const void* dy, float* ws,
   const size_t wl = (size_t)g.ring_off + 2 * YT * XW * CO * 2;
   static const bool ok = hipFuncSetAttribute((const void*)stem_wgrad_kernel<7, 7, 2, 2>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             160 * 1024) == hipSuccess &&
+                         hipFuncSetAttribute((const void*)stem_wgrad2_kernel<7, 7, 2, 2>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
                                              160 * 1024) == hipSuccess;
   if (!ok || wl > 160 * 1024) return MMAD_EUNSUPPORTED;
-  hipLaunchKernelGGL((stem_wgrad_kernel<7, 7, 2, 2>), dim3((unsigned)blocks), dim3(512), wl,
-                     as_stream(stream), g, (const u16*)x_unf, (const u16*)dy, ws);
+  // (the hoisted form's buffer offsets are 32-bit)
+  const bool small = (int64_t)g.di * g.hi * g.wo * 16 < (int64_t(1) << 30) &&
+                     (int64_t)g.do_ * g.ho * g.wo * CO * 2 < (int64_t(1) << 30);
+  if (wg2_on() && small)
+    hipLaunchKernelGGL((stem_wgrad2_kernel<7, 7, 2, 2>), dim3((unsigned)blocks), dim3(512), wl,
+                       as_stream(stream), g, (const u16*)x_unf, (const u16*)dy, ws);
+  else
+    hipLaunchKernelGGL((stem_wgrad_kernel<7, 7, 2, 2>), dim3((unsigned)blocks), dim3(512), wl,
+                       as_stream(stream), g, (const u16*)x_unf, (const u16*)dy, ws);
   return launch_status();
 }
 
