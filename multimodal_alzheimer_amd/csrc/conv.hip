@@ -903,7 +903,7 @@ __global__ __launch_bounds__(256) void pack_transpose_kernel(const float* __rest
 template <typename T>
 __global__ __launch_bounds__(256) void pack_batch_kernel(const mmad_pack_job* __restrict__ jobs,
                                                          int njobs) {
-  __shared__ float tile[128 * 33 > 64 * 65 ? 128 * 33 : 64 * 65];
+  __shared__ float tile[128 * 33];            // >= 64 x 65 and 32 x 129 (column-major)
   // job lookup: last job with tile0 <= blockIdx.x (jobs sorted by tile0)
   int lo = 0, hi = njobs - 1;
   const int64_t bid = blockIdx.x;
@@ -924,6 +924,33 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const mmad_pack_job* __
   const float* src = jb.w + (int64_t)b * R * Cc;
   T* wp = reinterpret_cast<T*>(jb.w_packed);
   const int cl = threadIdx.x & (TC - 1), rl = threadIdx.x / TC, rstep = 256 / TC;
+  // bf16 with 8-row groups inside one packed block: the tile is kept column-major and each
+  // thread stores 8 consecutive rows as one 16-byte vector (2-byte stores made this kernel
+  // store-issue bound)
+  const bool vec = sizeof(T) == 2 && jb.rdiv % 8 == 0 && (jb.ostride_b | jb.ostride_j1 | oj2) % 8 == 0;
+  if (vec) {
+    const int LDT = TR + 1;
+    for (int r = rl; r < TR; r += rstep) {
+      const int i = i0 + r, j = j0 + cl;
+      tile[cl * LDT + r] = (i < R && j < Cc) ? src[(int64_t)i * Cc + j] : 0.f;
+    }
+    __syncthreads();
+    const int RG = TR / 8;
+    for (int it = threadIdx.x; it < RG * TC; it += 256) {
+      const int rg = it % RG, c = it / RG;
+      const int i = i0 + rg * 8, j = j0 + c;
+      if (i >= R || j >= Cc) continue;           // (R is a multiple of 8: rdiv % 8 == 0)
+      const float* tp = tile + c * LDT + rg * 8;
+      u32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = pack_bf16x2(tp[2 * e], tp[2 * e + 1]);
+      const int64_t o = (int64_t)(b * (R / rdiv) + i / rdiv) * jb.ostride_b + i % rdiv +
+                        (int64_t)(j / jd) * jb.ostride_j1 +
+                        (int64_t)(jb.pad_ ? jd - 1 - j % jd : j % jd) * oj2;
+      *reinterpret_cast<u32x4*>(wp + o) = v;
+    }
+    return;
+  }
   for (int r = rl; r < TR; r += rstep) {
     const int i = i0 + r, j = j0 + cl;
     tile[r * LD + cl] = (i < R && j < Cc) ? src[(int64_t)i * Cc + j] : 0.f;
