@@ -220,18 +220,25 @@ __device__ __forceinline__ void sum_parts(int c, int C, int nparts, const float*
       q += parts[((int64_t)p * 2 + 1) * C + c];
     }
   }
-  sm[threadIdx.x] = s;
-  sm[1024 + threadIdx.x] = q;
-  __syncthreads();
-  for (int half = 32; half >= 1; half >>= 1) {
-    if (py < half) {
-      sm[threadIdx.x] += sm[threadIdx.x + half * FC];
-      sm[1024 + threadIdx.x] += sm[1024 + threadIdx.x + half * FC];
-    }
-    __syncthreads();
+  // the 4 part lanes of a channel inside one wave (lane bits 4-5) by shuffles, then the 16
+  // waves through LDS: one barrier instead of a six-level tree (this kernel is latency-bound)
+  s += __shfl_xor(s, 16, 64);
+  q += __shfl_xor(q, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  q += __shfl_xor(q, 32, 64);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < FC) {
+    sm[w * FC + cx] = s;
+    sm[1024 + w * FC + cx] = q;
   }
-  S = sm[cx];
-  Q = sm[1024 + cx];
+  __syncthreads();
+  S = 0.0;
+  Q = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {                 // fixed order: deterministic
+    S += sm[k * FC + cx];
+    Q += sm[1024 + k * FC + cx];
+  }
 }
 
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(

@@ -507,75 +507,19 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
   auto tr_off = [&](int rowb, int r, int col, int sw) -> uint32_t {
     return (uint32_t)(r * rowb + ((((col >> 3) ^ sw)) << 4) + (col & 7) * 2);
   };
-  uint32_t ya_lo[2][4], ya_hi[2][4];
+  // (the second position's rows are NS further: same swizzle, a constant offset)
+  uint32_t ya_lo[4], ya_hi[4];
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r0 = q * NS + rsel, col = i * 16 + 4 * p4;
-      ya_lo[q][i] = tr_off(WYROW, r0, col, wsz128(r0));
-      ya_hi[q][i] = tr_off(WYROW, r0 + 4, col, wsz128(r0 + 4));
-    }
+  for (int i = 0; i < 4; ++i) {
+    const int col = i * 16 + 4 * p4;
+    ya_lo[i] = tr_off(WYROW, rsel, col, wsz128(rsel));
+    ya_hi[i] = tr_off(WYROW, rsel + 4, col, wsz128(rsel + 4));
+  }
   const uint32_t xb_lo = tr_off(WXROW, rsel, cf * 16 + 4 * p4, wsz64(rsel));
   const uint32_t xb_hi = tr_off(WXROW, rsel + 4, cf * 16 + 4 * p4, wsz64(rsel + 4));
-  int dk[7];
-  uint32_t pmask[7], zmask[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const int t = min(t0 + k, 26);
-    const int kz = t / 9 - 1, ky = (t / 3) % 3 - 1, kx = t % 3 - 1;
-    dk[k] = kz * WPLANE + (ky * S + kx) * NS * WXROW;
-    uint32_t pm = 0, zm = 0;
-    for (int pq = 0; pq < S * S; ++pq) {
-      const int sy = pq / S + ky, sx = pq % S + kx;
-      if ((unsigned)sy < (unsigned)S && (unsigned)sx < (unsigned)S) pm |= 1u << pq;
-    }
-    for (int z = 0; z < S; ++z)
-      if ((unsigned)(z + kz) < (unsigned)S) zm |= 1u << z;
-    pmask[k] = k < nt ? (uint32_t)__builtin_amdgcn_readfirstlane(pm) : 0u;
-    zmask[k] = (uint32_t)__builtin_amdgcn_readfirstlane(zm);
-    dk[k] = __builtin_amdgcn_readfirstlane(dk[k]);
-  }
   auto tr8 = [](const char* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p);
   };
-  // one K step = output position POS (compile time) of the current plane: fragment reads
-  // (MFMAs separately); vm[k] = the positions where tap k is inside the sub-lattice on this
-  // plane (0 for the padding planes and for a wave's unused 7th tap slot)
-  struct WFr { bf16x8 a[4], b[7]; };
-  uint32_t vm[7];
-  int pbase = 0;                                    // plane tz's X offset in the ring
-  auto kread = [&](const char* yimg, auto qc, auto posc, WFr& f) {
-    constexpr int Q = decltype(qc)::value, POS = decltype(posc)::value;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      f.a[i] = __builtin_shufflevector(tr8(yimg + ya_lo[Q][i]), tr8(yimg + ya_hi[Q][i]),
-                                       0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      const bool ok = (vm[k] >> POS) & 1u;
-      const char* img = smem + (ok ? pbase + POS * NS * WXROW + dk[k] : WZERO_OFF);
-      f.b[k] = __builtin_shufflevector(tr8(img + xb_lo), tr8(img + xb_hi), 0, 1, 2, 3, 4, 5, 6, 7);
-    }
-  };
-  // MFMAs of a K step; a tap outside the sub-lattice (its reads came from the zero block)
-  // is skipped by a uniform branch -- the reads stay unconditional so the LDS counter
-  // waits before each MFMA group remain exact
-  auto kmma = [&](const WFr& f, auto posc) {
-    constexpr int POS = decltype(posc)::value;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-#ifndef LAT_WG_DENSE
-      if ((vm[k] >> POS) & 1u)
-#endif
-      {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[k], acc[i][k], 0, 0, 0);
-      }
-    }
-  };
-
   // dY of stage (plane o, pair m) into ring slot sl
   auto issue_y_at = [&](int64_t plane_vox0, int m, int sl) {
     const u16* base = dy + (plane_vox0 + (int64_t)d * (m / 2) * E + 2 * d * (m % 2)) * g.Nd;
@@ -588,44 +532,118 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
   issue_x(1);
   issue_y_at(plane_y0(0), 0, 0);
   issue_y_at(plane_y0(0), 1, 1);
-  for (int o = 0; o < nplane_out; ++o) {
-    const int tz = o % S;
-    const bool xnow = o + 2 < nplane_out;           // X plane o + 2 issued at stage 0
-    pbase = tz * WPLANE;
-#pragma unroll
-    for (int k = 0; k < 7; ++k)
-      vm[k] = ((zmask[k] >> tz) & 1u) ? pmask[k] : 0u;
-    const int64_t y_here = plane_y0(o);
-    const int64_t y_next = o + 1 < nplane_out ? plane_y0(o + 1) : y_here;
-    const int sl0 = (o * 8) % WYSLOTS;
-    auto stage = [&](auto mc) {
-      constexpr int M = decltype(mc)::value;
-      const int sl = (sl0 + M) % WYSLOTS;
-      // dY of this stage landed (issued two stages ago); younger: the next stage's dY and,
-      // at stages 1 and 2, the X plane issued at stage 0 right after stage 2's dY
-      const bool last = o + 1 == nplane_out && M == 7;
-      if ((M == 1 || M == 2) && xnow) wait_vm_lgkm0<5>();
-      else if (last) wait_vm_lgkm0<0>();
-      else wait_vm_lgkm0<1>();
-      raw_barrier();
-      if (M < 6) issue_y_at(y_here, M + 2, (sl + 2) % WYSLOTS);
-      else if (o + 1 < nplane_out) issue_y_at(y_next, M - 6, (sl + 2) % WYSLOTS);
-      if (M == 0 && xnow) issue_x(o + 2);
-      const char* yimg = smem + WY_OFF + sl * WYST;
-      WFr f0, f1;
-      kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, f0);
-      kread(yimg, std::integral_constant<int, 1>{}, std::integral_constant<int, 2 * M + 1>{}, f1);
-      kmma(f0, std::integral_constant<int, 2 * M>{});
-      kmma(f1, std::integral_constant<int, 2 * M + 1>{});
+
+  // The wave's tap group TG is a compile-time constant of its code path, and so is each
+  // K step's position: a tap whose (y, x) shift leaves the sub-lattice at that position has
+  // neither fragment reads nor MFMAs (no branches in the MFMA stream, 31 % fewer X reads).
+  // A tap whose z shift leaves it (first / last plane of a sub group) reads the zero block
+  // and its MFMAs add exact zeros.
+  struct WFr { bf16x8 a[4], b[7]; };
+  auto run = [&](auto tgc) {
+    constexpr int TG = decltype(tgc)::value;
+    constexpr int NT = TG == 3 ? 6 : 7;
+    auto yx_on = [](auto kc, auto posc) constexpr {
+      constexpr int K = decltype(kc)::value, POS = decltype(posc)::value;
+      constexpr int t = TG * 7 + K;
+      constexpr int ky = (t / 3) % 3 - 1, kx = t % 3 - 1;
+      constexpr int py = POS / S + ky, px = POS % S + kx;
+      return K < NT && py >= 0 && py < S && px >= 0 && px < S;
     };
-    stage(std::integral_constant<int, 0>{});
-    stage(std::integral_constant<int, 1>{});
-    stage(std::integral_constant<int, 2>{});
-    stage(std::integral_constant<int, 3>{});
-    stage(std::integral_constant<int, 4>{});
-    stage(std::integral_constant<int, 5>{});
-    stage(std::integral_constant<int, 6>{});
-    stage(std::integral_constant<int, 7>{});
+    bool zok[7];
+    int pbase = 0;                                  // plane tz's X offset in the ring
+    auto kread = [&](const char* yimg, auto qc, auto posc, WFr& f) {
+      constexpr int Q = decltype(qc)::value, POS = decltype(posc)::value;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        f.a[i] = __builtin_shufflevector(tr8(yimg + Q * NS * WYROW + ya_lo[i]),
+                                         tr8(yimg + Q * NS * WYROW + ya_hi[i]), 0, 1, 2, 3, 4,
+                                         5, 6, 7);
+      auto one = [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        if constexpr (yx_on(kc, posc)) {
+          constexpr int t = TG * 7 + K;
+          constexpr int dk = (t / 9 - 1) * WPLANE + (((t / 3) % 3 - 1) * S + t % 3 - 1) * NS * WXROW +
+                             POS * NS * WXROW;
+          const char* img = smem + (zok[K] ? pbase + dk : WZERO_OFF);
+          f.b[K] = __builtin_shufflevector(tr8(img + xb_lo), tr8(img + xb_hi), 0, 1, 2, 3, 4, 5,
+                                           6, 7);
+        }
+      };
+      one(std::integral_constant<int, 0>{});
+      one(std::integral_constant<int, 1>{});
+      one(std::integral_constant<int, 2>{});
+      one(std::integral_constant<int, 3>{});
+      one(std::integral_constant<int, 4>{});
+      one(std::integral_constant<int, 5>{});
+      one(std::integral_constant<int, 6>{});
+    };
+    auto kmma = [&](const WFr& f, auto posc) {
+      auto one = [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        if constexpr (yx_on(kc, posc)) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i][K] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[K], acc[i][K], 0, 0,
+                                                                0);
+        }
+      };
+      one(std::integral_constant<int, 0>{});
+      one(std::integral_constant<int, 1>{});
+      one(std::integral_constant<int, 2>{});
+      one(std::integral_constant<int, 3>{});
+      one(std::integral_constant<int, 4>{});
+      one(std::integral_constant<int, 5>{});
+      one(std::integral_constant<int, 6>{});
+    };
+
+    for (int o = 0; o < nplane_out; ++o) {
+      const int tz = o % S;
+      const bool xnow = o + 2 < nplane_out;         // X plane o + 2 issued at stage 0
+      pbase = tz * WPLANE;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const int kz = (TG * 7 + k) / 9 - 1;
+        zok[k] = (unsigned)(tz + kz) < (unsigned)S;
+      }
+      const int64_t y_here = plane_y0(o);
+      const int64_t y_next = o + 1 < nplane_out ? plane_y0(o + 1) : y_here;
+      const int sl0 = (o * 8) % WYSLOTS;
+      auto stage = [&](auto mc) {
+        constexpr int M = decltype(mc)::value;
+        const int sl = (sl0 + M) % WYSLOTS;
+        // dY of this stage landed (issued two stages ago); younger: the next stage's dY and,
+        // at stages 1 and 2, the X plane issued at stage 0 right after stage 2's dY
+        const bool last = o + 1 == nplane_out && M == 7;
+        if ((M == 1 || M == 2) && xnow) wait_vm_lgkm0<5>();
+        else if (last) wait_vm_lgkm0<0>();
+        else wait_vm_lgkm0<1>();
+        raw_barrier();
+        if (M < 6) issue_y_at(y_here, M + 2, (sl + 2) % WYSLOTS);
+        else if (o + 1 < nplane_out) issue_y_at(y_next, M - 6, (sl + 2) % WYSLOTS);
+        if (M == 0 && xnow) issue_x(o + 2);
+        const char* yimg = smem + WY_OFF + sl * WYST;
+        WFr f0, f1;
+        kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, f0);
+        kread(yimg, std::integral_constant<int, 1>{}, std::integral_constant<int, 2 * M + 1>{},
+              f1);
+        kmma(f0, std::integral_constant<int, 2 * M>{});
+        kmma(f1, std::integral_constant<int, 2 * M + 1>{});
+      };
+      stage(std::integral_constant<int, 0>{});
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
+      stage(std::integral_constant<int, 4>{});
+      stage(std::integral_constant<int, 5>{});
+      stage(std::integral_constant<int, 6>{});
+      stage(std::integral_constant<int, 7>{});
+    }
+  };
+  switch (tg) {                                     // wave-uniform
+    case 0: run(std::integral_constant<int, 0>{}); break;
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    default: run(std::integral_constant<int, 3>{}); break;
   }
 
   // partial slab [split][co][tap * Cs + ci]

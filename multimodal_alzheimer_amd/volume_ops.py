@@ -489,7 +489,7 @@ def _finalize(y, parts, bn, training):
             parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
             L.call("mmad_bn_stats", L.dtype_code(y.dtype), m, c, L.ptr(y), L.ptr(parts),
                    L.stream())
-        if parts.shape[0] > 1024:        # conv-epilogue partials: one row per 128 voxels
+        if parts.shape[0] > 4096:        # conv-epilogue partials: one row per tile
             group = -(-parts.shape[0] // 512)
             folded = torch.empty((-(-parts.shape[0] // group), 2, c), dtype=torch.float32,
                                  device=dev)

@@ -1,10 +1,12 @@
 #!/bin/bash
-# rocprof kernel trace of a short bench run + per-step kernel table (one step, in order)
+# Kernel stats + one step's kernel table of the bench (no tests, no PMC).
+#   gpurun -- bash tools/prof_step.sh <tag>
 set -e -o pipefail
-T=${1:-ps}
+OUT=gpurun_out/${1:-step}
+mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/$T
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/$T/prof -o run --output-format csv \
-  -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/$T/prof.log 2>&1
-python3 tools/prof_summary.py stats gpurun_out/$T/prof 60
-python3 tools/prof_summary.py step gpurun_out/$T/prof > gpurun_out/$T/step.txt
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv \
+  -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof.log 2>&1
+python3 tools/prof_summary.py stats $OUT/prof 40 > $OUT/stats.txt
+python3 tools/prof_summary.py step $OUT/prof > $OUT/step.txt
+python3 tools/step_breakdown.py $OUT/step.txt
