@@ -80,6 +80,23 @@ typedef struct mmad_pack_job {
 int mmad_conv_pack_job(const mmad_conv_desc* d, int dtype, int for_dgrad, const float* w,
                        void* w_packed, int64_t tile0, mmad_pack_job* job);
 int64_t mmad_pack_job_tiles(const mmad_pack_job* job);
+/* Both bf16 layouts of one conv weight from a single read (16 co x 16 ci x taps tiles):
+ * forward [co][tap][ci] into w_fwd and input-gradient [ci][tap'][co] into w_dgrad (tap'
+ * reversed when the dgrad runs as a forward conv), bit-identical to two
+ * mmad_conv_pack_weight calls.  MMAD_EUNSUPPORTED unless both layouts are unpadded and
+ * ci, co are multiples of 16 (bf16 only). */
+typedef struct mmad_pack_dual {
+  const float* w;
+  void* w_fwd;
+  void* w_dgrad;
+  int32_t co, ci, taps, flip;
+  int64_t tile0;
+} mmad_pack_dual;
+int mmad_conv_pack_dual_job(const mmad_conv_desc* d, int dtype, const float* w, void* w_fwd,
+                            void* w_dgrad, int64_t tile0, mmad_pack_dual* job);
+int64_t mmad_pack_dual_tiles(const mmad_pack_dual* job);
+int mmad_conv_pack_dual_batch(int dtype, int njobs, const mmad_pack_dual* jobs_device,
+                              int64_t total_tiles, void* stream);
 int mmad_conv_pack_batch(int dtype, int njobs, const mmad_pack_job* jobs_device,
                          int64_t total_tiles, void* stream);
 int64_t mmad_conv_unfolded_elems(const mmad_conv_desc* d);

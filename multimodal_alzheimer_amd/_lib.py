@@ -38,8 +38,15 @@ class PackJob(C.Structure):
                 [(n, C.c_int64) for n in ("ostride_b", "ostride_j1", "tile0")])
 
 
+class PackDual(C.Structure):
+    """mirror of mmad_pack_dual (include/mmad.h)"""
+    _fields_ = ([("w", C.c_void_p), ("w_fwd", C.c_void_p), ("w_dgrad", C.c_void_p)] +
+                [(n, C.c_int32) for n in ("co", "ci", "taps", "flip")] + [("tile0", C.c_int64)])
+
+
 _P = C.POINTER(ConvDesc)
 _PJ = C.POINTER(PackJob)
+_PD = C.POINTER(PackDual)
 _SIGS = {
     "mmad_abi_version": (_i32, []),
     "mmad_strerror": (C.c_char_p, [_i32]),
@@ -48,6 +55,9 @@ _SIGS = {
     "mmad_conv_pack_job": (_i32, [_P, _i32, _i32, _vp, _vp, _i64, _PJ]),
     "mmad_pack_job_tiles": (_i64, [_PJ]),
     "mmad_conv_pack_batch": (_i32, [_i32, _i32, _vp, _i64, _vp]),
+    "mmad_conv_pack_dual_job": (_i32, [_P, _i32, _vp, _vp, _vp, _i64, _PD]),
+    "mmad_pack_dual_tiles": (_i64, [_PD]),
+    "mmad_conv_pack_dual_batch": (_i32, [_i32, _i32, _vp, _i64, _vp]),
     "mmad_conv_unfolded_elems": (_i64, [_P]),
     "mmad_conv_unfold_input": (_i32, [_P, _i32, _vp, _i32, _vp, _vp]),
     "mmad_conv3d_stats_rows": (_i64, [_P, _i32]),

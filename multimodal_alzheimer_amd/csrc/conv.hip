@@ -969,6 +969,59 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const mmad_pack_job* __
   }
 }
 
+// Dual-layout pack (mmad_conv_pack_dual_batch): one 16 co x 16 ci x taps tile per block,
+// read once (rows of taps*16 contiguous floats per co) into LDS [co][tap][ci | pad], then
+// written as 16-byte bf16 vectors of 8 ci (forward rows) and of 8 co (dgrad rows).
+__global__ __launch_bounds__(256) void pack_dual_kernel(const mmad_pack_dual* __restrict__ jobs,
+                                                        int njobs) {
+  __shared__ float tile[16 * 27 * 17];
+  int lo = 0, hi = njobs - 1;
+  const int64_t bid = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].tile0 <= bid) lo = mid; else hi = mid - 1;
+  }
+  const mmad_pack_dual& jb = jobs[lo];
+  const int T = jb.taps, CI = jb.ci, CO = jb.co;
+  const int t = (int)(bid - jb.tile0), nci = CI / 16;
+  const int co0 = (t / nci) * 16, ci0 = (t % nci) * 16;
+  const int per_co = 16 * T, q4 = per_co / 4;    // a co's tile row: 16*T contiguous floats
+  for (int e = threadIdx.x; e < 16 * q4; e += 256) {
+    const int col = e / q4, rem0 = (e % q4) * 4;
+    const f32x4 v =
+        *reinterpret_cast<const f32x4*>(jb.w + ((int64_t)(co0 + col) * CI + ci0) * T + rem0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rem = rem0 + q, cil = rem / T, tap = rem % T;
+      tile[(col * T + tap) * 17 + cil] = v[q];
+    }
+  }
+  __syncthreads();
+  u16* wf = reinterpret_cast<u16*>(jb.w_fwd);
+  u16* wd = reinterpret_cast<u16*>(jb.w_dgrad);
+  const int items = 16 * T * 2;
+  for (int e = threadIdx.x; e < 2 * items; e += 256) {
+    const int it = e % items, half = it & 1, rest = it >> 1;
+    u32x4 v;
+    if (e < items) {                               // forward: [co][tap][ci]
+      const int col = rest / T, tap = rest % T;
+      const float* tp = tile + (col * T + tap) * 17 + half * 8;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = pack_bf16x2(tp[2 * q], tp[2 * q + 1]);
+      *reinterpret_cast<u32x4*>(wf + (int64_t)(co0 + col) * T * CI + (int64_t)tap * CI + ci0 +
+                                half * 8) = v;
+    } else {                                       // dgrad: [ci][tap'][co]
+      const int cil = rest / T, tap = rest % T;
+      const int tq = jb.flip ? T - 1 - tap : tap;
+      const float* tp = tile + ((half * 8) * T + tap) * 17 + cil;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = pack_bf16x2(tp[(2 * q) * T * 17], tp[(2 * q + 1) * T * 17]);
+      *reinterpret_cast<u32x4*>(wd + (int64_t)(ci0 + cil) * T * CO + (int64_t)tq * CO + co0 +
+                                half * 8) = v;
+    }
+  }
+}
+
 template <typename TI, typename TO>
 __global__ void unfold_w_kernel(const TI* __restrict__ x, TO* __restrict__ xu, int64_t rows,
                                 int Wi, int Wo, int KW, int sw, int pw, int dw) {
@@ -1410,6 +1463,43 @@ int mmad_conv_pack_job(const mmad_conv_desc* d, int dtype, int for_dgrad, const 
   j.tile0 = tile0;
   *job = j;
   return MMAD_OK;
+}
+
+int mmad_conv_pack_dual_job(const mmad_conv_desc* d, int dtype, const float* w, void* w_fwd,
+                            void* w_dgrad, int64_t tile0, mmad_pack_dual* job) {
+  if (!desc_ok(d)) return MMAD_EBADSHAPE;
+  if (dtype != MMAD_BF16) return MMAD_EUNSUPPORTED;
+  if (!w || !w_fwd || !w_dgrad || !job) return MMAD_ENULL;
+  if (unfolded(d)) return MMAD_EUNSUPPORTED;
+  const Geom gf = fwd_geom(d, dtype), gd = dgrad_geom(d, dtype);
+  if (!geom_ok(gf, dtype) || !geom_ok(gd, dtype) || gf.Kpad != gf.K || gd.Kpad != gd.K)
+    return MMAD_EUNSUPPORTED;
+  if (d->ci % 16 || d->co % 16 || gf.taps > 27) return MMAD_EUNSUPPORTED;
+  mmad_pack_dual j{};
+  j.w = w;
+  j.w_fwd = w_fwd;
+  j.w_dgrad = w_dgrad;
+  j.co = d->co;
+  j.ci = d->ci;
+  j.taps = gf.taps;
+  j.flip = dgrad_as_fwd(d) ? 1 : 0;
+  j.tile0 = tile0;
+  *job = j;
+  return MMAD_OK;
+}
+
+int64_t mmad_pack_dual_tiles(const mmad_pack_dual* job) {
+  return job ? (int64_t)(job->co / 16) * (job->ci / 16) : -1;
+}
+
+int mmad_conv_pack_dual_batch(int dtype, int njobs, const mmad_pack_dual* jobs,
+                              int64_t total_tiles, void* stream) {
+  if (njobs <= 0 || total_tiles <= 0 || total_tiles > INT32_MAX) return MMAD_EBADSHAPE;
+  if (!jobs) return MMAD_ENULL;
+  if (dtype != MMAD_BF16) return MMAD_EBADDTYPE;
+  hipLaunchKernelGGL(pack_dual_kernel, dim3((unsigned)total_tiles), dim3(256), 0,
+                     as_stream(stream), jobs, njobs);
+  return launch_status();
 }
 
 int64_t mmad_pack_job_tiles(const mmad_pack_job* job) {

@@ -140,7 +140,9 @@ def _weight_desc(weight, stride, padding, dilation):
 
 class PackPlan:
     """Repack a set of conv weights (forward layout, and the dgrad layout when gradients
-    are on) with ONE kernel launch per step instead of one or two per conv.
+    are on) with one or two kernel launches per step instead of one or two per conv: bf16
+    convs needing both layouts get them from a single read (mmad_conv_pack_dual_batch),
+    the rest go through the generic job batch.
 
     ``convs``: layers.Conv3d modules sharing one compute dtype.  ``run()`` refreshes every
     packed copy from the current fp32 master weights and hands each conv its buffers for
@@ -154,9 +156,25 @@ class PackPlan:
         self.entries = []
         jobs = []
         tiles = 0
+        duals = []
+        dtiles = 0
         for conv in convs:
             w = conv.weight
             d = _weight_desc(w, conv._stride3(), conv._pads(), conv._dilation3())
+            if with_dgrad and cdtype == torch.bfloat16:
+                # both layouts from one read of the fp32 weight when the shapes allow it
+                nf = lib.mmad_conv_packed_elems(d, dt, 0)
+                nd = lib.mmad_conv_packed_elems(d, dt, 1)
+                if nf > 0 and nd > 0:
+                    wp = torch.empty(nf, dtype=cdtype, device=w.device)
+                    wpt = torch.empty(nd, dtype=cdtype, device=w.device)
+                    job = L.PackDual()
+                    if lib.mmad_conv_pack_dual_job(d, dt, L.ptr(w), L.ptr(wp), L.ptr(wpt),
+                                                   dtiles, job) == 0:
+                        dtiles += lib.mmad_pack_dual_tiles(job)
+                        duals.append(job)
+                        self.entries.append((conv, w.data_ptr(), wp, wpt))
+                        continue
             bufs = []
             for fd in ((0, 1) if with_dgrad else (0,)):
                 n = lib.mmad_conv_packed_elems(d, dt, fd)
@@ -177,6 +195,11 @@ class PackPlan:
             raw = (L.PackJob * len(jobs))(*jobs)
             host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
             self.table = host.to(convs[0].weight.device)
+        self.nduals, self.dtiles = len(duals), dtiles
+        if duals:
+            raw = (L.PackDual * len(duals))(*duals)
+            host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
+            self.dtable = host.to(convs[0].weight.device)
         self.with_dgrad = with_dgrad
 
     def valid_for(self, convs, cdtype, with_dgrad):
@@ -189,6 +212,9 @@ class PackPlan:
         if self.njobs:
             L.call("mmad_conv_pack_batch", self.dt, self.njobs, L.ptr(self.table), self.tiles,
                    L.stream())
+        if self.nduals:
+            L.call("mmad_conv_pack_dual_batch", self.dt, self.nduals, L.ptr(self.dtable),
+                   self.dtiles, L.stream())
         for conv, _, wp, wpt in self.entries:
             conv._prepacked = (wp, wpt) if wp is not None or wpt is not None else None
 
