@@ -1183,6 +1183,10 @@ bool use_lattice8(const Geom& g, int dtype) {
   return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
          mmad_lattice8::ok(patch_geo(g));
 }
+bool use_pwgrad(const Geom& g, int dtype) {
+  return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
+         mmad_pwgrad::ok(patch_geo(g));
+}
 bool use_lattice_wgrad(const Geom& g, int dtype) {
   return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
          mmad_lattice::wgrad_ok(patch_geo(g));
@@ -1659,6 +1663,8 @@ int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype) {
   int64_t slabs = (int64_t)sp.splits * g.Nd * g.K * 4;
   if (!unfolded(d) && use_lattice_wgrad(g, dtype))
     slabs = std::max<int64_t>(slabs, mmad_lattice::wgrad_workspace(patch_geo(g)));
+  if (!unfolded(d) && use_pwgrad(g, dtype))
+    slabs = std::max<int64_t>(slabs, mmad_pwgrad::workspace(patch_geo(g)));
   if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on())
     slabs = std::max<int64_t>(slabs, mmad_stem::wgrad_blocks(d) * g.Nd * g.K * 4);
   const int64_t parts = (int64_t)1024 * 2 * g.Nd * 4;   // bias-gradient column sums
@@ -1694,9 +1700,11 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
     if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, stream);
     return MMAD_OK;
   }
-  if (!unfolded(d) && use_lattice_wgrad(g, dtype)) {
+  if (!unfolded(d) && (use_lattice_wgrad(g, dtype) || use_pwgrad(g, dtype))) {
     int splits = 0;
-    rc = mmad_lattice::wgrad(patch_geo(g), x, dy, (float*)workspace, &splits, stream);
+    rc = use_pwgrad(g, dtype)
+             ? mmad_pwgrad::wgrad(patch_geo(g), x, dy, (float*)workspace, &splits, stream)
+             : mmad_lattice::wgrad(patch_geo(g), x, dy, (float*)workspace, &splits, stream);
     if (rc) return rc;
     hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)cdiv(g.Cs, 64), (unsigned)g.Nd),
                        dim3(256), 0, st, (const float*)workspace, dw, splits, g.Nd, g.K, g.Cs,

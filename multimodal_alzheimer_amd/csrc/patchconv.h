@@ -45,3 +45,12 @@ int64_t tiles(const mmad_patch::Geo& g);
 int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,
         float* stats, void* stream);
 }  // namespace mmad_lattice8
+
+// Patch-resident weight gradient for dense stride-1 3^3 convs on 32-wide volumes
+// (pwgrad.hip, layer1): fp32 partial slabs [splits][Nd][27 * Cs] as mmad_lattice::wgrad.
+namespace mmad_pwgrad {
+bool ok(const mmad_patch::Geo& g);
+int64_t workspace(const mmad_patch::Geo& g);
+int wgrad(const mmad_patch::Geo& g, const void* x, const void* dy, float* ws, int* splits,
+          void* stream);
+}  // namespace mmad_pwgrad

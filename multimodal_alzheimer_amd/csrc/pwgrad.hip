@@ -1,0 +1,317 @@
+// Patch-resident weight gradient for dense stride-1 3^3 convolutions (dilation 1, padding 1)
+// on volumes 32 voxels wide, gfx950 (bf16 operands, fp32 accumulate): the MedicalNet layer1
+// convs (64 -> 64 at 32^3, reached from pkg/models/mri_models/anat_cnn.py:29-31).
+//
+// dW[co][tap][ci] = sum over output voxels v of dY[v][co] * X[v + tap - 1][ci].  The
+// row-gather wgrad (conv.hip wgrad_kernel) DMAs one gathered 32-voxel K row per tap, so
+// at 64 channels it issues three LDS-DMA instructions per eight MFMAs per wave and runs
+// issue-bound.  Here, as in the residue-class lattice wgrad (latticeconv.hip), a block keeps
+// the input planes it needs resident and builds every tap's fragments from them:
+//  * block = 64 output channels x 32 input channels x all 27 taps over a split
+//    (sample, 8-row y tile, z range); 8 waves = 2 (16-channel ci halves) x 4 tap groups of
+//    7 (6); per wave 4 x 7 accumulator tiles;
+//  * a K step is one output row (32 voxels): the dY rows are 32 consecutive x, and a tap's
+//    X rows are the 32 x of row (y + ky, z + kz) shifted by kx.  X plane images hold the
+//    tile's 10 rows x 34 x positions (the x = -1 / 32 padding as zero rows, and the
+//    padding rows / planes read past a buffer resource, i.e. zeros), so every tap's block
+//    of 32 rows is contiguous and no tap needs a validity test;
+//  * input planes stream through a 4-slot ring (plane o + 3 issued when output plane o
+//    starts); dY (2 output rows x 64 channels = 8 KiB per stage) through a 3-slot ring;
+//  * both operands are read with transposing ds_read_b64_tr_b16 fragment reads; the dY
+//    image is chunk-swizzled (conflict-free), the X image is not (its taps shift the row
+//    by kx, which a row-keyed swizzle cannot follow without per-read address math), so the
+//    X reads run 2-way bank-conflicted;
+//  * fp32 partial slabs [split][co][tap * Cs + ci], summed and transposed by conv.hip's
+//    wgrad_reduce_t_kernel.
+#include "common.h"
+#include "patchconv.h"
+
+namespace {
+
+constexpr int PW_KC = 32;                        // input channels per block
+constexpr int PW_TY = 8;                         // output rows per y tile
+constexpr int PW_XW = 32;                        // voxels per row (one K step)
+constexpr int PW_XR = PW_XW + 2;                 // x positions per image row group
+constexpr int PW_YR = PW_TY + 2;                 // y rows per plane image
+constexpr int PW_XROWS = PW_YR * PW_XR;          // 340 image rows of 64 B
+constexpr int PW_XDMA = (PW_XROWS + 15) / 16;    // 22 DMA instructions (16 rows each)
+constexpr int PW_XSLOT = PW_XDMA * 1024;
+constexpr int PW_XSLOTS = 4;
+constexpr int PW_YROW = 128;                     // dY rows: 64 co x 2 B
+constexpr int PW_YST = 2 * PW_XW * PW_YROW;      // 8 KiB: 2 K steps per stage
+constexpr int PW_YSLOTS = 3;
+constexpr int PW_Y_OFF = PW_XSLOTS * PW_XSLOT;
+constexpr int PW_LDS = PW_Y_OFF + PW_YSLOTS * PW_YST;
+constexpr int PW_NTHR = 512;
+constexpr uint32_t PW_OOB = 0x80000000u;
+
+struct PWG {
+  int nb, Cs, Nd, D, H, K;
+  int zr;                                        // output planes per split
+};
+
+__device__ __forceinline__ int pw_wsz128(int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); }
+
+__global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __restrict__ x,
+                                                         const u16* __restrict__ dy,
+                                                         float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware order: the co tiles and ci chunks of one split (same planes) stay together
+  const int nci = g.Cs / PW_KC, nco = g.Nd / 64;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int cot = tile % nco, t2 = tile / nco;
+  const int cit = t2 % nci, split = t2 / nci;
+  const int nyt = g.H / PW_TY, nzr = g.D / g.zr;
+  const int zi = split % nzr, yt = (split / nzr) % nyt, n = split / (nzr * nyt);
+  const int co0 = cot * 64, ci0 = cit * PW_KC, y0 = yt * PW_TY, z0 = zi * g.zr;
+
+  const int64_t vox = (int64_t)g.D * g.H * PW_XW;
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(x + n * vox * g.Cs), 0, (int)__builtin_amdgcn_readfirstlane((int)(vox * g.Cs * 2)),
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(dy + n * vox * g.Nd), 0, (int)__builtin_amdgcn_readfirstlane((int)(vox * g.Nd * 2)),
+      0x00020000);
+  const uint32_t smem_l = lds_addr_of(smem);
+
+  // X plane image DMA: instruction q of a plane = image rows 16q..16q+15 (row = yy*34 + xx);
+  // wave w issues q = w, w + 8, w + 16 (< 22).  Input plane iz adds iz * plane bytes (iz = -1
+  // wraps past the resource; iz = D lands past it: zeros either way)
+  // (the lane offsets are recomputed per plane: a few VALU per DMA; held in registers they
+  // were spilled by the MFMA loop and reloaded behind a full vmcnt drain)
+  const int nx = wave + 16 < PW_XDMA ? 3 : 2;
+  auto xoff = [&](int h) -> uint32_t {
+    const int q = wave + 8 * h, row = 16 * q + (lane >> 2);
+    const int yv = y0 - 1 + row / PW_XR, xv = row % PW_XR - 1;
+    const bool ok = row < PW_XROWS && (unsigned)yv < (unsigned)g.H &&
+                    (unsigned)xv < (unsigned)PW_XW;
+    return ok ? (uint32_t)(((yv * PW_XW + xv) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
+  };
+  const uint32_t xplane = (uint32_t)(g.H * PW_XW * g.Cs * 2);
+  auto issue_x = [&](int e) {                    // stream entry e = input plane z0 - 1 + e
+    const uint32_t pz = (uint32_t)(z0 - 1 + e) * xplane;
+    const uint32_t slot = smem_l + (uint32_t)((e % PW_XSLOTS) * PW_XSLOT);
+#pragma unroll
+    for (int h = 0; h < 3; ++h)
+      if (h < nx) buf_lds16_asm(xoff(h) + pz, rsx, slot + (uint32_t)((wave + 8 * h) * 1024));
+  };
+  // dY stage (output plane o, rows 2M, 2M + 1): image row r = q * 32 + x, one instruction
+  // per wave of 8 rows x 128 B, chunk-swizzled for the transposing reads
+  const int yr = wave * 8 + (lane >> 3);
+  const uint32_t ylane = (uint32_t)((yr * g.Nd + co0 + ((lane & 7) ^ pw_wsz128(yr)) * 8) * 2);
+  auto issue_y = [&](int o, int m, int sl) {
+    const uint32_t base = (uint32_t)(((z0 + o) * g.H + y0 + 2 * m) * PW_XW) * (uint32_t)g.Nd * 2;
+    buf_lds16_asm(base + ylane, rsy, smem_l + (uint32_t)(PW_Y_OFF + sl * PW_YST + wave * 1024));
+  };
+
+  const int cf = wave & 1, tg = wave >> 1;
+  const int t0 = tg * 7, nt = tg == 3 ? 6 : 7;
+  const int lk = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int rsel = 8 * lk + q4;
+  uint32_t ya_lo[4], ya_hi[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = i * 16 + 4 * p4;
+    ya_lo[i] = (uint32_t)(rsel * PW_YROW + (((col >> 3) ^ pw_wsz128(rsel)) << 4) + (col & 7) * 2);
+    ya_hi[i] = (uint32_t)((rsel + 4) * PW_YROW + (((col >> 3) ^ pw_wsz128(rsel + 4)) << 4) +
+                          (col & 7) * 2);
+  }
+  const uint32_t xb = (uint32_t)(rsel * 64 + cf * 32 + 8 * p4);
+  f32x4 acc[4][7];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto tr8 = [](const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p);
+  };
+  // prologue: stream entries 0..2 (planes z0-1..z0+1), dY stages 0 and 1
+  issue_x(0);
+  issue_x(1);
+  issue_x(2);
+  issue_y(0, 0, 0);
+  issue_y(0, 1, 1);
+  const int nstage = g.zr * 4;
+
+  struct PFr { bf16x8 a[4], b[7]; };
+  auto run = [&](auto tgc) {
+    constexpr int TG = decltype(tgc)::value;
+    constexpr int NT = TG == 3 ? 6 : 7;
+    // per plane: this lane's fragment base in the slots of planes z-1, z, z+1.  Made opaque
+    // (asm move) so the compiler cannot hoist one base per (tap, row) out of the plane loop
+    // (30 live VGPRs, spilled); every read is then base + an immediate offset
+    const char* xbase[3];
+    // one K step = output row YL of the current plane (compile time)
+    auto kread = [&](const char* yimg, auto qc, auto ylc, PFr& f) {
+      constexpr int Q = decltype(qc)::value, YL = decltype(ylc)::value;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        f.a[i] = __builtin_shufflevector(tr8(yimg + Q * PW_XW * PW_YROW + ya_lo[i]),
+                                         tr8(yimg + Q * PW_XW * PW_YROW + ya_hi[i]), 0, 1, 2, 3,
+                                         4, 5, 6, 7);
+      auto one = [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        if constexpr (K < NT) {
+          constexpr int t = TG * 7 + K;
+          constexpr int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;   // 0..2 (shift + 1)
+          constexpr int r0 = (YL + ky) * PW_XR + kx;
+          const char* img = xbase[kz] + r0 * 64;
+          f.b[K] = __builtin_shufflevector(tr8(img), tr8(img + 4 * 64), 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      };
+      one(std::integral_constant<int, 0>{});
+      one(std::integral_constant<int, 1>{});
+      one(std::integral_constant<int, 2>{});
+      one(std::integral_constant<int, 3>{});
+      one(std::integral_constant<int, 4>{});
+      one(std::integral_constant<int, 5>{});
+      one(std::integral_constant<int, 6>{});
+    };
+    auto kmma = [&](const PFr& f) {
+      auto one = [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        if constexpr (K < NT) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i][K] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[K], acc[i][K], 0, 0,
+                                                                0);
+        }
+      };
+      one(std::integral_constant<int, 0>{});
+      one(std::integral_constant<int, 1>{});
+      one(std::integral_constant<int, 2>{});
+      one(std::integral_constant<int, 3>{});
+      one(std::integral_constant<int, 4>{});
+      one(std::integral_constant<int, 5>{});
+      one(std::integral_constant<int, 6>{});
+    };
+#pragma unroll 1
+    for (int o = 0; o < g.zr; ++o) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        uint32_t b = (uint32_t)(((o + j) % PW_XSLOTS) * PW_XSLOT) + xb;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(b) : "v"(b));
+        xbase[j] = smem + b;
+      }
+      const bool xnext = o + 3 <= g.zr + 1;      // stream entry o + 3 exists
+      auto stage = [&](auto mc) {
+        constexpr int M = decltype(mc)::value;
+        const int s = o * 4 + M;
+        // dY(s) landed (and at M = 0 the planes of o, issued a plane earlier); younger: dY(s+1)
+        // and, at stages 1 and 2, the X plane issued at stage 0 right after stage 2's dY
+        if (s + 1 >= nstage) {
+          wait_vm_lgkm0<0>();
+        } else if ((M == 1 || M == 2) && xnext) {
+          if (nx == 3) wait_vm_lgkm0<4>();
+          else wait_vm_lgkm0<3>();
+        } else {
+          wait_vm_lgkm0<1>();
+        }
+        raw_barrier();
+        if (s + 2 < nstage) issue_y((s + 2) / 4, (s + 2) % 4, (s + 2) % PW_YSLOTS);
+        if (M == 0 && xnext) issue_x(o + 3);
+        // (opaque, defined after the barrier: otherwise the dY fragment addresses of all four
+        // stages are computed at the plane start and held -- 64 VGPRs, spilled)
+        int yoff = PW_Y_OFF + (s % PW_YSLOTS) * PW_YST;
+        asm volatile("" : "+s"(yoff));
+        const char* yimg = smem + yoff;
+        PFr f0, f1;
+        kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, f0);
+        kread(yimg, std::integral_constant<int, 1>{}, std::integral_constant<int, 2 * M + 1>{},
+              f1);
+        kmma(f0);
+        kmma(f1);
+      };
+      stage(std::integral_constant<int, 0>{});
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
+    }
+  };
+  switch (tg) {                                  // wave-uniform
+    case 0: run(std::integral_constant<int, 0>{}); break;
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    default: run(std::integral_constant<int, 3>{}); break;
+  }
+
+  // partial slab [split][co][tap * Cs + ci]
+  float* out = ws + (int64_t)split * g.Nd * g.K;
+  const int lr = lane & 15;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    if (k < nt) {
+      const int kcol = (t0 + k) * g.Cs + ci0 + cf * 16 + lr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          out[(int64_t)(co0 + i * 16 + lk * 4 + r) * g.K + kcol] = acc[i][k][r];
+    }
+  }
+}
+
+// MMAD_PWGRAD=0 routes these convs back to the row-gather wgrad_kernel (A/B switch)
+bool pw_on() {
+  static const bool v = [] {
+    const char* e = getenv("MMAD_PWGRAD");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return v;
+}
+
+// output planes per split: the largest divisor of D (>= 4) that still gives >= 256 blocks
+int pw_zr(const mmad_patch::Geo& q) {
+  const int64_t base = (int64_t)q.nb * (q.Hd / PW_TY) * (q.Cs / PW_KC) * (q.Nd / 64);
+  int zr = q.Dd;
+  while (zr > 4 && zr % 2 == 0 && base * (q.Dd / zr) < 256) zr /= 2;
+  return zr;
+}
+
+}  // namespace
+
+namespace mmad_pwgrad {
+
+bool ok(const mmad_patch::Geo& q) {
+  if (!pw_on()) return false;
+  if (q.KD != 3 || q.KH != 3 || q.KW != 3 || q.dd != 1 || q.dh != 1 || q.dw != 1) return false;
+  if (q.pd != 1 || q.ph != 1 || q.pw != 1) return false;
+  if (q.Ds != q.Dd || q.Hs != q.Hd || q.Ws != q.Wd || q.Wd != PW_XW) return false;
+  if (q.Hd % PW_TY || q.Dd < 4 || q.Cs % PW_KC || q.Nd % 64 || q.Kpad != 27 * q.Cs) return false;
+  if ((int64_t)q.Dd * q.Hd * PW_XW * std::max(q.Cs, q.Nd) * 2 >= (int64_t(1) << 30)) return false;
+  const int zr = pw_zr(q);
+  return q.Dd % zr == 0 && zr >= 2;
+}
+
+int64_t splits(const mmad_patch::Geo& q) {
+  return (int64_t)q.nb * (q.Hd / PW_TY) * (q.Dd / pw_zr(q));
+}
+
+int64_t workspace(const mmad_patch::Geo& q) {
+  return mmad_pwgrad::splits(q) * q.Nd * 27 * q.Cs * 4;
+}
+
+int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, int* nsplit,
+          void* stream) {
+  if (!mmad_pwgrad::ok(q)) return MMAD_EUNSUPPORTED;
+  static const bool attr = hipFuncSetAttribute((const void*)pwgrad_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               PW_LDS) == hipSuccess;
+  if (!attr) return MMAD_EUNSUPPORTED;
+  PWG g{};
+  g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.D = q.Dd; g.H = q.Hd; g.K = 27 * q.Cs;
+  g.zr = pw_zr(q);
+  const int64_t sp = mmad_pwgrad::splits(q);
+  const int64_t nblk = sp * (q.Cs / PW_KC) * (q.Nd / 64);
+  hipLaunchKernelGGL(pwgrad_kernel, dim3((unsigned)nblk), dim3(PW_NTHR), PW_LDS,
+                     as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  *nsplit = (int)sp;
+  return launch_status();
+}
+
+}  // namespace mmad_pwgrad
