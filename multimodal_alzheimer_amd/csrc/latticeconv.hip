@@ -621,7 +621,11 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
         if (M < 6) issue_y_at(y_here, M + 2, (sl + 2) % WYSLOTS);
         else if (o + 1 < nplane_out) issue_y_at(y_next, M - 6, (sl + 2) % WYSLOTS);
         if (M == 0 && xnow) issue_x(o + 2);
-        const char* yimg = smem + WY_OFF + sl * WYST;
+        // (opaque, defined after the barrier, so the fragment addresses of later stages are
+        // not computed early and held in VGPRs)
+        int yoff = WY_OFF + sl * WYST;
+        asm volatile("" : "+s"(yoff));
+        const char* yimg = smem + yoff;
         WFr f0, f1;
         kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, f0);
         kread(yimg, std::integral_constant<int, 1>{}, std::integral_constant<int, 2 * M + 1>{},
