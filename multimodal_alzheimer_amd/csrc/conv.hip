@@ -34,6 +34,7 @@
 //    accumulators, bf16 tile transposed through LDS into 16-byte channel-vector stores.
 #include "common.h"
 #include "patchconv.h"
+#include "pointwise.h"
 #include "stem.h"
 
 namespace {
@@ -1627,6 +1628,10 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!dy || !wpt || !dx) return MMAD_ENULL;
   if (unfolded(d)) return MMAD_EUNSUPPORTED;   // the raw input never needs a gradient
+  if (mmad_pw::ok(d, dtype)) {
+    const int rc = mmad_pw::dgrad(d, dy, wpt, dx, stream);
+    if (rc != MMAD_EUNSUPPORTED) return rc;
+  }
   if (dgrad_as_fwd(d)) {
     const Geom gf = dgrad_fwd_geom(d, dtype);
     if (!geom_ok(gf, dtype)) return MMAD_EUNSUPPORTED;
@@ -1683,6 +1688,8 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
   if (!geom_ok(g, dtype) || g.Nd % (dtype == MMAD_BF16 ? 8 : 4)) return MMAD_EUNSUPPORTED;
   hipStream_t st = as_stream(stream);
   int rc;
+  // (1x1x1 weight gradients stay here: hipBLASLt's heuristic offers no split-K algorithm
+  // for K = all voxels at this size and its single-pass one ran 5x slower than wgrad_kernel)
   if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on() && g.K == 392) {
     rc = mmad_stem::wgrad(d, x, dy, (float*)workspace, stream);
     if (rc) return rc;
