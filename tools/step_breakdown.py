@@ -4,12 +4,13 @@ import collections
 import re
 import sys
 
-RULES = [("igemm", "igemm fwd/dgrad"), ("lattice", "lattice conv"), ("patch_conv", "patch conv"), ("wgrad_kernel", "wgrad"),
+RULES = [("igemm", "igemm fwd/dgrad"), ("lattice_wgrad", "lattice wgrad"),
+         ("lattice", "lattice conv fwd/dgrad"), ("patch_conv", "patch conv"), ("wgrad_kernel", "wgrad"),
          ("reduce", "wgrad reduce"), ("slab", "wgrad reduce"), ("stem_fwd", "stem fwd"),
          ("stem_wgrad", "stem wgrad"), ("bnpool", "bnpool fused"), ("scale_shift", "bn apply"),
          ("colsum", "bn bwd reduce"), ("bn_bwd_apply", "bn bwd apply"),
-         ("finalize", "bn finalize"), ("fold", "bn finalize"), ("pack", "weight pack"),
-         ("unfold", "unfold"), ("FusedOpt", "adam"), ("TensorListMetadata", "adam"),
+         ("unfold", "stem input unfold"), ("finalize", "bn finalize"), ("fold", "bn finalize"),
+         ("pack", "weight pack"), ("pwgrad", "wgrad"), ("Cijk", "1x1 dgrad (hipBLASLt)"), ("FusedOpt", "adam"), ("TensorListMetadata", "adam"),
          ("CUDAFunctor_add", "residual add (torch)"), ("gap", "gap")]
 
 
