@@ -61,6 +61,25 @@ def dominant(d, grid_x, name="igemm_kernel<unsigned short, 256, 0, 256"):
     return "\n".join(out)
 
 
+def dispatches(d, name):
+    """Every dispatch of a kernel (name prefix) in launch order, grouped by its position
+    inside a step (the kernel serves several layers/directions per step)."""
+    rows = [r for r in csv.DictReader(open(f"{d}/run_kernel_trace.csv"))
+            if name in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    per = next((n for n in (6, 5, 4, 3, 2, 1)
+                if len(rows) % n == 0 and len(rows) // n in (13, 10, 20, 25)), 1)
+    groups = collections.defaultdict(list)
+    for i, r in enumerate(rows):
+        groups[i % per].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    out = [f"{len(rows)} dispatches of {name}, {per} per step"]
+    for k in sorted(groups):
+        v = groups[k]
+        out.append(f"position {k} of {per}: n={len(v)} avg={statistics.mean(v):.1f} us "
+                   f"median={statistics.median(v):.1f} us min={min(v):.1f} max={max(v):.1f}")
+    return "\n".join(out)
+
+
 def counter(d, name):
     rows = list(csv.DictReader(open(f"{d}/run_counter_collection.csv")))
     vals = [float(r["Counter_Value"]) for r in rows
@@ -121,6 +140,8 @@ if __name__ == "__main__":
         print(stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 30))
     elif mode == "dominant":
         print(dominant(sys.argv[2], int(sys.argv[3]), *sys.argv[4:5]))
+    elif mode == "dispatches":
+        print(dispatches(sys.argv[2], sys.argv[3]))
     elif mode == "step":
         print(step(sys.argv[2]))
     elif mode == "traffic":
