@@ -160,6 +160,23 @@ int mmad_bn_bwd_finalize(int c, int64_t count, int nparts, const float* parts,
 int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* relu_out,
                       const void* y, const float* mean, const float* invstd,
                       const float* coef, void* dy, void* gmask_out, void* stream);
+/* Residual pair relu(bn(y) + bn2(y2)) (BasicBlock with the shortcut-B downsample BN): both
+ * BNs' backward in one pass each over g / relu_out -- reduce2 writes both part buffers
+ * (parts2 = sums of g' and g'*xhat2), finalize2 both coefficient sets, apply2 dy and dy2.
+ * Bit-identical to the per-BN calls; fixed-channel layouts only (else MMAD_EUNSUPPORTED). */
+int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* relu_out,
+                        const void* y, const float* mean, const float* invstd, const void* y2,
+                        const float* mean2, const float* invstd2, float* parts, float* parts2,
+                        void* stream);
+int mmad_bn_bwd_finalize2(int c, int64_t count, int nparts, const float* parts,
+                          const float* gamma, const float* invstd, int training, float* dgamma,
+                          float* dbeta, float* coef, const float* parts2, const float* gamma2,
+                          const float* invstd2, int training2, float* dgamma2, float* dbeta2,
+                          float* coef2, void* stream);
+int mmad_bn_bwd_apply2(int dtype, int64_t m, int c, const void* g, const void* relu_out,
+                       const void* y, const float* mean, const float* invstd, const float* coef,
+                       void* dy, const void* y2, const float* mean2, const float* invstd2,
+                       const float* coef2, void* dy2, void* stream);
 /* BN + ReLU without residual (bn1 of every BasicBlock): the same two passes with the ReLU
  * mask recomputed from y as fma(y, scale, shift) > 0 (the forward's affine, so the mask
  * equals out > 0) instead of read from the ReLU output -- one tensor fewer per pass. */

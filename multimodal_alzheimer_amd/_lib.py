@@ -76,6 +76,10 @@ _SIGS = {
     "mmad_bn_bwd_reduce": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_bn_bwd_finalize": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "mmad_bn_bwd_apply": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_bn_bwd_reduce2": (_i32, [_i32, _i64, _i32] + [_vp] * 11),
+    "mmad_bn_bwd_finalize2": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
+                                     _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "mmad_bn_bwd_apply2": (_i32, [_i32, _i64, _i32] + [_vp] * 13),
     "mmad_relu_fwd": (_i32, [_i32, _i64, _vp, _vp, _vp]),
     "mmad_relu_bwd": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp]),
     "mmad_colsum_ws": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp]),

@@ -34,7 +34,10 @@ PartPlan part_plan(int64_t M) {
 // 256 / (CC / V) rows in flight per block; one LDS pass folds the row lanes.  Wide rows
 // (C / V > 256, e.g. ResNet-50's 2048 channels) are split over gridDim.y channel slabs of
 // CC = C / gridDim.y channels each.
-template <typename T, int MODE, int V>
+// DUAL (MODE 1 only): a second BN over the same gradient and ReLU mask (the shortcut BN of
+// a residual block, y2 = its input): parts2 gets (sum g', sum g' * xhat2) from the same pass,
+// so g and the mask are read once for both
+template <typename T, int MODE, int V, bool DUAL = false>
 __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t rpp,
                                                      const T* __restrict__ y,
                                                      const T* __restrict__ g,
@@ -44,8 +47,13 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
                                                      float* __restrict__ parts,
                                                      const uint8_t* __restrict__ act,
                                                      const float* __restrict__ msc,
-                                                     const float* __restrict__ msh) {
-  __shared__ float red[2][2048];
+                                                     const float* __restrict__ msh,
+                                                     const T* __restrict__ y2 = nullptr,
+                                                     const float* __restrict__ mean2 = nullptr,
+                                                     const float* __restrict__ invstd2 = nullptr,
+                                                     float* __restrict__ parts2 = nullptr) {
+  static_assert(!DUAL || MODE == 1, "dual partial sums: BN backward with a relu_out mask");
+  __shared__ float red[DUAL ? 3 : 2][2048];
   const int tid = threadIdx.x;
   const int CC = C / (int)gridDim.y;           // this block's channel slab
   const int cb = (int)blockIdx.y * CC;
@@ -54,21 +62,28 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
   const int cl = tid % lpr, rl = tid / lpr;
   const int64_t r0 = (int64_t)blockIdx.x * rpp;
   const int64_t r1 = min(M, r0 + rpp);
-  float s[V], q[V];
+  float s[V], q[V], q2[V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  for (int e = 0; e < V; ++e) { s[e] = 0.f; q[e] = 0.f; q2[e] = 0.f; }
   if (rl < rpar) {
-    float mu[V], is[V], sc[V], sh[V];
+    float mu[V], is[V], sc[V], sh[V], mu2[V], is2[V];
     if (MODE == 1 || MODE == 3 || MODE == 4) {
 #pragma unroll
       for (int e = 0; e < V; ++e) { mu[e] = mean[cb + cl * V + e]; is[e] = invstd[cb + cl * V + e]; }
+    }
+    if constexpr (DUAL) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        mu2[e] = mean2[cb + cl * V + e];
+        is2[e] = invstd2[cb + cl * V + e];
+      }
     }
     if (MODE == 4) {
 #pragma unroll
       for (int e = 0; e < V; ++e) { sc[e] = msc[cb + cl * V + e]; sh[e] = msh[cb + cl * V + e]; }
     }
     // one row's contribution, from its y / g / relu_out values
-    auto accum = [&](int64_t i, float* yv, float* gv, const float* ov) {
+    auto accum = [&](int64_t i, float* yv, float* gv, const float* ov, const float* y2v) {
       if (MODE == 1 || MODE == 3 || MODE == 4) {
         if (MODE == 4) {
           // ReLU mask of a BN+ReLU without residual, recomputed from its input y with the
@@ -87,6 +102,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
           s[e] += gv[e];
           q[e] += gv[e] * ((yv[e] - mu[e]) * is[e]);
         }
+        if constexpr (DUAL) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) q2[e] += gv[e] * ((y2v[e] - mu2[e]) * is2[e]);
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < V; ++e) {
@@ -103,7 +122,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
       // rows are still added in the same order
       constexpr int U = 4;
       for (; r + (U - 1) * rpar < r1; r += U * rpar) {
-        u32x4 yr[U], gr[U], orr[U];
+        u32x4 yr[U], gr[U], orr[U], y2r[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int64_t i = (r + u * rpar) * C + cb + cl * V;
@@ -111,22 +130,24 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
           if (NEED_G) gr[u] = *reinterpret_cast<const u32x4*>(g + i);
           if (MODE == 1 && relu_out != nullptr)
             orr[u] = *reinterpret_cast<const u32x4*>(relu_out + i);
+          if constexpr (DUAL) y2r[u] = *reinterpret_cast<const u32x4*>(y2 + i);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int64_t i = (r + u * rpar) * C + cb + cl * V;
-          float yv[V], gv[V], ov[V];
+          float yv[V], gv[V], ov[V], y2v[V];
           Chunk<T>::load(reinterpret_cast<const T*>(&yr[u]), yv);
           if (NEED_G) Chunk<T>::load(reinterpret_cast<const T*>(&gr[u]), gv);
           if (MODE == 1 && relu_out != nullptr)
             Chunk<T>::load(reinterpret_cast<const T*>(&orr[u]), ov);
-          accum(i, yv, gv, ov);
+          if constexpr (DUAL) Chunk<T>::load(reinterpret_cast<const T*>(&y2r[u]), y2v);
+          accum(i, yv, gv, ov, y2v);
         }
       }
     }
     for (; r < r1; r += rpar) {
       const int64_t i = r * C + cb + cl * V;
-      float yv[V], gv[V], ov[V];
+      float yv[V], gv[V], ov[V], y2v[V];
       if constexpr (V == Chunk<T>::N) Chunk<T>::load(y + i, yv);
       else for (int e = 0; e < V; ++e) yv[e] = Elt<T>::ld(y, i + e);
       if (NEED_G) {
@@ -137,20 +158,33 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
           else for (int e = 0; e < V; ++e) ov[e] = Elt<T>::ld(relu_out, i + e);
         }
       }
-      accum(i, yv, gv, ov);
+      if constexpr (DUAL) {
+        if constexpr (V == Chunk<T>::N) Chunk<T>::load(y2 + i, y2v);
+        else for (int e = 0; e < V; ++e) y2v[e] = Elt<T>::ld(y2, i + e);
+      }
+      accum(i, yv, gv, ov, y2v);
     }
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       red[0][rl * CC + cl * V + e] = s[e];
       red[1][rl * CC + cl * V + e] = q[e];
+      if constexpr (DUAL) red[DUAL ? 2 : 0][rl * CC + cl * V + e] = q2[e];
     }
   }
   __syncthreads();
   for (int c = tid; c < CC; c += 256) {
-    float ss = 0.f, qq = 0.f;
-    for (int k = 0; k < rpar; ++k) { ss += red[0][k * CC + c]; qq += red[1][k * CC + c]; }
+    float ss = 0.f, qq = 0.f, q2q = 0.f;
+    for (int k = 0; k < rpar; ++k) {
+      ss += red[0][k * CC + c];
+      qq += red[1][k * CC + c];
+      if constexpr (DUAL) q2q += red[DUAL ? 2 : 0][k * CC + c];
+    }
     parts[((int64_t)blockIdx.x * 2) * C + cb + c] = ss;
     parts[((int64_t)blockIdx.x * 2 + 1) * C + cb + c] = qq;
+    if constexpr (DUAL) {
+      parts2[((int64_t)blockIdx.x * 2) * C + cb + c] = ss;
+      parts2[((int64_t)blockIdx.x * 2 + 1) * C + cb + c] = q2q;
+    }
   }
 }
 
@@ -297,11 +331,10 @@ __global__ void bn_fold_kernel(int C, const float* __restrict__ gamma,
   bias[c] = sh;
 }
 
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
-    int C, int64_t count, int nparts, const float* __restrict__ parts,
-    const float* __restrict__ gamma, const float* __restrict__ invstd, int training,
-    float* dgamma, float* dbeta, float* coef) {
-  __shared__ double sm[2048];
+__device__ __forceinline__ void bwd_finalize(int C, int64_t count, int nparts,
+                                             const float* parts, const float* gamma,
+                                             const float* invstd, int training, float* dgamma,
+                                             float* dbeta, float* coef, double* sm) {
   const int c = blockIdx.x * FC + (threadIdx.x % FC);
   double S, Q;
   sum_parts(c, C, nparts, parts, sm, S, Q);
@@ -312,6 +345,33 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
   coef[c] = (float)k0;
   coef[C + c] = training ? (float)(k0 * S / (double)count) : 0.f;
   coef[2 * C + c] = training ? (float)(k0 * Q / (double)count) : 0.f;
+}
+
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
+    int C, int64_t count, int nparts, const float* __restrict__ parts,
+    const float* __restrict__ gamma, const float* __restrict__ invstd, int training,
+    float* dgamma, float* dbeta, float* coef) {
+  __shared__ double sm[2048];
+  bwd_finalize(C, count, nparts, parts, gamma, invstd, training, dgamma, dbeta, coef, sm);
+}
+
+// both BNs of a residual pair in one launch: blockIdx.y picks the set
+struct BwdFin {
+  const float* parts;
+  const float* gamma;
+  const float* invstd;
+  int training;
+  float* dgamma;
+  float* dbeta;
+  float* coef;
+};
+
+__global__ __launch_bounds__(1024) void bn_bwd_finalize2_kernel(int C, int64_t count,
+                                                                int nparts, BwdFin a, BwdFin b) {
+  __shared__ double sm[2048];
+  const BwdFin& f = blockIdx.y ? b : a;
+  bwd_finalize(C, count, nparts, f.parts, f.gamma, f.invstd, f.training, f.dgamma, f.dbeta,
+               f.coef, sm);
 }
 
 __global__ void sum_only_finalize_kernel(int C, int nparts, const float* __restrict__ parts,
@@ -438,12 +498,22 @@ __global__ void scale_shift_act_scalar_kernel(int64_t M, int C, const T* __restr
 
 // Fixed-channel form of bn_bwd_apply_kernel (C / V a power of two dividing 256): per-thread
 // channel vector constant, its mean/invstd/coef loaded once as vectors; two chunks a trip.
-template <typename T, bool MASKY = false>
+// DUAL: also the shortcut BN of a residual pair (input y2, gradient dy2), same masked g
+struct BwdApply2 {
+  const void* y2;
+  const float* mean2;
+  const float* invstd2;
+  const float* coef2;
+  void* dy2;
+};
+
+template <typename T, bool MASKY = false, bool DUAL = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
     int64_t nv, int cpr, int C, const T* __restrict__ g, const T* __restrict__ relu_out,
     const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ coef, T* __restrict__ dy, T* __restrict__ gmask,
-    const float* __restrict__ msc = nullptr, const float* __restrict__ msh = nullptr) {
+    const float* __restrict__ msc = nullptr, const float* __restrict__ msh = nullptr,
+    BwdApply2 d2 = {}) {
   constexpr int V = Chunk<T>::N;
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -459,21 +529,37 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
     ld_params<V>(msc + c0, sc);
     ld_params<V>(msh + c0, sh);
   }
-  auto one = [&](int64_t q, const float* gv0, const float* yv, const float* ov) {
-    float gv[V], dv[V];
+  const T* __restrict__ y2 = static_cast<const T*>(d2.y2);
+  T* __restrict__ dy2 = static_cast<T*>(d2.dy2);
+  float mu2[V], is2[V], j0[V], j1[V], j2[V];
+  if constexpr (DUAL) {
+    ld_params<V>(d2.mean2 + c0, mu2);
+    ld_params<V>(d2.invstd2 + c0, is2);
+    ld_params<V>(d2.coef2 + c0, j0);
+    ld_params<V>(d2.coef2 + C + c0, j1);
+    ld_params<V>(d2.coef2 + 2 * C + c0, j2);
+  }
+  auto one = [&](int64_t q, const float* gv0, const float* yv, const float* ov,
+                 const float* y2v) {
+    float gv[V], dv[V], dv2[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       if constexpr (MASKY) gv[e] = bn_affine(yv[e], sc[e], sh[e]) > 0.f ? gv0[e] : 0.f;
       else gv[e] = (relu_out && !(ov[e] > 0.f)) ? 0.f : gv0[e];
       const float xh = (yv[e] - mu[e]) * is[e];
       dv[e] = k0[e] * gv[e] - k1[e] - xh * k2[e];
+      if constexpr (DUAL) {
+        const float xh2 = (y2v[e] - mu2[e]) * is2[e];
+        dv2[e] = j0[e] * gv[e] - j1[e] - xh2 * j2[e];
+      }
     }
     Chunk<T>::store(dy + q * V, dv);
+    if constexpr (DUAL) Chunk<T>::store(dy2 + q * V, dv2);
     if (gmask) Chunk<T>::store(gmask + q * V, gv);
   };
   int64_t q = t0;
   for (; q + stride < nv; q += 2 * stride) {
-    float g0[V], g1[V], y0[V], y1[V], o0[V], o1[V];
+    float g0[V], g1[V], y0[V], y1[V], o0[V], o1[V], z0[V], z1[V];
     Chunk<T>::load(g + q * V, g0);
     Chunk<T>::load(g + (q + stride) * V, g1);
     Chunk<T>::load(y + q * V, y0);
@@ -482,15 +568,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
       Chunk<T>::load(relu_out + q * V, o0);
       Chunk<T>::load(relu_out + (q + stride) * V, o1);
     }
-    one(q, g0, y0, o0);
-    one(q + stride, g1, y1, o1);
+    if constexpr (DUAL) {
+      Chunk<T>::load(y2 + q * V, z0);
+      Chunk<T>::load(y2 + (q + stride) * V, z1);
+    }
+    one(q, g0, y0, o0, z0);
+    one(q + stride, g1, y1, o1, z1);
   }
   if (q < nv) {
-    float g0[V], y0[V], o0[V];
+    float g0[V], y0[V], o0[V], z0[V];
     Chunk<T>::load(g + q * V, g0);
     Chunk<T>::load(y + q * V, y0);
     if (relu_out) Chunk<T>::load(relu_out + q * V, o0);
-    one(q, g0, y0, o0);
+    if constexpr (DUAL) Chunk<T>::load(y2 + q * V, z0);
+    one(q, g0, y0, o0, z0);
   }
 }
 
@@ -786,6 +877,76 @@ int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* re
     if (c % 4 == 0) APPLY(float, 4); else APPLY(float, 1);
   }
 #undef APPLY
+  return launch_status();
+}
+
+// Residual pair (bn2(y) + bn_r(y2), then ReLU): both BNs' backward from one read of g and
+// the mask.  Same values, bit for bit, as reduce / finalize / apply called once per BN with
+// the same g and relu_out.  Fixed-channel layouts only (MMAD_EUNSUPPORTED otherwise: the
+// caller falls back to the per-BN calls).
+int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* relu_out,
+                        const void* y, const float* mean, const float* invstd, const void* y2,
+                        const float* mean2, const float* invstd2, float* parts, float* parts2,
+                        void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!g || !relu_out || !y || !mean || !invstd || !y2 || !mean2 || !invstd2 || !parts ||
+      !parts2)
+    return MMAD_ENULL;
+  const PartPlan pp = part_plan(m);
+  hipStream_t st = as_stream(stream);
+  auto go = [&](auto tag) -> int {
+    using T = decltype(tag);
+    constexpr int VEC = Chunk<T>::N;
+    int slabs = 1;
+    while (c % (slabs * 2 * VEC) == 0 && c / (slabs * VEC) > 256) slabs *= 2;
+    if (!(c % (slabs * VEC) == 0 && c / (slabs * VEC) <= 256)) return MMAD_EUNSUPPORTED;
+    hipLaunchKernelGGL((colsum_kernel<T, 1, VEC, true>), dim3((unsigned)pp.nparts, slabs),
+                       dim3(256), 0, st, m, c, pp.rpp, (const T*)y, (const T*)g,
+                       (const T*)relu_out, mean, invstd, parts, nullptr, nullptr, nullptr,
+                       (const T*)y2, mean2, invstd2, parts2);
+    return launch_status();
+  };
+  return dtype == MMAD_BF16 ? go(u16{}) : go(float{});
+}
+
+int mmad_bn_bwd_finalize2(int c, int64_t count, int nparts, const float* parts,
+                          const float* gamma, const float* invstd, int training, float* dgamma,
+                          float* dbeta, float* coef, const float* parts2, const float* gamma2,
+                          const float* invstd2, int training2, float* dgamma2, float* dbeta2,
+                          float* coef2, void* stream) {
+  if (c <= 0 || count <= 0 || nparts <= 0) return MMAD_EBADSHAPE;
+  if (!parts || !invstd || !coef || !parts2 || !invstd2 || !coef2) return MMAD_ENULL;
+  const BwdFin a{parts, gamma, invstd, training, dgamma, dbeta, coef};
+  const BwdFin b{parts2, gamma2, invstd2, training2, dgamma2, dbeta2, coef2};
+  hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((unsigned)cdiv(c, FC), 2), dim3(1024), 0,
+                     as_stream(stream), c, count, nparts, a, b);
+  return launch_status();
+}
+
+int mmad_bn_bwd_apply2(int dtype, int64_t m, int c, const void* g, const void* relu_out,
+                       const void* y, const float* mean, const float* invstd, const float* coef,
+                       void* dy, const void* y2, const float* mean2, const float* invstd2,
+                       const float* coef2, void* dy2, void* stream) {
+  if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
+  if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!g || !relu_out || !y || !mean || !invstd || !coef || !dy || !y2 || !mean2 || !invstd2 ||
+      !coef2 || !dy2)
+    return MMAD_ENULL;
+  const int vv = dtype == MMAD_BF16 ? 8 : 4;
+  if (!(c % vv == 0 && is_pow2(c / vv) && c / vv <= 256)) return MMAD_EUNSUPPORTED;
+  const int64_t nv = m * c / vv;
+  const BwdApply2 d2{y2, mean2, invstd2, coef2, dy2};
+  hipStream_t st = as_stream(stream);
+  if (dtype == MMAD_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_fc_kernel<u16, false, true>), dim3(ew_grid(nv)), dim3(256),
+                       0, st, nv, c / vv, c, (const u16*)g, (const u16*)relu_out, (const u16*)y,
+                       mean, invstd, coef, (u16*)dy, (u16*)nullptr, nullptr, nullptr, d2);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_fc_kernel<float, false, true>), dim3(ew_grid(nv)),
+                       dim3(256), 0, st, nv, c / vv, c, (const float*)g, (const float*)relu_out,
+                       (const float*)y, mean, invstd, coef, (float*)dy, (float*)nullptr, nullptr,
+                       nullptr, d2);
   return launch_status();
 }
 

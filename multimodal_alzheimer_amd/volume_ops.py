@@ -585,6 +585,39 @@ def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask,
     return dy, dgamma, dbeta, gmask
 
 
+_BN_DUAL = os.environ.get("MMAD_BN_DUAL", "1") != "0"
+
+
+def _bn_backward_pair(g, relu_out, y, mean, invstd, gamma, batch_stats, y2, mean2, invstd2,
+                      gamma2, batch_stats2, params, params2):
+    """Both BNs of relu(bn(y) + bn2(y2)) backward, g and relu_out read once per pass
+    (mmad_bn_bwd_reduce2 / _finalize2 / _apply2); equal bit for bit to two _bn_backward
+    calls.  Returns (dy, dgamma, dbeta, dy2, dgamma2, dbeta2)."""
+    m, c = _rows(y)
+    dev = y.device
+    dt = L.dtype_code(y.dtype)
+    nparts = L.load().mmad_bn_bwd_parts(m, c)
+    parts = torch.empty((2, nparts, 2, c), dtype=torch.float32, device=dev)
+    L.call("mmad_bn_bwd_reduce2", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y), L.ptr(mean),
+           L.ptr(invstd), L.ptr(y2), L.ptr(mean2), L.ptr(invstd2), L.ptr(parts[0]),
+           L.ptr(parts[1]), L.stream())
+    dgamma = grad_slot(params[0], (c,), dev)
+    dbeta = grad_slot(params[1], (c,), dev)
+    dgamma2 = grad_slot(params2[0], (c,), dev)
+    dbeta2 = grad_slot(params2[1], (c,), dev)
+    coef = torch.empty((2, 3 * c), dtype=torch.float32, device=dev)
+    L.call("mmad_bn_bwd_finalize2", c, m, nparts, L.ptr(parts[0]), L.ptr(gamma), L.ptr(invstd),
+           int(batch_stats), L.ptr(dgamma), L.ptr(dbeta), L.ptr(coef[0]), L.ptr(parts[1]),
+           L.ptr(gamma2), L.ptr(invstd2), int(batch_stats2), L.ptr(dgamma2), L.ptr(dbeta2),
+           L.ptr(coef[1]), L.stream())
+    dy = torch.empty_like(y)
+    dy2 = torch.empty_like(y2)
+    L.call("mmad_bn_bwd_apply2", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y), L.ptr(mean),
+           L.ptr(invstd), L.ptr(coef[0]), L.ptr(dy), L.ptr(y2), L.ptr(mean2), L.ptr(invstd2),
+           L.ptr(coef[1]), L.ptr(dy2), L.stream())
+    return dy, dgamma, dbeta, dy2, dgamma2, dbeta2
+
+
 class _BNActFn(torch.autograd.Function):
     """out = act(bn(y) [+ res | + bn_r(res)]) in one pass over y (and res)."""
 
@@ -618,6 +651,16 @@ class _BNActFn(torch.autograd.Function):
         if g.dtype != y.dtype:
             g = cast(g, y.dtype)
         gam = None if gamma is None else gamma.detach()
+        if (has_rbn and _BN_DUAL and out is not None and ctx.mask_affine is None
+                and _mask_from_y_ok(y)):
+            rg = None if rgamma is None else rgamma.detach()
+            dy, dgamma, dbeta, dres, drg, drb = _bn_backward_pair(
+                g, out, y, mean, invstd, gam, batch, rres, rmean, rinvstd, rg, rbatch,
+                ctx.params[0], ctx.params[1])
+            return (dy, None, dgamma if ctx.needs_input_grad[2] else None,
+                    dbeta if ctx.needs_input_grad[3] else None, dres, None,
+                    drg if ctx.needs_input_grad[6] else None,
+                    drb if ctx.needs_input_grad[7] else None, None)
         dy, dgamma, dbeta, gmask = _bn_backward(g, out, y, mean, invstd, gam, batch,
                                                 has_res and not has_rbn, ctx.params[0],
                                                 ctx.mask_affine)

@@ -174,6 +174,37 @@ def test_batchnorm_act(mode, dtype):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("training", [True, False])
+@pytest.mark.parametrize("c", [64, 512])
+def test_bn_residual_pair_dual_bitexact(dtype, training, c):
+    """relu(bn(y) + bn_r(res)) backward through the one-pass pair kernels
+    (mmad_bn_bwd_reduce2 / _finalize2 / _apply2) == the per-BN calls, bit for bit."""
+    n, d, h, w = 2, 4, 6, 5
+    y0 = rnd(n, c, d, h, w, seed=80, scale=2.0) + 0.5
+    r0 = rnd(n, c, d, h, w, seed=81)
+    g0 = rnd(n, c, d, h, w, seed=82)
+    res = {}
+    for dual in (False, True):
+        bn, rbn = _BN(c, 83), _BN(c, 84)
+        bn.training = rbn.training = training
+        yg = to_vol(y0, dtype).requires_grad_(True)
+        rg = to_vol(r0, dtype).requires_grad_(True)
+        old = V._BN_DUAL
+        V._BN_DUAL = dual
+        try:
+            out = V.batchnorm_act(yg, bn, relu=True, res=rg, res_bn=rbn)
+            out.backward(to_vol(g0, dtype))
+        finally:
+            V._BN_DUAL = old
+        torch.cuda.synchronize()
+        res[dual] = (out, yg.grad, rg.grad, bn.weight.grad, bn.bias.grad, rbn.weight.grad,
+                     rbn.bias.grad)
+    names = ("out", "dy", "dres", "dgamma", "dbeta", "dgamma_res", "dbeta_res")
+    for nm, a, b in zip(names, res[False], res[True]):
+        assert torch.equal(a, b), nm
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("training", [True, False])
 def test_bn_relu_maxpool_fused(dtype, training):
     """Fused stem tail maxpool(relu(bn(y))) == the unfused batchnorm_act -> max_pool3d chain
     (forward bit-exact incl. ties on ReLU zeros; backward to rounding), and both against
