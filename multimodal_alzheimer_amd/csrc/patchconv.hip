@@ -15,7 +15,7 @@
 // weights (64 x 64 bf16, 8 KiB) stream through a 3-deep LDS ring by LDS-DMA.  The tap
 // loop is compiled for the 3x3x3 dilation-1 stencil, so all tap offsets are constants.
 //
-//  * 4 waves of (TV/4) x 64 wave tiles (MFMA 16x16x32), each fragment read once
+//  * 8 (4) waves of 32 x 64 wave tiles (MFMA 16x16x32), each fragment read once
 //    per wave with ds_read_b128; wider layers run one block per 64-channel N slice;
 //  * patch rows are 128-byte voxel slices; 16-byte chunks XOR-swizzled by (patch x & 7),
 //    which makes every fragment read of every tap conflict-free (rows of a fragment are
@@ -38,12 +38,16 @@ namespace {
 // ring fit twice in the 160 KB LDS, so two blocks share a CU and one's per-tap barrier no
 // longer idles the MFMA pipes; measured against 4 x 8 x 8 boxes (one block per CU, twice
 // the tap reuse): layer1 fwd 90 -> 77 us, dgrad 85 -> 80 us, layer2.conv2 fwd 43 -> 37 us
-#ifndef MMAD_PATCH_TZ
-#define MMAD_PATCH_TZ 2
-#endif
-constexpr int TZ = MMAD_PATCH_TZ, TY = 8, TX = 8, TV = TZ * TY * TX;   // output voxels per tile
+// Output boxes TZ x 8 x 8.  TZ = 2 (two 4-wave blocks per CU) is the default; TZ = 4
+// (MMAD_PATCH_TZ4=1: one 8-wave block per CU, half the weight LDS-DMA per MAC, a 5-tap
+// weight lead) measured slower (layer1 fwd 77 vs 73 us).  Timing skeletons of the TZ = 2
+// form (the PATCH_NO_* build flags below, layer1 fwd): no MFMA 54 us, no MFMA and no
+// fragment reads 50 us, no MFMA and no weight DMA 42 us, no weight DMA 64 us -- the
+// per-tile patch prologue and epilogue, not the DMA bandwidth or the MFMAs, set the time.
+constexpr int TY = 8, TX = 8;
 constexpr int RB = 128;                                    // bytes per patch row / K slice
-constexpr int NST = 3;                                     // weight ring depth
+// weight ring depth: NST - 1 taps of weights in flight (an LDS-DMA lands ~1 us after issue)
+constexpr int nst_for(int tz) { return tz == 4 ? 6 : 3; }
 constexpr int LDS_MAX = 160 * 1024;
 
 struct PG {
@@ -58,16 +62,18 @@ struct PG {
 
 __device__ const u32x4 g_zero16[8] = {};
 
-template <int BN, int WGM, int WGN, int KS>
-__global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __restrict__ src,
+template <int BN, int WGM, int WGN, int KS, int TZ>
+__global__ __launch_bounds__(WGM * WGN * 64) void patch_conv_kernel(PG g, const u16* __restrict__ src,
                                                          const u16* __restrict__ wgt,
                                                          const float* __restrict__ bias,
                                                          u16* __restrict__ dst,
                                                          float* __restrict__ stats) {
-  static_assert(WGM * WGN == 4, "4 waves");
+  constexpr int NW = WGM * WGN, NTHR = NW * 64, TV = TZ * TY * TX, NST = nst_for(TZ);
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int WTM = TV / WGM, WTN = BN / WGN, TM = WTM / 16, TN = WTN / 16;
   constexpr int BSLOT = BN * RB;          // one tap's weights for the N tile
-  constexpr int BI = BN / 32;             // weight DMA instructions per wave per tap
+  constexpr int BI = BN * RB / 1024 / NW; // weight DMA instructions per wave per tap
+  static_assert(BI >= 1 && BI * NW * 1024 == BSLOT, "weight slot split over the waves");
   // compile-time patch geometry (cubic KS^3 stencil, dilation 1): every tap offset and
   // swizzle below folds to a constant, so the unrolled tap loop carries no index math
   constexpr int PX = TX + KS - 1, PY = TY + KS - 1, PZ = TZ + KS - 1;
@@ -93,8 +99,10 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
   const int z0 = bz * TZ, y0 = by * TY, x0 = bx * TX, n0 = nt * BN;
   const int lrow = lane >> 3;
 
+  // this sample's input (per-sample offsets fit 32 bits: checked in ok())
+  const u16* __restrict__ srcb = src + (int64_t)bn * g.Ds * g.Hs * g.Ws * g.Cs;
   auto issue_patch = [&](int cc) {
-    for (int q = wave; q < PROW8; q += 4) {
+    for (int q = wave; q < PROW8; q += NW) {
       const int r = q * 8 + lrow;
       const int px = r % PX, t2 = r / PX;          // constant divisors: mul-shift
       const int py = t2 % PY, pz = t2 / PY;
@@ -103,8 +111,7 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
       if (r < PROWS && (unsigned)z < (unsigned)g.Ds && (unsigned)y < (unsigned)g.Hs &&
           (unsigned)x < (unsigned)g.Ws) {
         const int chunk = (lane & 7) ^ (px & 7);
-        const int64_t vox = (((int64_t)bn * g.Ds + z) * g.Hs + y) * g.Ws + x;
-        p = src + vox * g.Cs + cc * 64 + chunk * 8;
+        p = srcb + (((z * g.Hs + y) * g.Ws + x) * g.Cs + cc * 64 + chunk * 8);
       }
       glds16_asm(p, lds_addr_of(patch + q * 1024));
     }
@@ -118,6 +125,9 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
   }
   // weights of stage (chunk cc, tap t) into ring slot `slot`
   auto issue_b = [&](int cc, int t, int slot) {
+#ifdef PATCH_NO_WDMA
+    return;
+#endif
     char* sb = ring + slot * BSLOT;
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
@@ -151,16 +161,33 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int p = pb[i] + delta;
+#ifdef PATCH_NO_AREAD                           // timing experiments (skeleton breakdown)
+      A[i] = bf16x8{};
+      asm volatile("" : "+v"(A[i]));
+#else
       A[i] = *reinterpret_cast<const bf16x8*>(patch + p * RB + ((c ^ ((ptx[i] + kx) & 7)) << 4));
+#endif
     }
     const char* sb = ring + slot * BSLOT;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int row = wn * WTN + j * 16 + lr;
+#ifdef PATCH_NO_BREAD
+      B[j] = bf16x8{};
+      asm volatile("" : "+v"(B[j]));
+#else
       B[j] = *reinterpret_cast<const bf16x8*>(sb + row * RB + ((c ^ (lr & 7)) << 4));
+#endif
     }
   };
   auto mma = [&](const bf16x8* A, const bf16x8* B) {
+#ifdef PATCH_NO_MFMA                            // timing experiment: memory/sync skeleton
+#pragma unroll
+    for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(A[i]));
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(B[j]));
+    return;
+#endif
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -168,14 +195,16 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
   };
 
-  // stage s = (chunk cc, tap t) lives in ring slot s % NST; weights run two taps ahead
+  // stage s = (chunk cc, tap t) lives in ring slot s % NST; weights run NST - 1 taps ahead
   const int S = g.nchunk * TAPS;
   issue_patch(0);
-  issue_b(0, 0, 0);
-  if (S > 1) issue_b(TAPS > 1 ? 0 : 1, TAPS > 1 ? 1 : 0, 1);
-  wait_vm_lgkm0<0>();
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < S) issue_b(s / TAPS, s % TAPS, s);
+  if (S >= NST - 1) wait_vm_lgkm0<(NST - 2) * BI>();   // the patch and stage 0 landed
+  else wait_vm_lgkm0<0>();
   raw_barrier();
-  if (S > 2) issue_b((2 / TAPS), 2 % TAPS, 2);
+  if (S > NST - 1) issue_b((NST - 1) / TAPS, (NST - 1) % TAPS, NST - 1);
   read_frags(0, 0, 0, fa0, fb0);
   for (int cc = 0; cc < g.nchunk; ++cc) {
 #pragma unroll
@@ -185,19 +214,19 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
       read_frags(t, slot, 1, fa1, fb1);
       mma(fa0, fb0);
       if (s + 1 < S) {
-        // weights of stage s+1 landed (s+2's, issued one tap ago, may still fly); every
-        // fragment read of stage s is done -> after the barrier its slot is free
-        if (s + 2 < S) wait_vm_lgkm0<BI>();
+        // weights of stage s+1 landed (s+2 .. s+NST-1 may still fly); every fragment read
+        // of stage s is done -> after the barrier its slot is free
+        if (s + NST - 1 < S) wait_vm_lgkm0<(NST - 2) * BI>();
         else wait_vm_lgkm0<0>();
         raw_barrier();
-        const int s3 = s + 3;
+        const int s3 = s + NST;
         if (t == TAPS - 1) {                   // next 64-channel chunk: reload the patch
           issue_patch(cc + 1);
           if (s3 < S) issue_b(s3 / TAPS, s3 % TAPS, slot);
           wait_vm_lgkm0<0>();
           raw_barrier();
         } else if (s3 < S) {
-          issue_b(t + 3 < TAPS ? cc : cc + 1, (t + 3) % TAPS, slot);
+          issue_b(t + NST < TAPS ? cc : cc + 1, (t + NST) % TAPS, slot);
         }
         read_frags((t + 1) % TAPS, (slot + 1) % NST, 0, fa0, fb0);
       }
@@ -206,11 +235,14 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
   }
   __syncthreads();                             // patch / ring reused by the epilogue
 
-  auto dst_vox = [&](int row, int64_t& dv) -> bool {
-    const int z = z0 + (row >> 6), y = y0 + ((row >> 3) & 7), x = x0 + (row & 7);
-    dv = (((int64_t)bn * g.Dd + z) * g.Hd + y) * g.Wd + x;
-    return z < g.Dd && y < g.Hd && x < g.Wd;
+  // output rows: box-relative voxel offsets in 32 bits from one 64-bit tile base; a box
+  // wholly inside the volume (every box of a 32^3 / 16^3 layer) skips the per-row checks
+  const bool full = z0 + TZ <= g.Dd && y0 + TY <= g.Hd && x0 + TX <= g.Wd;
+  const int64_t vbase = (((int64_t)bn * g.Dd + z0) * g.Hd + y0) * g.Wd + x0;
+  auto row_ok = [&](int row) {
+    return full || (z0 + (row >> 6) < g.Dd && y0 + ((row >> 3) & 7) < g.Hd && x0 + (row & 7) < g.Wd);
   };
+  auto row_off = [&](int row) { return ((row >> 6) * g.Hd + ((row >> 3) & 7)) * g.Wd + (row & 7); };
   constexpr int CROW = BN * 2 + 16;
   u16* ctile = reinterpret_cast<u16*>(smem);
   float cs[TN], cq[TN];
@@ -219,8 +251,8 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
     cs[j] = 0.f;
     cq[j] = 0.f;
     const int col = wn * WTN + j * 16 + lr;
-    const int co = n0 + col;
-    const float bv = (bias != nullptr && co < g.Nd) ? bias[co] : 0.f;
+    const int co = n0 + col;                   // < Nd: Nd % 64 == 0 (ok())
+    const float bv = bias != nullptr ? bias[co] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -228,8 +260,7 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
         const int row = wm * WTM + i * 16 + lk * 4 + r;
         const float v = acc[i][j][r] + bv;
         ctile[row * (CROW / 2) + col] = f2bf(v);
-        int64_t dv;
-        if (dst_vox(row, dv) && co < g.Nd) {
+        if (row_ok(row)) {
           cs[j] += v;
           cq[j] += v * v;
         }
@@ -237,18 +268,18 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
   }
   __syncthreads();
   constexpr int CPR = BN / 8;
+  u16* __restrict__ dstb = dst + vbase * g.Nd + n0;
+  const u16* __restrict__ resb = g.res != nullptr ? g.res + vbase * g.Nd + n0 : nullptr;
 #pragma unroll
-  for (int h = 0; h < TV * CPR / 256; ++h) {
-    const int q = tid + 256 * h;
+  for (int h = 0; h < TV * CPR / NTHR; ++h) {
+    const int q = tid + NTHR * h;
     const int row = q / CPR, c8 = q % CPR;
-    const int co = n0 + c8 * 8;
-    int64_t dv;
-    if (dst_vox(row, dv) && co < g.Nd) {
+    if (row_ok(row)) {
+      const int o = row_off(row) * g.Nd + c8 * 8;
       u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
                                                 row * CROW + c8 * 16);
-      if (g.res != nullptr || g.relu)
-        v = epi_res_relu(v, g.res ? g.res + dv * g.Nd + co : nullptr, g.relu);
-      *reinterpret_cast<u32x4*>(dst + dv * g.Nd + co) = v;
+      if (g.res != nullptr || g.relu) v = epi_res_relu(v, resb ? resb + o : nullptr, g.relu);
+      *reinterpret_cast<u32x4*>(dstb + o) = v;
     }
   }
   if (stats != nullptr) {
@@ -279,10 +310,8 @@ __global__ __launch_bounds__(256) void patch_conv_kernel(PG g, const u16* __rest
           ss += red[(w - 1) * 2 * BN + col];
           qs += red[(w - 1) * 2 * BN + BN + col];
         }
-        if (co < g.Nd) {
-          stats[((int64_t)mt * 2) * g.Nd + co] = ss;
-          stats[((int64_t)mt * 2 + 1) * g.Nd + co] = qs;
-        }
+        stats[((int64_t)mt * 2) * g.Nd + co] = ss;
+        stats[((int64_t)mt * 2 + 1) * g.Nd + co] = qs;
       }
     }
   }
@@ -297,7 +326,13 @@ int patch_mode() {
 // fully unrolled tap loop; wider layers run one block per 64-channel slice of the same box
 int bn_for(const mmad_patch::Geo&) { return 64; }
 
-PG make_pg(const mmad_patch::Geo& q) {
+// output-box depth: 2 (two 4-wave blocks per CU) unless MMAD_PATCH_TZ4=1 (4: one 8-wave block)
+int tz_for(const mmad_patch::Geo&) {
+  static const int v = [] { const char* e = getenv("MMAD_PATCH_TZ4"); return e && atoi(e) ? 4 : 2; }();
+  return v;
+}
+
+PG make_pg(const mmad_patch::Geo& q, int TZ) {
   PG g{};
   g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.Kpad = q.Kpad;
   g.Ds = q.Ds; g.Hs = q.Hs; g.Ws = q.Ws; g.Dd = q.Dd; g.Hd = q.Hd; g.Wd = q.Wd;
@@ -317,23 +352,24 @@ PG make_pg(const mmad_patch::Geo& q) {
   return g;
 }
 
-size_t lds_bytes(const PG& g, int bn, int wgm) {
-  const size_t main = (size_t)g.ring_off + (size_t)NST * bn * RB;
-  const size_t epi = (size_t)TV * (bn * 2 + 16) + (size_t)(wgm - 1) * 2 * bn * 4;
+size_t lds_bytes(const PG& g, int bn, int wgm, int TZ) {
+  const size_t main = (size_t)g.ring_off + (size_t)nst_for(TZ) * bn * RB;
+  const size_t epi = (size_t)TZ * TY * TX * (bn * 2 + 16) + (size_t)(wgm - 1) * 2 * bn * 4;
   return std::max(main, epi);
 }
 
-template <int BN, int WGM, int WGN, int KS>
+template <int BN, int WGM, int WGN, int KS, int TZ>
 int launch(const PG& g, const void* src, const void* wp, const float* bias, void* dst,
            float* stats, hipStream_t st) {
-  const size_t lds = lds_bytes(g, BN, WGM);
-  static const bool ok = hipFuncSetAttribute((const void*)patch_conv_kernel<BN, WGM, WGN, KS>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             LDS_MAX) == hipSuccess;
+  const size_t lds = lds_bytes(g, BN, WGM, TZ);
+  static const bool ok = hipFuncSetAttribute(
+                             (const void*)patch_conv_kernel<BN, WGM, WGN, KS, TZ>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX) == hipSuccess;
   if (!ok || lds > (size_t)LDS_MAX) return MMAD_EUNSUPPORTED;
   const int64_t nblk = (int64_t)g.nb * g.ntz * g.nty * g.ntx * g.nbn;
-  hipLaunchKernelGGL((patch_conv_kernel<BN, WGM, WGN, KS>), dim3((unsigned)nblk), dim3(256), lds,
-                     st, g, (const u16*)src, (const u16*)wp, bias, (u16*)dst, stats);
+  hipLaunchKernelGGL((patch_conv_kernel<BN, WGM, WGN, KS, TZ>), dim3((unsigned)nblk),
+                     dim3(WGM * WGN * 64), lds, st, g, (const u16*)src, (const u16*)wp, bias,
+                     (u16*)dst, stats);
   return launch_status();
 }
 
@@ -348,24 +384,28 @@ bool ok(const Geo& q) {
   if (mode == 1 && (q.Cs > 128 || q.Nd > 128)) return false;   // narrow layers only
   // compiled stencil: 3x3x3, dilation 1 (MedicalNet layer1/layer2 convs and their dgrads)
   if (q.KD != 3 || q.KH != 3 || q.KW != 3 || q.dd != 1 || q.dh != 1 || q.dw != 1) return false;
-  const PG g = make_pg(q);
-  if (lds_bytes(g, bn_for(q), bn_for(q) == 64 ? 4 : 2) > (size_t)LDS_MAX) return false;
-  const int64_t vox = (int64_t)q.nb * q.Ds * q.Hs * q.Ws;
-  return vox * q.Cs < (int64_t(1) << 40) && (int64_t)q.nb * g.ntz * g.nty * g.ntx * g.nbn <
-                                                 (int64_t(1) << 31);
+  const int tz = tz_for(q);
+  const PG g = make_pg(q, tz);
+  if (lds_bytes(g, bn_for(q), tz == 4 ? 8 : 4, tz) > (size_t)LDS_MAX) return false;
+  // per-sample input / output offsets in 32 bits (the patch DMA and epilogue index math)
+  const int64_t ivox = (int64_t)q.Ds * q.Hs * q.Ws, ovox = (int64_t)q.Dd * q.Hd * q.Wd;
+  return ivox * q.Cs < (int64_t(1) << 31) && ovox * q.Nd < (int64_t(1) << 31) &&
+         (int64_t)q.nb * g.ntz * g.nty * g.ntx * g.nbn < (int64_t(1) << 31);
 }
 
 int64_t tiles(const Geo& q) {
-  const PG g = make_pg(q);
+  const PG g = make_pg(q, tz_for(q));
   return (int64_t)q.nb * g.ntz * g.nty * g.ntx;
 }
 
 int fwd(const Geo& q, const void* src, const void* wp, const float* bias, void* dst,
         float* stats, void* stream) {
   if (!ok(q)) return MMAD_EUNSUPPORTED;
-  const PG g = make_pg(q);
+  const int tz = tz_for(q);
+  const PG g = make_pg(q, tz);
   hipStream_t st = as_stream(stream);
-  return launch<64, 4, 1, 3>(g, src, wp, bias, dst, stats, st);
+  if (tz == 4) return launch<64, 8, 1, 3, 4>(g, src, wp, bias, dst, stats, st);
+  return launch<64, 4, 1, 3, 2>(g, src, wp, bias, dst, stats, st);
 }
 
 }  // namespace mmad_patch
