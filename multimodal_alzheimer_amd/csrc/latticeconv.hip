@@ -19,10 +19,11 @@
 //    "patch", and each tap's fragments are read from it at a shifted row -- one LDS-DMA per
 //    input voxel per channel chunk per tile instead of one per tap;
 //  * only the weights stream per tap (128 output channels x 32 input channels = 8 KiB per
-//    stage, 3-slot ring, two stages in flight): per wave one 1 KiB LDS-DMA per stage where
-//    the row-gather implicit GEMM (conv.hip) issues eight;
-//  * the plane the next channel chunk needs is loaded as soon as the current chunk's last
-//    tap on that plane has run (the loop walks taps plane by plane), 18 stages ahead;
+//    tap, 24 KiB per 3-tap stage, a 3-slot ring with two stages in flight): per wave three
+//    1 KiB LDS-DMAs per stage;
+//  * the loop walks (chunk, kz) groups of three stages that read ONE input plane each, so
+//    the patch is a 2-slot plane ring: the next group's plane is loaded while the current
+//    group runs (3 stages ahead);
 //  * 8 waves = 4 x 2 wave tiles of 128 rows x 64 channels; wave wm takes the positions of
 //    one diagonal of the 4 x 4 plane, (t, (t + wm) & 3), so every wave loses the same number
 //    of fragments to padding on every tap (a row of the plane would idle the edge waves);
@@ -51,8 +52,16 @@ constexpr int BNL = 128;                  // output channels per tile
 constexpr int TPS = 3;                    // taps per stage (one kx row)
 constexpr int BTAP = BNL * RBL;           // one tap's weights: 8 KiB
 constexpr int BSLOT = TPS * BTAP;         // one stage: 24 KiB
-constexpr int NSTL = 2;                   // weight ring slots
-constexpr int RING_OFF = 3 * PLANE;
+// weight ring slots: NSTL - 1 stages of weights in flight (an LDS-DMA lands ~1 us after
+// issue, about one stage of MFMAs); the patch holds 2 plane slots, since a stage group
+// (one kz plane of one chunk) reads a single plane and the next group's plane streams in
+// during it
+#ifndef LAT_NSTL
+#define LAT_NSTL 3
+#endif
+constexpr int NSTL = LAT_NSTL;
+constexpr int NPS = 2;                    // patch plane slots
+constexpr int RING_OFF = NPS * PLANE;
 constexpr int MAIN_LDS = RING_OFF + NSTL * BSLOT;
 constexpr int CROW = BNL * 2 + 16;
 constexpr int EPI_LDS = PL * CROW + 3 * 2 * BNL * 4;
@@ -167,9 +176,9 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
     pvox[k] = (((int64_t)n * E + rz) * E + ry + d * ty) * E + rx + d * tx;
     pchunk[k] = (lane & 3) ^ swz(row);
   }
-  auto issue_plane = [&](int p, int cc) {
-    const int64_t zoff = (int64_t)(tz - 1 + p) * plane_vox;
-    char* pb = smem + p * PLANE;
+  auto issue_plane = [&](int kz, int cc, int slot) {
+    const int64_t zoff = (int64_t)(tz + kz) * plane_vox;
+    char* pb = smem + slot * PLANE;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const u16* a = src + (pvox[k] + zoff) * g.Cs + cc * KC + pchunk[k] * 8;
@@ -178,8 +187,10 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   };
   // ---- weight DMA: stage (chunk cc, first tap t) into ring slot sl: 3 consecutive taps
   // (one kx row), 16 rows per wave per tap
-  // 2*TN instructions of 16 rows per tap, 6*TN per stage: wave w issues q = w + 8h
-  constexpr int NQ = TPS * 2 * TN;
+  // 2*TN instructions of 16 rows per tap, 6*TN per stage: wave w issues q = w + 8h (the
+  // same count WI on every wave -- surplus slots repeat the last row -- so the counted
+  // vmcnt waits below hold on every wave)
+  constexpr int NQ = TPS * 2 * TN, WI = (NQ + 7) / 8;
   const u16* wq[3];
   int wq_off[3];
 #pragma unroll
@@ -192,29 +203,18 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   }
   auto issue_b = [&](int cc, int t, int sl) {
 #pragma unroll
-    for (int h = 0; h < 3; ++h)
-      if (wave + 8 * h < NQ)
-        glds16_asm(wq[h] + t * g.Cs + cc * KC, lds_addr_of(ring + sl * BSLOT + wq_off[h]));
+    for (int h = 0; h < WI; ++h)
+      glds16_asm(wq[h] + t * g.Cs + cc * KC, lds_addr_of(ring + sl * BSLOT + wq_off[h]));
   };
 
-  // stage list: chunk-major, then the valid kz planes, then ky; a stage runs kx = -1, 0, 1
+  // stage list: chunk-major, then the valid kz planes, then ky; a stage runs kx = -1, 0, 1.
+  // Group u = (chunk, kz) of 3 stages reads plane slot u % 2.
   const int kz0 = tz == 0 ? 0 : -1, kz1 = tz == S - 1 ? 0 : 1;
-  const int nspc = (kz1 - kz0 + 1) * 3;             // stages per chunk
-  const int nstage = g.nchunk * nspc;
-  auto stage_of = [&](int s, int& cc, int& kz, int& ky) {
-    cc = s / nspc;
-    const int r = s - cc * nspc;
-    kz = kz0 + r / 3;
-    ky = r % 3 - 1;
-  };
-  // a plane slot is reloaded (next chunk) at the stage after its last stage of this chunk
-  auto plane_due = [&](int s, int& p, int& cc) -> bool {
-    if (s < 1) return false;
-    const int c = (s - 1) / nspc, r = (s - 1) - c * nspc;
-    if (r % 3 != 2 || c + 1 >= g.nchunk) return false;
-    p = kz0 + r / 3 + 1;
-    cc = c + 1;
-    return true;
+  const int nkz = kz1 - kz0 + 1;
+  const int ngrp = g.nchunk * nkz;                  // (chunk, kz) groups
+  const int nstage = ngrp * 3;
+  auto issue_group_plane = [&](int u) {
+    issue_plane(kz0 + u % nkz, u / nkz, u % NPS);
   };
 
   // wave tiles: wm -> diagonal positions (t, (t + wm) & 3), wn -> 64 output channels
@@ -228,57 +228,54 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto stage_w = [&](int s, int& cc, int& t) {       // packed-weight tap of stage s, kx = -1
-    int kz, ky;
-    stage_of(s, cc, kz, ky);
-    t = (kz + 1) * 9 + (ky + 1) * 3;
+  auto issue_stage_b = [&](int s) {                 // weights of stage s (kx = -1 .. 1)
+    const int u = s / 3, ky = s % 3 - 1;
+    const int cc = u / nkz, kz = kz0 + u % nkz;
+    issue_b(cc, (kz + 1) * 9 + (ky + 1) * 3, s % NSTL);
   };
-  // prologue: the chunk-0 planes, weights of stage 0
-  for (int p = 0; p < 3; ++p) {
-    const int kz = p - 1;
-    if (kz >= kz0 && kz <= kz1) issue_plane(p, 0);
-  }
-  {
-    int cc, t;
-    stage_w(0, cc, t);
-    issue_b(cc, t, 0);
-  }
+  // prologue: plane of group 0, weights of stage 0, plane of group 1, weights of stages
+  // 1 .. NSTL-2; everything lands before stage 0 (one tile per CU: paid once)
+  issue_group_plane(0);
+  issue_stage_b(0);
+  if (ngrp > 1) issue_group_plane(1);
+#pragma unroll
+  for (int s = 1; s < NSTL - 1; ++s)
+    if (s < nstage) issue_stage_b(s);
   // Main loop, compiled once per wave diagonal WM with the three ky stages of a (chunk,
   // kz) group unrolled, so every padding test in the stage bodies is a compile-time
   // constant: no branch sits between a fragment read and its MFMA, and the next tap's reads
   // stay in flight during each tap's MFMAs.
-  bool plane_prev = false;                          // a plane was issued at stage s-1
-  auto one_stage = [&](int s) {
-    // B(s) (issued at stage s-1) must have landed; a plane issued after it may still fly
-    if (plane_prev) wait_vm_lgkm0<4>();
-    else wait_vm_lgkm0<0>();
+  //
+  // Stage s = 3u + r waits for its weights (issued at stage s - NSTL + 1); younger are the
+  // weights of the next NSTL - 2 stages and, for 0 < r <= NSTL - 2, the plane of group
+  // u + 1 (issued at stage 3u, before that stage's weights, so the wait at stage 3u + 3 --
+  // its first use -- forces it).
+  auto one_stage = [&](int s, auto rc, bool plane_young) {
+    constexpr int R = decltype(rc)::value;
+    constexpr int YW = (NSTL - 2) * WI;             // younger weight DMAs per wave
+    constexpr bool PW = R != 0 && R <= NSTL - 2;    // group plane issued inside the window
+    if (s == 0 || s + NSTL - 2 >= nstage) wait_vm_lgkm0<0>();
+    else if (PW && plane_young) wait_vm_lgkm0<YW + 4>();
+    else wait_vm_lgkm0<YW>();
     raw_barrier();
-    plane_prev = false;
+    if (R == 0 && s > 0 && s / 3 + 1 < ngrp) issue_group_plane(s / 3 + 1);
 #ifndef LAT_NO_B
-    if (s + 1 < nstage) {
-      int cc, t;
-      stage_w(s + 1, cc, t);
-      issue_b(cc, t, (s + 1) % NSTL);
-    }
+    if (s + NSTL - 1 < nstage) issue_stage_b(s + NSTL - 1);
 #endif
-    int p, pc;
-    if (plane_due(s, p, pc)) {
-      issue_plane(p, pc);
-      plane_prev = true;
-    }
   };
   auto run = [&](auto wmc) {
     constexpr int WM = decltype(wmc)::value;
-    const int ngrp = nstage / 3;                    // (chunk, kz) groups
-    for (int g2 = 0; g2 < ngrp; ++g2) {
-      const int kz = kz0 + g2 % (kz1 - kz0 + 1);
-      const char* apl = smem + (kz + 1) * PLANE + a_lane;
-      const int s0 = g2 * 3;
-      one_stage(s0);
+    for (int u = 0; u < ngrp; ++u) {
+      const char* apl = smem + (u % NPS) * PLANE + a_lane;
+      const int s0 = u * 3;
+      // the plane of group u + 1 was issued at stage s0 (u >= 1) and is younger than the
+      // weights waited for at stages s0 + 1 .. s0 + NSTL - 2
+      const bool py = u >= 1 && u + 1 < ngrp;
+      one_stage(s0, std::integral_constant<int, 0>{}, py);
       stage_body<TN, WM, -1>(acc, ring + (s0 % NSTL) * BSLOT + b_lane, apl);
-      one_stage(s0 + 1);
+      one_stage(s0 + 1, std::integral_constant<int, 1>{}, py);
       stage_body<TN, WM, 0>(acc, ring + ((s0 + 1) % NSTL) * BSLOT + b_lane, apl);
-      one_stage(s0 + 2);
+      one_stage(s0 + 2, std::integral_constant<int, 2>{}, py);
       stage_body<TN, WM, 1>(acc, ring + ((s0 + 2) % NSTL) * BSLOT + b_lane, apl);
     }
   };
