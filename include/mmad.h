@@ -143,6 +143,27 @@ int mmad_bn_finalize(int c, int64_t count, int nparts, const float* parts,
                      float* mean, float* invstd, float* scale, float* shift,
                      int64_t* num_batches_tracked, void* stream);
                      /* num_batches_tracked (nullable) += 1 with the running-stat update */
+/* mmad_bn_finalize's arguments for one BN (all but c / count) */
+typedef struct mmad_bn_fin {
+  int nparts;
+  const float* parts;
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  float momentum;
+  float eps;
+  int training;
+  float* mean;
+  float* invstd;
+  float* scale;
+  float* shift;
+  int64_t* num_batches_tracked;
+} mmad_bn_fin;
+/* the two BNs of a residual pair (same c and count: bn2 and the shortcut BN) in one launch;
+ * each set exactly as one mmad_bn_finalize call */
+int mmad_bn_finalize2(int c, int64_t count, const mmad_bn_fin* a, const mmad_bn_fin* b,
+                      void* stream);
 /* out = act(y*scale + shift + R), R = res*rscale + rshift | res | 0; act = relu|id */
 int mmad_scale_shift_act(int dtype, int64_t m, int c, const void* y, const float* scale,
                          const float* shift, const void* res, const float* rscale,

@@ -44,6 +44,16 @@ class PackDual(C.Structure):
                 [(n, C.c_int32) for n in ("co", "ci", "taps", "flip")] + [("tile0", C.c_int64)])
 
 
+class BnFin(C.Structure):
+    """mirror of mmad_bn_fin (include/mmad.h)"""
+    _fields_ = ([("nparts", C.c_int32)] +
+                [(n, C.c_void_p) for n in ("parts", "gamma", "beta", "running_mean",
+                                           "running_var")] +
+                [("momentum", C.c_float), ("eps", C.c_float), ("training", C.c_int32)] +
+                [(n, C.c_void_p) for n in ("mean", "invstd", "scale", "shift",
+                                           "num_batches_tracked")])
+
+
 _P = C.POINTER(ConvDesc)
 _PJ = C.POINTER(PackJob)
 _PD = C.POINTER(PackDual)
@@ -70,6 +80,7 @@ _SIGS = {
     "mmad_bn_parts_fold": (_i32, [_i32, _i32, _vp, _i32, _vp, _vp]),
     "mmad_bn_finalize": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _i32,
                                 _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_bn_finalize2": (_i32, [_i32, _i64, C.POINTER(BnFin), C.POINTER(BnFin), _vp]),
     "mmad_scale_shift_act": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
                                     _vp]),
     "mmad_bn_bwd_parts": (_i64, [_i64, _i32]),

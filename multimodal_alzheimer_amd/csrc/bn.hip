@@ -275,12 +275,13 @@ __device__ __forceinline__ void sum_parts(int c, int C, int nparts, const float*
   }
 }
 
-__global__ __launch_bounds__(1024) void bn_finalize_kernel(
-    int C, int64_t count, int nparts, const float* __restrict__ parts,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
-    float* running_var, float momentum, float eps, int training, float* mean_out,
-    float* invstd_out, float* scale_out, float* shift_out, int64_t* nbt) {
-  __shared__ double sm[2048];
+__device__ __forceinline__ void finalize_body(int C, int64_t count, int nparts,
+                                              const float* parts, const float* gamma,
+                                              const float* beta, float* running_mean,
+                                              float* running_var, float momentum, float eps,
+                                              int training, float* mean_out, float* invstd_out,
+                                              float* scale_out, float* shift_out, int64_t* nbt,
+                                              double* sm) {
   const int c = blockIdx.x * FC + (threadIdx.x % FC);
   double S, Q;
   if (training) {
@@ -310,6 +311,26 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
   if (invstd_out) invstd_out[c] = is;
   if (scale_out) scale_out[c] = gm * is;
   if (shift_out) shift_out[c] = bt - (float)mean * gm * is;
+}
+
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(
+    int C, int64_t count, int nparts, const float* __restrict__ parts,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
+    float* running_var, float momentum, float eps, int training, float* mean_out,
+    float* invstd_out, float* scale_out, float* shift_out, int64_t* nbt) {
+  __shared__ double sm[2048];
+  finalize_body(C, count, nparts, parts, gamma, beta, running_mean, running_var, momentum, eps,
+                training, mean_out, invstd_out, scale_out, shift_out, nbt, sm);
+}
+
+// the two BNs of a residual pair (main and shortcut) in one launch: blockIdx.y picks the set
+__global__ __launch_bounds__(1024) void bn_finalize2_kernel(int C, int64_t count, mmad_bn_fin a,
+                                                            mmad_bn_fin b) {
+  __shared__ double sm[2048];
+  const mmad_bn_fin& f = blockIdx.y ? b : a;
+  finalize_body(C, count, f.nparts, f.parts, f.gamma, f.beta, f.running_mean, f.running_var,
+                f.momentum, f.eps, f.training, f.mean, f.invstd, f.scale, f.shift,
+                f.num_batches_tracked, sm);
 }
 
 // eval-mode BN folded into the preceding conv: scale = gamma / sqrt(var + eps),
@@ -703,6 +724,19 @@ int mmad_colsum_ws(int dtype, int64_t m, int c, const void* y, float* parts, flo
   if (rc) return rc;
   hipLaunchKernelGGL(sum_only_finalize_kernel, dim3((unsigned)cdiv(c, FC)), dim3(1024), 0,
                      as_stream(stream), c, part_plan(m).nparts, parts, out);
+  return launch_status();
+}
+
+int mmad_bn_finalize2(int c, int64_t count, const mmad_bn_fin* a, const mmad_bn_fin* b,
+                      void* stream) {
+  if (c <= 0 || count <= 0) return MMAD_EBADSHAPE;
+  if (!a || !b) return MMAD_ENULL;
+  for (const mmad_bn_fin* f : {a, b}) {
+    if (f->training && (!f->parts || f->nparts <= 0)) return MMAD_ENULL;
+    if (!f->training && (!f->running_mean || !f->running_var)) return MMAD_ENULL;
+  }
+  hipLaunchKernelGGL(bn_finalize2_kernel, dim3((unsigned)cdiv(c, FC), 2), dim3(1024), 0,
+                     as_stream(stream), c, count, *a, *b);
   return launch_status();
 }
 

@@ -498,8 +498,9 @@ def _rows(t):
     return t.numel() // c, c
 
 
-def _finalize(y, parts, bn, training):
-    """batch (or running) statistics -> mean, invstd, scale, shift; updates running stats."""
+def _finalize_args(y, parts, bn, training):
+    """(mmad_bn_fin for this BN, (mean, invstd, scale, shift, use_batch)); folds very long
+    partial-sum lists first and counts the running-statistics update."""
     m, c = _rows(y)
     dev = y.device
     mean = torch.empty(c, dtype=torch.float32, device=dev)
@@ -509,6 +510,11 @@ def _finalize(y, parts, bn, training):
     gamma = None if bn.weight is None else bn.weight.detach()
     beta = None if bn.bias is None else bn.bias.detach()
     use_batch = training or bn.running_mean is None
+    f = L.BnFin()
+    f.gamma, f.beta = _addr(gamma), _addr(beta)
+    f.eps = float(bn.eps)
+    f.mean, f.invstd, f.scale, f.shift = _addr(mean), _addr(invstd), _addr(scale), _addr(shift)
+    keep = [gamma, beta]
     if use_batch:
         if parts is None:
             nparts = L.load().mmad_bn_stats_parts(m, c)
@@ -532,16 +538,43 @@ def _finalize(y, parts, bn, training):
             nbt = bn.num_batches_tracked
             if nbt.dtype != torch.int64 or nbt.device != dev:
                 raise L.MMADError("num_batches_tracked must be an int64 tensor on the device")
-        L.call("mmad_bn_finalize", c, m, parts.shape[0], L.ptr(parts), L.ptr(gamma),
-               L.ptr(beta), L.ptr(bn.running_mean if update else None),
-               L.ptr(bn.running_var if update else None), float(bn.momentum or 0.0),
-               float(bn.eps), 1, L.ptr(mean), L.ptr(invstd), L.ptr(scale), L.ptr(shift),
-               L.ptr(nbt), L.stream())
+        f.nparts, f.parts = parts.shape[0], _addr(parts)
+        f.running_mean = _addr(bn.running_mean if update else None)
+        f.running_var = _addr(bn.running_var if update else None)
+        f.momentum = float(bn.momentum or 0.0)
+        f.training = 1
+        f.num_batches_tracked = _addr(nbt)
+        keep.append(parts)
     else:
-        L.call("mmad_bn_finalize", c, m, 0, None, L.ptr(gamma), L.ptr(beta),
-               L.ptr(bn.running_mean), L.ptr(bn.running_var), 0.0, float(bn.eps), 0,
-               L.ptr(mean), L.ptr(invstd), L.ptr(scale), L.ptr(shift), None, L.stream())
-    return mean, invstd, scale, shift, use_batch
+        f.nparts, f.parts = 0, None
+        f.running_mean, f.running_var = _addr(bn.running_mean), _addr(bn.running_var)
+        f.momentum, f.training, f.num_batches_tracked = 0.0, 0, None
+    f._keep = keep                       # the tensors the struct points at stay alive
+    return f, (mean, invstd, scale, shift, use_batch)
+
+
+def _addr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _finalize(y, parts, bn, training):
+    """batch (or running) statistics -> mean, invstd, scale, shift; updates running stats."""
+    m, c = _rows(y)
+    f, out = _finalize_args(y, parts, bn, training)
+    L.call("mmad_bn_finalize", c, m, f.nparts, f.parts, f.gamma, f.beta, f.running_mean,
+           f.running_var, f.momentum, f.eps, f.training, f.mean, f.invstd, f.scale, f.shift,
+           f.num_batches_tracked, L.stream())
+    return out
+
+
+def _finalize_pair(y, parts, bn, res, res_parts, rbn, training):
+    """_finalize for bn(y) and the shortcut rbn(res) of a residual pair in one launch
+    (mmad_bn_finalize2; each set computed exactly as by _finalize)."""
+    m, c = _rows(y)
+    fa, a = _finalize_args(y, parts, bn, training)
+    fb, b = _finalize_args(res, res_parts, rbn, training)
+    L.call("mmad_bn_finalize2", c, m, C.byref(fa), C.byref(fb), L.stream())
+    return a, b
 
 
 def _mask_from_y_ok(y):
@@ -625,11 +658,15 @@ class _BNActFn(torch.autograd.Function):
     def forward(ctx, y, parts, gamma, beta, res, res_parts, rgamma, rbeta, cfg):
         bn, relu, training, rbn = cfg
         L.require_device(y)
-        mean, invstd, scale, shift, batch = _finalize(y, parts, bn, training)
         rscale = rshift = rmean = rinvstd = None
         rbatch = False
-        if rbn is not None:
-            rmean, rinvstd, rscale, rshift, rbatch = _finalize(res, res_parts, rbn, training)
+        if rbn is not None and _BN_DUAL:
+            (mean, invstd, scale, shift, batch), (rmean, rinvstd, rscale, rshift, rbatch) = \
+                _finalize_pair(y, parts, bn, res, res_parts, rbn, training)
+        else:
+            mean, invstd, scale, shift, batch = _finalize(y, parts, bn, training)
+            if rbn is not None:
+                rmean, rinvstd, rscale, rshift, rbatch = _finalize(res, res_parts, rbn, training)
         out = torch.empty_like(y)
         m, c = _rows(y)
         L.call("mmad_scale_shift_act", L.dtype_code(y.dtype), m, c, L.ptr(y), L.ptr(scale),

@@ -176,8 +176,9 @@ def test_batchnorm_act(mode, dtype):
 @pytest.mark.parametrize("training", [True, False])
 @pytest.mark.parametrize("c", [64, 512])
 def test_bn_residual_pair_dual_bitexact(dtype, training, c):
-    """relu(bn(y) + bn_r(res)) backward through the one-pass pair kernels
-    (mmad_bn_bwd_reduce2 / _finalize2 / _apply2) == the per-BN calls, bit for bit."""
+    """relu(bn(y) + bn_r(res)) forward statistics (mmad_bn_finalize2) and backward through
+    the one-pass pair kernels (mmad_bn_bwd_reduce2 / _finalize2 / _apply2) == the per-BN
+    calls, bit for bit (outputs, gradients, running statistics)."""
     n, d, h, w = 2, 4, 6, 5
     y0 = rnd(n, c, d, h, w, seed=80, scale=2.0) + 0.5
     r0 = rnd(n, c, d, h, w, seed=81)
@@ -197,8 +198,10 @@ def test_bn_residual_pair_dual_bitexact(dtype, training, c):
             V._BN_DUAL = old
         torch.cuda.synchronize()
         res[dual] = (out, yg.grad, rg.grad, bn.weight.grad, bn.bias.grad, rbn.weight.grad,
-                     rbn.bias.grad)
-    names = ("out", "dy", "dres", "dgamma", "dbeta", "dgamma_res", "dbeta_res")
+                     rbn.bias.grad, bn.running_mean, bn.running_var, rbn.running_mean,
+                     rbn.running_var, bn.num_batches_tracked, rbn.num_batches_tracked)
+    names = ("out", "dy", "dres", "dgamma", "dbeta", "dgamma_res", "dbeta_res", "running_mean",
+             "running_var", "running_mean_res", "running_var_res", "nbt", "nbt_res")
     for nm, a, b in zip(names, res[False], res[True]):
         assert torch.equal(a, b), nm
 
