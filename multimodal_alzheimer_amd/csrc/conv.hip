@@ -1059,7 +1059,21 @@ __global__ __launch_bounds__(256) void unfold_w_rows_kernel(const TI* __restrict
   __shared__ float row[UNF_RB * UNF_MAXW];
   const int64_t r0 = (int64_t)blockIdx.x * UNF_RB;
   const int nr = (int)min((int64_t)UNF_RB, rows - r0);
-  for (int k = threadIdx.x; k < nr * Wi; k += 256) row[k] = (float)x[r0 * Wi + k];
+  // all of a thread's loads issued before any is used (one memory round trip per block,
+  // not one per loop trip: the rolled loop waited on each load, 55 us at 128^3 x 8)
+  constexpr int PER = UNF_RB * UNF_MAXW / 256;
+  const int nel = nr * Wi;
+  float v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = threadIdx.x + 256 * i;
+    v[i] = k < nel ? (float)x[r0 * Wi + k] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = threadIdx.x + 256 * i;
+    if (k < nel) row[k] = v[i];
+  }
   __syncthreads();
   for (int k = threadIdx.x; k < nr * Wo; k += 256) {
     const int r = k / Wo, xo = k - r * Wo;
