@@ -163,9 +163,11 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
 
   // ---- patch DMA: plane slot p <- absolute plane tz - 1 + p of chunk cc (32 rows per
   // wave: 4 instructions of 16 rows x 64 B); every row is a real voxel (no halo rows)
+  // (per-lane DMA offsets in 32 bits from uniform bases: this sample's volume and the
+  // packed weights, both < 2^31 elements -- checked in ok(); fewer VGPRs than pointers)
   const int lrow = lane >> 2;
-  int64_t pvox[4];
-  int pchunk[4];
+  const u16* __restrict__ srcn = src + (int64_t)n * E * E * E * g.Cs;
+  uint32_t pofs[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int row = (wave * 4 + k) * 16 + lrow;
@@ -173,17 +175,15 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
     const int q = q0 + s;
     const int rz = q / (d * d), ry = (q / d) % d, rx = q % d;
     const int ty = pos / S, tx = pos % S;
-    pvox[k] = (((int64_t)n * E + rz) * E + ry + d * ty) * E + rx + d * tx;
-    pchunk[k] = (lane & 3) ^ swz(row);
+    const int vox = (rz * E + ry + d * ty) * E + rx + d * tx;
+    pofs[k] = (uint32_t)(vox * g.Cs + ((lane & 3) ^ swz(row)) * 8);
   }
   auto issue_plane = [&](int kz, int cc, int slot) {
-    const int64_t zoff = (int64_t)(tz + kz) * plane_vox;
+    const u16* base = srcn + (int64_t)(tz + kz) * plane_vox * g.Cs + cc * KC;
     char* pb = smem + slot * PLANE;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const u16* a = src + (pvox[k] + zoff) * g.Cs + cc * KC + pchunk[k] * 8;
-      glds16_asm(a, lds_addr_of(pb + (wave * 4 + k) * 1024));
-    }
+    for (int k = 0; k < 4; ++k)
+      glds16_asm(base + pofs[k], lds_addr_of(pb + (wave * 4 + k) * 1024));
   };
   // ---- weight DMA: stage (chunk cc, first tap t) into ring slot sl: 3 consecutive taps
   // (one kx row), 16 rows per wave per tap
@@ -191,20 +191,21 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   // same count WI on every wave -- surplus slots repeat the last row -- so the counted
   // vmcnt waits below hold on every wave)
   constexpr int NQ = TPS * 2 * TN, WI = (NQ + 7) / 8;
-  const u16* wq[3];
+  uint32_t wofs[3];
   int wq_off[3];
 #pragma unroll
   for (int h = 0; h < 3; ++h) {
     const int q = min(wave + 8 * h, NQ - 1);
     const int tk = q / (2 * TN), rb = q % (2 * TN);
     const int row = rb * 16 + lrow;
-    wq[h] = wgt + (int64_t)(n0 + row) * g.Kpad + (((lane & 3) ^ swz(row)) * 8) + tk * g.Cs;
+    wofs[h] = (uint32_t)((n0 + row) * g.Kpad + (((lane & 3) ^ swz(row)) * 8) + tk * g.Cs);
     wq_off[h] = tk * BTAP + rb * 1024;
   }
   auto issue_b = [&](int cc, int t, int sl) {
+    const u16* base = wgt + t * g.Cs + cc * KC;
 #pragma unroll
     for (int h = 0; h < WI; ++h)
-      glds16_asm(wq[h] + t * g.Cs + cc * KC, lds_addr_of(ring + sl * BSLOT + wq_off[h]));
+      glds16_asm(base + wofs[h], lds_addr_of(ring + sl * BSLOT + wq_off[h]));
   };
 
   // stage list: chunk-major, then the valid kz planes, then ky; a stage runs kx = -1, 0, 1.
@@ -687,6 +688,10 @@ bool ok(const mmad_patch::Geo& q) {
   if (q.Ds != E || q.Hs != E || q.Ws != E || q.Dd != E || q.Hd != E || q.Wd != E) return false;
   if ((d * d * d) % NS) return false;
   if (q.Cs % KC || q.Nd % 64 || q.Kpad != 27 * q.Cs) return false;
+  // 32-bit per-lane DMA offsets (lattice_conv_kernel): one sample's volume, the packed weights
+  if ((int64_t)E * E * E * q.Cs >= (int64_t(1) << 31) ||
+      (int64_t)q.Nd * q.Kpad >= (int64_t(1) << 31))
+    return false;
   // one 512-thread block per CU: tiles too few for the CUs even at 64 channels leave the
   // row-gather implicit GEMM (more, smaller blocks) ahead
   if (lattice_mode() == 1 && mmad_lattice::tiles(q) * (q.Nd / 64) < 256) return false;
