@@ -149,6 +149,7 @@ __global__ __launch_bounds__(256) void loss_kernel(int B, int C, const double* _
   double num = 0.0, den = 0.0;
   const int igamma = (int)gamma;
   const bool int_gamma = (double)igamma == gamma && igamma >= 0 && igamma <= 16;
+  double lse_first = 0.0;                        // this thread's first sample's lse, reused
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const int64_t t = y[b];
     if (t < 0 || t >= C) { if (err) *err = 1; continue; }
@@ -157,6 +158,7 @@ __global__ __launch_bounds__(256) void loss_kernel(int B, int C, const double* _
     double se = 0.0;
     for (int c = 0; c < C; ++c) se += exp(x[(int64_t)b * C + c] - mx);
     const double lse = mx + log(se);
+    if (b == (int)threadIdx.x) lse_first = lse;
     const double logpt = x[(int64_t)b * C + t] - lse;
     if (mode == 0) {
       const double wt = w ? w[t] : 1.0;
@@ -175,8 +177,10 @@ __global__ __launch_bounds__(256) void loss_kernel(int B, int C, const double* _
   red[1][threadIdx.x] = den;
   __syncthreads();
   if (threadIdx.x == 0) {
+    // threads >= B hold +0.0 partials: leaving them out changes no bit of the sums
     double a = 0.0, d = 0.0;
-    for (int k = 0; k < (int)blockDim.x; ++k) { a += red[0][k]; d += red[1][k]; }
+    const int nk = min((int)blockDim.x, B);
+    for (int k = 0; k < nk; ++k) { a += red[0][k]; d += red[1][k]; }
     red[0][0] = a;
     red[1][0] = d;
     *loss = a / d;
@@ -187,11 +191,14 @@ __global__ __launch_bounds__(256) void loss_kernel(int B, int C, const double* _
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const int64_t t = y[b];
     if (t < 0 || t >= C) continue;
-    double mx = -__builtin_inf();
-    for (int c = 0; c < C; ++c) mx = fmax(mx, x[(int64_t)b * C + c]);
-    double se = 0.0;
-    for (int c = 0; c < C; ++c) se += exp(x[(int64_t)b * C + c] - mx);
-    const double lse = mx + log(se);
+    double lse = lse_first;
+    if (b != (int)threadIdx.x) {
+      double mx = -__builtin_inf();
+      for (int c = 0; c < C; ++c) mx = fmax(mx, x[(int64_t)b * C + c]);
+      double se = 0.0;
+      for (int c = 0; c < C; ++c) se += exp(x[(int64_t)b * C + c] - mx);
+      lse = mx + log(se);
+    }
     double coef;
     if (mode == 0) {
       coef = (w ? w[t] : 1.0) / den_all;
@@ -417,7 +424,9 @@ int mmad_loss_fwd(int b, int c, const double* logits, const int64_t* labels, con
                   double gamma, int mode, double* loss, double* dlogits, void* stream) {
   if (b <= 0 || c <= 0 || (mode != 0 && mode != 1)) return MMAD_EBADSHAPE;
   if (!logits || !labels || !loss || !dlogits) return MMAD_ENULL;
-  hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, as_stream(stream), b, c, logits, labels,
+  // one wave for small batches (the usual 8-16 samples), up to 256 threads beyond
+  const unsigned nt = (unsigned)std::min(256, (int)cdiv(b, 64) * 64);
+  hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(nt), 0, as_stream(stream), b, c, logits, labels,
                      weight, gamma, mode, loss, dlogits, (int*)nullptr);
   return launch_status();
 }
