@@ -126,6 +126,12 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy,
 int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype); /* bytes */
 int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,
                       float* dw, float* dbias, void* workspace, void* stream);
+/* Same, with the split-K slab reduction (and dbias) queued on reduce_stream after an event
+ * on stream: the memory-bound reduction overlaps the kernels that follow on stream.  The
+ * caller keeps workspace / dy alive for reduce_stream and joins it before reading dw. */
+int mmad_conv3d_wgrad_split(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,
+                            float* dw, float* dbias, void* workspace, void* stream,
+                            void* reduce_stream);
 
 /* ---- BatchNorm3d / BatchNorm1d (+ fused ReLU and residual add) -------------------
  * Replaces nn.BatchNorm3d/1d + nn.ReLU + the residual `out += residual; relu`
@@ -170,23 +176,30 @@ int mmad_scale_shift_act(int dtype, int64_t m, int c, const void* y, const float
                          const float* rshift, int relu, void* out, void* stream);
 int64_t mmad_bn_bwd_parts(int64_t m, int c);
 /* partial sums of g' and g'*xhat with g' = g * (relu_out > 0 | 1) */
-int mmad_bn_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* relu_out,
-                       const void* y, const float* mean, const float* invstd,
-                       float* parts, void* stream);
+/* g2 (may be NULL, here and in every BN / BN+pool backward below that takes it): a second
+ * gradient of the same output (a block input read by both conv1 and the shortcut); the
+ * kernels use as_stored(g + g2) -- the value torch's own gradient accumulation would hand
+ * them -- so the separate add pass disappears.  Generic (non fixed-channel) layouts of
+ * mmad_bn_bwd_apply return MMAD_EUNSUPPORTED with g2: the caller adds it first. */
+int mmad_bn_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* g2,
+                       const void* relu_out, const void* y, const float* mean,
+                       const float* invstd, float* parts, void* stream);
 /* dgamma, dbeta (fp32, may be NULL) and the apply coefficients for mmad_bn_bwd_apply */
 int mmad_bn_bwd_finalize(int c, int64_t count, int nparts, const float* parts,
                          const float* gamma, const float* invstd, int training,
                          float* dgamma, float* dbeta, float* coef, void* stream);
 /* dy = coef0[c]*g' - coef1[c] - xhat*coef2[c]; optionally also gmask_out = g' */
-int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* relu_out,
-                      const void* y, const float* mean, const float* invstd,
-                      const float* coef, void* dy, void* gmask_out, void* stream);
+int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* g2,
+                      const void* relu_out, const void* y, const float* mean,
+                      const float* invstd, const float* coef, void* dy, void* gmask_out,
+                      void* stream);
 /* Residual pair relu(bn(y) + bn2(y2)) (BasicBlock with the shortcut-B downsample BN): both
  * BNs' backward in one pass each over g / relu_out -- reduce2 writes both part buffers
  * (parts2 = sums of g' and g'*xhat2), finalize2 both coefficient sets, apply2 dy and dy2.
  * Bit-identical to the per-BN calls; fixed-channel layouts only (else MMAD_EUNSUPPORTED). */
-int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* relu_out,
-                        const void* y, const float* mean, const float* invstd, const void* y2,
+int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* g2,
+                        const void* relu_out, const void* y, const float* mean,
+                        const float* invstd, const void* y2,
                         const float* mean2, const float* invstd2, float* parts, float* parts2,
                         void* stream);
 int mmad_bn_bwd_finalize2(int c, int64_t count, int nparts, const float* parts,
@@ -194,8 +207,8 @@ int mmad_bn_bwd_finalize2(int c, int64_t count, int nparts, const float* parts,
                           float* dbeta, float* coef, const float* parts2, const float* gamma2,
                           const float* invstd2, int training2, float* dgamma2, float* dbeta2,
                           float* coef2, void* stream);
-int mmad_bn_bwd_apply2(int dtype, int64_t m, int c, const void* g, const void* relu_out,
-                       const void* y, const float* mean, const float* invstd, const float* coef,
+int mmad_bn_bwd_apply2(int dtype, int64_t m, int c, const void* g, const void* g2,
+                       const void* relu_out, const void* y, const float* mean, const float* invstd, const float* coef,
                        void* dy, const void* y2, const float* mean2, const float* invstd2,
                        const float* coef2, void* dy2, void* stream);
 /* BN + ReLU without residual (bn1 of every BasicBlock): the same two passes with the ReLU
@@ -231,13 +244,13 @@ int mmad_maxpool3d_bwd(int dtype, int n, int c, int di, int hi, int wi, int do_,
 int mmad_bnpool_fwd(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho, int wo,
                     int k, int s, int p, const void* y, const float* scale, const float* shift,
                     void* out, uint8_t* argmax, void* ymax, void* stream);
-int mmad_bnpool_bwd_reduce(int dtype, int64_t m, int c, const void* g, const uint8_t* argmax,
-                           const void* ymax, const float* mean, const float* invstd,
-                           float* parts, void* stream);   /* m = pooled rows */
+int mmad_bnpool_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* g2,
+                           const uint8_t* argmax, const void* ymax, const float* mean,
+                           const float* invstd, float* parts, void* stream); /* m = pooled rows */
 int mmad_bnpool_bwd_apply(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho,
-                          int wo, int k, int s, int p, const void* g, const uint8_t* argmax,
-                          const void* y, const float* mean, const float* invstd,
-                          const float* coef, void* dy, void* stream);
+                          int wo, int k, int s, int p, const void* g, const void* g2,
+                          const uint8_t* argmax, const void* y, const float* mean,
+                          const float* invstd, const float* coef, void* dy, void* stream);
 int mmad_gap_fwd(int dtype, int n, int64_t s, int c, const void* x, float* y, void* stream);
 /* same, partitioned over voxel slabs so small batches still fill the GPU; ws holds
  * mmad_gap_fwd_ws_elems(n, s, c) floats of partial sums (summed in a fixed order) */

@@ -75,6 +75,7 @@ _SIGS = {
     "mmad_conv3d_dgrad": (_i32, [_P, _i32, _vp, _vp, _vp, _vp]),
     "mmad_conv3d_wgrad_workspace": (_i64, [_P, _i32]),
     "mmad_conv3d_wgrad": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_conv3d_wgrad_split": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_bn_stats_parts": (_i64, [_i64, _i32]),
     "mmad_bn_stats": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_bn_parts_fold": (_i32, [_i32, _i32, _vp, _i32, _vp, _vp]),
@@ -84,13 +85,13 @@ _SIGS = {
     "mmad_scale_shift_act": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
                                     _vp]),
     "mmad_bn_bwd_parts": (_i64, [_i64, _i32]),
-    "mmad_bn_bwd_reduce": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_bn_bwd_reduce": (_i32, [_i32, _i64, _i32] + [_vp] * 8),
     "mmad_bn_bwd_finalize": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
-    "mmad_bn_bwd_apply": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "mmad_bn_bwd_reduce2": (_i32, [_i32, _i64, _i32] + [_vp] * 11),
+    "mmad_bn_bwd_apply": (_i32, [_i32, _i64, _i32] + [_vp] * 10),
+    "mmad_bn_bwd_reduce2": (_i32, [_i32, _i64, _i32] + [_vp] * 12),
     "mmad_bn_bwd_finalize2": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
                                      _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
-    "mmad_bn_bwd_apply2": (_i32, [_i32, _i64, _i32] + [_vp] * 13),
+    "mmad_bn_bwd_apply2": (_i32, [_i32, _i64, _i32] + [_vp] * 14),
     "mmad_relu_fwd": (_i32, [_i32, _i64, _vp, _vp, _vp]),
     "mmad_relu_bwd": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp]),
     "mmad_colsum_ws": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp]),
@@ -98,8 +99,8 @@ _SIGS = {
     "mmad_maxpool3d_fwd": (_i32, [_i32] * 12 + [_vp, _vp, _vp, _vp]),
     "mmad_maxpool3d_bwd": (_i32, [_i32] * 12 + [_vp, _vp, _vp, _vp]),
     "mmad_bnpool_fwd": (_i32, [_i32] * 12 + [_vp] * 7),
-    "mmad_bnpool_bwd_reduce": (_i32, [_i32, _i64, _i32] + [_vp] * 7),
-    "mmad_bnpool_bwd_apply": (_i32, [_i32] * 12 + [_vp] * 8),
+    "mmad_bnpool_bwd_reduce": (_i32, [_i32, _i64, _i32] + [_vp] * 8),
+    "mmad_bnpool_bwd_apply": (_i32, [_i32] * 12 + [_vp] * 9),
     "mmad_gap_fwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_gap_fwd_ws_elems": (_i64, [_i32, _i64, _i32]),
     "mmad_conv3d_fwd_ex": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),

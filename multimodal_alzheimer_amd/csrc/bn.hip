@@ -37,7 +37,10 @@ PartPlan part_plan(int64_t M) {
 // DUAL (MODE 1 only): a second BN over the same gradient and ReLU mask (the shortcut BN of
 // a residual block, y2 = its input): parts2 gets (sum g', sum g' * xhat2) from the same pass,
 // so g and the mask are read once for both
-template <typename T, int MODE, int V, bool DUAL = false>
+// g2 (MODE 1 / 3, may be NULL): a second gradient of the same output (the block input's
+// other consumer, volume_ops twin outputs); g is then as_stored(g + g2), rounded as torch's
+// own gradient accumulation rounds it, so no separate add pass is needed
+template <typename T, int MODE, int V, bool DUAL = false, bool G2 = false>
 __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t rpp,
                                                      const T* __restrict__ y,
                                                      const T* __restrict__ g,
@@ -51,7 +54,8 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
                                                      const T* __restrict__ y2 = nullptr,
                                                      const float* __restrict__ mean2 = nullptr,
                                                      const float* __restrict__ invstd2 = nullptr,
-                                                     float* __restrict__ parts2 = nullptr) {
+                                                     float* __restrict__ parts2 = nullptr,
+                                                     const T* __restrict__ g2 = nullptr) {
   static_assert(!DUAL || MODE == 1, "dual partial sums: BN backward with a relu_out mask");
   __shared__ float red[DUAL ? 3 : 2][2048];
   const int tid = threadIdx.x;
@@ -122,12 +126,13 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
       // rows are still added in the same order
       constexpr int U = 4;
       for (; r + (U - 1) * rpar < r1; r += U * rpar) {
-        u32x4 yr[U], gr[U], orr[U], y2r[U];
+        u32x4 yr[U], gr[U], orr[U], y2r[U], g2r[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int64_t i = (r + u * rpar) * C + cb + cl * V;
           yr[u] = *reinterpret_cast<const u32x4*>(y + i);
           if (NEED_G) gr[u] = *reinterpret_cast<const u32x4*>(g + i);
+          if (NEED_G && G2) g2r[u] = *reinterpret_cast<const u32x4*>(g2 + i);
           if (MODE == 1 && relu_out != nullptr)
             orr[u] = *reinterpret_cast<const u32x4*>(relu_out + i);
           if constexpr (DUAL) y2r[u] = *reinterpret_cast<const u32x4*>(y2 + i);
@@ -138,6 +143,12 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
           float yv[V], gv[V], ov[V], y2v[V];
           Chunk<T>::load(reinterpret_cast<const T*>(&yr[u]), yv);
           if (NEED_G) Chunk<T>::load(reinterpret_cast<const T*>(&gr[u]), gv);
+          if constexpr (NEED_G && G2) {
+            float hv[V];
+            Chunk<T>::load(reinterpret_cast<const T*>(&g2r[u]), hv);
+#pragma unroll
+            for (int e = 0; e < V; ++e) gv[e] = as_stored<T>(gv[e] + hv[e]);
+          }
           if (MODE == 1 && relu_out != nullptr)
             Chunk<T>::load(reinterpret_cast<const T*>(&orr[u]), ov);
           if constexpr (DUAL) Chunk<T>::load(reinterpret_cast<const T*>(&y2r[u]), y2v);
@@ -153,6 +164,13 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
       if (NEED_G) {
         if constexpr (V == Chunk<T>::N) Chunk<T>::load(g + i, gv);
         else for (int e = 0; e < V; ++e) gv[e] = Elt<T>::ld(g, i + e);
+        if constexpr (G2) {
+          float hv[V];
+          if constexpr (V == Chunk<T>::N) Chunk<T>::load(g2 + i, hv);
+          else for (int e = 0; e < V; ++e) hv[e] = Elt<T>::ld(g2, i + e);
+#pragma unroll
+          for (int e = 0; e < V; ++e) gv[e] = as_stored<T>(gv[e] + hv[e]);
+        }
         if (MODE == 1 && relu_out != nullptr) {
           if constexpr (V == Chunk<T>::N) Chunk<T>::load(relu_out + i, ov);
           else for (int e = 0; e < V; ++e) ov[e] = Elt<T>::ld(relu_out, i + e);
@@ -206,25 +224,35 @@ template <typename T, int MODE>
 int launch_colsum(int64_t M, int C, const void* y, const void* g, const void* ro,
                   const float* mean, const float* invstd, float* parts, hipStream_t st,
                   const uint8_t* act = nullptr, const float* msc = nullptr,
-                  const float* msh = nullptr) {
+                  const float* msh = nullptr, const void* g2 = nullptr) {
   const PartPlan pp = part_plan(M);
   constexpr int VEC = Chunk<T>::N;
   dim3 grid((unsigned)pp.nparts);
   // channel slabs for wide rows: the smallest power-of-two split whose slab fits one block
   int slabs = 1;
   while (C % (slabs * 2 * VEC) == 0 && C / (slabs * VEC) > 256) slabs *= 2;
+  // g2: its own instantiation, so the kernels without one keep their registers
+#define COLSUM(VV, G)                                                                       \
+  hipLaunchKernelGGL((colsum_kernel<T, MODE, VV, false, G>), grid, dim3(256), 0, st, M, C, \
+                     pp.rpp, (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act, \
+                     msc, msh, nullptr, nullptr, nullptr, nullptr, (const T*)g2)
   if (C % (slabs * VEC) == 0 && C / (slabs * VEC) <= 256) {
     grid.y = (unsigned)slabs;
-    hipLaunchKernelGGL((colsum_kernel<T, MODE, VEC>), grid, dim3(256), 0, st, M, C, pp.rpp,
-                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act, msc,
-                       msh);
+    if constexpr (MODE == 1 || MODE == 3) {
+      if (g2 != nullptr) COLSUM(VEC, true); else COLSUM(VEC, false);
+    } else {
+      COLSUM(VEC, false);
+    }
   } else if (C <= 256) {
-    hipLaunchKernelGGL((colsum_kernel<T, MODE, 1>), grid, dim3(256), 0, st, M, C, pp.rpp,
-                       (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act, msc,
-                       msh);
+    if constexpr (MODE == 1 || MODE == 3) {
+      if (g2 != nullptr) COLSUM(1, true); else COLSUM(1, false);
+    } else {
+      COLSUM(1, false);
+    }
   } else {
     return MMAD_EUNSUPPORTED;
   }
+#undef COLSUM
   return launch_status();
 }
 
@@ -528,13 +556,13 @@ struct BwdApply2 {
   void* dy2;
 };
 
-template <typename T, bool MASKY = false, bool DUAL = false>
+template <typename T, bool MASKY = false, bool DUAL = false, bool G2 = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
     int64_t nv, int cpr, int C, const T* __restrict__ g, const T* __restrict__ relu_out,
     const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ coef, T* __restrict__ dy, T* __restrict__ gmask,
     const float* __restrict__ msc = nullptr, const float* __restrict__ msh = nullptr,
-    BwdApply2 d2 = {}) {
+    BwdApply2 d2 = {}, const T* __restrict__ g2 = nullptr) {
   constexpr int V = Chunk<T>::N;
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -578,11 +606,22 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
     if constexpr (DUAL) Chunk<T>::store(dy2 + q * V, dv2);
     if (gmask) Chunk<T>::store(gmask + q * V, gv);
   };
+  // g2 (may be NULL): second gradient of the same output, summed as torch accumulates it
+  auto add_g2 = [&](int64_t qq, float* gv) {
+    float hv[V];
+    Chunk<T>::load(g2 + qq * V, hv);
+#pragma unroll
+    for (int e = 0; e < V; ++e) gv[e] = as_stored<T>(gv[e] + hv[e]);
+  };
   int64_t q = t0;
   for (; q + stride < nv; q += 2 * stride) {
     float g0[V], g1[V], y0[V], y1[V], o0[V], o1[V], z0[V], z1[V];
     Chunk<T>::load(g + q * V, g0);
     Chunk<T>::load(g + (q + stride) * V, g1);
+    if constexpr (G2) {
+      add_g2(q, g0);
+      add_g2(q + stride, g1);
+    }
     Chunk<T>::load(y + q * V, y0);
     Chunk<T>::load(y + (q + stride) * V, y1);
     if (relu_out) {
@@ -599,6 +638,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
   if (q < nv) {
     float g0[V], y0[V], o0[V], z0[V];
     Chunk<T>::load(g + q * V, g0);
+    if constexpr (G2) add_g2(q, g0);
     Chunk<T>::load(y + q * V, y0);
     if (relu_out) Chunk<T>::load(relu_out + q * V, o0);
     if constexpr (DUAL) Chunk<T>::load(y2 + q * V, z0);
@@ -798,15 +838,17 @@ int mmad_scale_shift_act(int dtype, int64_t m, int c, const void* y, const float
   return launch_status();
 }
 
-int mmad_bn_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* relu_out,
-                       const void* y, const float* mean, const float* invstd, float* parts,
-                       void* stream) {
+int mmad_bn_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* g2,
+                       const void* relu_out, const void* y, const float* mean,
+                       const float* invstd, float* parts, void* stream) {
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
   if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
   if (!g || !y || !mean || !invstd || !parts) return MMAD_ENULL;
   if (dtype == MMAD_BF16)
-    return launch_colsum<u16, 1>(m, c, y, g, relu_out, mean, invstd, parts, as_stream(stream));
-  return launch_colsum<float, 1>(m, c, y, g, relu_out, mean, invstd, parts, as_stream(stream));
+    return launch_colsum<u16, 1>(m, c, y, g, relu_out, mean, invstd, parts, as_stream(stream),
+                                 nullptr, nullptr, nullptr, g2);
+  return launch_colsum<float, 1>(m, c, y, g, relu_out, mean, invstd, parts, as_stream(stream),
+                                 nullptr, nullptr, nullptr, g2);
 }
 
 // BN + ReLU (no residual) backward with the ReLU mask recomputed from y: the same partial
@@ -846,17 +888,17 @@ int mmad_bn_relu_bwd_apply(int dtype, int64_t m, int c, const void* g, const voi
   return launch_status();
 }
 
-int mmad_bnpool_bwd_reduce(int dtype, int64_t m, int c, const void* g, const uint8_t* argmax,
-                           const void* ymax, const float* mean, const float* invstd,
-                           float* parts, void* stream) {
+int mmad_bnpool_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* g2,
+                           const uint8_t* argmax, const void* ymax, const float* mean,
+                           const float* invstd, float* parts, void* stream) {
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
   if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
   if (!g || !argmax || !ymax || !mean || !invstd || !parts) return MMAD_ENULL;
   if (dtype == MMAD_BF16)
     return launch_colsum<u16, 3>(m, c, ymax, g, nullptr, mean, invstd, parts, as_stream(stream),
-                                 argmax);
+                                 argmax, nullptr, nullptr, g2);
   return launch_colsum<float, 3>(m, c, ymax, g, nullptr, mean, invstd, parts, as_stream(stream),
-                                 argmax);
+                                 argmax, nullptr, nullptr, g2);
 }
 
 int mmad_bn_fold(int c, const float* gamma, const float* beta, const float* running_mean,
@@ -881,9 +923,10 @@ int mmad_bn_bwd_finalize(int c, int64_t count, int nparts, const float* parts,
   return launch_status();
 }
 
-int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* relu_out,
-                      const void* y, const float* mean, const float* invstd, const float* coef,
-                      void* dy, void* gmask, void* stream) {
+int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* g2,
+                      const void* relu_out, const void* y, const float* mean,
+                      const float* invstd, const float* coef, void* dy, void* gmask,
+                      void* stream) {
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
   if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
   if (!g || !y || !mean || !invstd || !coef || !dy) return MMAD_ENULL;
@@ -895,16 +938,20 @@ int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* re
   const int vv = dtype == MMAD_BF16 ? 8 : 4;
   if (c % vv == 0 && is_pow2(c / vv) && c / vv <= 256) {
     const int64_t nv = m * c / vv;
-    if (dtype == MMAD_BF16)
-      hipLaunchKernelGGL(bn_bwd_apply_fc_kernel<u16>, dim3(ew_grid(nv)), dim3(256), 0, st, nv,
-                         c / vv, c, (const u16*)g, (const u16*)relu_out, (const u16*)y, mean,
-                         invstd, coef, (u16*)dy, (u16*)gmask);
-    else
-      hipLaunchKernelGGL(bn_bwd_apply_fc_kernel<float>, dim3(ew_grid(nv)), dim3(256), 0, st, nv,
-                         c / vv, c, (const float*)g, (const float*)relu_out, (const float*)y,
-                         mean, invstd, coef, (float*)dy, (float*)gmask);
+#define APPLYFC(T, G)                                                                         \
+  hipLaunchKernelGGL((bn_bwd_apply_fc_kernel<T, false, false, G>), dim3(ew_grid(nv)), dim3(256), \
+                     0, st, nv, c / vv, c, (const T*)g, (const T*)relu_out, (const T*)y, mean,  \
+                     invstd, coef, (T*)dy, (T*)gmask, nullptr, nullptr, BwdApply2{},           \
+                     (const T*)g2)
+    if (dtype == MMAD_BF16) {
+      if (g2 != nullptr) APPLYFC(u16, true); else APPLYFC(u16, false);
+    } else {
+      if (g2 != nullptr) APPLYFC(float, true); else APPLYFC(float, false);
+    }
+#undef APPLYFC
     return launch_status();
   }
+  if (g2 != nullptr) return MMAD_EUNSUPPORTED;   // generic layouts: the caller adds g2 first
   if (dtype == MMAD_BF16) {
     if (c % 8 == 0) APPLY(u16, 8); else APPLY(u16, 1);
   } else {
@@ -918,8 +965,9 @@ int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* re
 // the mask.  Same values, bit for bit, as reduce / finalize / apply called once per BN with
 // the same g and relu_out.  Fixed-channel layouts only (MMAD_EUNSUPPORTED otherwise: the
 // caller falls back to the per-BN calls).
-int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* relu_out,
-                        const void* y, const float* mean, const float* invstd, const void* y2,
+int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* g2,
+                        const void* relu_out, const void* y, const float* mean,
+                        const float* invstd, const void* y2,
                         const float* mean2, const float* invstd2, float* parts, float* parts2,
                         void* stream) {
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
@@ -935,10 +983,12 @@ int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* 
     int slabs = 1;
     while (c % (slabs * 2 * VEC) == 0 && c / (slabs * VEC) > 256) slabs *= 2;
     if (!(c % (slabs * VEC) == 0 && c / (slabs * VEC) <= 256)) return MMAD_EUNSUPPORTED;
-    hipLaunchKernelGGL((colsum_kernel<T, 1, VEC, true>), dim3((unsigned)pp.nparts, slabs),
-                       dim3(256), 0, st, m, c, pp.rpp, (const T*)y, (const T*)g,
-                       (const T*)relu_out, mean, invstd, parts, nullptr, nullptr, nullptr,
-                       (const T*)y2, mean2, invstd2, parts2);
+    auto k = g2 != nullptr ? colsum_kernel<T, 1, VEC, true, true>
+                           : colsum_kernel<T, 1, VEC, true, false>;
+    hipLaunchKernelGGL(k, dim3((unsigned)pp.nparts, slabs), dim3(256), 0, st, m, c, pp.rpp,
+                       (const T*)y, (const T*)g, (const T*)relu_out, mean, invstd, parts,
+                       nullptr, nullptr, nullptr, (const T*)y2, mean2, invstd2, parts2,
+                       (const T*)g2);
     return launch_status();
   };
   return dtype == MMAD_BF16 ? go(u16{}) : go(float{});
@@ -958,8 +1008,8 @@ int mmad_bn_bwd_finalize2(int c, int64_t count, int nparts, const float* parts,
   return launch_status();
 }
 
-int mmad_bn_bwd_apply2(int dtype, int64_t m, int c, const void* g, const void* relu_out,
-                       const void* y, const float* mean, const float* invstd, const float* coef,
+int mmad_bn_bwd_apply2(int dtype, int64_t m, int c, const void* g, const void* g2,
+                       const void* relu_out, const void* y, const float* mean, const float* invstd, const float* coef,
                        void* dy, const void* y2, const float* mean2, const float* invstd2,
                        const float* coef2, void* dy2, void* stream) {
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
@@ -972,15 +1022,16 @@ int mmad_bn_bwd_apply2(int dtype, int64_t m, int c, const void* g, const void* r
   const int64_t nv = m * c / vv;
   const BwdApply2 d2{y2, mean2, invstd2, coef2, dy2};
   hipStream_t st = as_stream(stream);
-  if (dtype == MMAD_BF16)
-    hipLaunchKernelGGL((bn_bwd_apply_fc_kernel<u16, false, true>), dim3(ew_grid(nv)), dim3(256),
-                       0, st, nv, c / vv, c, (const u16*)g, (const u16*)relu_out, (const u16*)y,
-                       mean, invstd, coef, (u16*)dy, (u16*)nullptr, nullptr, nullptr, d2);
-  else
-    hipLaunchKernelGGL((bn_bwd_apply_fc_kernel<float, false, true>), dim3(ew_grid(nv)),
-                       dim3(256), 0, st, nv, c / vv, c, (const float*)g, (const float*)relu_out,
-                       (const float*)y, mean, invstd, coef, (float*)dy, (float*)nullptr, nullptr,
-                       nullptr, d2);
+#define APPLY2(T, G)                                                                         \
+  hipLaunchKernelGGL((bn_bwd_apply_fc_kernel<T, false, true, G>), dim3(ew_grid(nv)), dim3(256), \
+                     0, st, nv, c / vv, c, (const T*)g, (const T*)relu_out, (const T*)y, mean, \
+                     invstd, coef, (T*)dy, (T*)nullptr, nullptr, nullptr, d2, (const T*)g2)
+  if (dtype == MMAD_BF16) {
+    if (g2 != nullptr) APPLY2(u16, true); else APPLY2(u16, false);
+  } else {
+    if (g2 != nullptr) APPLY2(float, true); else APPLY2(float, false);
+  }
+#undef APPLY2
   return launch_status();
 }
 

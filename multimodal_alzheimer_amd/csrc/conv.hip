@@ -1693,32 +1693,56 @@ int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype) {
 int mmad_colsum_ws(int dtype, int64_t m, int c, const void* y, float* parts, float* out,
                    void* stream);
 
-int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,
-                      float* dw, float* dbias, void* workspace, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// make `rst` wait for everything queued on `st` so far (one reusable event per device: a
+// wait binds to the record made before it, also under stream capture)
+int fork_stream(hipStream_t st, hipStream_t rst) {
+  static hipEvent_t ev[16] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return MMAD_EHIP;
+  if (!ev[dev]) {
+    const int rc = hip_status(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
+    if (rc) return rc;
+  }
+  int rc = hip_status(hipEventRecord(ev[dev], st));
+  if (rc) return rc;
+  return hip_status(hipStreamWaitEvent(rst, ev[dev], 0));
+}
+
+// weight gradient: the split-K kernel on `st`, then the slab reduction (and the bias
+// gradient) on `rst` -- a second stream lets the memory-bound reduction overlap the
+// latency-bound BN backward kernels that follow on `st`
+int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* dy, float* dw,
+                 float* dbias, void* workspace, hipStream_t st, hipStream_t rst) {
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!x || !dy || !dw || !workspace) return MMAD_ENULL;
   const Geom g = fwd_geom(d, dtype);
   if (!geom_ok(g, dtype) || g.Nd % (dtype == MMAD_BF16 ? 8 : 4)) return MMAD_EUNSUPPORTED;
-  hipStream_t st = as_stream(stream);
+  void* const stream = st;
+  void* const rstream = rst;
   int rc;
   // (1x1x1 weight gradients stay here: hipBLASLt's heuristic offers no split-K algorithm
   // for K = all voxels at this size and its single-pass one ran 5x slower than wgrad_kernel)
   if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on() && g.K == 392) {
     rc = mmad_stem::wgrad(d, x, dy, (float*)workspace, stream);
     if (rc) return rc;
+    if (rst != st && (rc = fork_stream(st, rst))) return rc;
     // (one slab per block: sum 16-slab groups in place first, so no thread walks them all)
     const int nb = (int)mmad_stem::wgrad_blocks(d);
     const int64_t total = (int64_t)g.Nd * g.K;
     constexpr int G = 16;
     hipLaunchKernelGGL(slab_group_sum_kernel, dim3(grid_for(total * cdiv(nb, G))), dim3(256), 0,
-                       st, (float*)workspace, nb, total, G);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, st,
+                       rst, (float*)workspace, nb, total, G);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, rst,
                        (const float*)workspace, dw, nb, g.Nd, g.K, g.Cs, g.cs_shift, g.taps,
                        d->kw, G);
     rc = launch_status();
     if (rc) return rc;
-    if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, stream);
+    if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, rstream);
     return MMAD_OK;
   }
   if (!unfolded(d) && (use_lattice_wgrad(g, dtype) || use_pwgrad(g, dtype))) {
@@ -1727,12 +1751,13 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
              ? mmad_pwgrad::wgrad(patch_geo(g), x, dy, (float*)workspace, &splits, stream)
              : mmad_lattice::wgrad(patch_geo(g), x, dy, (float*)workspace, &splits, stream);
     if (rc) return rc;
+    if (rst != st && (rc = fork_stream(st, rst))) return rc;
     hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)cdiv(g.Cs, 64), (unsigned)g.Nd),
-                       dim3(256), 0, st, (const float*)workspace, dw, splits, g.Nd, g.K, g.Cs,
+                       dim3(256), 0, rst, (const float*)workspace, dw, splits, g.Nd, g.K, g.Cs,
                        g.taps);
     rc = launch_status();
     if (rc) return rc;
-    if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, stream);
+    if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, rstream);
     return MMAD_OK;
   }
   const WSplit sp = wgrad_split(g, dtype);
@@ -1748,25 +1773,44 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
     rc = sp.bmw == 64 ? launch_wgrad<float, 64>(g, sp, x, dy, (float*)workspace, st)
                       : launch_wgrad<float, 128>(g, sp, x, dy, (float*)workspace, st);
   if (rc) return rc;
+  if (rst != st && (rc = fork_stream(st, rst))) return rc;
   const int64_t total = (int64_t)g.Nd * g.K;
   // (the transposing reduce writes whole [ci][taps] runs of dW; scattered 4-byte dW stores
   // from an element-wise reduce cost ~2x in partial-line writes)
   if (!unfolded(d) && g.taps > 1 && g.taps <= 32)
     hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)cdiv(g.Cs, 64), (unsigned)g.Nd),
-                       dim3(256), 0, st, (const float*)workspace, dw, sp.splits, g.Nd, g.K,
+                       dim3(256), 0, rst, (const float*)workspace, dw, sp.splits, g.Nd, g.K,
                        g.Cs, g.taps);
   else if (sp.splits >= 8)
     hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
-                       st, (const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.cs_shift,
+                       rst, (const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.cs_shift,
                        g.taps, unfolded(d) ? d->kw : 0, 1);
   else
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, st,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, rst,
                        (const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.cs_shift,
                        g.taps, unfolded(d) ? d->kw : 0, 1);
   rc = launch_status();
   if (rc) return rc;
-  if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, stream);
+  if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, rstream);
   return MMAD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,
+                      float* dw, float* dbias, void* workspace, void* stream) {
+  return conv3d_wgrad(d, dtype, x, dy, dw, dbias, workspace, as_stream(stream),
+                      as_stream(stream));
+}
+
+int mmad_conv3d_wgrad_split(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,
+                            float* dw, float* dbias, void* workspace, void* stream,
+                            void* reduce_stream) {
+  if (!reduce_stream) return MMAD_ENULL;
+  return conv3d_wgrad(d, dtype, x, dy, dw, dbias, workspace, as_stream(stream),
+                      as_stream(reduce_stream));
 }
 
 }  // extern "C"

@@ -44,16 +44,25 @@ def _eval_fused_ok(block, x):
             and x.dim() == 5)
 
 
-def _conv_bn_act(conv, bn, x, relu=True, res=None, res_conv=None, res_bn=None, res_x=None):
+def _conv_bn_act(conv, bn, x, relu=True, res=None, res_conv=None, res_bn=None, res_x=None,
+                 twin=False):
     y, parts = conv.forward_stats(x)
     if res_conv is not None:
         r, rparts = res_conv.forward_stats(res_x)
-        return V.batchnorm_act(y, bn, parts, relu=relu, res=r, res_bn=res_bn, res_parts=rparts)
-    return V.batchnorm_act(y, bn, parts, relu=relu, res=res)
+        return V.batchnorm_act(y, bn, parts, relu=relu, res=r, res_bn=res_bn, res_parts=rparts,
+                               twin=twin)
+    return V.batchnorm_act(y, bn, parts, relu=relu, res=res, twin=twin)
+
+
+# A block's input feeds conv1 and the shortcut: the shortcut reads the producer's twin alias
+# (volume_ops "twin outputs"), so the two gradients meet inside the producer's BN backward
+# instead of in a separate add.  ResNet sets twin_out on every block whose output feeds
+# another block.
 
 
 class BasicBlock(nn.Module):
     expansion = 1
+    twin_out = False
 
     def __init__(self, cin, planes, stride=1, dilation=1, downsample=None):
         super().__init__()
@@ -72,10 +81,11 @@ class BasicBlock(nn.Module):
             if y is not None:
                 return y
         h = _conv_bn_act(self.conv1, self.bn1, x)
+        xr = V.take_twin(x)
         if self.downsample is None:
-            return _conv_bn_act(self.conv2, self.bn2, h, res=x)
+            return _conv_bn_act(self.conv2, self.bn2, h, res=xr, twin=self.twin_out)
         return _conv_bn_act(self.conv2, self.bn2, h, res_conv=self.downsample[0],
-                            res_bn=self.downsample[1], res_x=x)
+                            res_bn=self.downsample[1], res_x=xr, twin=self.twin_out)
 
     def _eval_fused(self, x):
         """3 (or 2) kernels per block instead of 4-5 conv / BN / add passes: BN folded into
@@ -94,6 +104,7 @@ class BasicBlock(nn.Module):
 
 class Bottleneck(nn.Module):
     expansion = 4
+    twin_out = False
 
     def __init__(self, cin, planes, stride=1, dilation=1, downsample=None):
         super().__init__()
@@ -110,11 +121,12 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         h = _conv_bn_act(self.conv1, self.bn1, x)
+        xr = V.take_twin(x)
         h = _conv_bn_act(self.conv2, self.bn2, h)
         if self.downsample is None:
-            return _conv_bn_act(self.conv3, self.bn3, h, res=x)
+            return _conv_bn_act(self.conv3, self.bn3, h, res=xr, twin=self.twin_out)
         return _conv_bn_act(self.conv3, self.bn3, h, res_conv=self.downsample[0],
-                            res_bn=self.downsample[1], res_x=x)
+                            res_bn=self.downsample[1], res_x=xr, twin=self.twin_out)
 
 
 class ResNet(nn.Module):
@@ -136,6 +148,9 @@ class ResNet(nn.Module):
         self.layer2 = self._stage(block, 128, counts[1], 2, 1)
         self.layer3 = self._stage(block, 256, counts[2], 1, 2)
         self.layer4 = self._stage(block, 512, counts[3], 1, 4)
+        blocks = [b for s in (self.layer1, self.layer2, self.layer3, self.layer4) for b in s]
+        for b in blocks[:-1]:
+            b.twin_out = True        # feeds the next block (conv1 + shortcut)
         # MedicalNet's segmentation head; every reference caller replaces it
         # (anat_cnn.py:79).  Kept so MedicalNet state_dicts load without surprises.
         self.conv_seg = nn.Sequential(
@@ -167,8 +182,12 @@ class ResNet(nn.Module):
         # conv output (volume_ops.batchnorm_relu_maxpool)
         if self.conv1.weight.is_cuda and not _eval_fused_ok(self, x):
             V.prepack(self)          # every conv weight repacked in one launch per step
+        V.clear_twins()
         y, parts = self.conv1.forward_stats(x)
         mp = self.maxpool
+        # no twin for the pooled stem output: the pool backward reads each pooled gradient
+        # from 8 cells, so a second gradient there costs more than torch's one add pass
+        # (measured: bnpool3s2_bwd 100 -> 127 us, colsum +7 us vs the 15 us add)
         x = V.batchnorm_relu_maxpool(y, self.bn1, parts, mp.kernel_size, mp.stride, mp.padding)
         return self.layer4(self.layer3(self.layer2(self.layer1(x))))
 

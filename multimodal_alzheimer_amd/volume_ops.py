@@ -83,6 +83,14 @@ _BN_UPDATES = [0]
 # is off unless MMAD_WGRAD_STREAM=1 (A/B switch); the gradient all-reduce still uses the
 # side stream (data_parallel.GradAllReduce).
 WGRAD_STREAM = os.environ.get("MMAD_WGRAD_STREAM", "0") == "1"
+# MMAD_REDUCE_STREAM=1: only the split-K slab REDUCTION of each weight gradient goes to the
+# side stream (the wgrad kernel stays on the main stream), to overlap the latency-bound BN
+# backward kernels that follow (mmad_conv3d_wgrad_split).  The same side stream carries the
+# data-parallel all-reduce, so it stays ordered after every reduction it reads; the main
+# stream joins it at the end of backward.  Measured 2 % SLOWER on the ResNet-10 step
+# (2148-2167 vs 2196-2205 vol/s, interleaved on one MI355X): the reduction blocks wait for
+# CU slots behind the one-block-per-CU conv kernels and then delay the next one.  Off.
+REDUCE_STREAM = os.environ.get("MMAD_REDUCE_STREAM", "0") == "1"
 _SIDE = {}
 _JOIN_PENDING = set()
 
@@ -386,7 +394,8 @@ class _Conv3dFn(torch.autograd.Function):
             if side is not main:
                 side.wait_stream(main)          # gy (and src) complete
             with torch.cuda.stream(side):
-                dw, db = _wgrad(ctx, d, dt, src, gy, weight, ctx.wparam)
+                rside = grad_stream(gy.device) if REDUCE_STREAM and side is main else None
+                dw, db = _wgrad(ctx, d, dt, src, gy, weight, ctx.wparam, rside)
             if side is not main:
                 # memory first used on the side stream stays reserved until it is done
                 for t in (src, gy, dw, db):
@@ -398,8 +407,9 @@ class _Conv3dFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
-def _wgrad(ctx, d, dt, src, gy, weight, wparam=None):
-    """dW (torch layout, fp32) and the bias gradient of one conv, on the current stream.
+def _wgrad(ctx, d, dt, src, gy, weight, wparam=None, rside=None):
+    """dW (torch layout, fp32) and the bias gradient of one conv, on the current stream
+    (its slab reduction on ``rside`` when given: REDUCE_STREAM).
     When the weight parameter carries a gradient slot (``_mmad_grad_view``: its slice of
     a data-parallel bucket, data_parallel.GradAllReduce) and has no gradient yet, dW is
     written straight into it; autograd then adopts that tensor as ``.grad`` as-is."""
@@ -415,8 +425,20 @@ def _wgrad(ctx, d, dt, src, gy, weight, wparam=None):
         dw = torch.empty((d.co, d.ci, d.kd, d.kh, d.kw) if padded else weight.shape,
                          dtype=torch.float32, device=gy.device)
     db = torch.empty(d.co, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
-    L.call("mmad_conv3d_wgrad", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db), L.ptr(ws),
-           L.stream())
+    # a dW that autograd will not adopt as-is (an existing .grad it is added into, or the
+    # channel-padded copy cut below) is read on the main stream: no split then
+    if rside is not None and not padded and (wparam is None or wparam.grad is None):
+        L.call("mmad_conv3d_wgrad_split", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db),
+               L.ptr(ws), L.stream(), rside.cuda_stream)
+        # what the side stream reads or writes stays allocated until it has run; dW (and
+        # anything derived from it) is read only after the join
+        for t in (ws, gy, dw, db):
+            if t is not None:
+                t.record_stream(rside)
+        _queue_join(torch.cuda.current_stream(), rside)
+    else:
+        L.call("mmad_conv3d_wgrad", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db),
+               L.ptr(ws), L.stream())
     if padded:                             # cut the zero-lane channels back off
         taps = d.kd * d.kh * d.kw
         dw = _pad_rows(dw, d.co, d.ci * taps, ctx.ci_real * taps, weight.shape)
@@ -577,6 +599,62 @@ def _finalize_pair(y, parts, bn, res, res_parts, rbn, training):
     return a, b
 
 
+# ---- twin outputs ---------------------------------------------------------------------
+# A residual block reads its input twice (conv1 and the shortcut), so autograd would sum
+# the two gradients of that tensor in a separate add pass before the producer's BN
+# backward.  A producer asked for a twin (batchnorm_act / batchnorm_relu_maxpool with
+# twin=True) also returns a second alias of its output; the block routes its shortcut
+# through that alias (take_twin), each gradient reaches the producer's backward on its own,
+# and the BN backward kernels add them while loading (g2 of mmad_bn_bwd_* /
+# mmad_bnpool_bwd_*), rounded as torch's accumulation rounds them: same values, one pass
+# fewer.  MMAD_TWIN=0 turns it off.
+TWIN = os.environ.get("MMAD_TWIN", "1") != "0"
+_TWINS = {}
+
+
+def _twin_wanted(flag, y):
+    return bool(flag) and TWIN and torch.is_grad_enabled() and y.dim() == 5
+
+
+def _register_twin(out, alias):
+    _TWINS[id(out)] = alias
+
+
+def take_twin(x):
+    """the second alias of ``x`` if its producer made one (each alias is handed out once),
+    else ``x`` itself"""
+    alias = _TWINS.pop(id(x), None)
+    return alias if alias is not None and alias._base is x else x
+
+
+def clear_twins():
+    """drop twins nobody took (called at the start of each backbone forward)"""
+    _TWINS.clear()
+
+
+def _sum_grads(g, g2):
+    """g + g2 in g's dtype (the value torch's gradient accumulation produces)"""
+    out = torch.empty_like(g)
+    L.call("mmad_add", L.dtype_code(g.dtype), g.numel(), L.ptr(g), L.ptr(g2), L.ptr(out),
+           L.stream())
+    return out
+
+
+def _twin_grads(g, g2, like):
+    """(g, g2) as the backward kernels take them: NDHWC / contiguous in like's dtype, g2
+    None when absent; g None only when neither exists"""
+    if g is None:
+        g, g2 = g2, None
+    out = []
+    for t in (g, g2):
+        if t is not None:
+            t = _cl(t) if like.dim() == 5 else t.contiguous()
+            if t.dtype != like.dtype:
+                t = cast(t, like.dtype)
+        out.append(t)
+    return out
+
+
 def _mask_from_y_ok(y):
     """the fixed-channel apply kernel (and so the y-mask variant) covers this layout"""
     c = y.shape[1]
@@ -585,13 +663,15 @@ def _mask_from_y_ok(y):
 
 
 def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask,
-                 params=(None, None), mask_affine=None):
+                 params=(None, None), mask_affine=None, g2=None):
     """BN (+ReLU) backward.  ``mask_affine`` = (scale, shift) of a BN+ReLU without residual:
     the ReLU mask is then recomputed from y (mmad_bn_relu_bwd_*) instead of read from
-    ``relu_out``."""
+    ``relu_out``.  ``g2``: a twin's gradient, summed into g by the kernels."""
     m, c = _rows(y)
     dev = y.device
     dt = L.dtype_code(y.dtype)
+    if g2 is not None and (mask_affine is not None or not _mask_from_y_ok(y)):
+        g, g2 = _sum_grads(g, g2), None
     nparts = L.load().mmad_bn_bwd_parts(m, c)
     parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
     if mask_affine is not None:
@@ -599,7 +679,7 @@ def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask,
         L.call("mmad_bn_relu_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(y), L.ptr(mean),
                L.ptr(invstd), L.ptr(sc), L.ptr(sh), L.ptr(parts), L.stream())
     else:
-        L.call("mmad_bn_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y),
+        L.call("mmad_bn_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(g2), L.ptr(relu_out), L.ptr(y),
                L.ptr(mean), L.ptr(invstd), L.ptr(parts), L.stream())
     dgamma = grad_slot(params[0], (c,), dev)
     dbeta = grad_slot(params[1], (c,), dev)
@@ -613,7 +693,7 @@ def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask,
                L.ptr(invstd), L.ptr(mask_affine[0]), L.ptr(mask_affine[1]), L.ptr(coef),
                L.ptr(dy), L.stream())
     else:
-        L.call("mmad_bn_bwd_apply", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y),
+        L.call("mmad_bn_bwd_apply", dt, m, c, L.ptr(g), L.ptr(g2), L.ptr(relu_out), L.ptr(y),
                L.ptr(mean), L.ptr(invstd), L.ptr(coef), L.ptr(dy), L.ptr(gmask), L.stream())
     return dy, dgamma, dbeta, gmask
 
@@ -622,7 +702,7 @@ _BN_DUAL = os.environ.get("MMAD_BN_DUAL", "1") != "0"
 
 
 def _bn_backward_pair(g, relu_out, y, mean, invstd, gamma, batch_stats, y2, mean2, invstd2,
-                      gamma2, batch_stats2, params, params2):
+                      gamma2, batch_stats2, params, params2, g2=None):
     """Both BNs of relu(bn(y) + bn2(y2)) backward, g and relu_out read once per pass
     (mmad_bn_bwd_reduce2 / _finalize2 / _apply2); equal bit for bit to two _bn_backward
     calls.  Returns (dy, dgamma, dbeta, dy2, dgamma2, dbeta2)."""
@@ -631,9 +711,9 @@ def _bn_backward_pair(g, relu_out, y, mean, invstd, gamma, batch_stats, y2, mean
     dt = L.dtype_code(y.dtype)
     nparts = L.load().mmad_bn_bwd_parts(m, c)
     parts = torch.empty((2, nparts, 2, c), dtype=torch.float32, device=dev)
-    L.call("mmad_bn_bwd_reduce2", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y), L.ptr(mean),
-           L.ptr(invstd), L.ptr(y2), L.ptr(mean2), L.ptr(invstd2), L.ptr(parts[0]),
-           L.ptr(parts[1]), L.stream())
+    L.call("mmad_bn_bwd_reduce2", dt, m, c, L.ptr(g), L.ptr(g2), L.ptr(relu_out), L.ptr(y),
+           L.ptr(mean), L.ptr(invstd), L.ptr(y2), L.ptr(mean2), L.ptr(invstd2),
+           L.ptr(parts[0]), L.ptr(parts[1]), L.stream())
     dgamma = grad_slot(params[0], (c,), dev)
     dbeta = grad_slot(params[1], (c,), dev)
     dgamma2 = grad_slot(params2[0], (c,), dev)
@@ -645,9 +725,9 @@ def _bn_backward_pair(g, relu_out, y, mean, invstd, gamma, batch_stats, y2, mean
            L.ptr(coef[1]), L.stream())
     dy = torch.empty_like(y)
     dy2 = torch.empty_like(y2)
-    L.call("mmad_bn_bwd_apply2", dt, m, c, L.ptr(g), L.ptr(relu_out), L.ptr(y), L.ptr(mean),
-           L.ptr(invstd), L.ptr(coef[0]), L.ptr(dy), L.ptr(y2), L.ptr(mean2), L.ptr(invstd2),
-           L.ptr(coef[1]), L.ptr(dy2), L.stream())
+    L.call("mmad_bn_bwd_apply2", dt, m, c, L.ptr(g), L.ptr(g2), L.ptr(relu_out), L.ptr(y),
+           L.ptr(mean), L.ptr(invstd), L.ptr(coef[0]), L.ptr(dy), L.ptr(y2), L.ptr(mean2),
+           L.ptr(invstd2), L.ptr(coef[1]), L.ptr(dy2), L.stream())
     return dy, dgamma, dbeta, dy2, dgamma2, dbeta2
 
 
@@ -656,7 +736,7 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, parts, gamma, beta, res, res_parts, rgamma, rbeta, cfg):
-        bn, relu, training, rbn = cfg
+        bn, relu, training, rbn, twin = cfg
         L.require_device(y)
         rscale = rshift = rmean = rinvstd = None
         rbatch = False
@@ -678,29 +758,34 @@ class _BNActFn(torch.autograd.Function):
         ctx.mask_affine = (scale, shift) if masky else None
         ctx.cfg = (relu, batch, rbatch, res is not None, rbn is not None)
         ctx.params = ((gamma, beta), (rgamma, rbeta))   # gradient-slot lookup (grad_slot)
+        if twin:
+            ctx.set_materialize_grads(False)            # an unused twin gets no gradient
+            return out, out.view(out.shape)
         return out
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, g2=None):
         y, out, mean, invstd, gamma, rres, rmean, rinvstd, rgamma = ctx.saved_tensors
         relu, batch, rbatch, has_res, has_rbn = ctx.cfg
-        g = _cl(g) if y.dim() == 5 else g.contiguous()
-        if g.dtype != y.dtype:
-            g = cast(g, y.dtype)
+        g, g2 = _twin_grads(g, g2, y)
+        if g is None:
+            return (None,) * 9
         gam = None if gamma is None else gamma.detach()
         if (has_rbn and _BN_DUAL and out is not None and ctx.mask_affine is None
                 and _mask_from_y_ok(y)):
             rg = None if rgamma is None else rgamma.detach()
             dy, dgamma, dbeta, dres, drg, drb = _bn_backward_pair(
                 g, out, y, mean, invstd, gam, batch, rres, rmean, rinvstd, rg, rbatch,
-                ctx.params[0], ctx.params[1])
+                ctx.params[0], ctx.params[1], g2)
             return (dy, None, dgamma if ctx.needs_input_grad[2] else None,
                     dbeta if ctx.needs_input_grad[3] else None, dres, None,
                     drg if ctx.needs_input_grad[6] else None,
                     drb if ctx.needs_input_grad[7] else None, None)
+        if g2 is not None and has_rbn:      # per-BN calls below both read g
+            g, g2 = _sum_grads(g, g2), None
         dy, dgamma, dbeta, gmask = _bn_backward(g, out, y, mean, invstd, gam, batch,
                                                 has_res and not has_rbn, ctx.params[0],
-                                                ctx.mask_affine)
+                                                ctx.mask_affine, g2)
         dres = drg = drb = None
         if has_rbn:
             rg = None if rgamma is None else rgamma.detach()
@@ -714,11 +799,14 @@ class _BNActFn(torch.autograd.Function):
                 drb if ctx.needs_input_grad[7] else None, None)
 
 
-def batchnorm_act(y, bn, parts=None, relu=False, res=None, res_bn=None, res_parts=None):
+def batchnorm_act(y, bn, parts=None, relu=False, res=None, res_bn=None, res_parts=None,
+                  twin=False):
     """bn(y) (+ res or res_bn(res)) then optional ReLU, torch BatchNorm semantics.
 
     ``bn`` / ``res_bn`` are nn.BatchNorm modules (parameters + running buffers);
     ``parts`` are the conv-epilogue partial sums of y when y came from conv3d.
+    ``twin``: the output will be read by two consumers; the second one takes its alias
+    with take_twin (see "twin outputs" above).
     """
     if y.dim() == 5:
         _check_vol(y)
@@ -730,10 +818,15 @@ def batchnorm_act(y, bn, parts=None, relu=False, res=None, res_bn=None, res_part
         if y.dim() == 5:
             _check_vol(res)
     training = bn.training or not bn.track_running_stats
-    return _BNActFn.apply(y, parts, bn.weight, bn.bias, res, res_parts,
-                          None if res_bn is None else res_bn.weight,
-                          None if res_bn is None else res_bn.bias,
-                          (bn, relu, training, res_bn))
+    twin = _twin_wanted(twin, y)
+    out = _BNActFn.apply(y, parts, bn.weight, bn.bias, res, res_parts,
+                         None if res_bn is None else res_bn.weight,
+                         None if res_bn is None else res_bn.bias,
+                         (bn, relu, training, res_bn, twin))
+    if twin:
+        out, alias = out
+        _register_twin(out, alias)
+    return out
 
 
 class _BNReluPoolFn(torch.autograd.Function):
@@ -741,7 +834,7 @@ class _BNReluPoolFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, parts, gamma, beta, cfg):
-        bn, training, k, s, p = cfg
+        bn, training, k, s, p, twin = cfg
         mean, invstd, scale, shift, batch = _finalize(y, parts, bn, training)
         n, c, di, hi, wi = y.shape
         do, ho, wo = ((v + 2 * p - k) // s + 1 for v in (di, hi, wi))
@@ -755,22 +848,27 @@ class _BNReluPoolFn(torch.autograd.Function):
         ctx.params = (gamma, beta)
         ctx.geo = (n, c, di, hi, wi, do, ho, wo, k, s, p)
         ctx.batch = batch
+        if twin:
+            ctx.set_materialize_grads(False)
+            return out, out.view(out.shape)
         return out
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, g2=None):
         y, am, ymax, mean, invstd, gamma = ctx.saved_tensors
         n, c, di, hi, wi, do, ho, wo, k, s, p = ctx.geo
-        g = _cl(g)
-        if g.dtype != y.dtype:
-            g = cast(g, y.dtype)
+        g, g2 = _twin_grads(g, g2, y)
+        if g is None:
+            return (None,) * 5
+        if g2 is not None and not (c % 4 == 0 and k == 3 and s == 2 and p == 1):
+            g, g2 = _sum_grads(g, g2), None      # generic geometry: the apply takes one g
         dt = L.dtype_code(y.dtype)
         dev = y.device
         mp = n * do * ho * wo
         nparts = L.load().mmad_bn_bwd_parts(mp, c)
         parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
-        L.call("mmad_bnpool_bwd_reduce", dt, mp, c, L.ptr(g), L.ptr(am), L.ptr(ymax),
-               L.ptr(mean), L.ptr(invstd), L.ptr(parts), L.stream())
+        L.call("mmad_bnpool_bwd_reduce", dt, mp, c, L.ptr(g), L.ptr(g2), L.ptr(am),
+               L.ptr(ymax), L.ptr(mean), L.ptr(invstd), L.ptr(parts), L.stream())
         dgamma = grad_slot(ctx.params[0], (c,), dev)
         dbeta = grad_slot(ctx.params[1], (c,), dev)
         coef = torch.empty(3 * c, dtype=torch.float32, device=dev)
@@ -780,18 +878,24 @@ class _BNReluPoolFn(torch.autograd.Function):
                L.stream())
         dy = torch.empty_like(y)
         L.call("mmad_bnpool_bwd_apply", dt, n, c, di, hi, wi, do, ho, wo, k, s, p, L.ptr(g),
-               L.ptr(am), L.ptr(y), L.ptr(mean), L.ptr(invstd), L.ptr(coef), L.ptr(dy),
+               L.ptr(g2), L.ptr(am), L.ptr(y), L.ptr(mean), L.ptr(invstd), L.ptr(coef), L.ptr(dy),
                L.stream())
         return (dy, None, dgamma if ctx.needs_input_grad[2] else None,
                 dbeta if ctx.needs_input_grad[3] else None, None)
 
 
-def batchnorm_relu_maxpool(y, bn, parts, kernel_size, stride, padding):
-    """max_pool3d(relu(bn(y)), k, s, p) fused (MedicalNet stem: bn1 -> relu -> maxpool)."""
+def batchnorm_relu_maxpool(y, bn, parts, kernel_size, stride, padding, twin=False):
+    """max_pool3d(relu(bn(y)), k, s, p) fused (MedicalNet stem: bn1 -> relu -> maxpool);
+    ``twin`` as in batchnorm_act."""
     _check_vol(y)
     training = bn.training or not bn.track_running_stats
-    return _BNReluPoolFn.apply(y, parts, bn.weight, bn.bias,
-                               (bn, training, int(kernel_size), int(stride), int(padding)))
+    twin = _twin_wanted(twin, y)
+    out = _BNReluPoolFn.apply(y, parts, bn.weight, bn.bias,
+                              (bn, training, int(kernel_size), int(stride), int(padding), twin))
+    if twin:
+        out, alias = out
+        _register_twin(out, alias)
+    return out
 
 
 # ------------------------------------------------------------------------------- pooling
