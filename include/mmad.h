@@ -244,13 +244,16 @@ int mmad_maxpool3d_bwd(int dtype, int n, int c, int di, int hi, int wi, int do_,
 int mmad_bnpool_fwd(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho, int wo,
                     int k, int s, int p, const void* y, const float* scale, const float* shift,
                     void* out, uint8_t* argmax, void* ymax, void* stream);
+/* m = pooled rows; with g2 the summed gradient as_stored(g + g2) is also written to gsum
+ * (the apply then reads gsum as its g: the pool backward reads each pooled gradient from up
+ * to 8 cells, so it takes one summed tensor, not two) */
 int mmad_bnpool_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* g2,
-                           const uint8_t* argmax, const void* ymax, const float* mean,
-                           const float* invstd, float* parts, void* stream); /* m = pooled rows */
+                           void* gsum, const uint8_t* argmax, const void* ymax,
+                           const float* mean, const float* invstd, float* parts, void* stream);
 int mmad_bnpool_bwd_apply(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho,
-                          int wo, int k, int s, int p, const void* g, const void* g2,
-                          const uint8_t* argmax, const void* y, const float* mean,
-                          const float* invstd, const float* coef, void* dy, void* stream);
+                          int wo, int k, int s, int p, const void* g, const uint8_t* argmax,
+                          const void* y, const float* mean, const float* invstd,
+                          const float* coef, void* dy, void* stream);
 int mmad_gap_fwd(int dtype, int n, int64_t s, int c, const void* x, float* y, void* stream);
 /* same, partitioned over voxel slabs so small batches still fill the GPU; ws holds
  * mmad_gap_fwd_ws_elems(n, s, c) floats of partial sums (summed in a fixed order) */
@@ -267,6 +270,11 @@ int mmad_linear_fwd(int b, int in, int out, const float* x, const float* w,
                     const float* bias, int relu, float* y, void* stream);
 int mmad_linear_bwd(int b, int in, int out, const float* x, const float* w,
                     const float* dy, float* dx, float* dw, float* dbias, void* stream);
+/* Same in one launch, with the backward of a fused ReLU: ymask = the forward output of
+ * mmad_linear_fwd(relu=1) (NULL: no ReLU); the gradient is taken as ymask > 0 ? dy : 0. */
+int mmad_linear_bwd_ex(int b, int in, int out, const float* x, const float* w,
+                       const float* dy, const float* ymask, float* dx, float* dw, float* dbias,
+                       void* stream);
 int mmad_concat_cols(int b, int n_in, const float* const* srcs, const int* widths,
                      float* dst, void* stream);
 int mmad_split_cols(int b, int n_out, const float* src, float* const* dsts,
@@ -318,6 +326,16 @@ int mmad_dropout_bwd(int dtype, int64_t n, float p, const void* g, const uint8_t
 int mmad_loss_fwd(int b, int c, const double* logits, const int64_t* labels,
                   const double* weight, double gamma, int mode, double* loss,
                   double* dlogits, void* stream);
+/* Same on MMAD_F32 or MMAD_F64 logits (fp32 widened exactly on load); logits64 (may be
+ * NULL) receives the f64 logits -- general_step's f64 cast of the model output
+ * (anat_cnn.py:102-104) fused into the loss launch. */
+int mmad_loss_fwd_ex(int b, int c, int logits_dtype, const void* logits,
+                     const int64_t* labels, const double* weight, double gamma, int mode,
+                     double* logits64, double* loss, double* dlogits, void* stream);
+/* d logits = (out_dtype) (dlogits * gloss[0] (+ gout[i] when gout != NULL)): the loss
+ * backward and the f64 cast's backward in one pass (n = B*C). */
+int mmad_loss_bwd(int64_t n, const double* dlogits, const double* gloss, const double* gout,
+                  int out_dtype, void* dx, void* stream);
 
 /* ---- test-set bootstrap (Base_Model.bootstrap_metric, pkg/models/base_model.py:219-239) --
  * For each of ndraw drawings d (idx[d][0..n) = the drawing's sample indices, as drawn by

@@ -99,8 +99,8 @@ _SIGS = {
     "mmad_maxpool3d_fwd": (_i32, [_i32] * 12 + [_vp, _vp, _vp, _vp]),
     "mmad_maxpool3d_bwd": (_i32, [_i32] * 12 + [_vp, _vp, _vp, _vp]),
     "mmad_bnpool_fwd": (_i32, [_i32] * 12 + [_vp] * 7),
-    "mmad_bnpool_bwd_reduce": (_i32, [_i32, _i64, _i32] + [_vp] * 8),
-    "mmad_bnpool_bwd_apply": (_i32, [_i32] * 12 + [_vp] * 9),
+    "mmad_bnpool_bwd_reduce": (_i32, [_i32, _i64, _i32] + [_vp] * 9),
+    "mmad_bnpool_bwd_apply": (_i32, [_i32] * 12 + [_vp] * 8),
     "mmad_gap_fwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_gap_fwd_ws_elems": (_i64, [_i32, _i64, _i32]),
     "mmad_conv3d_fwd_ex": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
@@ -114,6 +114,7 @@ _SIGS = {
     "mmad_gap_bwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_linear_fwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp]),
     "mmad_linear_bwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_linear_bwd_ex": (_i32, [_i32, _i32, _i32] + [_vp] * 8),
     "mmad_concat_cols": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp]),
     "mmad_split_cols": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp]),
     "mmad_cast": (_i32, [_i32, _i32, _i64, _vp, _vp, _vp]),
@@ -121,6 +122,9 @@ _SIGS = {
     "mmad_dropout_fwd_dev": (_i32, [_i32, _i64, _f32, _vp, _vp, _vp, _vp, _vp]),
     "mmad_dropout_bwd": (_i32, [_i32, _i64, _f32, _vp, _vp, _vp, _vp]),
     "mmad_loss_fwd": (_i32, [_i32, _i32, _vp, _vp, _vp, _f64, _i32, _vp, _vp, _vp]),
+    "mmad_loss_fwd_ex": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _f64, _i32, _vp, _vp, _vp,
+                                _vp]),
+    "mmad_loss_bwd": (_i32, [_i64, _vp, _vp, _vp, _i32, _vp, _vp]),
     "mmad_gather_channels": (_i32, [_i32, _i32, _vp, _i64, _i64, _i32, _i64, _i32, _i32, _vp,
                                     _vp]),
     "mmad_pad_rows": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp]),

@@ -59,6 +59,10 @@ class FocalLoss(nn.Module):
             loss = loss * target.numel()
         return loss
 
+    def fused_spec(self):
+        """(weight, gamma, mode) for head_ops.logits_and_loss"""
+        return (None, float(self.gamma), 1) if self.size_average else None
+
 
 def make_criterion(hparams):
     """anat_cnn.py:81-85: focal loss iff hparams['fl_gamma'] is truthy, else weighted CE."""
@@ -69,6 +73,18 @@ def make_criterion(hparams):
 
 def _to_f64(y_hat):
     return cast(y_hat, torch.float64)
+
+
+def _logits_and_loss(criterion, out, y):
+    """(y_hat = out as f64, criterion(y_hat, y)) -- anat_cnn.py:102-104 -- with the cast
+    and our losses fused into one launch each way when the criterion allows it."""
+    spec = getattr(criterion, "fused_spec", None)
+    spec = spec() if spec is not None else None
+    if spec is not None and out.dim() == 2 and out.dtype in (torch.float32, torch.float64) \
+            and out.is_cuda:
+        return head_ops.logits_and_loss(out, y, *spec)
+    y_hat = _to_f64(out)
+    return y_hat, criterion(y_hat, y)
 
 
 # -------------------------------------------------------------------------- base model
@@ -219,7 +235,7 @@ def build_conv_seg(hparams, n_in):
         mods.append(Lyr.ReLU())
         n_in = n_out
     mods += [Lyr.Linear(n_in, hparams["n_classes"]), Lyr.ReLU()]
-    return nn.Sequential(*mods)
+    return Lyr.Sequential(*mods)
 
 
 def _resnet_backbone(hparams):
@@ -365,8 +381,7 @@ class Anat_CNN(Base_Model):
     def general_step(self, batch, batch_idx, mode):
         x = batch[self.batch_key].unsqueeze(1)   # raw f64 volume; conv 1 unfolds + casts it
         y = batch["label"]
-        y_hat = _to_f64(self.forward(x))
-        loss = self.criterion(y_hat, y)
+        y_hat, loss = _logits_and_loss(self.criterion, self.forward(x), y)
         if mode != "pred":
             self.log(mode + "_loss", loss, on_step=True, prog_bar=True)
         return {"loss": loss, "outputs": y_hat, "labels": y}

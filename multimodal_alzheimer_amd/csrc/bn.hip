@@ -37,9 +37,10 @@ PartPlan part_plan(int64_t M) {
 // DUAL (MODE 1 only): a second BN over the same gradient and ReLU mask (the shortcut BN of
 // a residual block, y2 = its input): parts2 gets (sum g', sum g' * xhat2) from the same pass,
 // so g and the mask are read once for both
-// g2 (MODE 1 / 3, may be NULL): a second gradient of the same output (the block input's
-// other consumer, volume_ops twin outputs); g is then as_stored(g + g2), rounded as torch's
-// own gradient accumulation rounds it, so no separate add pass is needed
+// G2 (MODE 1 / 3): a second gradient of the same output (the block input's other consumer,
+// volume_ops twin outputs); g is then as_stored(g + g2), rounded as torch's own gradient
+// accumulation rounds it, so no separate add pass is needed.  MODE 3 also stores that sum
+// to gsum (the pool backward's input).
 template <typename T, int MODE, int V, bool DUAL = false, bool G2 = false>
 __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t rpp,
                                                      const T* __restrict__ y,
@@ -55,7 +56,8 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
                                                      const float* __restrict__ mean2 = nullptr,
                                                      const float* __restrict__ invstd2 = nullptr,
                                                      float* __restrict__ parts2 = nullptr,
-                                                     const T* __restrict__ g2 = nullptr) {
+                                                     const T* __restrict__ g2 = nullptr,
+                                                     T* __restrict__ gsum = nullptr) {
   static_assert(!DUAL || MODE == 1, "dual partial sums: BN backward with a relu_out mask");
   __shared__ float red[DUAL ? 3 : 2][2048];
   const int tid = threadIdx.x;
@@ -148,6 +150,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
             Chunk<T>::load(reinterpret_cast<const T*>(&g2r[u]), hv);
 #pragma unroll
             for (int e = 0; e < V; ++e) gv[e] = as_stored<T>(gv[e] + hv[e]);
+            if constexpr (MODE == 3) Chunk<T>::store(gsum + i, gv);
           }
           if (MODE == 1 && relu_out != nullptr)
             Chunk<T>::load(reinterpret_cast<const T*>(&orr[u]), ov);
@@ -170,6 +173,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
           else for (int e = 0; e < V; ++e) hv[e] = Elt<T>::ld(g2, i + e);
 #pragma unroll
           for (int e = 0; e < V; ++e) gv[e] = as_stored<T>(gv[e] + hv[e]);
+          if constexpr (MODE == 3) {
+            if constexpr (V == Chunk<T>::N) Chunk<T>::store(gsum + i, gv);
+            else for (int e = 0; e < V; ++e) Elt<T>::st(gsum, i + e, gv[e]);
+          }
         }
         if (MODE == 1 && relu_out != nullptr) {
           if constexpr (V == Chunk<T>::N) Chunk<T>::load(relu_out + i, ov);
@@ -224,7 +231,8 @@ template <typename T, int MODE>
 int launch_colsum(int64_t M, int C, const void* y, const void* g, const void* ro,
                   const float* mean, const float* invstd, float* parts, hipStream_t st,
                   const uint8_t* act = nullptr, const float* msc = nullptr,
-                  const float* msh = nullptr, const void* g2 = nullptr) {
+                  const float* msh = nullptr, const void* g2 = nullptr,
+                  void* gsum = nullptr) {
   const PartPlan pp = part_plan(M);
   constexpr int VEC = Chunk<T>::N;
   dim3 grid((unsigned)pp.nparts);
@@ -235,7 +243,7 @@ int launch_colsum(int64_t M, int C, const void* y, const void* g, const void* ro
 #define COLSUM(VV, G)                                                                       \
   hipLaunchKernelGGL((colsum_kernel<T, MODE, VV, false, G>), grid, dim3(256), 0, st, M, C, \
                      pp.rpp, (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act, \
-                     msc, msh, nullptr, nullptr, nullptr, nullptr, (const T*)g2)
+                     msc, msh, nullptr, nullptr, nullptr, nullptr, (const T*)g2, (T*)gsum)
   if (C % (slabs * VEC) == 0 && C / (slabs * VEC) <= 256) {
     grid.y = (unsigned)slabs;
     if constexpr (MODE == 1 || MODE == 3) {
@@ -889,16 +897,18 @@ int mmad_bn_relu_bwd_apply(int dtype, int64_t m, int c, const void* g, const voi
 }
 
 int mmad_bnpool_bwd_reduce(int dtype, int64_t m, int c, const void* g, const void* g2,
-                           const uint8_t* argmax, const void* ymax, const float* mean,
-                           const float* invstd, float* parts, void* stream) {
+                           void* gsum, const uint8_t* argmax, const void* ymax,
+                           const float* mean, const float* invstd, float* parts,
+                           void* stream) {
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
   if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
   if (!g || !argmax || !ymax || !mean || !invstd || !parts) return MMAD_ENULL;
+  if (g2 && !gsum) return MMAD_ENULL;
   if (dtype == MMAD_BF16)
     return launch_colsum<u16, 3>(m, c, ymax, g, nullptr, mean, invstd, parts, as_stream(stream),
-                                 argmax, nullptr, nullptr, g2);
+                                 argmax, nullptr, nullptr, g2, gsum);
   return launch_colsum<float, 3>(m, c, ymax, g, nullptr, mean, invstd, parts, as_stream(stream),
-                                 argmax, nullptr, nullptr, g2);
+                                 argmax, nullptr, nullptr, g2, gsum);
 }
 
 int mmad_bn_fold(int c, const float* gamma, const float* beta, const float* running_mean,
@@ -988,7 +998,7 @@ int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* 
     hipLaunchKernelGGL(k, dim3((unsigned)pp.nparts, slabs), dim3(256), 0, st, m, c, pp.rpp,
                        (const T*)y, (const T*)g, (const T*)relu_out, mean, invstd, parts,
                        nullptr, nullptr, nullptr, (const T*)y2, mean2, invstd2, parts2,
-                       (const T*)g2);
+                       (const T*)g2, (T*)nullptr);
     return launch_status();
   };
   return dtype == MMAD_BF16 ? go(u16{}) : go(float{});

@@ -32,31 +32,38 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(int B, int IN, int OUT,
   }
 }
 
-// dx[b][i] = sum_o dy[b][o] w[o][i]   (thread per (b, i), coalesced over i)
-__global__ void linear_dx_kernel(int B, int IN, int OUT, const float* __restrict__ w,
-                                 const float* __restrict__ dy, float* __restrict__ dx) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= (int64_t)B * IN) return;
-  const int b = (int)(t / IN), i = (int)(t % IN);
-  float s = 0.f;
-  for (int o = 0; o < OUT; ++o) s += dy[(int64_t)b * OUT + o] * w[(int64_t)o * IN + i];
-  dx[t] = s;
-}
-
-// dw[o][i] = sum_b dy[b][o] x[b][i]; dbias[o] = sum_b dy[b][o]
-__global__ void linear_dw_kernel(int B, int IN, int OUT, const float* __restrict__ x,
-                                 const float* __restrict__ dy, float* __restrict__ dw,
-                                 float* __restrict__ dbias) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t < (int64_t)OUT * IN) {
+// Linear backward in one launch: blocks [0, nbx) compute dx, the rest dw / dbias.
+//   dx[b][i] = sum_o g[b][o] w[o][i]   (thread per (b, i), coalesced over i)
+//   dw[o][i] = sum_b g[b][o] x[b][i];  dbias[o] = sum_b g[b][o]
+// g = dy, or with ymask (the forward's ReLU output) g = ymask > 0 ? dy : 0 -- the fused
+// Linear+ReLU's backward, same values as a separate ReLU-backward pass
+__global__ void linear_bwd_kernel(int B, int IN, int OUT, int nbx, const float* __restrict__ x,
+                                  const float* __restrict__ w, const float* __restrict__ dy,
+                                  const float* __restrict__ ymask, float* __restrict__ dx,
+                                  float* __restrict__ dw, float* __restrict__ dbias) {
+  auto gval = [&](int64_t k) {
+    const float v = dy[k];
+    return ymask == nullptr || ymask[k] > 0.f ? v : 0.f;
+  };
+  if ((int)blockIdx.x < nbx) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= (int64_t)B * IN) return;
+    const int b = (int)(t / IN), i = (int)(t % IN);
+    float s = 0.f;
+    for (int o = 0; o < OUT; ++o) s += gval((int64_t)b * OUT + o) * w[(int64_t)o * IN + i];
+    dx[t] = s;
+    return;
+  }
+  const int64_t t = (blockIdx.x - nbx) * (int64_t)blockDim.x + threadIdx.x;
+  if (dw != nullptr && t < (int64_t)OUT * IN) {
     const int o = (int)(t / IN), i = (int)(t % IN);
     float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dy[(int64_t)b * OUT + o] * x[(int64_t)b * IN + i];
+    for (int b = 0; b < B; ++b) s += gval((int64_t)b * OUT + o) * x[(int64_t)b * IN + i];
     dw[t] = s;
   }
   if (dbias && t < OUT) {
     float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dy[(int64_t)b * OUT + t];
+    for (int b = 0; b < B; ++b) s += gval((int64_t)b * OUT + t);
     dbias[t] = s;
   }
 }
@@ -139,13 +146,23 @@ __global__ void dropout_bwd_kernel(int64_t n, float p, const T* __restrict__ g,
 
 // mode 0: weighted CE (mean = sum w_y nll / sum w_y); mode 1: focal, pt detached.
 // One block; thread per sample (loop), f64 throughout; block reduction in fixed order.
-__global__ __launch_bounds__(256) void loss_kernel(int B, int C, const double* __restrict__ x,
+// TI = float: the logits arrive in fp32 and are widened on load (exactly, as the f64 cast
+// general_step applies first); x64 (may be NULL) then receives that f64 copy.
+template <typename TI>
+__global__ __launch_bounds__(256) void loss_kernel(int B, int C, const TI* __restrict__ xin,
                                                    const int64_t* __restrict__ y,
                                                    const double* __restrict__ w, double gamma,
                                                    int mode, double* __restrict__ loss,
                                                    double* __restrict__ dx,
-                                                   int* __restrict__ err) {
+                                                   int* __restrict__ err,
+                                                   double* __restrict__ x64) {
   __shared__ double red[2][256];
+  struct Wide {
+    const TI* p;
+    __device__ double operator[](int64_t i) const { return (double)p[i]; }
+  } x{xin};
+  if (x64 != nullptr)
+    for (int64_t i = threadIdx.x; i < (int64_t)B * C; i += blockDim.x) x64[i] = x[i];
   double num = 0.0, den = 0.0;
   const int igamma = (int)gamma;
   const bool int_gamma = (double)igamma == gamma && igamma >= 0 && igamma <= 16;
@@ -214,6 +231,20 @@ __global__ __launch_bounds__(256) void loss_kernel(int B, int C, const double* _
       dx[(int64_t)b * C + c] = coef * (sm - (c == t ? 1.0 : 0.0));
     }
   }
+}
+
+// d logits = cast(dlogits * gloss (+ gout)): the loss's backward (autograd's f64 product with
+// the incoming scalar gradient, plus the f64 logits' own gradient when they are used) and
+// the f64 -> out_dtype cast's backward in one pass
+__global__ void loss_bwd_kernel(int64_t n, const double* __restrict__ dl,
+                                const double* __restrict__ gl, const double* __restrict__ go,
+                                int out_dtype, void* __restrict__ dx) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double v = dl[i] * gl[0];
+  if (go != nullptr) v = v + go[i];
+  if (out_dtype == MMAD_F32) static_cast<float*>(dx)[i] = (float)v;
+  else static_cast<double*>(dx)[i] = v;
 }
 
 // Bootstrap of the test-set classification metrics (pkg/models/base_model.py:219-239):
@@ -307,22 +338,20 @@ int mmad_linear_fwd(int b, int in, int out, const float* x, const float* w, cons
 
 int mmad_linear_bwd(int b, int in, int out, const float* x, const float* w, const float* dy,
                     float* dx, float* dw, float* dbias, void* stream) {
+  return mmad_linear_bwd_ex(b, in, out, x, w, dy, nullptr, dx, dw, dbias, stream);
+}
+
+int mmad_linear_bwd_ex(int b, int in, int out, const float* x, const float* w, const float* dy,
+                       const float* ymask, float* dx, float* dw, float* dbias, void* stream) {
   if (b <= 0 || in <= 0 || out <= 0) return MMAD_EBADSHAPE;
   if (!dy) return MMAD_ENULL;
-  hipStream_t st = as_stream(stream);
-  if (dx) {
-    if (!w) return MMAD_ENULL;
-    hipLaunchKernelGGL(linear_dx_kernel, dim3((unsigned)cdiv((int64_t)b * in, 256)), dim3(256), 0,
-                       st, b, in, out, w, dy, dx);
-    int rc = launch_status();
-    if (rc) return rc;
-  }
-  if (dw || dbias) {
-    if (!x || !dw) return MMAD_ENULL;
-    const int64_t n = std::max<int64_t>((int64_t)out * in, out);
-    hipLaunchKernelGGL(linear_dw_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, b, in,
-                       out, x, dy, dw, dbias);
-  }
+  if (dx && !w) return MMAD_ENULL;
+  if ((dw || dbias) && (!x || !dw)) return MMAD_ENULL;
+  const int nbx = dx ? (int)cdiv((int64_t)b * in, 256) : 0;
+  const int nbw = (dw || dbias) ? (int)cdiv(std::max<int64_t>((int64_t)out * in, out), 256) : 0;
+  if (nbx + nbw == 0) return MMAD_OK;
+  hipLaunchKernelGGL(linear_bwd_kernel, dim3((unsigned)(nbx + nbw)), dim3(256), 0,
+                     as_stream(stream), b, in, out, nbx, x, w, dy, ymask, dx, dw, dbias);
   return launch_status();
 }
 
@@ -422,12 +451,37 @@ int mmad_dropout_bwd(int dtype, int64_t n, float p, const void* g, const uint8_t
 
 int mmad_loss_fwd(int b, int c, const double* logits, const int64_t* labels, const double* weight,
                   double gamma, int mode, double* loss, double* dlogits, void* stream) {
+  return mmad_loss_fwd_ex(b, c, MMAD_F64, logits, labels, weight, gamma, mode, nullptr, loss,
+                          dlogits, stream);
+}
+
+int mmad_loss_fwd_ex(int b, int c, int logits_dtype, const void* logits, const int64_t* labels,
+                     const double* weight, double gamma, int mode, double* logits64,
+                     double* loss, double* dlogits, void* stream) {
   if (b <= 0 || c <= 0 || (mode != 0 && mode != 1)) return MMAD_EBADSHAPE;
   if (!logits || !labels || !loss || !dlogits) return MMAD_ENULL;
   // one wave for small batches (the usual 8-16 samples), up to 256 threads beyond
   const unsigned nt = (unsigned)std::min(256, (int)cdiv(b, 64) * 64);
-  hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(nt), 0, as_stream(stream), b, c, logits, labels,
-                     weight, gamma, mode, loss, dlogits, (int*)nullptr);
+  hipStream_t st = as_stream(stream);
+  if (logits_dtype == MMAD_F64)
+    hipLaunchKernelGGL(loss_kernel<double>, dim3(1), dim3(nt), 0, st, b, c,
+                       (const double*)logits, labels, weight, gamma, mode, loss, dlogits,
+                       (int*)nullptr, logits64);
+  else if (logits_dtype == MMAD_F32)
+    hipLaunchKernelGGL(loss_kernel<float>, dim3(1), dim3(nt), 0, st, b, c, (const float*)logits,
+                       labels, weight, gamma, mode, loss, dlogits, (int*)nullptr, logits64);
+  else
+    return MMAD_EBADDTYPE;
+  return launch_status();
+}
+
+int mmad_loss_bwd(int64_t n, const double* dlogits, const double* gloss, const double* gout,
+                  int out_dtype, void* dx, void* stream) {
+  if (n <= 0) return MMAD_EBADSHAPE;
+  if (!dlogits || !gloss || !dx) return MMAD_ENULL;
+  if (out_dtype != MMAD_F64 && out_dtype != MMAD_F32) return MMAD_EBADDTYPE;
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), n, dlogits, gloss, gout, out_dtype, dx);
   return launch_status();
 }
 

@@ -404,17 +404,6 @@ struct Packed {
     if constexpr (sizeof(T) == 4) return __uint_as_float(w[e]);
     else return __uint_as_float((e & 1) ? (w[e >> 1] & 0xffff0000u) : (w[e >> 1] << 16));
   }
-  // this += o, rounded to T per element (torch's gradient accumulation of two bf16 grads)
-  __device__ __forceinline__ void add_rounded(const Packed& o) {
-    if constexpr (sizeof(T) == 4) {
-#pragma unroll
-      for (int e = 0; e < V; ++e) w[e] = __float_as_uint(get(e) + o.get(e));
-    } else {
-#pragma unroll
-      for (int i = 0; i < W; ++i)
-        w[i] = pack_bf16x2(get(2 * i) + o.get(2 * i), get(2 * i + 1) + o.get(2 * i + 1));
-    }
-  }
 };
 
 template <typename T, int V>
@@ -435,12 +424,11 @@ __device__ __forceinline__ void store_packed(T* p, const float* v) {
 // V = 4 channels per thread in both dtypes (8-byte bf16 / 16-byte fp32 accesses): the 8
 // windows' argmax bytes, pooled gradients and the cell's 8 inputs stay packed, so the cell
 // fits in ~100 VGPRs (4+ waves per SIMD; 8 bf16 channels per thread needed 247)
-template <typename T, int V, bool G2 = false>
+template <typename T, int V>
 __device__ __forceinline__ void bnpool3s2_bwd_cell(
     const PoolG& g, const T* __restrict__ gp, const uint8_t* __restrict__ am,
     const T* __restrict__ y, T* __restrict__ dy, int64_t nb, int ad, int ah, int aw, int c0,
-    const float* mu, const float* k0, const float* k1, const float* kt,
-    const T* __restrict__ gp2) {
+    const float* mu, const float* k0, const float* k1, const float* kt) {
   static_assert(V == 4, "argmax bytes are read as one 32-bit word");
   uint32_t a4[8];
   Packed<T, V> graw[8], yraw[8];
@@ -454,11 +442,6 @@ __device__ __forceinline__ void bnpool3s2_bwd_cell(
     const uint32_t w = *reinterpret_cast<const uint32_t*>(am + o);
     a4[q] = ok ? w : 0;          // 0: no active window (the 0x80 bit is never set)
     graw[q].load(gp + o);
-    if constexpr (G2) {            // second gradient of the pooled output (twin consumer)
-      Packed<T, V> h;
-      h.load(gp2 + o);
-      graw[q].add_rounded(h);
-    }
     const int id = min(2 * ad + qd, g.di - 1), ih = min(2 * ah + qh, g.hi - 1);
     const int iw = min(2 * aw + qw, g.wi - 1);
     yraw[q].load(y + (((nb * g.di + id) * g.hi + ih) * g.wi + iw) * g.c + c0);
@@ -489,11 +472,11 @@ __device__ __forceinline__ void bnpool3s2_bwd_cell(
   }
 }
 
-template <typename T, int V, bool G2 = false>
+template <typename T, int V>
 __global__ __launch_bounds__(256) void bnpool3s2_bwd_apply_kernel(
     PoolG g, const T* __restrict__ gp, const uint8_t* __restrict__ am, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
-    const float* __restrict__ coef, T* __restrict__ dy, const T* __restrict__ gp2) {
+    const float* __restrict__ coef, T* __restrict__ dy) {
   const int cv = g.c / V;
   const int cd = (g.di + 1) >> 1, ch = (g.hi + 1) >> 1, cw = (g.wi + 1) >> 1;
   const int64_t total = (int64_t)g.n * cd * ch * cw * cv;
@@ -506,17 +489,17 @@ __global__ __launch_bounds__(256) void bnpool3s2_bwd_apply_kernel(
     const int ad = (int)(v % cd);
     float mu[V], k0[V], k1[V], kt[V];
     bnbwd_params<V>(g.c, c0, mean, invstd, coef, mu, k0, k1, kt);
-    bnpool3s2_bwd_cell<T, V, G2>(g, gp, am, y, dy, v / cd, ad, ah, aw, c0, mu, k0, k1, kt, gp2);
+    bnpool3s2_bwd_cell<T, V>(g, gp, am, y, dy, v / cd, ad, ah, aw, c0, mu, k0, k1, kt);
   }
 }
 
 // Same, one block per row of cells (blockIdx.y = ah, blockIdx.z = n*cd + ad), power-of-two
 // channel-vector count: shift/mask index math (see bnpool3_fwd_rows_kernel).
-template <typename T, int V, bool G2 = false>
+template <typename T, int V>
 __global__ __launch_bounds__(256) void bnpool3s2_bwd_rows_kernel(
     PoolG g, int cv_shift, const T* __restrict__ gp, const uint8_t* __restrict__ am,
     const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
-    const float* __restrict__ coef, T* __restrict__ dy, const T* __restrict__ gp2) {
+    const float* __restrict__ coef, T* __restrict__ dy) {
   const int cd = (g.di + 1) >> 1, cw = (g.wi + 1) >> 1;
   const int ah = blockIdx.y, ad = blockIdx.z % cd;
   const int64_t nb = blockIdx.z / cd;
@@ -525,8 +508,7 @@ __global__ __launch_bounds__(256) void bnpool3s2_bwd_rows_kernel(
   float mu[V], k0[V], k1[V], kt[V];
   bnbwd_params<V>(g.c, c0, mean, invstd, coef, mu, k0, k1, kt);
   for (int e = threadIdx.x; e < items; e += 256)
-    bnpool3s2_bwd_cell<T, V, G2>(g, gp, am, y, dy, nb, ad, ah, e >> cv_shift, c0, mu, k0, k1,
-                                 kt, gp2);
+    bnpool3s2_bwd_cell<T, V>(g, gp, am, y, dy, nb, ad, ah, e >> cv_shift, c0, mu, k0, k1, kt);
 }
 
 // Fused backward, dense pass: for every input voxel, g' = sum of the pooled gradients of the
@@ -736,26 +718,20 @@ int bnpool_fwd(const PoolG& g, const void* y, const float* scale, const float* s
 template <typename T>
 int bnpool_bwd_apply(const PoolG& g, const void* gp, const uint8_t* am, const void* y,
                      const float* mean, const float* invstd, const float* coef, void* dy,
-                     hipStream_t st, const void* gp2) {
+                     hipStream_t st) {
   constexpr int VEC = Chunk<T>::N;
   const int64_t vox = (int64_t)g.n * g.di * g.hi * g.wi;
   const int cd = (g.di + 1) >> 1, ch = (g.hi + 1) >> 1;
   const int cv4 = g.c / 4;   // the k3 s2 cell kernels take 4 channels per thread
   if (g.c % 4 == 0 && g.k == 3 && g.s == 2 && g.p == 1 && is_pow2(cv4) && cv4 <= 256 &&
-      rows_on() && (int64_t)g.n * cd < 65536 && ch < 65536) {
-    auto k = gp2 != nullptr ? bnpool3s2_bwd_rows_kernel<T, 4, true>
-                            : bnpool3s2_bwd_rows_kernel<T, 4, false>;
-    hipLaunchKernelGGL(k, dim3(1, (unsigned)ch, (unsigned)(g.n * cd)), dim3(256), 0, st, g,
-                       ilog2(cv4), (const T*)gp, am, (const T*)y, mean, invstd, coef, (T*)dy,
-                       (const T*)gp2);
-  } else if (g.c % 4 == 0 && g.k == 3 && g.s == 2 && g.p == 1) {
-    auto k = gp2 != nullptr ? bnpool3s2_bwd_apply_kernel<T, 4, true>
-                            : bnpool3s2_bwd_apply_kernel<T, 4, false>;
-    hipLaunchKernelGGL(k, dim3(grid_of(vox * g.c / 4 / 8 + 1)), dim3(256), 0, st, g,
-                       (const T*)gp, am, (const T*)y, mean, invstd, coef, (T*)dy,
-                       (const T*)gp2);
-  } else if (gp2 != nullptr)
-    return MMAD_EUNSUPPORTED;     // generic pool geometry: the caller adds the twin first
+      rows_on() && (int64_t)g.n * cd < 65536 && ch < 65536)
+    hipLaunchKernelGGL((bnpool3s2_bwd_rows_kernel<T, 4>),
+                       dim3(1, (unsigned)ch, (unsigned)(g.n * cd)), dim3(256), 0, st, g,
+                       ilog2(cv4), (const T*)gp, am, (const T*)y, mean, invstd, coef, (T*)dy);
+  else if (g.c % 4 == 0 && g.k == 3 && g.s == 2 && g.p == 1)
+    hipLaunchKernelGGL((bnpool3s2_bwd_apply_kernel<T, 4>), dim3(grid_of(vox * g.c / 4 / 8 + 1)),
+                       dim3(256), 0, st, g, (const T*)gp, am, (const T*)y, mean, invstd, coef,
+                       (T*)dy);
   else if (g.c % VEC == 0)
     hipLaunchKernelGGL((bnpool_bwd_apply_kernel<T, VEC>), dim3(grid_of(vox * g.c / VEC)),
                        dim3(256), 0, st, g, (const T*)gp, am, (const T*)y, mean, invstd, coef,
@@ -853,18 +829,16 @@ int mmad_bnpool_fwd(int dtype, int n, int c, int di, int hi, int wi, int do_, in
 }
 
 int mmad_bnpool_bwd_apply(int dtype, int n, int c, int di, int hi, int wi, int do_, int ho,
-                          int wo, int k, int s, int p, const void* g, const void* g2,
-                          const uint8_t* argmax, const void* y, const float* mean,
-                          const float* invstd, const float* coef, void* dy, void* stream) {
+                          int wo, int k, int s, int p, const void* g, const uint8_t* argmax,
+                          const void* y, const float* mean, const float* invstd,
+                          const float* coef, void* dy, void* stream) {
   PoolG pg{n, c, di, hi, wi, do_, ho, wo, k, s, p};
   if (!pool_ok(pg) || k * k * k > 127) return MMAD_EBADSHAPE;
   if (!g || !argmax || !y || !mean || !invstd || !coef || !dy) return MMAD_ENULL;
   if (dtype == MMAD_BF16)
-    return bnpool_bwd_apply<u16>(pg, g, argmax, y, mean, invstd, coef, dy, as_stream(stream),
-                                 g2);
+    return bnpool_bwd_apply<u16>(pg, g, argmax, y, mean, invstd, coef, dy, as_stream(stream));
   if (dtype == MMAD_F32)
-    return bnpool_bwd_apply<float>(pg, g, argmax, y, mean, invstd, coef, dy, as_stream(stream),
-                                   g2);
+    return bnpool_bwd_apply<float>(pg, g, argmax, y, mean, invstd, coef, dy, as_stream(stream));
   return MMAD_EBADDTYPE;
 }
 

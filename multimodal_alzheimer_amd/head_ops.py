@@ -42,10 +42,6 @@ class _LinearFn(torch.autograd.Function):
             g = cast(g, torch.float32)
         b, n_in = x.shape
         n_out = weight.shape[0]
-        if ctx.relu:
-            gm = torch.empty_like(g)
-            L.call("mmad_relu_bwd", L.F32, g.numel(), L.ptr(g), L.ptr(y), L.ptr(gm), L.stream())
-            g = gm
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
@@ -54,8 +50,9 @@ class _LinearFn(torch.autograd.Function):
             dw = grad_slot(ctx.params[0], tuple(weight.shape), g.device)
             if ctx.has_bias:
                 db = grad_slot(ctx.params[1], (n_out,), g.device)
-        L.call("mmad_linear_bwd", b, n_in, n_out, L.ptr(x), L.ptr(weight.detach()), L.ptr(g),
-               L.ptr(dx), L.ptr(dw), L.ptr(db), L.stream())
+        # one launch: dx and dW / dbias, the fused ReLU's mask taken from the saved output
+        L.call("mmad_linear_bwd_ex", b, n_in, n_out, L.ptr(x), L.ptr(weight.detach()), L.ptr(g),
+               L.ptr(y if ctx.relu else None), L.ptr(dx), L.ptr(dw), L.ptr(db), L.stream())
         return dx, (dw if ctx.needs_input_grad[1] else None), db, None
 
 
@@ -163,6 +160,52 @@ class _LossFn(torch.autograd.Function):
         if ctx.in_dtype != torch.float64:
             grad = cast(grad, ctx.in_dtype)
         return grad, None, None, None, None
+
+
+class _LogitsLossFn(torch.autograd.Function):
+    """(logits as f64, loss(f64 logits, target)): general_step's f64 cast of the model output
+    (anat_cnn.py:102-104) and the loss in one launch (mmad_loss_fwd_ex); backward: the loss
+    gradient times the incoming scalar, plus the f64 logits' own gradient if any, cast back
+    to the logits' dtype in one launch (mmad_loss_bwd).  Same values as cast + _LossFn."""
+
+    @staticmethod
+    def forward(ctx, logits, target, weight, gamma, mode):
+        L.require_device(logits, target)
+        x = logits.contiguous()
+        t = target.contiguous().to(torch.int64) if target.dtype != torch.int64 else \
+            target.contiguous()
+        b, c = x.shape
+        w = None if weight is None else weight.detach().to(torch.float64).contiguous()
+        y64 = torch.empty((b, c), dtype=torch.float64, device=x.device)
+        loss = torch.empty((), dtype=torch.float64, device=x.device)
+        dx = torch.empty_like(y64)
+        L.call("mmad_loss_fwd_ex", b, c, L.dtype_code(x.dtype), L.ptr(x), L.ptr(t), L.ptr(w),
+               float(gamma), int(mode), L.ptr(y64), L.ptr(loss), L.ptr(dx), L.stream())
+        ctx.save_for_backward(dx)
+        ctx.in_dtype = logits.dtype
+        ctx.set_materialize_grads(False)
+        return y64, loss
+
+    @staticmethod
+    def backward(ctx, g_y64, g_loss):
+        if g_loss is None:
+            return (None if g_y64 is None else cast(g_y64.contiguous(), ctx.in_dtype),
+                    None, None, None, None)
+        (dx,) = ctx.saved_tensors
+        gl = g_loss.detach().to(torch.float64).contiguous()
+        go = None if g_y64 is None else g_y64.detach().to(torch.float64).contiguous()
+        out = torch.empty(dx.shape, dtype=ctx.in_dtype, device=dx.device)
+        L.call("mmad_loss_bwd", dx.numel(), L.ptr(dx), L.ptr(gl), L.ptr(go),
+               L.dtype_code(ctx.in_dtype), L.ptr(out), L.stream())
+        return out, None, None, None, None
+
+
+def logits_and_loss(logits, target, weight, gamma, mode):
+    """(logits.to(float64), loss) for (B, C) fp32 / f64 logits: mode 0 weighted CE with
+    ``weight``, mode 1 focal with ``gamma`` (see _LogitsLossFn)."""
+    if logits.dim() != 2 or logits.dtype not in (torch.float32, torch.float64):
+        raise L.MMADError("logits_and_loss expects (B, C) fp32 / f64 logits")
+    return _LogitsLossFn.apply(logits, target.reshape(-1), weight, float(gamma), int(mode))
 
 
 def weighted_cross_entropy(logits, target, weight=None):

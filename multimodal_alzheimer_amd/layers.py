@@ -105,6 +105,29 @@ class Linear(nn.Linear):
         return head_ops.linear(x, self.weight, self.bias)
 
 
+class Sequential(nn.Sequential):
+    """nn.Sequential (same modules, indices, state_dict keys and slicing) whose
+    ``Linear -> ReLU`` pairs run as one fused launch each way (head_ops.linear(relu=True):
+    the ReLU in the dot-product epilogue, its mask in the linear backward).  A pair with
+    module hooks runs unfused."""
+
+    def forward(self, x):
+        mods = list(self._modules.values())
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            nxt = mods[i + 1] if i + 1 < len(mods) else None
+            if (type(m) is Linear and type(nxt) is ReLU and x.dim() == 2 and
+                    not (m._forward_hooks or m._forward_pre_hooks or nxt._forward_hooks or
+                         nxt._forward_pre_hooks)):
+                x = head_ops.linear(x, m.weight, m.bias, relu=True)
+                i += 2
+                continue
+            x = m(x)
+            i += 1
+        return x
+
+
 class Dropout(nn.Dropout):
     def forward(self, x):
         return head_ops.dropout(x, self.p, self.training)
@@ -117,6 +140,12 @@ class CrossEntropyLoss(nn.CrossEntropyLoss):
         if self.ignore_index != -100 or self.label_smoothing != 0.0 or self.reduction != "mean":
             raise NotImplementedError("only weighted 'mean' cross entropy")
         return head_ops.weighted_cross_entropy(input, target, self.weight)
+
+    def fused_spec(self):
+        """(weight, gamma, mode) for head_ops.logits_and_loss"""
+        if self.ignore_index != -100 or self.label_smoothing != 0.0 or self.reduction != "mean":
+            return None
+        return self.weight, 0.0, 0
 
 
 _TORCH_TO_HIP = {

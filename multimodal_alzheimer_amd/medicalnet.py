@@ -185,10 +185,8 @@ class ResNet(nn.Module):
         V.clear_twins()
         y, parts = self.conv1.forward_stats(x)
         mp = self.maxpool
-        # no twin for the pooled stem output: the pool backward reads each pooled gradient
-        # from 8 cells, so a second gradient there costs more than torch's one add pass
-        # (measured: bnpool3s2_bwd 100 -> 127 us, colsum +7 us vs the 15 us add)
-        x = V.batchnorm_relu_maxpool(y, self.bn1, parts, mp.kernel_size, mp.stride, mp.padding)
+        x = V.batchnorm_relu_maxpool(y, self.bn1, parts, mp.kernel_size, mp.stride, mp.padding,
+                                     twin=True)
         return self.layer4(self.layer3(self.layer2(self.layer1(x))))
 
     def forward(self, x):

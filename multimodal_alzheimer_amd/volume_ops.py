@@ -860,15 +860,18 @@ class _BNReluPoolFn(torch.autograd.Function):
         g, g2 = _twin_grads(g, g2, y)
         if g is None:
             return (None,) * 5
-        if g2 is not None and not (c % 4 == 0 and k == 3 and s == 2 and p == 1):
-            g, g2 = _sum_grads(g, g2), None      # generic geometry: the apply takes one g
         dt = L.dtype_code(y.dtype)
         dev = y.device
         mp = n * do * ho * wo
         nparts = L.load().mmad_bn_bwd_parts(mp, c)
         parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
-        L.call("mmad_bnpool_bwd_reduce", dt, mp, c, L.ptr(g), L.ptr(g2), L.ptr(am),
-               L.ptr(ymax), L.ptr(mean), L.ptr(invstd), L.ptr(parts), L.stream())
+        # a twin's gradient: the reduce also writes the summed gradient, which the apply
+        # (reading each pooled gradient from up to 8 cells) then takes as its one input
+        gsum = torch.empty_like(g) if g2 is not None else None
+        L.call("mmad_bnpool_bwd_reduce", dt, mp, c, L.ptr(g), L.ptr(g2), L.ptr(gsum),
+               L.ptr(am), L.ptr(ymax), L.ptr(mean), L.ptr(invstd), L.ptr(parts), L.stream())
+        if gsum is not None:
+            g = gsum
         dgamma = grad_slot(ctx.params[0], (c,), dev)
         dbeta = grad_slot(ctx.params[1], (c,), dev)
         coef = torch.empty(3 * c, dtype=torch.float32, device=dev)
@@ -878,7 +881,7 @@ class _BNReluPoolFn(torch.autograd.Function):
                L.stream())
         dy = torch.empty_like(y)
         L.call("mmad_bnpool_bwd_apply", dt, n, c, di, hi, wi, do, ho, wo, k, s, p, L.ptr(g),
-               L.ptr(g2), L.ptr(am), L.ptr(y), L.ptr(mean), L.ptr(invstd), L.ptr(coef), L.ptr(dy),
+               L.ptr(am), L.ptr(y), L.ptr(mean), L.ptr(invstd), L.ptr(coef), L.ptr(dy),
                L.stream())
         return (dy, None, dgamma if ctx.needs_input_grad[2] else None,
                 dbeta if ctx.needs_input_grad[3] else None, None)
