@@ -519,8 +519,7 @@ class Anat_PET_CNN(Base_Model):
         x_pet = batch["pet1451"].unsqueeze(1)
         x_mri = batch["mri"].unsqueeze(1)
         y = batch["label"]
-        y_hat = _to_f64(self(x_pet, x_mri))
-        loss = self.criterion(y_hat, y)
+        y_hat, loss = _logits_and_loss(self.criterion, self(x_pet, x_mri), y)
         self.log(mode + "_loss", loss, on_step=True, prog_bar=True)
         return {"loss": loss, "outputs": y_hat, "labels": y}
 
@@ -588,8 +587,7 @@ class PET_MRI_EF(Base_Model):
         from .volume_ops import StackedVolumes
         x = StackedVolumes([batch["pet1451"], batch["mri"]])
         y = batch["label"]
-        y_hat = _to_f64(self.forward(x))
-        loss = self.criterion(y_hat, y)
+        y_hat, loss = _logits_and_loss(self.criterion, self.forward(x), y)
         if mode != "pred":
             self.log(mode + "_loss", loss, on_step=True)
         if mode in ("train", "val"):
@@ -665,8 +663,7 @@ class PET_MRI_FMF(Base_Model):
         x_pet = batch["pet1451"].unsqueeze(1)      # raw f64; conv 1 unfolds + casts (:124-127)
         x_mri = batch["mri"].unsqueeze(1)
         y = batch["label"]
-        y_hat = _to_f64(self.forward(x_pet=x_pet, x_mri=x_mri))
-        loss = self.criterion(y_hat, y)
+        y_hat, loss = _logits_and_loss(self.criterion, self.forward(x_pet=x_pet, x_mri=x_mri), y)
         if mode != "pred":
             self.log(mode + "_loss", loss, on_step=True)
         if mode in ("train", "val"):
@@ -801,8 +798,7 @@ class All_Modalities_Fusion(Base_Model):
         x_mri = batch["mri"].unsqueeze(1)
         x_tab = cast(batch["tabular"].unsqueeze(1), torch.float32)
         y = batch["label"]
-        y_hat = _to_f64(self(x_pet, x_mri, x_tab))
-        loss = self.criterion(y_hat, y)
+        y_hat, loss = _logits_and_loss(self.criterion, self(x_pet, x_mri, x_tab), y)
         self.log(mode + "_loss", loss, on_step=True, prog_bar=True)
         return {"loss": loss, "outputs": y_hat, "labels": y}
 
