@@ -197,8 +197,12 @@ int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* g2
  * BNs' backward in one pass each over g / relu_out -- reduce2 writes both part buffers
  * (parts2 = sums of g' and g'*xhat2), finalize2 both coefficient sets, apply2 dy and dy2.
  * Bit-identical to the per-BN calls; fixed-channel layouts only (else MMAD_EUNSUPPORTED). */
+/* g_rows > 0 (reduce2 / apply2): g is the compact (N, C) gradient of a global average pool
+ * (mmad_gap_bwd_compact) and row r of the BN input reads its sample's row g[r / g_rows]
+ * -- the same values as the broadcast mmad_gap_bwd output, never materialised; requires
+ * m % g_rows == 0 and m < 2^31.  0: g is a dense [m][c] gradient. */
 int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* g2,
-                        const void* relu_out, const void* y, const float* mean,
+                        int64_t g_rows, const void* relu_out, const void* y, const float* mean,
                         const float* invstd, const void* y2,
                         const float* mean2, const float* invstd2, float* parts, float* parts2,
                         void* stream);
@@ -208,7 +212,7 @@ int mmad_bn_bwd_finalize2(int c, int64_t count, int nparts, const float* parts,
                           const float* invstd2, int training2, float* dgamma2, float* dbeta2,
                           float* coef2, void* stream);
 int mmad_bn_bwd_apply2(int dtype, int64_t m, int c, const void* g, const void* g2,
-                       const void* relu_out, const void* y, const float* mean, const float* invstd, const float* coef,
+                       int64_t g_rows, const void* relu_out, const void* y, const float* mean, const float* invstd, const float* coef,
                        void* dy, const void* y2, const float* mean2, const float* invstd2,
                        const float* coef2, void* dy2, void* stream);
 /* BN + ReLU without residual (bn1 of every BasicBlock): the same two passes with the ReLU
@@ -261,6 +265,10 @@ int64_t mmad_gap_fwd_ws_elems(int n, int64_t s, int c);
 int mmad_gap_fwd_ws(int dtype, int n, int64_t s, int c, const void* x, float* y, float* ws,
                     void* stream);
 int mmad_gap_bwd(int dtype, int n, int64_t s, int c, const float* dy, void* dx, void* stream);
+/* The same values without the broadcast: dx[n][c] = (dtype) (dy[n][c] / s), for consumers
+ * that take a pooled gradient as broadcast rows (g_rows in mmad_bn_bwd_reduce2 / _apply2). */
+int mmad_gap_bwd_compact(int dtype, int n, int64_t s, int c, const float* dy, void* dx,
+                         void* stream);
 
 /* ---- fusion / classifier MLP head (fp32) ----------------------------------------
  * nn.Linear (+ReLU) of conv_seg (anat_cnn.py:68-76), reduce_dim_mri / stage2out /

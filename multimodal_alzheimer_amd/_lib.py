@@ -88,10 +88,10 @@ _SIGS = {
     "mmad_bn_bwd_reduce": (_i32, [_i32, _i64, _i32] + [_vp] * 8),
     "mmad_bn_bwd_finalize": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "mmad_bn_bwd_apply": (_i32, [_i32, _i64, _i32] + [_vp] * 10),
-    "mmad_bn_bwd_reduce2": (_i32, [_i32, _i64, _i32] + [_vp] * 12),
+    "mmad_bn_bwd_reduce2": (_i32, [_i32, _i64, _i32, _vp, _vp, _i64] + [_vp] * 10),
     "mmad_bn_bwd_finalize2": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
                                      _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
-    "mmad_bn_bwd_apply2": (_i32, [_i32, _i64, _i32] + [_vp] * 14),
+    "mmad_bn_bwd_apply2": (_i32, [_i32, _i64, _i32, _vp, _vp, _i64] + [_vp] * 12),
     "mmad_relu_fwd": (_i32, [_i32, _i64, _vp, _vp, _vp]),
     "mmad_relu_bwd": (_i32, [_i32, _i64, _vp, _vp, _vp, _vp]),
     "mmad_colsum_ws": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp, _vp]),
@@ -112,6 +112,7 @@ _SIGS = {
     "mmad_affine_norm": (_i32, [_i64, _vp, _f64, _f64, _vp, _vp]),
     "mmad_gap_fwd_ws": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp, _vp]),
     "mmad_gap_bwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "mmad_gap_bwd_compact": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_linear_fwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp]),
     "mmad_linear_bwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_linear_bwd_ex": (_i32, [_i32, _i32, _i32] + [_vp] * 8),

@@ -41,7 +41,9 @@ PartPlan part_plan(int64_t M) {
 // volume_ops twin outputs); g is then as_stored(g + g2), rounded as torch's own gradient
 // accumulation rounds it, so no separate add pass is needed.  MODE 3 also stores that sum
 // to gsum (the pool backward's input).
-template <typename T, int MODE, int V, bool DUAL = false, bool G2 = false>
+// GB (DUAL only): g is a global-average-pool gradient given compactly as [N][C] rows, row r of
+// the BN input reading g[r / gS] (the pooled gradient's broadcast is never materialised)
+template <typename T, int MODE, int V, bool DUAL = false, bool G2 = false, bool GB = false>
 __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t rpp,
                                                      const T* __restrict__ y,
                                                      const T* __restrict__ g,
@@ -57,8 +59,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
                                                      const float* __restrict__ invstd2 = nullptr,
                                                      float* __restrict__ parts2 = nullptr,
                                                      const T* __restrict__ g2 = nullptr,
-                                                     T* __restrict__ gsum = nullptr) {
+                                                     T* __restrict__ gsum = nullptr,
+                                                     uint32_t gS = 0) {
   static_assert(!DUAL || MODE == 1, "dual partial sums: BN backward with a relu_out mask");
+  static_assert(!GB || (DUAL && V == Chunk<T>::N), "broadcast g: the pair kernel, 16-byte rows");
   __shared__ float red[DUAL ? 3 : 2][2048];
   const int tid = threadIdx.x;
   const int CC = C / (int)gridDim.y;           // this block's channel slab
@@ -133,7 +137,11 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
         for (int u = 0; u < U; ++u) {
           const int64_t i = (r + u * rpar) * C + cb + cl * V;
           yr[u] = *reinterpret_cast<const u32x4*>(y + i);
-          if (NEED_G) gr[u] = *reinterpret_cast<const u32x4*>(g + i);
+          if constexpr (GB)
+            gr[u] = *reinterpret_cast<const u32x4*>(
+                g + (int64_t)((uint32_t)(r + u * rpar) / gS) * C + cb + cl * V);
+          else if (NEED_G)
+            gr[u] = *reinterpret_cast<const u32x4*>(g + i);
           if (NEED_G && G2) g2r[u] = *reinterpret_cast<const u32x4*>(g2 + i);
           if (MODE == 1 && relu_out != nullptr)
             orr[u] = *reinterpret_cast<const u32x4*>(relu_out + i);
@@ -165,7 +173,8 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
       if constexpr (V == Chunk<T>::N) Chunk<T>::load(y + i, yv);
       else for (int e = 0; e < V; ++e) yv[e] = Elt<T>::ld(y, i + e);
       if (NEED_G) {
-        if constexpr (V == Chunk<T>::N) Chunk<T>::load(g + i, gv);
+        if constexpr (GB) Chunk<T>::load(g + (int64_t)((uint32_t)r / gS) * C + cb + cl * V, gv);
+        else if constexpr (V == Chunk<T>::N) Chunk<T>::load(g + i, gv);
         else for (int e = 0; e < V; ++e) gv[e] = Elt<T>::ld(g, i + e);
         if constexpr (G2) {
           float hv[V];
@@ -564,14 +573,22 @@ struct BwdApply2 {
   void* dy2;
 };
 
-template <typename T, bool MASKY = false, bool DUAL = false, bool G2 = false>
+template <typename T, bool MASKY = false, bool DUAL = false, bool G2 = false, bool GB = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
     int64_t nv, int cpr, int C, const T* __restrict__ g, const T* __restrict__ relu_out,
     const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ coef, T* __restrict__ dy, T* __restrict__ gmask,
     const float* __restrict__ msc = nullptr, const float* __restrict__ msh = nullptr,
-    BwdApply2 d2 = {}, const T* __restrict__ g2 = nullptr) {
+    BwdApply2 d2 = {}, const T* __restrict__ g2 = nullptr, uint32_t gS = 0) {
   constexpr int V = Chunk<T>::N;
+  // GB: g compact [N][C] (see colsum_kernel); vector q is row q / cpr, cpr a power of two
+  const int cpr_shift = __builtin_ctz(cpr);
+  auto g_at = [&](int64_t qq) -> const T* {
+    if constexpr (GB)
+      return g + (int64_t)((uint32_t)(qq >> cpr_shift) / gS) * C + (qq & (cpr - 1)) * V;
+    else
+      return g + qq * V;
+  };
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int c0 = (int)(t0 & (cpr - 1)) * V;
@@ -624,8 +641,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
   int64_t q = t0;
   for (; q + stride < nv; q += 2 * stride) {
     float g0[V], g1[V], y0[V], y1[V], o0[V], o1[V], z0[V], z1[V];
-    Chunk<T>::load(g + q * V, g0);
-    Chunk<T>::load(g + (q + stride) * V, g1);
+    Chunk<T>::load(g_at(q), g0);
+    Chunk<T>::load(g_at(q + stride), g1);
     if constexpr (G2) {
       add_g2(q, g0);
       add_g2(q + stride, g1);
@@ -645,7 +662,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fc_kernel(
   }
   if (q < nv) {
     float g0[V], y0[V], o0[V], z0[V];
-    Chunk<T>::load(g + q * V, g0);
+    Chunk<T>::load(g_at(q), g0);
     if constexpr (G2) add_g2(q, g0);
     Chunk<T>::load(y + q * V, y0);
     if (relu_out) Chunk<T>::load(relu_out + q * V, o0);
@@ -976,7 +993,7 @@ int mmad_bn_bwd_apply(int dtype, int64_t m, int c, const void* g, const void* g2
 // the same g and relu_out.  Fixed-channel layouts only (MMAD_EUNSUPPORTED otherwise: the
 // caller falls back to the per-BN calls).
 int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* g2,
-                        const void* relu_out, const void* y, const float* mean,
+                        int64_t g_rows, const void* relu_out, const void* y, const float* mean,
                         const float* invstd, const void* y2,
                         const float* mean2, const float* invstd2, float* parts, float* parts2,
                         void* stream) {
@@ -985,6 +1002,8 @@ int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* 
   if (!g || !relu_out || !y || !mean || !invstd || !y2 || !mean2 || !invstd2 || !parts ||
       !parts2)
     return MMAD_ENULL;
+  if (g_rows < 0 || (g_rows > 0 && (m % g_rows || m >= (int64_t(1) << 31))))
+    return MMAD_EBADSHAPE;
   const PartPlan pp = part_plan(m);
   hipStream_t st = as_stream(stream);
   auto go = [&](auto tag) -> int {
@@ -993,12 +1012,14 @@ int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* 
     int slabs = 1;
     while (c % (slabs * 2 * VEC) == 0 && c / (slabs * VEC) > 256) slabs *= 2;
     if (!(c % (slabs * VEC) == 0 && c / (slabs * VEC) <= 256)) return MMAD_EUNSUPPORTED;
-    auto k = g2 != nullptr ? colsum_kernel<T, 1, VEC, true, true>
-                           : colsum_kernel<T, 1, VEC, true, false>;
+    auto k = g_rows > 0 ? (g2 != nullptr ? colsum_kernel<T, 1, VEC, true, true, true>
+                                          : colsum_kernel<T, 1, VEC, true, false, true>)
+                        : (g2 != nullptr ? colsum_kernel<T, 1, VEC, true, true>
+                                          : colsum_kernel<T, 1, VEC, true, false>);
     hipLaunchKernelGGL(k, dim3((unsigned)pp.nparts, slabs), dim3(256), 0, st, m, c, pp.rpp,
                        (const T*)y, (const T*)g, (const T*)relu_out, mean, invstd, parts,
                        nullptr, nullptr, nullptr, (const T*)y2, mean2, invstd2, parts2,
-                       (const T*)g2, (T*)nullptr);
+                       (const T*)g2, (T*)nullptr, (uint32_t)g_rows);
     return launch_status();
   };
   return dtype == MMAD_BF16 ? go(u16{}) : go(float{});
@@ -1019,7 +1040,7 @@ int mmad_bn_bwd_finalize2(int c, int64_t count, int nparts, const float* parts,
 }
 
 int mmad_bn_bwd_apply2(int dtype, int64_t m, int c, const void* g, const void* g2,
-                       const void* relu_out, const void* y, const float* mean, const float* invstd, const float* coef,
+                       int64_t g_rows, const void* relu_out, const void* y, const float* mean, const float* invstd, const float* coef,
                        void* dy, const void* y2, const float* mean2, const float* invstd2,
                        const float* coef2, void* dy2, void* stream) {
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
@@ -1032,15 +1053,23 @@ int mmad_bn_bwd_apply2(int dtype, int64_t m, int c, const void* g, const void* g
   const int64_t nv = m * c / vv;
   const BwdApply2 d2{y2, mean2, invstd2, coef2, dy2};
   hipStream_t st = as_stream(stream);
-#define APPLY2(T, G)                                                                         \
-  hipLaunchKernelGGL((bn_bwd_apply_fc_kernel<T, false, true, G>), dim3(ew_grid(nv)), dim3(256), \
-                     0, st, nv, c / vv, c, (const T*)g, (const T*)relu_out, (const T*)y, mean, \
-                     invstd, coef, (T*)dy, (T*)nullptr, nullptr, nullptr, d2, (const T*)g2)
+  if (g_rows < 0 || (g_rows > 0 && (m % g_rows || m >= (int64_t(1) << 31))))
+    return MMAD_EBADSHAPE;
+#define APPLY2(T, G, B)                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_fc_kernel<T, false, true, G, B>), dim3(ew_grid(nv)),       \
+                     dim3(256), 0, st, nv, c / vv, c, (const T*)g, (const T*)relu_out,        \
+                     (const T*)y, mean, invstd, coef, (T*)dy, (T*)nullptr, nullptr, nullptr,  \
+                     d2, (const T*)g2, (uint32_t)g_rows)
+#define APPLY2G(T, B)                                                                        \
+  do {                                                                                       \
+    if (g2 != nullptr) APPLY2(T, true, B); else APPLY2(T, false, B);                         \
+  } while (0)
   if (dtype == MMAD_BF16) {
-    if (g2 != nullptr) APPLY2(u16, true); else APPLY2(u16, false);
+    if (g_rows > 0) APPLY2G(u16, true); else APPLY2G(u16, false);
   } else {
-    if (g2 != nullptr) APPLY2(float, true); else APPLY2(float, false);
+    if (g_rows > 0) APPLY2G(float, true); else APPLY2G(float, false);
   }
+#undef APPLY2G
 #undef APPLY2
   return launch_status();
 }

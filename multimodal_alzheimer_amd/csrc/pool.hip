@@ -632,11 +632,10 @@ __global__ void gap_fold_kernel(int n, int P, int C, int64_t S, const float* __r
 }
 
 template <typename T, int V>
-__global__ void gap_bwd_kernel(int n, int64_t S, int C, const float* __restrict__ dy,
+__global__ void gap_bwd_kernel(int n, int64_t S, int C, float inv, const float* __restrict__ dy,
                                T* __restrict__ dx) {
   const int cv = C / V;
   const int64_t total = (int64_t)n * S * cv;
-  const float inv = 1.f / (float)S;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int c0 = (int)(t % cv) * V;
@@ -776,16 +775,21 @@ int gap_fwd(int n, int64_t s, int c, const void* x, float* y, hipStream_t st, fl
   return launch_status();
 }
 
+// dx = dy / s broadcast over s rows per sample; compact: one row per sample (the (n, c)
+// values a broadcast-gradient consumer expands itself, see mmad_bn_bwd_reduce2)
 template <typename T>
-int gap_bwd(int n, int64_t s, int c, const float* dy, void* dx, hipStream_t st) {
+int gap_bwd(int n, int64_t s, int c, const float* dy, void* dx, hipStream_t st,
+            bool compact = false) {
   constexpr int VEC = Chunk<T>::N;
-  const int64_t tot = (int64_t)n * s * c;
+  const float inv = 1.f / (float)s;
+  const int64_t rows = compact ? 1 : s;
+  const int64_t tot = (int64_t)n * rows * c;
   if (c % VEC == 0)
     hipLaunchKernelGGL((gap_bwd_kernel<T, VEC>), dim3(grid_of(tot / VEC)), dim3(256), 0, st, n,
-                       s, c, dy, (T*)dx);
+                       rows, c, inv, dy, (T*)dx);
   else
-    hipLaunchKernelGGL((gap_bwd_kernel<T, 1>), dim3(grid_of(tot)), dim3(256), 0, st, n, s, c,
-                       dy, (T*)dx);
+    hipLaunchKernelGGL((gap_bwd_kernel<T, 1>), dim3(grid_of(tot)), dim3(256), 0, st, n, rows, c,
+                       inv, dy, (T*)dx);
   return launch_status();
 }
 
@@ -870,6 +874,15 @@ int mmad_gap_bwd(int dtype, int n, int64_t s, int c, const float* dy, void* dx, 
   if (!dy || !dx) return MMAD_ENULL;
   if (dtype == MMAD_BF16) return gap_bwd<u16>(n, s, c, dy, dx, as_stream(stream));
   if (dtype == MMAD_F32) return gap_bwd<float>(n, s, c, dy, dx, as_stream(stream));
+  return MMAD_EBADDTYPE;
+}
+
+int mmad_gap_bwd_compact(int dtype, int n, int64_t s, int c, const float* dy, void* dx,
+                         void* stream) {
+  if (n <= 0 || s <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!dy || !dx) return MMAD_ENULL;
+  if (dtype == MMAD_BF16) return gap_bwd<u16>(n, s, c, dy, dx, as_stream(stream), true);
+  if (dtype == MMAD_F32) return gap_bwd<float>(n, s, c, dy, dx, as_stream(stream), true);
   return MMAD_EBADDTYPE;
 }
 

@@ -702,7 +702,7 @@ _BN_DUAL = os.environ.get("MMAD_BN_DUAL", "1") != "0"
 
 
 def _bn_backward_pair(g, relu_out, y, mean, invstd, gamma, batch_stats, y2, mean2, invstd2,
-                      gamma2, batch_stats2, params, params2, g2=None):
+                      gamma2, batch_stats2, params, params2, g2=None, g_rows=0):
     """Both BNs of relu(bn(y) + bn2(y2)) backward, g and relu_out read once per pass
     (mmad_bn_bwd_reduce2 / _finalize2 / _apply2); equal bit for bit to two _bn_backward
     calls.  Returns (dy, dgamma, dbeta, dy2, dgamma2, dbeta2)."""
@@ -711,8 +711,8 @@ def _bn_backward_pair(g, relu_out, y, mean, invstd, gamma, batch_stats, y2, mean
     dt = L.dtype_code(y.dtype)
     nparts = L.load().mmad_bn_bwd_parts(m, c)
     parts = torch.empty((2, nparts, 2, c), dtype=torch.float32, device=dev)
-    L.call("mmad_bn_bwd_reduce2", dt, m, c, L.ptr(g), L.ptr(g2), L.ptr(relu_out), L.ptr(y),
-           L.ptr(mean), L.ptr(invstd), L.ptr(y2), L.ptr(mean2), L.ptr(invstd2),
+    L.call("mmad_bn_bwd_reduce2", dt, m, c, L.ptr(g), L.ptr(g2), g_rows, L.ptr(relu_out),
+           L.ptr(y), L.ptr(mean), L.ptr(invstd), L.ptr(y2), L.ptr(mean2), L.ptr(invstd2),
            L.ptr(parts[0]), L.ptr(parts[1]), L.stream())
     dgamma = grad_slot(params[0], (c,), dev)
     dbeta = grad_slot(params[1], (c,), dev)
@@ -725,9 +725,9 @@ def _bn_backward_pair(g, relu_out, y, mean, invstd, gamma, batch_stats, y2, mean
            L.ptr(coef[1]), L.stream())
     dy = torch.empty_like(y)
     dy2 = torch.empty_like(y2)
-    L.call("mmad_bn_bwd_apply2", dt, m, c, L.ptr(g), L.ptr(g2), L.ptr(relu_out), L.ptr(y),
-           L.ptr(mean), L.ptr(invstd), L.ptr(coef[0]), L.ptr(dy), L.ptr(y2), L.ptr(mean2),
-           L.ptr(invstd2), L.ptr(coef[1]), L.ptr(dy2), L.stream())
+    L.call("mmad_bn_bwd_apply2", dt, m, c, L.ptr(g), L.ptr(g2), g_rows, L.ptr(relu_out),
+           L.ptr(y), L.ptr(mean), L.ptr(invstd), L.ptr(coef[0]), L.ptr(dy), L.ptr(y2),
+           L.ptr(mean2), L.ptr(invstd2), L.ptr(coef[1]), L.ptr(dy2), L.stream())
     return dy, dgamma, dbeta, dy2, dgamma2, dbeta2
 
 
@@ -767,16 +767,23 @@ class _BNActFn(torch.autograd.Function):
     def backward(ctx, g, g2=None):
         y, out, mean, invstd, gamma, rres, rmean, rinvstd, rgamma = ctx.saved_tensors
         relu, batch, rbatch, has_res, has_rbn = ctx.cfg
-        g, g2 = _twin_grads(g, g2, y)
+        pair = (has_rbn and _BN_DUAL and out is not None and ctx.mask_affine is None
+                and _mask_from_y_ok(y))
+        # a global-average-pool gradient arrives as a broadcast view: the pair kernels read
+        # its per-sample rows in place; every other path materialises it (_twin_grads)
+        g_rows = _gap_rows(g, y) if pair and y.numel() // y.shape[1] < 2 ** 31 else 0
+        if g_rows:
+            g2 = _twin_grads(g2, None, y)[0]
+        else:
+            g, g2 = _twin_grads(g, g2, y)
         if g is None:
             return (None,) * 9
         gam = None if gamma is None else gamma.detach()
-        if (has_rbn and _BN_DUAL and out is not None and ctx.mask_affine is None
-                and _mask_from_y_ok(y)):
+        if pair:
             rg = None if rgamma is None else rgamma.detach()
             dy, dgamma, dbeta, dres, drg, drb = _bn_backward_pair(
                 g, out, y, mean, invstd, gam, batch, rres, rmean, rinvstd, rg, rbatch,
-                ctx.params[0], ctx.params[1], g2)
+                ctx.params[0], ctx.params[1], g2, g_rows)
             return (dy, None, dgamma if ctx.needs_input_grad[2] else None,
                     dbeta if ctx.needs_input_grad[3] else None, dres, None,
                     drg if ctx.needs_input_grad[6] else None,
@@ -934,6 +941,21 @@ def max_pool3d(x, kernel_size, stride=None, padding=0):
     return _MaxPoolFn.apply(x, int(kernel_size), int(stride or kernel_size), int(padding))
 
 
+# MMAD_GAP_BCAST=0: the GAP backward writes the broadcast gradient out in full (A/B switch)
+GAP_BCAST = os.environ.get("MMAD_GAP_BCAST", "1") != "0"
+
+
+def _gap_rows(g, like):
+    """rows per sample when g is _GapFn's stride-0 broadcast gradient for ``like``, else 0"""
+    if g is None or g.dim() != 5 or tuple(g.shape) != tuple(like.shape) or \
+            g.dtype != like.dtype:
+        return 0
+    n, c, d, h, w = g.shape
+    if g.stride()[1:] != (1, 0, 0, 0) or g.stride(0) != c:
+        return 0
+    return d * h * w
+
+
 class _GapFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
@@ -958,6 +980,14 @@ class _GapFn(torch.autograd.Function):
         g = g.contiguous()
         if g.dtype != torch.float32:
             g = cast(g, torch.float32)
+        if GAP_BCAST:
+            # the input gradient g/s per (sample, channel), handed on as a stride-0 broadcast
+            # view: a BN-pair backward reads its rows in place (g_rows of
+            # mmad_bn_bwd_reduce2 / _apply2); any other consumer materialises it
+            rows = torch.empty((n, c), dtype=ctx.dtype, device=g.device)
+            L.call("mmad_gap_bwd_compact", L.dtype_code(ctx.dtype), n, s, c, L.ptr(g),
+                   L.ptr(rows), L.stream())
+            return rows.view(n, c, 1, 1, 1).expand(ctx.shape)
         dx = _empty_vol(*ctx.shape, ctx.dtype, g.device)
         L.call("mmad_gap_bwd", L.dtype_code(ctx.dtype), n, s, c, L.ptr(g), L.ptr(dx), L.stream())
         return dx

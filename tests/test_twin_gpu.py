@@ -1,6 +1,8 @@
 """Twin outputs (volume_ops "twin outputs"): a residual block's input gradient from conv1
 and from the shortcut meet inside the producer's BN backward kernels (g2 of
-mmad_bn_bwd_* / mmad_bnpool_bwd_*) instead of in torch's gradient-accumulation add.
+mmad_bn_bwd_* / mmad_bnpool_bwd_*) instead of in torch's gradient-accumulation add.  Also
+the broadcast global-average-pool gradient (volume_ops.GAP_BCAST: the last BN pair reads
+the pooled gradient's per-sample rows in place instead of a materialised broadcast).
 
 The kernels add g2 as torch adds two gradients of one tensor (fp32 sum, then one rounding to
 the storage dtype), so the whole training step must be BIT-identical with and without twins:
@@ -49,9 +51,11 @@ def test_twin_step_bit_identical(depth, precision, n, size, monkeypatch):
                                dtype=torch.float64),
              "label": torch.randint(0, 2, (n,), generator=g, device=DEV)}
     monkeypatch.setattr(V, "TWIN", True)
+    monkeypatch.setattr(V, "GAP_BCAST", True)
     la, lossa = _step(ma, batch)
     assert not V._TWINS, "every twin made in the step was taken by its block"
     monkeypatch.setattr(V, "TWIN", False)
+    monkeypatch.setattr(V, "GAP_BCAST", False)     # and the materialised GAP gradient
     lb, lossb = _step(mb, batch)
     assert torch.equal(la, lb) and torch.equal(lossa, lossb)
     pb = dict(mb.named_parameters())
