@@ -252,6 +252,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(timed=True)
+    t_issue = time.perf_counter() - t0     # host time to enqueue the K steps (diagnostic)
     torch.cuda.synchronize()
     volume_ops.FWD_PROBES.clear()
     if world > 1:
@@ -294,6 +295,9 @@ def main():
         result["hbm_roofline_frac_m2"] = per_gpu * M2_BYTES_PER_VOL / PEAK_HBM
     if args.graph:
         result["config"]["step_launch"] = "hip graph replay"
+    # host time spent enqueueing each step: close to ms_per_step means the run was bound by
+    # the host (Python / launch overhead), not by the GPU
+    result["host_issue_ms_per_step"] = t_issue / args.steps * 1e3
     if reducer is not None and dp_events:
         # main-stream time from the end of backward to averaged gradients: the part of the
         # all-reduce that backward did not hide (plus the copies of non-slot gradients)
