@@ -10,9 +10,11 @@ all-reduce (N>1) + Adam; all parameters trainable (lr_pretrained set).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
-Rank 0 prints one JSON line.  ``roofline`` times the dominant kernel (layer4.0.conv2
-forward, the largest implicit-GEMM launch) with HIP events recorded around each of its
-launches inside the timed region, on the stream it runs on;
+At N=1 (config 2) the step is captured once as a HIP graph and replayed (``--eager``
+launches it from Python every step, as the N>1 path does).  Rank 0 prints one JSON line.
+``roofline`` times the dominant kernel (layer4.0.conv2 forward, the lattice conv) with HIP
+events recorded around each of its launches, on the stream it runs on -- inside the timed
+region when eager, over eager steps just before the capture when graph-replayed;
 ``cpu_baseline`` times the CPU oracle (torch fp32, the reference path) on a bounded sample.
 """
 import argparse
@@ -58,9 +60,10 @@ def dominant_desc(batch, size):
     return volume_ops._desc_tuple(d), 2.0 * batch * s ** 3 * 512 * 512 * 27
 
 
-def dominant_kernel_roofline(events, batch, size, dtype):
-    """Average duration of the dominant kernel's launches inside the timed region, from the
-    HIP event pairs volume_ops recorded around each launch on its own stream."""
+def dominant_kernel_roofline(events, batch, size, dtype, where="timed region"):
+    """Average duration of the dominant kernel's launches, from the HIP event pairs
+    volume_ops recorded around each launch on its own stream (inside the timed region for
+    eager runs; over eager steps just before the capture for graph-replayed runs)."""
     _, flops = dominant_desc(batch, size)
     if not events:
         return None
@@ -83,7 +86,7 @@ def dominant_kernel_roofline(events, batch, size, dtype):
             "unit": "TFLOP/s", "frac": flops / sec / peak, "traffic": traffic,
             "flop_per_launch": flops, "executed_flop_per_launch": executed,
             "executed_frac": executed / sec / peak,
-            "avg_launch_ms": sec * 1e3, "launches": len(events)}
+            "avg_launch_ms": sec * 1e3, "launches": len(events), "probe": where}
 
 
 def host_cores():
@@ -162,7 +165,9 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured HIP graph (graph_step.GraphedTrainStep;"
-                         " N=1 only, no dominant-kernel probe)")
+                         " N=1 only); the default for N=1 on the config-2 workload")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel of every step from Python (the N>1 path)")
     ap.add_argument("--workload", default="mri", choices=["mri", "fusion", "three"],
                     help="mri: BASELINE config 2 (the metric); fusion: config 3/4, PET+MRI "
                          "ResNet-10 x2 + MLP head, focal loss, pairs/sec; three: config 5, "
@@ -231,10 +236,32 @@ def main():
                 dp_events.append((e0, e1))
         opt.step()
 
-    if args.graph:
-        if dp:
-            raise SystemExit("--graph does not combine with the RCCL all-reduce path")
-        args.no_roofline = True          # the per-launch event probe is not captured
+    # N=1: the whole step (general_step, backward, Adam) is captured once as a HIP graph and
+    # replayed -- the same kernels, bit-identical to eager steps (tests/test_graph_step_gpu.py);
+    # eager, the host needs ~2.9 of the GPU's ~3.5 ms per step to enqueue it, so a slower or
+    # busier host makes the run launch-bound (measured: 1713 vol/s on one box).  N>1 runs
+    # eager: the RCCL all-reduce is launched from autograd hooks.
+    use_graph = args.graph or (not dp and args.workload == "mri" and not args.eager)
+    if use_graph and dp:
+        raise SystemExit("--graph does not combine with the RCCL all-reduce path")
+    events = []
+    if use_graph:
+        if rank == 0 and not args.no_roofline:
+            # the dominant-kernel probe (HIP events around its launches) cannot sit inside a
+            # graph: time it over warm eager steps before the capture instead, on a side
+            # stream as the capture's own warm-up runs (eager work on the default stream
+            # ahead of a capture made the capture's end fault on this ROCm stack)
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    step()
+                volume_ops.FWD_PROBES[dominant_desc(B, S)[0]] = events
+                for _ in range(max(10, args.warmup)):
+                    step()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            volume_ops.FWD_PROBES.clear()
         gstep = GraphedTrainStep(model, opt, batch, warmup=max(1, args.warmup))
         gstep()
 
@@ -245,8 +272,7 @@ def main():
             step()
     if world > 1:
         dist.barrier()
-    events = []
-    if rank == 0 and not args.no_roofline:
+    if rank == 0 and not args.no_roofline and not use_graph:
         volume_ops.FWD_PROBES[dominant_desc(B, S)[0]] = events
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -293,8 +319,7 @@ def main():
         result["step_mfma_frac"] = per_gpu * FLOP_PER_VOL[S] / (
             PEAK_BF16 if cdtype == torch.bfloat16 else PEAK_F32)
         result["hbm_roofline_frac_m2"] = per_gpu * M2_BYTES_PER_VOL / PEAK_HBM
-    if args.graph:
-        result["config"]["step_launch"] = "hip graph replay"
+    result["config"]["step_launch"] = "hip graph replay" if use_graph else "eager"
     # host time spent enqueueing each step: close to ms_per_step means the run was bound by
     # the host (Python / launch overhead), not by the GPU
     result["host_issue_ms_per_step"] = t_issue / args.steps * 1e3
@@ -305,7 +330,9 @@ def main():
                         "exposed_allreduce_ms": sum(a.elapsed_time(b) for a, b in dp_events)
                         / len(dp_events), "backend": "rccl"}
     if rank == 0 and not args.no_roofline:
-        result["roofline"] = dominant_kernel_roofline(events, B, S, cdtype)
+        result["roofline"] = dominant_kernel_roofline(
+            events, B, S, cdtype,
+            "eager steps before the graph capture" if use_graph else "timed region")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(S)
     if rank == 0:
