@@ -125,3 +125,29 @@ def test_twin_bn_relu_maxpool_matches_summed_gradient(c):
         bn.weight.grad = bn.bias.grad = None
     for a, b in zip(*outs):
         assert torch.equal(a, b), c
+
+
+@pytest.mark.parametrize("shape", [
+    # (N, Ci, S, Co, k, pad, dil): the igemm wgrad (layer2-like), the lattice wgrad (layer4
+    # dilation 4 on 16^3), the 1^3 shortcut
+    (2, 64, 16, 128, 3, 1, 1), (2, 256, 16, 128, 3, 4, 4), (2, 128, 16, 64, 1, 0, 1)],
+    ids=["igemm", "lattice", "pointwise"])
+def test_wgrad_split_stream_matches(shape, monkeypatch):
+    """mmad_conv3d_wgrad_split (split-K reduction on the side stream, REDUCE_STREAM) writes
+    the same dW bits as mmad_conv3d_wgrad; the step joins the side stream before reading."""
+    n, ci, s, co, k, p, d = shape
+    torch.manual_seed(9)
+    x = torch.randn(n, ci, s, s, s, device=DEV).to(torch.bfloat16).to(
+        memory_format=torch.channels_last_3d)
+    gy = torch.randn(n, co, s, s, s, device=DEV).to(torch.bfloat16).to(
+        memory_format=torch.channels_last_3d)
+    w0 = torch.randn(co, ci, k, k, k, device=DEV) * 0.05
+    grads = []
+    for split in (False, True):
+        monkeypatch.setattr(V, "REDUCE_STREAM", split)
+        w = w0.clone().requires_grad_(True)
+        y = V.conv3d(x, w, None, (1, 1, 1), (p, p, p), (d, d, d), torch.bfloat16)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        grads.append(w.grad.clone())
+    assert torch.equal(grads[0], grads[1])
