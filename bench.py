@@ -208,7 +208,8 @@ def main():
     reducer = None
     if dp:
         broadcast_module_state(model)          # identical replicas, as DDP
-        reducer = GradAllReduce(model.parameters(), bucket_mb=4.0)
+        reducer = GradAllReduce(model.parameters(),
+                                bucket_mb=float(os.environ.get("MMAD_DP_BUCKET_MB", "4")))
     B, S = args.batch, args.size
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)   # this rank's shard
     batch = {"mri": torch.rand((B, S, S, S), device="cuda", dtype=torch.float64, generator=g),
