@@ -32,8 +32,12 @@ from . import volume_ops
 
 
 class GraphedTrainStep:
-    def __init__(self, model, optimizer, batch, warmup=3):
+    def __init__(self, model, optimizer, batch, warmup=3, reducer=None):
+        """``reducer``: a data_parallel.GradAllReduce whose bucket all-reduces (launched from
+        the backward's hooks) and ``finish()`` are captured with the step (experimental:
+        bench.py --graph under torchrun; checked at one rank only)."""
         self.model, self.optimizer = model, optimizer
+        self.reducer = reducer
         self.static = {k: v.clone() if torch.is_tensor(v) else v for k, v in batch.items()}
         dev = next(model.parameters()).device
         for g in optimizer.param_groups:
@@ -51,11 +55,15 @@ class GraphedTrainStep:
         with torch.cuda.graph(self.graph):
             self.out = model.general_step(self.static, 0, "train")
             self.out["loss"].backward()
+            if reducer is not None:
+                reducer.finish()
             optimizer.step()
 
     def _eager(self):
         self.optimizer.zero_grad(set_to_none=True)
         self.model.general_step(self.static, 0, "train")["loss"].backward()
+        if self.reducer is not None:
+            self.reducer.finish()
         self.optimizer.step()
 
     def __call__(self, batch=None):
