@@ -246,20 +246,17 @@ def main():
     use_graph = args.graph or (not dp and args.workload == "mri" and not args.eager)
     events = []
     if use_graph:
-        if rank == 0 and not args.no_roofline:
+        if not args.no_roofline:
             # the dominant-kernel probe (HIP events around its launches) cannot sit inside a
-            # graph: time it over warm eager steps before the capture instead, on a side
-            # stream as the capture's own warm-up runs (eager work on the default stream
-            # ahead of a capture made the capture's end fault on this ROCm stack)
-            side = torch.cuda.Stream()
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                for _ in range(3):
-                    step()
+            # graph: time it over warm eager steps before the capture instead.  Every rank
+            # runs these steps (each issues the bucket all-reduces under RCCL, so the ranks'
+            # collective sequences stay aligned); rank 0 records the events.
+            for _ in range(3):
+                step()
+            if rank == 0:
                 volume_ops.FWD_PROBES[dominant_desc(B, S)[0]] = events
-                for _ in range(max(10, args.warmup)):
-                    step()
-            torch.cuda.current_stream().wait_stream(side)
+            for _ in range(max(10, args.warmup)):
+                step()
             torch.cuda.synchronize()
             volume_ops.FWD_PROBES.clear()
         # with the RCCL path (explicit --graph only) the bucket all-reduces are captured too

@@ -58,6 +58,10 @@ class GraphedTrainStep:
             if reducer is not None:
                 reducer.finish()
             optimizer.step()
+        # keep the graph-owned output buffers, not their autograd graph: a live grad_fn chain
+        # would keep every parameter's AccumulateGrad node (created on the capture stream)
+        # alive, and later eager steps would reuse those nodes across streams
+        self.out = {k: v.detach() if torch.is_tensor(v) else v for k, v in self.out.items()}
 
     def _eager(self):
         self.optimizer.zero_grad(set_to_none=True)

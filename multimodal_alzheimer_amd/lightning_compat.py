@@ -53,10 +53,16 @@ except ImportError:
             self._hparams = AttributeDict({k: v for k, v in src.items() if k not in ignore})
 
         def log(self, name, value, *a, **k):
-            self.logged[name] = value
+            # detached, as Lightning's result collection stores logged tensors: a logged loss
+            # that kept its grad_fn would hold the step's whole autograd graph -- and the
+            # parameters' AccumulateGrad nodes with the stream they were created on -- alive
+            # into the next step (torch then warns of an AccumulateGrad stream mismatch, and
+            # a graph capture after eager default-stream steps faulted at capture_end)
+            self.logged[name] = value.detach() if torch.is_tensor(value) else value
 
         def log_dict(self, d, *a, **k):
-            self.logged.update(d)
+            for name, value in d.items():
+                self.log(name, value)
 
         @property
         def device(self):

@@ -76,6 +76,16 @@ def param_value(base_seed, name, shape):
     return v.astype(np.float32).reshape(shape)
 
 
+def sample_index(name, n, k=1024):
+    """Sorted distinct element indices (at most k of n) at which the full-size fixtures
+    record a tensor: a pure function of the tensor's name, so the GPU tests pick the same
+    elements without the fixture shipping them."""
+    if n <= k:
+        return np.arange(n, dtype=np.int64)
+    idx = (uniform(name_seed(0x5A3B1E, name), k).astype(np.float64) * n).astype(np.int64)
+    return np.unique(np.minimum(idx, n - 1))
+
+
 def fill_state_dict(state_dict, base_seed):
     """Return {key: np.float32 array} for every float entry of a state_dict."""
     out = {}

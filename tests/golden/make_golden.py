@@ -25,7 +25,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 sys.path.insert(0, REPO)
 
-from oracle import prng, medicalnet_ref  # noqa: E402
+from oracle import prng, medicalnet_ref, models_ref  # noqa: E402
 
 W2 = [0.20314960629921264, 0.7968503937007874]              # pkg/inference/test_tab.py:25-28
 W3 = [0.4651162790697675, 0.6712473572938689, 0.8636363636363636]   # test_tab.py:36-40
@@ -125,6 +125,49 @@ def run_case(model, batch, out):
         if "running" in name:
             summarize("buf/", name, b, out)
     out["state_dict_keys"] = np.array(list(model.state_dict().keys()))
+
+
+def record_samples(prefix, model, out):
+    """Gradients of a config-size case: the elements prng.sample_index picks, + stats."""
+    for name, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        a = p.grad.detach().double().numpy().ravel()
+        out[f"{prefix}samp/{name}"] = a[prng.sample_index(name, a.size)]
+        out[f"{prefix}stats/{name}"] = np.array([a.sum(), np.abs(a).sum(),
+                                                 np.sqrt((a * a).sum())])
+
+
+def run_full_case(model, ref64, batch, inputs, out):
+    """A BASELINE-size case (128^3, batch 8): eval logits on fresh weights, one train-mode
+    general_step + backward of the reference code in fp32 (gradients at sampled elements,
+    running statistics in full), then the same train step in float64 on the oracle
+    restatement loaded with the same weights -- the exact answer the GPU tests measure both
+    the reference's fp32 error and their own against."""
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    model.eval()
+    with torch.no_grad():
+        out["eval_logits"] = model.general_step(batch, 0, "val")["outputs"].numpy()
+    model.train()
+    res = model.general_step(batch, 0, "train")
+    res["loss"].backward()
+    out["train_logits"] = res["outputs"].detach().numpy()
+    out["train_loss"] = np.array(res["loss"].item())
+    record_samples("grad/", model, out)
+    for name, b in model.named_buffers():
+        if "running" in name:
+            summarize("buf/", name, b, out)
+    out["state_dict_keys"] = np.array(list(model.state_dict().keys()))
+    del res
+    model.zero_grad(set_to_none=True)
+    ref64.load_state_dict(sd0)
+    ref64 = ref64.double().train()
+    y64 = ref64(*inputs(batch))
+    loss64 = ref64.criterion(y64, batch["label"])
+    loss64.backward()
+    out["train_logits64"] = y64.detach().numpy()
+    out["train_loss64"] = np.array(loss64.item())
+    record_samples("grad64/", ref64, out)
 
 
 def batch_for(shape, n_classes, seed, keys=("mri",)):
@@ -381,6 +424,68 @@ def fmf_concat_bn():
     load_prng_weights(m, 29)
     out = {"seed": np.array(29), "shape": np.array([2, 32, 32, 32])}
     run_case(m, batch_for((2, 32, 32, 32), 3, 30, keys=("pet1451", "mri")), out)
+    return out
+
+
+def _live_seed(build, batch, seed):
+    """First weight seed (upwards in steps of 1000) whose train-mode logits keep a positive
+    entry in every sample (the head's final ReLU, anat_cnn.py:77, otherwise zeroes every
+    gradient); forward only, so the search stays cheap at 128^3."""
+    for s in range(seed, seed + 50000, 1000):
+        m = build()
+        load_prng_weights(m, s)
+        m.train()
+        with torch.no_grad():
+            y = m.general_step(batch, 0, "train")["outputs"]
+        if (y > 0).any(dim=1).all():
+            return s
+    raise RuntimeError("no live seed")
+
+
+FULL = (8, 128, 128, 128)          # BASELINE configs 2 and 3: batch 8 of 1 x 128^3
+
+
+@case
+def anat_r10_128():
+    """BASELINE config 2 at its full size: Anat_CNN ResNet-10, 8 x 1 x 128^3, weighted CE
+    (anat_cnn.py:13-109, the reference code itself; MedicalNet from the restatement)."""
+    from pkg.models.mri_models.anat_cnn import Anat_CNN
+    batch = batch_for(FULL, 2, 1301)
+    torch.manual_seed(0)
+    seed = _live_seed(lambda: Anat_CNN(anat_hparams(10)), batch, 1300)
+    m = Anat_CNN(anat_hparams(10))
+    load_prng_weights(m, seed)
+    out = {"seed": np.array(seed), "shape": np.array(FULL)}
+    run_full_case(m, models_ref.AnatCNNRef(anat_hparams(10)), batch,
+                  lambda b: (b["mri"].unsqueeze(1).double(),), out)
+    return out
+
+
+def pair_stage1(h, depth):
+    return dict(h, resnet_depth=depth, linear_out=[], conv_out=[], filter_size=[],
+                batchnorm_begin=False, batchnorm_dense=False)
+
+
+@case
+def pair_r10_128():
+    """BASELINE config 3 at its full size: PET+MRI ResNet-10 x2 + MLP head, 8 pairs of
+    1 x 128^3, focal loss gamma 2.  The two branches are the reference's own PET_CNN_ResNet
+    (pet_resnet_cnn.py:12-138) and Anat_CNN (anat_cnn.py:13-109); the two-backbone head
+    wiring is a BUILD EXTENSION (oracle ResNetPairFusionRef), so this
+    fixture is pinned for the branches and unpinned for the head."""
+    from pkg.models.mri_models.anat_cnn import Anat_CNN
+    from pkg.models.pet_models.pet_resnet_cnn import PET_CNN_ResNet
+    h = anat_hparams(10, fl_gamma=2)
+    torch.manual_seed(0)
+    m = models_ref.ResNetPairFusionRef(h, PET_CNN_ResNet(pair_stage1(h, 10)),
+                                       Anat_CNN(pair_stage1(h, 10)))
+    load_prng_weights(m, 1400)
+    ref64 = models_ref.ResNetPairFusionRef(h, models_ref.PETResNetRef(pair_stage1(h, 10)),
+                                           models_ref.AnatCNNRef(pair_stage1(h, 10)))
+    out = {"seed": np.array(1400), "shape": np.array(FULL)}
+    run_full_case(m, ref64, batch_for(FULL, 2, 1401, keys=("pet1451", "mri")),
+                  lambda b: (b["pet1451"].unsqueeze(1).double(), b["mri"].unsqueeze(1).double()),
+                  out)
     return out
 
 

@@ -143,3 +143,47 @@ def test_graph_replay_follows_lr_scheduler():
     torch.cuda.synchronize()
     for k, v in m.named_parameters():
         assert torch.equal(v, before[k]), k
+
+
+def test_capture_after_eager_default_stream_steps():
+    """Eager steps on the default stream, then GraphedTrainStep (its warm-up on a side
+    stream, the capture on torch's capture stream), then replays: bit-identical to the same
+    sequence run eagerly.  This once faulted at capture_end: the logged loss kept each step's
+    autograd graph -- and the parameters' AccumulateGrad nodes, bound to the stream they were
+    created on -- alive into the next step, so the captured backward synchronised with the
+    default stream.  Now nothing holds a finished step's graph."""
+    torch.manual_seed(11)
+    a = M.Anat_CNN(_hparams("bf16")).cuda()
+    b = copy.deepcopy(a)
+    batches = [_batch(20 + i) for i in range(3)]
+    n_eager, warm = 2, 1
+
+    def eager(m, opt, batch):
+        opt.zero_grad(set_to_none=True)
+        out = m.general_step(batch, 0, "train")
+        out["loss"].backward()
+        opt.step()
+        return out["loss"].detach().clone()
+
+    opt_a = a.configure_optimizers()
+    for _ in range(n_eager):
+        eager(a, opt_a, batches[0])
+    for grp in opt_a.param_groups:
+        grp["capturable"] = True
+        grp["lr"] = torch.tensor(float(grp["lr"]), device="cuda")
+    for _ in range(warm):
+        eager(a, opt_a, batches[0])
+    losses_a = [eager(a, opt_a, batches[i]) for i in range(3)]
+
+    opt_b = b.configure_optimizers()
+    for _ in range(n_eager):
+        eager(b, opt_b, batches[0])          # default stream
+    assert b.logged["train_loss"].grad_fn is None
+    gs = GraphedTrainStep(b, opt_b, batches[0], warmup=warm)
+    assert gs.out["loss"].grad_fn is None
+    losses_b = [gs(batches[i])["loss"].clone() for i in range(3)]
+    torch.cuda.synchronize()
+    for la, lb in zip(losses_a, losses_b):
+        assert torch.equal(la, lb)
+    for (na, pa), (nb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(pa, pb), na
