@@ -19,7 +19,7 @@ OBJ = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(PKG, "libmmad_hip.so")
 ARCH = os.environ.get("MMAD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+FLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 
 

@@ -60,6 +60,7 @@ _PD = C.POINTER(PackDual)
 _SIGS = {
     "mmad_abi_version": (_i32, []),
     "mmad_strerror": (C.c_char_p, [_i32]),
+    "mmad_set_kernel_variant": (_i32, [C.c_char_p, _i32]),
     "mmad_conv_packed_elems": (_i64, [_P, _i32, _i32]),
     "mmad_conv_pack_weight": (_i32, [_P, _i32, _vp, _vp, _i32, _vp]),
     "mmad_conv_pack_job": (_i32, [_P, _i32, _i32, _vp, _vp, _i64, _PJ]),

@@ -699,6 +699,7 @@ bool ok(const mmad_patch::Geo& q) {
 }
 
 int64_t tiles(const mmad_patch::Geo& q) {
+  if (mmad_lattice_zp::ok(q)) return mmad_lattice_zp::tiles(q);
   return (int64_t)q.nb * q.dd * q.dd * q.dd / NS * S;
 }
 
@@ -761,6 +762,7 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
 int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias,
         void* dst, float* stats, void* stream) {
   if (!mmad_lattice::ok(q)) return MMAD_EUNSUPPORTED;
+  if (mmad_lattice_zp::ok(q)) return mmad_lattice_zp::fwd(q, src, wp, bias, dst, stats, stream);
   static const bool attr =
       hipFuncSetAttribute((const void*)lattice_conv_kernel<4>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&

@@ -1,0 +1,474 @@
+// Residue-class ("lattice") conv, plane-pair form: layer4's dilation-4 3x3x3 convs
+// (16^3 grid, 4^3 sub-lattices) forward and -- over reversed taps -- input gradient, gfx950
+// bf16 with fp32 accumulation.  Same arithmetic and data layouts as latticeconv.hip
+// (packed weights [Nd][27 * Cs], k = tap * Cs + ci; BN partial sums one row per tile);
+// what changes is the tile, so that every CU gets the same work and every SIMD runs one
+// wave with its accumulators in AGPRs:
+//  * latticeconv.hip's tile is one z-plane of 32 subs; the planes at the sub-lattice's
+//    z-edges have one kz tap in the padding, so half the tiles carry 2/3 of the work of the
+//    others and, at one tile per CU, their CUs idle for a third of the launch.  Here a tile
+//    is TWO neighbouring z-planes (tz0 = 0 or 2) of 16 subs: every tile holds one edge plane
+//    and one interior plane, 5 of the 6 (plane, kz) pairs -- equal work everywhere;
+//  * 8 waves (two per SIMD): wave (wm, wn) owns the positions of the 4 x 4 plane's
+//    diagonal wm in BOTH planes (8 fragments of 16 subs = 128 rows) x 64 output channels
+//    (TN = 4 16-column MFMA tiles; TN = 2 for 64-channel tiles).  Diagonals lose different
+//    numbers of fragments to (y, x) padding (26 / 25 / 24 / 25 of 36 position-taps), but
+//    waves w and w + 4 share a SIMD (waves go to SIMDs in a cyclic order of 4) and hold
+//    diagonals wm and wm + 2, whose sums are equal on every ky row: every SIMD carries the
+//    same MFMA work between two barriers;
+//  * fragment registers roll: each A fragment register is refilled for the next tap right
+//    after the current tap's MFMAs read it (one A set and two B sets live, ~190 VGPRs with
+//    the 128 accumulators) -- a full second fragment set made the compiler shuffle
+//    accumulators (one wave per SIMD with 256 accumulators in AGPRs fared worse still: the
+//    MFMA results rotate through registers and spill the overflow to VGPRs);
+//  * a stage = (channel chunk, kz, ky): the three kx taps' weights (3 x BW rows x 64 B)
+//    through a 3-slot ring, two stages in flight; both output planes use the same kz
+//    weights, so every B fragment feeds 16 A fragments;
+//  * input planes (16 subs x 16 positions x 32 channels = 16 KiB) through a 4-slot ring:
+//    per chunk the pair reads 3 real planes (tz0 - 1 .. tz0 + 2 minus the padding one), each
+//    loaded once and read by every kz whose shift lands on it; planes of the next chunk
+//    stream in 3 to 9 stages ahead;
+//  * padding taps are skipped per fragment at compile time (wave diagonal, plane pair and
+//    tap are template constants in the main loop), as in latticeconv.hip.
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
+#include <utility>
+
+#include "common.h"
+#include "patchconv.h"
+
+namespace {
+
+constexpr int S = 4;                      // sub-lattice extent
+constexpr int NS = 16;                    // subs (sample x class) per tile
+constexpr int PP = S * S * NS;            // rows per plane: 256
+constexpr int RBL = 64;                   // bytes per LDS row: 32 bf16 channels
+constexpr int KC = RBL / 2;
+constexpr int ZPL = PP * RBL;             // 16 KiB per plane
+constexpr int NPS = 4;                    // plane ring slots
+constexpr int TPS = 3;                    // taps per stage
+constexpr int NSTL = 3;                   // weight ring slots (two stages in flight)
+constexpr int NTHR = 512;
+constexpr int NW = NTHR / 64;
+constexpr int ROWS = 2 * PP;              // tile rows: 512
+
+template <int TN>
+struct ZC {
+  static constexpr int BW = 32 * TN;               // output channels per tile
+  static constexpr int BTAP = BW * RBL;
+  static constexpr int BSLOT = TPS * BTAP;
+  static constexpr int RING_OFF = NPS * ZPL;
+  static constexpr int MAIN = RING_OFF + NSTL * BSLOT;
+  static constexpr int CROW = BW * 2 + 16;
+  static constexpr int EPI = ROWS * CROW + 3 * 2 * BW * 4;
+  static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
+  static constexpr int NQ = TPS * BW / 16;          // weight DMA instructions per stage
+  // ... per wave: the same count on every wave (surplus slots repeat the last rows: the
+  // same bytes to the same place), so the counted vmcnt waits hold on every wave
+  static constexpr int WI = (NQ + NW - 1) / NW;
+};
+
+struct ZG {
+  int Cs, Nd, Kpad, nchunk, nbn;
+  const u16* res;
+  int relu;
+};
+
+__device__ __forceinline__ int swz(int row) { return 3 * ((row >> 3) & 1); }
+
+// position i (row y = i) of diagonal D in the 4 x 4 plane, shifted by (KY, KX): inside?
+template <int D, int KY, int KX>
+__device__ constexpr bool yx_ok(int i) {
+  return i + KY >= 0 && i + KY < S && ((i + D) & 3) + KX >= 0 && ((i + D) & 3) + KX < S;
+}
+// output plane L (0, 1) of pair P reads input plane tz0 + L + KZ: inside the sub-lattice?
+template <int P, int L, int KZ>
+__device__ constexpr bool z_ok() {
+  return 2 * P + L + KZ >= 0 && 2 * P + L + KZ < S;
+}
+// ring index (0..2) of the input plane output plane L reads at KZ, among the pair's three
+// real planes of a chunk (pair 0 reads absolute planes 0..2, pair 1 planes 1..3)
+template <int P, int L, int KZ>
+__device__ constexpr int plane_idx() {
+  return 2 * P + L + KZ - (P == 0 ? 0 : 1);
+}
+
+// A fragment (L, i) of tap (KY, KX): is it inside the sub-lattice (y, x and z)?
+template <int WM, int P, int KZ, int KY, int KX, int L, int I>
+__device__ constexpr bool frag_ok() {
+  return z_ok<P, L, KZ>() && yx_ok<WM, KY, KX>(I);
+}
+template <int WM, int I, int KY, int KX>
+__device__ constexpr int frag_pos() {
+  return (I + KY) * S + ((I + WM) & 3) + KX;
+}
+constexpr int NF = 8;                     // A fragments per wave: 2 planes x 4 positions
+
+template <int TN, int KX>
+__device__ __forceinline__ void read_b(const char* bsl, bf16x8 (&b)[TN]) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+    b[j] = *reinterpret_cast<const bf16x8*>(bsl + (KX + 1) * ZC<TN>::BTAP + j * 16 * RBL);
+}
+
+// fragment F = L * 4 + I of tap (KY, KX), if inside, into a[F]
+template <int WM, int P, int KZ, int KY, int KX, int F>
+__device__ __forceinline__ void read_a(const char* const (&pl)[3], bf16x8 (&a)[NF]) {
+  constexpr int L = F / 4, I = F % 4;
+  if constexpr (frag_ok<WM, P, KZ, KY, KX, L, I>()) {
+    constexpr int ps = frag_pos<WM, I, KY, KX>();
+    a[F] = *reinterpret_cast<const bf16x8*>(pl[plane_idx<P, L, KZ>()] + ps * 16 * RBL);
+  }
+}
+
+template <int TN, int WM, int P, int KZ, int KY, int KX, int F>
+__device__ __forceinline__ void mma_a(f32x4 (&acc)[NF][TN], const bf16x8 (&a)[NF],
+                                      const bf16x8 (&b)[TN]) {
+  constexpr int L = F / 4, I = F % 4;
+  if constexpr (frag_ok<WM, P, KZ, KY, KX, L, I>()) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      acc[F][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[F], b[j], acc[F][j], 0, 0, 0);
+  }
+}
+
+// One stage (kz, ky; kx = -1, 0, 1), rolling registers: each A fragment register is refilled
+// for the next tap right after the current tap's MFMAs have read it, so one set of A
+// fragments and two sets of B fragments are live, and each refill has the other fragments'
+// MFMAs (and the partner wave) to land behind.
+template <int TN, int WM, int P, int KZ, int KY>
+__device__ __forceinline__ void stage_body(f32x4 (&acc)[NF][TN], const char* bsl,
+                                           const char* const (&pl)[3]) {
+  bf16x8 a[NF], b0[TN], b1[TN];
+  read_b<TN, -1>(bsl, b0);
+  [&]<int... F>(std::integer_sequence<int, F...>) {
+    (read_a<WM, P, KZ, KY, -1, F>(pl, a), ...);
+  }(std::make_integer_sequence<int, NF>{});
+  read_b<TN, 0>(bsl, b1);
+  [&]<int... F>(std::integer_sequence<int, F...>) {
+    ((mma_a<TN, WM, P, KZ, KY, -1, F>(acc, a, b0), read_a<WM, P, KZ, KY, 0, F>(pl, a)), ...);
+  }(std::make_integer_sequence<int, NF>{});
+  read_b<TN, 1>(bsl, b0);
+  [&]<int... F>(std::integer_sequence<int, F...>) {
+    ((mma_a<TN, WM, P, KZ, KY, 0, F>(acc, a, b1), read_a<WM, P, KZ, KY, 1, F>(pl, a)), ...);
+  }(std::make_integer_sequence<int, NF>{});
+  [&]<int... F>(std::integer_sequence<int, F...>) {
+    (mma_a<TN, WM, P, KZ, KY, 1, F>(acc, a, b0), ...);
+  }(std::make_integer_sequence<int, NF>{});
+}
+
+// planes issued at chunk-relative stage R of a non-last chunk (pair P): count
+template <int P, int R>
+__device__ constexpr int planes_at() {
+  return P == 0 ? (R == 0 ? 2 : R == 6 ? 1 : 0) : (R == 0 || R == 3 || R == 6 ? 1 : 0);
+}
+
+template <int TN>
+__global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __restrict__ src, const u16* __restrict__ wgt,
+                       const float* __restrict__ bias, u16* __restrict__ dst,
+                       float* __restrict__ stats) {
+  using C = ZC<TN>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem + C::RING_OFF;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int nt = tile % g.nbn;                      // channel tile fastest: the tiles of one
+  const int t2 = tile / g.nbn;                      // (group, pair) share their input planes
+  const int pair = t2 & 1, gid = t2 >> 1;
+  const int n = gid >> 2, rz = gid & 3;             // 64 classes = 4 groups of 16: rz fixed
+  constexpr int E = 16, PV = 4 * E * E;             // grid extent; voxels per plane step
+  const int tz0 = 2 * pair;
+  const int n0 = nt * C::BW;
+
+  // ---- plane DMA: instruction k of wave w = position 2w + k, lane >> 2 = sub, lane & 3 =
+  // 16-byte chunk (swizzled); sub s = class rz*16 + s -> (ry, rx) = (s >> 2, s & 3)
+  constexpr int PI = 16 / NW;                       // plane DMA instructions per wave
+  const u16* __restrict__ srcn = src + (int64_t)n * E * E * E * g.Cs;
+  uint32_t pofs[PI];
+  {
+    const int s = lane >> 2, ry = s >> 2, rx = s & 3;
+#pragma unroll
+    for (int k = 0; k < PI; ++k) {
+      const int pos = wave * PI + k, ty = pos >> 2, tx = pos & 3;
+      const int row = pos * NS + s;
+      const int vox = (rz * E + ry + 4 * ty) * E + rx + 4 * tx;
+      pofs[k] = (uint32_t)(vox * g.Cs + ((lane & 3) ^ swz(row)) * 8);
+    }
+  }
+  // plane jj (0..2) of chunk c -> ring slot (3c + jj) & 3; absolute plane z
+  auto issue_plane = [&](int c, int jj) {
+    const int z = jj + (pair == 0 ? 0 : 1);
+    const u16* base = srcn + (int64_t)z * PV * g.Cs + c * KC;
+    char* pb = smem + ((3 * c + jj) & 3) * ZPL;
+#pragma unroll
+    for (int k = 0; k < PI; ++k)
+      glds16_asm(base + pofs[k], lds_addr_of(pb + (wave * PI + k) * 1024));
+  };
+  // ---- weight DMA: stage (chunk c, kz, ky) -> taps t0 .. t0 + 2 into ring slot sl;
+  // instruction q = wave + NW h: tap q / (BW/16), rows 16 * (q % (BW/16)) ..
+  uint32_t wofs[C::WI];
+  int wq_off[C::WI];
+#pragma unroll
+  for (int h = 0; h < C::WI; ++h) {
+    const int q = min(wave + NW * h, C::NQ - 1);
+    const int tk = q / (C::BW / 16), rb = q % (C::BW / 16);
+    const int row = rb * 16 + (lane >> 2);
+    wofs[h] = (uint32_t)((n0 + row) * g.Kpad + (((lane & 3) ^ swz(row)) * 8) + tk * g.Cs);
+    wq_off[h] = tk * C::BTAP + rb * 1024;
+  }
+  const int nstage = g.nchunk * 9;
+  auto issue_stage_b = [&](int s) {
+    const int c = s / 9, r = s % 9;
+    const u16* base = wgt + (r * 3) * g.Cs + c * KC;   // taps (kz,ky) row: t0 = 3 r
+    char* sb = ring + (s % NSTL) * C::BSLOT;
+#pragma unroll
+    for (int h = 0; h < C::WI; ++h)
+      glds16_asm(base + wofs[h], lds_addr_of(sb + wq_off[h]));
+  };
+
+  // waves w and w + 4 share a SIMD: give them diagonals wm and wm + 2
+  const int wn = wave & 1, wm = wave >> 1;
+  const int lr = lane & 15, lk = lane >> 4;
+  const uint32_t a_lane = lr * RBL + ((lk ^ swz(lr)) << 4);
+  const uint32_t b_lane = (wn * 16 * TN + lr) * RBL + ((lk ^ swz(lr)) << 4);
+  f32x4 acc[NF][TN];                                // [L * 4 + i][j]
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: the first chunk's planes needed before its plane issues (pair 0: planes 0, 1;
+  // pair 1: all three), then the weights of stages 0 and 1
+  issue_plane(0, 0);
+  issue_plane(0, 1);
+  if (pair == 1) issue_plane(0, 2);
+  issue_stage_b(0);
+  issue_stage_b(1);
+
+  // Stage s = 9c + R (R = 3 (kz+1) + ky+1) waits for its weights (issued at stage s - 2);
+  // younger are the ops issued at stage s - 1: its planes and the weights of stage s + 1.
+  // A plane is older than the weights of the stage that first reads it (issued 3 or more
+  // stages ahead), so the same wait covers it.  Issue schedule per chunk c (slot reuse
+  // checked against each plane's last reader):
+  //   pair 0: R 0 -> (c, 2), (c + 1, 0); R 6 -> (c + 1, 1)
+  //   pair 1: R 0 -> (c + 1, 0); R 3 -> (c + 1, 1); R 6 -> (c + 1, 2)
+  auto run = [&](auto wmc, auto pc) {
+    constexpr int WM = decltype(wmc)::value, P = decltype(pc)::value;
+    for (int c = 0; c < g.nchunk; ++c) {
+      const bool more = c + 1 < g.nchunk;
+      const int sb0 = 3 * c;
+      const char* const pl[3] = {smem + ((sb0 + 0) & 3) * ZPL + a_lane,
+                                 smem + ((sb0 + 1) & 3) * ZPL + a_lane,
+                                 smem + ((sb0 + 2) & 3) * ZPL + a_lane};
+      auto stage = [&](auto rc) {
+        constexpr int R = decltype(rc)::value;
+        constexpr int KZ = R / 3 - 1, KY = R % 3 - 1;
+        const int s = 9 * c + R;
+        // younger than this stage's weights: stage s-1's planes (R - 1 of this chunk) and
+        // the weights of stage s + 1
+        constexpr int PY = R >= 1 ? planes_at<P, R - 1>() : 0;
+        if (s == 0) {
+          wait_vm_lgkm0<C::WI>();
+        } else if (s + 1 >= nstage) {
+          wait_vm_lgkm0<0>();
+        } else if (more) {
+          wait_vm_lgkm0<C::WI + PI * PY>();
+        } else {
+          // last chunk: pair 0 still issued (c, 2) at R 0; nothing else of chunk c + 1
+          constexpr int PYL = (P == 0 && R == 1) ? 1 : 0;
+          wait_vm_lgkm0<C::WI + PI * PYL>();
+        }
+        raw_barrier();
+        if constexpr (P == 0) {
+          if constexpr (R == 0) {
+            issue_plane(c, 2);
+            if (more) issue_plane(c + 1, 0);
+          } else if constexpr (R == 6) {
+            if (more) issue_plane(c + 1, 1);
+          }
+        } else {
+          if constexpr (R == 0 || R == 3 || R == 6) {
+            if (more) issue_plane(c + 1, R / 3);
+          }
+        }
+        if (s + 2 < nstage) issue_stage_b(s + 2);
+        int boff = C::RING_OFF + (s % NSTL) * C::BSLOT;
+        asm volatile("" : "+s"(boff));              // per-stage base stays opaque (no early
+        stage_body<TN, WM, P, KZ, KY>(acc, smem + boff + b_lane, pl);   // address hoisting)
+      };
+      stage(std::integral_constant<int, 0>{});
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
+      stage(std::integral_constant<int, 4>{});
+      stage(std::integral_constant<int, 5>{});
+      stage(std::integral_constant<int, 6>{});
+      stage(std::integral_constant<int, 7>{});
+      stage(std::integral_constant<int, 8>{});
+    }
+  };
+  auto by_pair = [&](auto wmc) {
+    if (pair == 0) run(wmc, std::integral_constant<int, 0>{});
+    else run(wmc, std::integral_constant<int, 1>{});
+  };
+  switch (wm) {                                     // wave-uniform
+    case 0: by_pair(std::integral_constant<int, 0>{}); break;
+    case 1: by_pair(std::integral_constant<int, 1>{}); break;
+    case 2: by_pair(std::integral_constant<int, 2>{}); break;
+    default: by_pair(std::integral_constant<int, 3>{}); break;
+  }
+  __syncthreads();                                  // planes / ring reused by the epilogue
+
+  // ---- epilogue: tile row = L * 256 + pos * 16 + sub; acc[L * 4 + i][j][e] is row
+  // (L, pos(wm, i), sub lk * 4 + e), column wn * 16 TN + j * 16 + lr
+  auto dst_vox = [&](int row) -> int64_t {
+    const int l = row >> 8, pos = (row >> 4) & 15, s = row & 15;
+    const int ty = pos >> 2, tx = pos & 3;
+    return (((int64_t)n * E + rz + 4 * (tz0 + l)) * E + (s >> 2) + 4 * ty) * E + (s & 3) + 4 * tx;
+  };
+  u16* ctile = reinterpret_cast<u16*>(smem);
+  float cs[TN], cq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    cs[j] = 0.f;
+    cq[j] = 0.f;
+    const int col = wn * 16 * TN + j * 16 + lr;
+    const float bv = bias != nullptr ? bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int l = 0; l < 2; ++l)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pos = i * S + ((i + wm) & 3);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = l * PP + pos * NS + lk * 4 + e;
+          const float v = acc[l * 4 + i][j][e] + bv;
+          ctile[row * (C::CROW / 2) + col] = f2bf(v);
+          cs[j] += v;
+          cq[j] += v * v;
+        }
+      }
+  }
+  __syncthreads();
+  constexpr int CPR = C::BW / 8;
+#pragma unroll 4
+  for (int hh = 0; hh < ROWS * CPR / NTHR; ++hh) {
+    const int qd = tid + NTHR * hh;
+    const int row = qd / CPR, c8 = qd % CPR;
+    const int64_t o = dst_vox(row) * g.Nd + n0 + c8 * 8;
+    u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
+                                              row * C::CROW + c8 * 16);
+    if (g.res != nullptr || g.relu) v = epi_res_relu(v, g.res ? g.res + o : nullptr, g.relu);
+    *reinterpret_cast<u32x4*>(dst + o) = v;
+  }
+  if (stats != nullptr) {
+    float* red = reinterpret_cast<float*>(smem + ROWS * C::CROW);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      cs[j] += __shfl_xor(cs[j], 16, 64);
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 16, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+    }
+    if (wm > 0 && lk == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * 16 * TN + j * 16 + lr;
+        red[(wm - 1) * 2 * C::BW + col] = cs[j];
+        red[(wm - 1) * 2 * C::BW + C::BW + col] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && lk == 0) {
+      const int mt = gid * 2 + pair;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * 16 * TN + j * 16 + lr;
+        float ss = cs[j], qs = cq[j];
+        for (int w = 1; w < 4; ++w) {               // fixed order: deterministic
+          ss += red[(w - 1) * 2 * C::BW + col];
+          qs += red[(w - 1) * 2 * C::BW + C::BW + col];
+        }
+        stats[((int64_t)mt * 2) * g.Nd + n0 + col] = ss;
+        stats[((int64_t)mt * 2 + 1) * g.Nd + n0 + col] = qs;
+      }
+    }
+  }
+}
+
+// MMAD_LATTICE_ZP: 1 (default) plane-pair kernel where it fills the CUs, 0 the one-plane
+// latticeconv.hip kernel, 2 plane-pair at any size; mmad_set_kernel_variant("lattice_zp", v)
+// overrides it at run time (tests compare both forms in one process)
+std::atomic<int> g_zp_mode{-1};
+int zp_mode() {
+  int v = g_zp_mode.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("MMAD_LATTICE_ZP");
+    v = e ? atoi(e) : 1;
+    int expect = -1;
+    g_zp_mode.compare_exchange_strong(expect, v);
+    v = g_zp_mode.load(std::memory_order_relaxed);
+  }
+  return v;
+}
+
+}  // namespace
+
+namespace mmad_lattice_zp {
+
+// the caller (mmad_lattice) has checked the residue-class geometry; this form needs d = 4
+// (16^3 grids, 64 classes per sample) and enough tiles to give every CU one
+bool ok(const mmad_patch::Geo& q) {
+  if (zp_mode() <= 0 || q.dd != 4 || q.Cs % KC || q.Nd % 64) return false;
+  if (q.Cs / KC < 2) return false;
+  return (int64_t)q.nb * 8 * (q.Nd / 64) >= 256 || zp_mode() == 2;
+}
+
+static bool wide(const mmad_patch::Geo& q) {
+  return q.Nd % 128 == 0 && (int64_t)q.nb * 8 * (q.Nd / 128) >= 256;
+}
+
+int64_t tiles(const mmad_patch::Geo& q) { return (int64_t)q.nb * 8; }
+
+int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias, void* dst,
+        float* stats, void* stream) {
+  static const bool attr =
+      hipFuncSetAttribute((const void*)lattice_zp_kernel<4>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, ZC<4>::LDS) == hipSuccess &&
+      hipFuncSetAttribute((const void*)lattice_zp_kernel<2>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, ZC<2>::LDS) == hipSuccess;
+  if (!attr) return MMAD_EUNSUPPORTED;
+  const bool w = wide(q);
+  ZG g{};
+  g.Cs = q.Cs; g.Nd = q.Nd; g.Kpad = q.Kpad;
+  g.nchunk = q.Cs / KC;
+  g.nbn = q.Nd / (w ? 128 : 64);
+  g.res = reinterpret_cast<const u16*>(q.res);
+  g.relu = q.relu;
+  const int64_t nblk = mmad_lattice_zp::tiles(q) * g.nbn;
+  if (w)
+    hipLaunchKernelGGL(lattice_zp_kernel<4>, dim3((unsigned)nblk), dim3(NTHR), ZC<4>::LDS,
+                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
+                       stats);
+  else
+    hipLaunchKernelGGL(lattice_zp_kernel<2>, dim3((unsigned)nblk), dim3(NTHR), ZC<2>::LDS,
+                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
+                       stats);
+  return launch_status();
+}
+
+}  // namespace mmad_lattice_zp
+
+extern "C" int mmad_set_kernel_variant(const char* name, int value) {
+  if (name != nullptr && std::strcmp(name, "lattice_zp") == 0) {
+    const int prev = zp_mode();
+    if (value >= 0) g_zp_mode.store(value, std::memory_order_relaxed);
+    return prev;
+  }
+  return -1;
+}

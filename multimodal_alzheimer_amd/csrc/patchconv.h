@@ -38,6 +38,15 @@ int wgrad(const mmad_patch::Geo& g, const void* x, const void* dy, float* ws, in
           void* stream);
 }  // namespace mmad_lattice
 
+// Plane-pair form of the residue-class conv for d = 4 (latticezp.hip): two z-planes of 16
+// subs per tile, one wave per SIMD; mmad_lattice::fwd / tiles route to it when ok().
+namespace mmad_lattice_zp {
+bool ok(const mmad_patch::Geo& g);
+int64_t tiles(const mmad_patch::Geo& g);
+int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,
+        float* stats, void* stream);
+}  // namespace mmad_lattice_zp
+
 // Residue-class conv for dilation-2 3^3 convs on a 16^3 grid (lattice8.hip, layer3).
 namespace mmad_lattice8 {
 bool ok(const mmad_patch::Geo& g);

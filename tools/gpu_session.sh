@@ -1,12 +1,14 @@
 #!/bin/bash
-# One GPU-box session: the new full-size oracle tests (verbose, printed errors), then the
-# whole -m gpu suite.  A pytest exit of 0 or 1 (tests ran; some may have failed) lets the
-# next step run; any other status (timeout 124/137, abort, segfault) ends the session.
-#   gpurun --timeout 1100 -- bash tools/gpu_session.sh <tag> [pytest -k expr]
+# One GPU-box session: the new kernel's equality test, the graph-capture regression test, the
+# full-size oracle tests, the whole -m gpu suite, then bench lines (plane-pair lattice on / off).
+# A pytest exit of 0 or 1 (tests ran; some may have failed) lets the next step run; any other
+# status (timeout 124/137, abort, segfault) ends the session.
+#   gpurun --timeout 1100 -- bash tools/gpu_session.sh <tag>
 TAG=${1:-r03}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+PYT="python -u -m pytest -v --timeout 200 --timeout-method thread"
 step() {    # step <name> <seconds> <cmd...>
   local name=$1 secs=$2; shift 2
   timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1
@@ -14,7 +16,12 @@ step() {    # step <name> <seconds> <cmd...>
   echo "$name rc=$rc"; tail -3 $OUT/$name.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step fullsize 300 python -u -m pytest tests/test_fullsize_oracle_gpu.py -v -s --timeout 240 --timeout-method thread
-step suite 700 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread --ignore=tests/test_fullsize_oracle_gpu.py
+step zp 240 $PYT tests/test_lattice_zp_gpu.py
+step capture 200 $PYT tests/test_graph_step_gpu.py -k capture_after_eager
+step fullsize 300 $PYT -s tests/test_fullsize_oracle_gpu.py
+step suite 700 $PYT tests -m gpu --ignore=tests/test_fullsize_oracle_gpu.py --ignore=tests/test_lattice_zp_gpu.py
 grep -E "FAILED|ERROR" $OUT/suite.log | head -20
+grep -c "AccumulateGrad" $OUT/*.log
+step bench1 240 python -u bench.py --steps 20 --warmup 5
+step bench0 240 env MMAD_LATTICE_ZP=0 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline
 echo session done
