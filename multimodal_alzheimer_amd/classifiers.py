@@ -325,6 +325,16 @@ class MergedAdam(torch.optim.Adam):
             groups.append(g)
         return {"state": state, "param_groups": groups}
 
+    def ref_group_index(self):
+        """merged group of each reference (per-tensor) group, in reference order"""
+        idx, gidx = self._merged_index()
+        return [gidx[idx[id(ps[0])]] for ps in self._ref_groups]
+
+    # optimizer-implementation keys: how THIS optimizer runs, not training state.  A
+    # checkpoint from the reference (torch 1.13 Adam: fused None, capturable False) must not
+    # turn off the fused multi-tensor Adam here, nor a captured step's device-resident lr.
+    _IMPL_KEYS = ("fused", "foreach", "capturable", "differentiable")
+
     def load_state_dict(self, state_dict):
         saved = state_dict["param_groups"]
         per_tensor = (len(self._ref_groups) != len(self.param_groups) and
@@ -346,7 +356,55 @@ class MergedAdam(torch.optim.Adam):
                 base += len(g["params"])
                 groups.append(src)
             state_dict = {"state": state, "param_groups": groups}
-        super().load_state_dict(state_dict)
+        groups = [dict(g) for g in state_dict["param_groups"]]
+        if len(groups) == len(self.param_groups):
+            for g, cur in zip(groups, self.param_groups):
+                for k in self._IMPL_KEYS:
+                    if k in cur:
+                        g[k] = cur[k]    # also moves Adam's step counters where fused needs them
+        lrs = [cur["lr"] for cur in self.param_groups]
+        super().load_state_dict({"state": state_dict["state"], "param_groups": groups})
+        for cur, old in zip(self.param_groups, lrs):
+            if torch.is_tensor(old):     # a captured step reads this tensor: keep it, refill it
+                new = cur["lr"]
+                old.fill_(new.item() if torch.is_tensor(new) else float(new))
+                cur["lr"] = old
+
+
+class MergedPlateau(ReduceLROnPlateau):
+    """ReduceLROnPlateau over a MergedAdam whose ``state_dict`` lists ``min_lrs`` and
+    ``_last_lr`` per reference (per-tensor) group, as torch 1.13's scheduler on the
+    reference's optimizer does (anat_cnn.py:129-134): a checkpoint resumes in either
+    direction.  ``load_state_dict`` takes either length."""
+
+    def _ref_index(self):
+        opt = self.optimizer
+        return opt.ref_group_index() if isinstance(opt, MergedAdam) else None
+
+    def state_dict(self):
+        sd = super().state_dict()
+        ri = self._ref_index()
+        if ri is not None and len(ri) != len(self.optimizer.param_groups):
+            for k in ("min_lrs", "_last_lr"):
+                if isinstance(sd.get(k), (list, tuple)) and \
+                        len(sd[k]) == len(self.optimizer.param_groups):
+                    sd[k] = [sd[k][m] for m in ri]
+        return sd
+
+    def load_state_dict(self, state_dict):
+        sd = dict(state_dict)
+        ri = self._ref_index()
+        n = len(self.optimizer.param_groups)
+        if ri is not None and len(ri) != n:
+            for k in ("min_lrs", "_last_lr"):
+                v = sd.get(k)
+                if isinstance(v, (list, tuple)) and len(v) == len(ri):
+                    merged = [None] * n
+                    for r, m in enumerate(ri):
+                        if merged[m] is None:
+                            merged[m] = v[r]
+                    sd[k] = merged
+        super().load_state_dict(sd)
 
 
 def _adam(groups, hparams, device):
@@ -357,7 +415,7 @@ def _adam(groups, hparams, device):
 def _with_scheduler(opt, hparams):
     if hparams.get("reduce_factor_lr_schedule"):
         return {"optimizer": opt,
-                "lr_scheduler": ReduceLROnPlateau(opt, factor=hparams["reduce_factor_lr_schedule"]),
+                "lr_scheduler": MergedPlateau(opt, factor=hparams["reduce_factor_lr_schedule"]),
                 "monitor": "val_loss_epoch"}
     return opt
 

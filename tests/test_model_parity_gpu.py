@@ -350,3 +350,17 @@ def test_adam_step_matches_reference_adam():
     for (k, p), (_, q) in zip(ref.named_parameters(), m.named_parameters()):
         err = (q.detach().cpu() - p.detach()).abs().max().item()
         assert err <= 1e-6 * max(1.0, p.abs().max().item()), (k, err)
+    # resume from the reference optimizer's checkpoint state (torch Adam groups: fused
+    # unset): the product keeps its fused multi-tensor Adam and steps on identically
+    import copy
+    opt.load_state_dict(copy.deepcopy(ref_opt.state_dict()))
+    assert all(g["fused"] for g in opt.param_groups)
+    for (k, p), (_, q) in zip(ref.named_parameters(), m.named_parameters()):
+        gr = torch.randn(p.shape, generator=gen) * 1e-2
+        p.grad = gr.clone()
+        q.grad = gr.to(DEV)
+    ref_opt.step()
+    opt.step()
+    for (k, p), (_, q) in zip(ref.named_parameters(), m.named_parameters()):
+        err = (q.detach().cpu() - p.detach()).abs().max().item()
+        assert err <= 1e-6 * max(1.0, p.abs().max().item()), (k, err)

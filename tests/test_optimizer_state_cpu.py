@@ -6,6 +6,7 @@ anat_pet_fusion.py:94-117); the product runs Adam on groups merged per learning 
 layout, so Lightning's ``optimizer_states`` resume in either direction."""
 import copy
 
+import pytest
 import torch
 
 import multimodal_alzheimer_amd as M
@@ -114,3 +115,65 @@ def test_stage1_checkpoints_feed_fusion(tmp_path):
     assert list(got) == list(sd)
     for k, v in sd.items():
         assert torch.equal(got[k], v), k
+
+
+def test_resume_keeps_optimizer_implementation_and_device_lr():
+    """A reference checkpoint (torch 1.13 Adam groups: fused None, capturable False) resumed
+    into MergedAdam keeps this optimizer's own implementation flags, and a tensor lr (what a
+    captured step reads) stays the same tensor object, refilled with the checkpoint's lr."""
+    h = G.anat_hparams(10)
+    m = M.Anat_CNN(h)
+    opt = m.configure_optimizers()
+    ref = copy.deepcopy(m)
+    ref_opt = torch.optim.Adam(_ref_groups_anat(ref, h), weight_decay=h["l2_reg"])
+    _fake_grads(ref.parameters(), 3)
+    ref_opt.step()
+    sd = copy.deepcopy(ref_opt.state_dict())
+    for g in sd["param_groups"]:
+        g.update(fused=None, foreach=None, capturable=False, lr=g["lr"] * 0.25)
+    lr_tensors = []
+    for g in opt.param_groups:
+        g["foreach"] = True
+        g["lr"] = torch.tensor(float(g["lr"]))
+        lr_tensors.append(g["lr"])
+    opt.load_state_dict(sd)
+    for g, t in zip(opt.param_groups, lr_tensors):
+        assert g["foreach"] is True
+        assert g["lr"] is t
+    assert sorted(float(t) for t in lr_tensors) == pytest.approx(sorted(
+        [h["lr_pretrained"] * 0.25, h["lr"] * 0.25]), rel=1e-6)     # fp32 lr tensors
+
+
+def test_plateau_scheduler_state_round_trips_reference_layout():
+    """ReduceLROnPlateau on the merged optimizer saves min_lrs / _last_lr per reference
+    group, so the reference's torch scheduler (one entry per per-tensor group) resumes from
+    it and reduces every group; and the reference's scheduler state loads back."""
+    from torch.optim.lr_scheduler import ReduceLROnPlateau
+    h = G.anat_hparams(10, fl_gamma=2, reduce_factor_lr_schedule=0.5)
+    m = M.Anat_PET_CNN(h, pet_model=M.Small_PET_CNN(G.pet_hparams()),
+                       mri_model=M.Anat_CNN(G.anat_hparams(10)))
+    cfg = m.configure_optimizers()
+    opt, sched = cfg["optimizer"], cfg["lr_scheduler"]
+    sched.step(1.0)
+    ssd = sched.state_dict()
+    n_ref = len(opt.state_dict()["param_groups"])
+    assert len(ssd["min_lrs"]) == n_ref and len(ssd["_last_lr"]) == n_ref
+    ref_groups = [{"params": p, "lr": h["lr"]} for p in m.model_fuse.parameters()]
+    ref_groups += [{"params": p, "lr": h["lr"]} for p in m.reduce_dim_mri.parameters()]
+    ref_groups += [{"params": p, "lr": h["lr_pretrained"]} for p in m.model_pet.parameters()]
+    ref_groups += [{"params": p, "lr": h["lr_pretrained"]} for p in m.model_mri.parameters()]
+    ref_opt = torch.optim.Adam(ref_groups)
+    ref_opt.load_state_dict(copy.deepcopy(opt.state_dict()))
+    ref_sched = ReduceLROnPlateau(ref_opt, factor=0.5, patience=0)
+    ref_sched.load_state_dict(copy.deepcopy(ssd))
+    ref_sched.patience = 0
+    ref_sched.step(2.0)                           # no improvement: every group reduced
+    assert ref_opt.param_groups[0]["lr"] == h["lr"] * 0.5
+    assert ref_opt.param_groups[-1]["lr"] == h["lr_pretrained"] * 0.5
+    sched.load_state_dict(copy.deepcopy(ref_sched.state_dict()))
+    assert len(sched.min_lrs) == len(opt.param_groups)
+    opt.load_state_dict(copy.deepcopy(ref_opt.state_dict()))
+    sched.patience = 0
+    sched.step(4.0)
+    assert sorted(g["lr"] for g in opt.param_groups) == sorted(
+        [h["lr"] * 0.25, h["lr_pretrained"] * 0.25])
