@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counters of one kernel of tools/probe_kernel.py:  bash tools/exp_pmc1.sh <layer> <op> <name-substring>
+# SQ counters of one kernel of tools/probe_kernel.py:  bash tools/pmc_kernel.sh <layer> <op> <name-substring>
 set -o pipefail
 L=$1; OP=$2; K=$3
 OUT=gpurun_out/pmc1_$L$OP

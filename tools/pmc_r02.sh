@@ -8,7 +8,7 @@ OUT=gpurun_out/pmc_r02.txt
 for spec in "l4c2 fwd lattice_conv_kernel" "l4c2 wgrad lattice_wgrad" "stem fwd stem_fwdq" "stem wgrad stem_wgrad2" "l1c wgrad pwgrad" "l1c fwd patch_conv" "l3c2 fwd lattice8"; do
   set -- $spec
   echo "== $1 $2 ($3)" >> $OUT
-  bash tools/exp_pmc1.sh $1 $2 $3 > gpurun_out/pmc_tmp.txt 2>&1 || exit 1
+  bash tools/pmc_kernel.sh $1 $2 $3 > gpurun_out/pmc_tmp.txt 2>&1 || exit 1
   cat gpurun_out/pmc_tmp.txt >> $OUT
   python3 - gpurun_out/pmc_tmp.txt >> $OUT <<'PY'
 import sys
