@@ -51,7 +51,7 @@ def build(force=False, verbose=False):
     objs = [o for o, _ in results]
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(map(os.path.getmtime, objs)):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
-               "-L/opt/rocm/lib", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib"]
+               "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

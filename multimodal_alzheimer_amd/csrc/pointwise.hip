@@ -1,27 +1,140 @@
-// 1x1x1 stride-1 convolutions (MedicalNet shortcut B downsample of layers 3 and 4, reached
-// from pkg/models/mri_models/anat_cnn.py:29-31) are plain GEMMs over NDHWC rows, so their
-// input gradient goes to hipBLASLt instead of the implicit-GEMM kernel (whose 32-deep K
-// stages and row gathers are built for 27-tap convs: layer4's shortcut dgrad 25.6 -> 18.8 us,
-// layer3's 14.2 -> 10.8 us).  The forward keeps conv.hip's implicit GEMM, whose epilogue
-// produces the BN partial sums; the weight gradient (wgrad below) is kept for experiments
-// but not routed: hipBLASLt returned no split-K algorithm for K = 32768 and its single-pass
-// kernels took 140-165 us.  Internal to libmmad_hip.so; host code only.
+// Input gradient of the 1x1x1 stride-1 convolutions (MedicalNet shortcut B downsample of
+// layers 3 and 4, reached from pkg/models/mri_models/anat_cnn.py:29-31) as a plain MFMA GEMM
+// over NDHWC rows, gfx950 bf16 with fp32 accumulation.  Internal to libmmad_hip.so.
 //
-// Row-major NDHWC tensors are column-major with the channel as the leading dimension:
-//   dgrad  dX[M][ci] = dY[M][co] . Wd[ci][co]^T   ->  D(ci x M) = op_T(Wd: co x ci) . dY(co x M)
-//   wgrad  dW[co][ci] = sum_m dY[m][co] X[m][ci]   ->  D(ci x co) = X(ci x M) . op_T(dY: co x M)
-// (fp32 accumulation; dW written in fp32, the torch layout [co][ci][1][1][1]).
-#include <hipblaslt/hipblaslt.h>
-
-#include <algorithm>
+//   dX[m][ci] = sum_co dY[m][co] * Wd[ci][co]      (Wd: the dgrad-packed weights [ci][co])
+//
+// Both operands are K-contiguous rows (K = co), the layout the MFMA fragments read, so the
+// kernel is the implicit GEMM without its gather: a block owns 128 voxel rows and ALL ci
+// columns (128 or 256), so every dY byte is read once; K streams through a 3-slot LDS ring
+// in 64-deep chunks (128-byte rows, 16-byte slots XOR-swizzled by row & 7 on the source
+// address so the LDS-DMA image stays lane-linear and the fragment reads are conflict-free),
+// two chunks in flight; 8 waves = 2 (64 rows) x 4 (ci quarters); the tile leaves through LDS
+// as 16-byte channel vectors.  The step has two such launches (layer4: 32768 x 256 x 512,
+// layer3: 32768 x 128 x 256 at batch 8): bandwidth-bound on the dY read (M x K x 2 bytes).
+// Replaces the hipBLASLt GEMM used before round 3 (Cijk_* kernels, 18.8 / 10.8 us).
 #include <cstdlib>
-#include <map>
-#include <tuple>
 
 #include "common.h"
 #include "pointwise.h"
 
 namespace {
+
+constexpr int TM = 128;                   // voxel rows per block
+constexpr int KS = 64;                    // K elements per stage (128-byte rows)
+constexpr int RB = KS * 2;
+constexpr int NST = 3;                    // ring slots: two stages in flight
+constexpr int NTHR = 512;
+constexpr int NW = NTHR / 64;
+
+template <int BN>
+struct PC {
+  static constexpr int TN = BN / 64;                // 16-column MFMA tiles per wave
+  static constexpr int A_BYTES = TM * RB;
+  static constexpr int SLOT = (TM + BN) * RB;
+  static constexpr int NQ = SLOT / 1024;            // 1 KiB DMA instructions per stage
+  static constexpr int WI = NQ / NW;
+  static_assert(NQ % NW == 0, "DMA split over the waves");
+  static constexpr int CROW = BN * 2 + 16;
+  static constexpr int EPI = TM * CROW;
+  static constexpr int MAIN = NST * SLOT;
+  static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
+};
+
+__device__ __forceinline__ int swz8(int row) { return row & 7; }
+
+template <int BN>
+__global__ __launch_bounds__(NTHR) void pw_dgrad_kernel(int K, const u16* __restrict__ dy,
+                                                        const u16* __restrict__ wd,
+                                                        u16* __restrict__ dx) {
+  using C = PC<BN>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t m0 = (int64_t)blockIdx.x * TM;
+  const int nstage = K / KS;
+
+  // DMA instruction q = wave + NW h: rows 8q .. 8q + 7 of the stage image (A rows first,
+  // then B rows); lane -> row 8q + (lane >> 3), 16-byte slot lane & 7 (source slot swizzled)
+  const u16* srcp[C::WI];
+  uint32_t lofs[C::WI];
+#pragma unroll
+  for (int h = 0; h < C::WI; ++h) {
+    const int q = wave + NW * h;
+    const int row = q * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ swz8(row);
+    srcp[h] = row < TM ? dy + (m0 + row) * K + ch * 8 : wd + (int64_t)(row - TM) * K + ch * 8;
+    lofs[h] = q * 1024;
+  }
+  auto issue = [&](int s) {
+    char* slot = smem + (s % NST) * C::SLOT;
+#pragma unroll
+    for (int h = 0; h < C::WI; ++h)
+      glds16_asm(srcp[h] + s * KS, lds_addr_of(slot + lofs[h]));
+  };
+
+  const int wm = wave & 1, wn = wave >> 1;          // 64 rows x BN/4 columns per wave
+  const int lr = lane & 15, lk = lane >> 4;
+  f32x4 acc[4][C::TN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (nstage > 1) issue(1);
+  for (int s = 0; s < nstage; ++s) {
+    if (s + 1 < nstage) wait_vm_lgkm0<C::WI>();       // this stage landed, the next in flight
+    else wait_vm_lgkm0<0>();
+    raw_barrier();
+    if (s + 2 < nstage) issue(s + 2);
+    const char* slot = smem + (s % NST) * C::SLOT;
+#pragma unroll
+    for (int kk = 0; kk < KS / 32; ++kk) {          // two 32-deep MFMA k steps per stage
+      bf16x8 a[4], b[C::TN];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + lr;
+        a[i] = *reinterpret_cast<const bf16x8*>(slot + row * RB + (((kk * 4 + lk) ^ swz8(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) {
+        const int row = wn * 16 * C::TN + j * 16 + lr;
+        b[j] = *reinterpret_cast<const bf16x8*>(slot + C::A_BYTES + row * RB +
+                                                (((kk * 4 + lk) ^ swz8(row)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();                                  // ring reused by the epilogue
+
+  // acc[i][j][e]: row wm*64 + i*16 + lk*4 + e, column wn*16*TN + j*16 + lr
+  u16* ctile = reinterpret_cast<u16*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wm * 64 + i * 16 + lk * 4 + e;
+        const int col = wn * 16 * C::TN + j * 16 + lr;
+        ctile[row * (C::CROW / 2) + col] = f2bf(acc[i][j][e]);
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;                       // 16-byte vectors per row
+#pragma unroll
+  for (int hh = 0; hh < TM * CPR / NTHR; ++hh) {
+    const int qd = tid + NTHR * hh;
+    const int row = qd / CPR, c8 = qd % CPR;
+    *reinterpret_cast<u32x4*>(dx + (m0 + row) * BN + c8 * 8) =
+        *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) + row * C::CROW +
+                                        c8 * 16);
+  }
+}
 
 bool pw_on() {
   static const bool v = [] {
@@ -31,90 +144,6 @@ bool pw_on() {
   return v;
 }
 
-hipblasLtHandle_t handle() {
-  static hipblasLtHandle_t h = [] {
-    hipblasLtHandle_t x = nullptr;
-    if (hipblasLtCreate(&x) != HIPBLAS_STATUS_SUCCESS) x = nullptr;
-    return x;
-  }();
-  return h;
-}
-
-// one GEMM shape: descriptors and the heuristic's first algorithm, built on first use
-// (eagerly, before any graph capture: warm-up steps run every shape first)
-struct Plan {
-  hipblasLtMatmulDesc_t op = nullptr;
-  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, d = nullptr;
-  hipblasLtMatmulAlgo_t algo{};
-  size_t ws = 0;
-  bool ok = false;
-};
-
-using Key = std::tuple<int, int, int, int, int, int, size_t>;   // ta, tb, m, n, k, dtype, ws
-
-const Plan& plan_for(hipblasOperation_t ta, hipblasOperation_t tb, int m, int n, int k,
-                     hipDataType dt, size_t ws_max) {
-  static std::map<Key, Plan> cache;
-  const Key key{(int)ta, (int)tb, m, n, k, (int)dt, ws_max};
-  auto it = cache.find(key);
-  if (it != cache.end()) return it->second;
-  Plan p;
-  hipblasLtHandle_t h = handle();
-  bool good = h != nullptr;
-  good = good && hipblasLtMatmulDescCreate(&p.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) ==
-                     HIPBLAS_STATUS_SUCCESS;
-  good = good && hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta,
-                                                 sizeof(ta)) == HIPBLAS_STATUS_SUCCESS;
-  good = good && hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb,
-                                                 sizeof(tb)) == HIPBLAS_STATUS_SUCCESS;
-  const uint64_t ar = ta == HIPBLAS_OP_N ? m : k, ac = ta == HIPBLAS_OP_N ? k : m;
-  const uint64_t br = tb == HIPBLAS_OP_N ? k : n, bc = tb == HIPBLAS_OP_N ? n : k;
-  good = good && hipblasLtMatrixLayoutCreate(&p.a, HIP_R_16BF, ar, ac, (int64_t)ar) ==
-                     HIPBLAS_STATUS_SUCCESS;
-  good = good && hipblasLtMatrixLayoutCreate(&p.b, HIP_R_16BF, br, bc, (int64_t)br) ==
-                     HIPBLAS_STATUS_SUCCESS;
-  good = good && hipblasLtMatrixLayoutCreate(&p.d, dt, m, n, m) == HIPBLAS_STATUS_SUCCESS;
-  hipblasLtMatmulPreference_t pref = nullptr;
-  good = good && hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS;
-  uint64_t wmax = ws_max;
-  good = good && hipblasLtMatmulPreferenceSetAttribute(
-                     pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wmax, sizeof(wmax)) ==
-                     HIPBLAS_STATUS_SUCCESS;
-  if (good) {
-    // a long-K product (the weight gradient: K = all voxels) wants a split-K algorithm; the
-    // heuristic's first answer is not always one (measured: 165 us instead of ~25 us), so
-    // take the first candidate that uses workspace when K dwarfs the output
-    hipblasLtMatmulHeuristicResult_t res[8];
-    int nres = 0;
-    good = hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.a, p.b, p.d, p.d, pref, 8, res, &nres) ==
-               HIPBLAS_STATUS_SUCCESS &&
-           nres > 0;
-    int pick = 0;
-    if (good && ws_max > 0 && (int64_t)k > 16 * (int64_t)std::max(m, n))
-      for (int i = 0; i < nres; ++i)
-        if (res[i].workspaceSize > 0 && res[i].workspaceSize <= ws_max) { pick = i; break; }
-    good = good && res[pick].workspaceSize <= ws_max;
-    if (good) {
-      p.algo = res[pick].algo;
-      p.ws = res[pick].workspaceSize;
-    }
-  }
-  if (pref) hipblasLtMatmulPreferenceDestroy(pref);
-  p.ok = good;
-  return cache.emplace(key, p).first->second;
-}
-
-int run(hipblasOperation_t ta, hipblasOperation_t tb, int m, int n, int k, const void* A,
-        const void* B, void* D, hipDataType dt, void* ws, size_t ws_max, void* stream) {
-  const Plan& p = plan_for(ta, tb, m, n, k, dt, ws_max);
-  if (!p.ok) return MMAD_EUNSUPPORTED;
-  const float alpha = 1.f, beta = 0.f;
-  const hipblasStatus_t s = hipblasLtMatmul(handle(), p.op, &alpha, A, p.a, B, p.b, &beta, D,
-                                            p.d, D, p.d, &p.algo, p.ws ? ws : nullptr, p.ws,
-                                            as_stream(stream));
-  return s == HIPBLAS_STATUS_SUCCESS ? launch_status() : MMAD_EUNSUPPORTED;
-}
-
 }  // namespace
 
 namespace mmad_pw {
@@ -122,28 +151,28 @@ namespace mmad_pw {
 bool ok(const mmad_conv_desc* d, int dtype) {
   if (!pw_on() || dtype != MMAD_BF16) return false;
   if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->sd != 1 || d->sh != 1 || d->sw != 1) return false;
-  if (d->pd || d->ph || d->pw || d->ci % 64 || d->co % 64) return false;   // unpadded K
+  if (d->pd || d->ph || d->pw || d->co % KS || (d->ci != 128 && d->ci != 256)) return false;
   if (d->di != d->do_ || d->hi != d->ho || d->wi != d->wo) return false;
   const int64_t m = (int64_t)d->n * d->di * d->hi * d->wi;
-  return m < (int64_t(1) << 31);   // (the hipBLASLt handle is created on the first GEMM)
-}
-
-int64_t wgrad_workspace(const mmad_conv_desc* d) {
-  (void)d;
-  return WGRAD_WS;
+  return m % TM == 0 && m * d->co < (int64_t(1) << 40);
 }
 
 int dgrad(const mmad_conv_desc* d, const void* dy, const void* wpt, void* dx, void* stream) {
-  const int m = d->n * d->di * d->hi * d->wi;
-  return run(HIPBLAS_OP_T, HIPBLAS_OP_N, d->ci, m, d->co, wpt, dy, dx, HIP_R_16BF, nullptr, 0,
-             stream);
-}
-
-int wgrad(const mmad_conv_desc* d, const void* x, const void* dy, float* dw, void* ws,
-          void* stream) {
-  const int m = d->n * d->di * d->hi * d->wi;
-  return run(HIPBLAS_OP_N, HIPBLAS_OP_T, d->ci, d->co, m, x, dy, dw, HIP_R_32F, ws, WGRAD_WS,
-             stream);
+  static const bool attr =
+      hipFuncSetAttribute((const void*)pw_dgrad_kernel<128>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, PC<128>::LDS) == hipSuccess &&
+      hipFuncSetAttribute((const void*)pw_dgrad_kernel<256>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, PC<256>::LDS) == hipSuccess;
+  if (!attr) return MMAD_EUNSUPPORTED;
+  const int64_t m = (int64_t)d->n * d->di * d->hi * d->wi;
+  const dim3 grid((unsigned)(m / TM));
+  if (d->ci == 256)
+    hipLaunchKernelGGL(pw_dgrad_kernel<256>, grid, dim3(NTHR), PC<256>::LDS, as_stream(stream),
+                       d->co, (const u16*)dy, (const u16*)wpt, (u16*)dx);
+  else
+    hipLaunchKernelGGL(pw_dgrad_kernel<128>, grid, dim3(NTHR), PC<128>::LDS, as_stream(stream),
+                       d->co, (const u16*)dy, (const u16*)wpt, (u16*)dx);
+  return launch_status();
 }
 
 }  // namespace mmad_pw

@@ -24,4 +24,10 @@ grep -E "FAILED|ERROR" $OUT/suite.log | head -20
 grep -c "AccumulateGrad" $OUT/*.log
 step bench1 240 python -u bench.py --steps 20 --warmup 5
 step bench0 240 env MMAD_LATTICE_ZP=0 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline
+step benchpw 240 env MMAD_PW_GEMM=0 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline
+step prof 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline
+python3 tools/prof_summary.py stats $OUT/prof 40 > $OUT/stats.txt
+python3 tools/prof_summary.py step $OUT/prof > $OUT/step.txt
+python3 tools/step_breakdown.py $OUT/step.txt > $OUT/breakdown.txt
+cat $OUT/breakdown.txt
 echo session done
