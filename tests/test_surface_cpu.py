@@ -160,3 +160,19 @@ def test_metrics_fallback_f1():
     f(torch.tensor([[0.9, 0.1], [0.2, 0.8], [0.3, 0.7], [0.6, 0.4]]), torch.tensor([0, 1, 0, 0]))
     # class 0: tp=2 fp=0 fn=1 -> 0.8; class 1: tp=1 fp=1 fn=0 -> 0.667
     np.testing.assert_allclose(f.compute().item(), (0.8 + 2 / 3) / 2, rtol=1e-6)
+
+
+def test_logged_values_hold_no_autograd_graph():
+    """self.log / log_dict store detached tensors (as Lightning's result collection does):
+    a logged loss keeping its grad_fn would hold the step's autograd graph -- and every
+    parameter's AccumulateGrad node, bound to the stream it was created on -- into the next
+    step (the cause of the AccumulateGrad stream-mismatch warning and of a graph-capture
+    fault after eager default-stream steps)."""
+    import multimodal_alzheimer_amd as M
+    m = M.Anat_CNN(G.anat_hparams(10))
+    w = torch.nn.Parameter(torch.ones(3))
+    loss = (w * 2).sum()
+    m.log("train_loss", loss)
+    m.log_dict({"val_loss": loss * 1, "f1": 0.5})
+    assert m.logged["train_loss"].grad_fn is None and m.logged["val_loss"].grad_fn is None
+    assert m.logged["f1"] == 0.5
