@@ -54,9 +54,11 @@ int mmad_abi_version(void);                 /* == MMAD_ABI_VERSION */
 #define MMAD_ABI_VERSION 1
 const char* mmad_strerror(int status);
 /* Kernel-variant switch (the run-time twin of the MMAD_* environment A/B switches; no
- * reference counterpart): name "lattice_zp" = 1 plane-pair residue-class conv (default),
- * 0 the one-plane form, 2 plane-pair at any size.  value < 0 only queries.  Returns the
- * previous value, -1 for an unknown name.  Not thread-safe against concurrent launches. */
+ * reference counterpart): "lattice_zp" = 1 plane-pair residue-class conv (default), 0 the
+ * one-plane form, 2 plane-pair at any size; "lattice" / "lattice8" = 1 residue-class convs
+ * where their tiles fill the CUs (default), 2 at any size, 0 off.  value < 0 only queries.
+ * Returns the previous value, -1 for an unknown name.  Not thread-safe against concurrent
+ * launches. */
 int mmad_set_kernel_variant(const char* name, int value);
 
 /* ---- 3D convolution as MFMA implicit GEMM --------------------------------------

@@ -20,6 +20,7 @@
 //    reloaded as soon as the current chunk's last stage on them has run;
 //  * epilogue as the implicit GEMM: bias, BN partial sums (one row per tile), optional
 //    residual + ReLU, bf16 tile transposed through LDS into 16-byte channel stores.
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -51,6 +52,7 @@ struct L8 {
   int nb, Cs, Nd, Kpad, nbn, nchunk;
   const u16* res;
   int relu;
+  int D, H, W, nz;                         // ragged grids: extents, planes per class
 };
 
 __device__ __forceinline__ int swz8(int row) { return 3 * ((row >> 3) & 1); }
@@ -114,7 +116,11 @@ __device__ __forceinline__ void stage8(f32x4 (&acc)[8][TN], const char* bsl, con
 
 // TN = 16-column MFMA tiles per wave: 2 (64-channel tiles) or 1 (32 channels, for layers
 // whose 64-channel tiling leaves CUs idle)
-template <int TN>
+// RAG: ragged grids (any D x H x W with ceil(H / 2), ceil(W / 2) <= 8: the reference's
+// 91 x 109 x 91 MNI volumes give 12 x 14 x 12 at layer3), as latticeconv.hip's RAG form:
+// the positions / planes a class lacks are LDS-DMA'd as zeros (buffer resource, offset past
+// its end) and skipped in the epilogue.
+template <int TN, bool RAG>
 __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __restrict__ src,
                                                             const u16* __restrict__ wgt,
                                                             const float* __restrict__ bias,
@@ -129,7 +135,8 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
   const int nt = tile % g.nbn;
   const int t2 = tile / g.nbn;
-  const int tz = t2 % S8, n = t2 / S8;
+  const int NZ = RAG ? g.nz : S8;
+  const int tz = t2 % NZ, n = t2 / NZ;
   constexpr int BW = 16 * TN * 2;                  // output channels of this tile
   const int n0 = nt * BW;
   constexpr int E = 2 * S8;                          // 16
@@ -142,21 +149,47 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   const int lrow = lane >> 2;
   int64_t pvox[4];
   int pch[4];
+  int rzk[4];                                       // RAG: class z residue, -huge off-grid
+  uint32_t pofs[4];                                 // RAG: byte offset in this sample
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int row = (wave * 4 + k) * 16 + lrow;
     const int pos = row >> 3, c = row & 7;
     const int ty = pos >> 3, tx = pos & 7;
-    pvox[k] = (((int64_t)n * E + (c >> 2)) * E + ((c >> 1) & 1) + 2 * ty) * E + (c & 1) + 2 * tx;
     pch[k] = (lane & 3) ^ swz8(row);
+    if constexpr (RAG) {
+      const int y = ((c >> 1) & 1) + 2 * ty, x = (c & 1) + 2 * tx;
+      pofs[k] = (uint32_t)((((c >> 2) * g.H + y) * g.W + x) * g.Cs + pch[k] * 8) * 2u;
+      rzk[k] = (y < g.H && x < g.W) ? (c >> 2) : -(1 << 20);
+      pvox[k] = 0;
+    } else {
+      pvox[k] = (((int64_t)n * E + (c >> 2)) * E + ((c >> 1) & 1) + 2 * ty) * E + (c & 1) + 2 * tx;
+      pofs[k] = 0;
+      rzk[k] = 0;
+    }
   }
+  const int64_t svox = RAG ? (int64_t)g.D * g.H * g.W : (int64_t)E * E * E;
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(src + (int64_t)n * svox * g.Cs), 0,
+      RAG ? (int)__builtin_amdgcn_readfirstlane((uint32_t)(svox * g.Cs * 2)) : 0, 0x00020000);
   auto issue_plane = [&](int p, int cc) {
-    const int64_t zoff = (int64_t)2 * (tz - 1 + p) * E * E;
     char* pb = smem + p * PLANE8;
+    if constexpr (RAG) {
+      constexpr uint32_t OOB = 0x80000000u;         // >= any per-sample volume (ok())
+      const int zp = 2 * (tz - 1 + p);
+      const uint32_t zoff = (uint32_t)(zp * g.H * g.W * g.Cs + cc * KC8) * 2u;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      glds16_asm(src + (pvox[k] + zoff) * g.Cs + cc * KC8 + pch[k] * 8,
-                 lds_addr_of(pb + (wave * 4 + k) * 1024));
+      for (int k = 0; k < 4; ++k) {
+        const bool ok = rzk[k] >= 0 && rzk[k] + zp >= 0 && rzk[k] + zp < g.D;
+        buf_lds16_asm(ok ? pofs[k] + zoff : OOB, rsx, lds_addr_of(pb + (wave * 4 + k) * 1024));
+      }
+    } else {
+      const int64_t zoff = (int64_t)2 * (tz - 1 + p) * E * E;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        glds16_asm(src + (pvox[k] + zoff) * g.Cs + cc * KC8 + pch[k] * 8,
+                   lds_addr_of(pb + (wave * 4 + k) * 1024));
+    }
   };
   // ---- weight DMA: 3 taps x BW rows x 64 B = 6*TN instructions; wave w issues q = w
   // and q = w + 8 (while < 6*TN); instruction q = tap q / (2TN), rows (q % 2TN) * 16 ..
@@ -179,7 +212,7 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
         glds16_asm(wq[h] + t * g.Cs + cc * KC8, lds_addr_of(ring + sl * BSLOT8 + wslot_off[h]));
   };
 
-  const int kz0 = tz == 0 ? 0 : -1, kz1 = tz == S8 - 1 ? 0 : 1;
+  const int kz0 = tz == 0 ? 0 : -1, kz1 = tz == NZ - 1 ? 0 : 1;
   const int nkz = kz1 - kz0 + 1;
   const int nspc = nkz * 3;
   const int nstage = g.nchunk * nspc;
@@ -270,13 +303,30 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
 
   // ---- epilogue: acc[q][j][e] is tile row (ty*8 + 2*(q&3))*8 + lk*4 + e with
   // ty = 2*wm + (q >> 2), column wn*32 + j*16 + lr
+  // (RAG: -1 for a row outside the grid)
   auto dst_vox = [&](int row) -> int64_t {
     const int pos = row >> 3, c = row & 7;
     const int ty = pos >> 3, tx = pos & 7;
+    if constexpr (RAG) {
+      const int z = (c >> 2) + 2 * tz, y = ((c >> 1) & 1) + 2 * ty, x = (c & 1) + 2 * tx;
+      if (z >= g.D || y >= g.H || x >= g.W) return -1;
+      return (((int64_t)n * g.D + z) * g.H + y) * g.W + x;
+    }
     return (((int64_t)n * E + (c >> 2) + 2 * tz) * E + ((c >> 1) & 1) + 2 * ty) * E + (c & 1) +
            2 * tx;
   };
   u16* ctile = reinterpret_cast<u16*>(smem);
+  // RAG: which of this lane's 32 accumulator rows lie inside the grid (bit q*4 + e)
+  uint32_t vmask = 0xffffffffu;
+  if constexpr (RAG) {
+    vmask = 0;
+#pragma unroll 1
+    for (int b = 0; b < 32; ++b) {
+      const int q = b >> 2, e = b & 3;
+      const int row = ((2 * wm + (q >> 2)) * S8 + 2 * (q & 3)) * NC + lk * 4 + e;
+      if (dst_vox(row) >= 0) vmask |= 1u << b;
+    }
+  }
   float cs[TN], cq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -292,8 +342,10 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
         const int row = (ty * S8 + 2 * (q & 3)) * NC + lk * 4 + e;
         const float v = acc[q][j][e] + bv;
         ctile[row * (CROW8 / 2) + col] = f2bf(v);
-        cs[j] += v;
-        cq[j] += v * v;
+        if ((vmask >> (q * 4 + e)) & 1u) {
+          cs[j] += v;
+          cq[j] += v * v;
+        }
       }
     }
   }
@@ -303,7 +355,9 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   for (int hh = 0; hh < PL8 * CPR / NT8; ++hh) {
     const int qd = tid + NT8 * hh;
     const int row = qd / CPR, c8 = qd % CPR;
-    const int64_t o = dst_vox(row) * g.Nd + n0 + c8 * 8;
+    const int64_t dv = dst_vox(row);
+    if (RAG && dv < 0) continue;
+    const int64_t o = dv * g.Nd + n0 + c8 * 8;
     u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
                                               row * CROW8 + c8 * 16);
     if (g.res != nullptr || g.relu) v = epi_res_relu(v, g.res ? g.res + o : nullptr, g.relu);
@@ -328,7 +382,7 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
     }
     __syncthreads();
     if (wm == 0 && lk == 0) {
-      const int mt = n * S8 + tz;
+      const int mt = n * NZ + tz;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = wn * 16 * TN + j * 16 + lr;
@@ -344,8 +398,17 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   }
 }
 
+// MMAD_LATTICE8: 1 (default) where the tiles fill the CUs, 2 at any size, 0 off;
+// mmad_set_kernel_variant("lattice8", v) overrides it at run time
+std::atomic<int> g_lattice8_mode{-1};
 int lattice8_mode() {
-  static const int v = [] { const char* e = getenv("MMAD_LATTICE8"); return e ? atoi(e) : 1; }();
+  int v = g_lattice8_mode.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("MMAD_LATTICE8");
+    int expect = -1;
+    g_lattice8_mode.compare_exchange_strong(expect, e ? atoi(e) : 1);
+    v = g_lattice8_mode.load(std::memory_order_relaxed);
+  }
   return v;
 }
 
@@ -353,47 +416,74 @@ int lattice8_mode() {
 
 namespace mmad_lattice8 {
 
+int set_mode(int v) {
+  const int prev = lattice8_mode();
+  if (v >= 0) g_lattice8_mode.store(v, std::memory_order_relaxed);
+  return prev;
+}
+
+static bool exact8(const mmad_patch::Geo& q) {
+  constexpr int E = 2 * S8;
+  return q.Ds == E && q.Hs == E && q.Ws == E && q.Dd == E && q.Hd == E && q.Wd == E;
+}
+// ragged grids (MMAD_LATTICE_RAGGED, default on): same extents in and out, at most 8 x 8
+// positions per class plane, one sample's bytes addressable by a 32-bit buffer offset
+static bool ragged8(const mmad_patch::Geo& q) {
+  static const int mode = [] {
+    const char* e = getenv("MMAD_LATTICE_RAGGED");
+    return e ? atoi(e) : 1;
+  }();
+  return mode > 0 && !exact8(q) && q.Ds == q.Dd && q.Hs == q.Hd && q.Ws == q.Wd &&
+         (q.Hs + 1) / 2 <= S8 && (q.Ws + 1) / 2 <= S8 &&
+         (int64_t)q.Ds * q.Hs * q.Ws * q.Cs * 2 < (int64_t(1) << 31);
+}
+static int planes8(const mmad_patch::Geo& q) { return exact8(q) ? S8 : (q.Ds + 1) / 2; }
+
 bool ok(const mmad_patch::Geo& q) {
   if (lattice8_mode() <= 0) return false;
   if (q.KD != 3 || q.KH != 3 || q.KW != 3) return false;
   if (q.dd != 2 || q.dh != 2 || q.dw != 2 || q.pd != 2 || q.ph != 2 || q.pw != 2) return false;
-  constexpr int E = 2 * S8;
-  if (q.Ds != E || q.Hs != E || q.Ws != E || q.Dd != E || q.Hd != E || q.Wd != E) return false;
+  if (!exact8(q) && !ragged8(q)) return false;
   if (q.Cs % KC8 || q.Nd % 32 || q.Kpad != 27 * q.Cs) return false;
   // one 512-thread block per CU: with too few tiles even at 32 channels the row-gather
   // GEMM's more, smaller blocks win
-  if (lattice8_mode() == 1 && (int64_t)q.nb * S8 * (q.Nd / 32) < 256) return false;
-  return (int64_t)q.nb * E * E * E * q.Cs < (int64_t(1) << 40);
+  if (lattice8_mode() == 1 && (int64_t)q.nb * planes8(q) * (q.Nd / 32) < 256) return false;
+  return (int64_t)q.nb * q.Ds * q.Hs * q.Ws * q.Cs < (int64_t(1) << 40);
 }
 
-int64_t tiles(const mmad_patch::Geo& q) { return (int64_t)q.nb * S8; }
+int64_t tiles(const mmad_patch::Geo& q) { return (int64_t)q.nb * planes8(q); }
 
 int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias,
         void* dst, float* stats, void* stream) {
   if (!mmad_lattice8::ok(q)) return MMAD_EUNSUPPORTED;
   static const bool attr =
-      hipFuncSetAttribute((const void*)lattice8_conv_kernel<2>,
+      hipFuncSetAttribute((const void*)lattice8_conv_kernel<2, false>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) == hipSuccess &&
-      hipFuncSetAttribute((const void*)lattice8_conv_kernel<1>,
+      hipFuncSetAttribute((const void*)lattice8_conv_kernel<1, false>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) == hipSuccess &&
+      hipFuncSetAttribute((const void*)lattice8_conv_kernel<2, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) == hipSuccess &&
+      hipFuncSetAttribute((const void*)lattice8_conv_kernel<1, true>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) == hipSuccess;
   if (!attr) return MMAD_EUNSUPPORTED;
+  const bool rag = !exact8(q);
+  const int nz = planes8(q);
   // 64-channel tiles when they give every CU a block, else 32
-  const bool wide = q.Nd % BN8 == 0 && (int64_t)q.nb * S8 * (q.Nd / BN8) >= 256;
+  const bool wide = q.Nd % BN8 == 0 && (int64_t)q.nb * nz * (q.Nd / BN8) >= 256;
   L8 g{};
   g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.Kpad = q.Kpad;
   g.nbn = q.Nd / (wide ? BN8 : 32);
   g.nchunk = q.Cs / KC8;
   g.res = reinterpret_cast<const u16*>(q.res);
   g.relu = q.relu;
-  const int64_t nblk = (int64_t)q.nb * S8 * g.nbn;
-  if (wide)
-    hipLaunchKernelGGL(lattice8_conv_kernel<2>, dim3((unsigned)nblk), dim3(NT8), LDS8,
-                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                       stats);
-  else
-    hipLaunchKernelGGL(lattice8_conv_kernel<1>, dim3((unsigned)nblk), dim3(NT8), LDS8,
-                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                       stats);
+  g.D = q.Ds; g.H = q.Hs; g.W = q.Ws; g.nz = nz;
+  const int64_t nblk = (int64_t)q.nb * nz * g.nbn;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(NT8), LDS8, as_stream(stream), g,
+                       (const u16*)src, (const u16*)wp, bias, (u16*)dst, stats);
+  };
+  if (wide) rag ? go(lattice8_conv_kernel<2, true>) : go(lattice8_conv_kernel<2, false>);
+  else rag ? go(lattice8_conv_kernel<1, true>) : go(lattice8_conv_kernel<1, false>);
   return launch_status();
 }
 

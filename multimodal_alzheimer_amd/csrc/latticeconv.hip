@@ -34,6 +34,7 @@
 //    channel-vector stores; tiles walk the XCDs in contiguous ranges (the 4 channel tiles
 //    and neighbouring planes of one sub group share an L2).
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -74,6 +75,7 @@ struct LG {
   const u16* res;
   int relu;
   int prio;                                         // s_setprio 1 for waves 4-7 (A/B switch)
+  int D, H, W, nz;                                  // ragged grids: extents, planes per class
 };
 
 __device__ __forceinline__ int swz(int row) { return 3 * ((row >> 3) & 1); }
@@ -137,8 +139,14 @@ __device__ __forceinline__ void stage_body(f32x4 (&acc)[8][TN], const char* bsl,
 }
 
 // TN = 16-column MFMA tiles per wave: 4 (128-channel tiles) or 2 (64-channel tiles, for
-// layers whose 128-channel tiling leaves CUs idle)
-template <int TN>
+// layers whose 128-channel tiling leaves CUs idle).
+// RAG: ragged grids (any D x H x W with ceil(H / d), ceil(W / d) <= 4, e.g. the reference's
+// 91 x 109 x 91 MNI volumes, 12 x 14 x 12 at layer4): a class's sub-lattice is then up to
+// 4 x 4 positions per plane and nz planes deep, and the positions / planes it lacks are read
+// as zeros (buffer-resource LDS-DMA past the resource's end, no branch) -- exactly the conv's
+// zero padding -- and skipped in the epilogue (no store, no BN sum).  The tap skipping stays
+// compile-time on the 4 x 4 plane.
+template <int TN, bool RAG>
 __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __restrict__ src,
                                                             const u16* __restrict__ wgt,
                                                             const float* __restrict__ bias,
@@ -153,8 +161,9 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
   const int nt = tile % g.nbn;
   const int t2 = tile / g.nbn;
-  const int tz = t2 % S, gid = t2 / S;
-  const int d = g.d, E = S * d;                     // grid extent per dimension
+  const int NZ = RAG ? g.nz : S;                    // planes per class
+  const int tz = t2 % NZ, gid = t2 / NZ;
+  const int d = g.d, E = S * d;                     // grid extent per dimension (4d grids)
   const int gpn = d * d * d / NS;                   // sub groups per sample
   const int n = gid / gpn, q0 = (gid % gpn) * NS;   // sample, first class of the group
   constexpr int BW = 32 * TN;                      // output channels of this tile
@@ -166,24 +175,48 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   // (per-lane DMA offsets in 32 bits from uniform bases: this sample's volume and the
   // packed weights, both < 2^31 elements -- checked in ok(); fewer VGPRs than pointers)
   const int lrow = lane >> 2;
-  const u16* __restrict__ srcn = src + (int64_t)n * E * E * E * g.Cs;
+  const int64_t svox = RAG ? (int64_t)g.D * g.H * g.W : (int64_t)E * E * E;
+  const u16* __restrict__ srcn = src + (int64_t)n * svox * g.Cs;
   uint32_t pofs[4];
-#pragma unroll
+  int rzk[4];                                       // RAG: the row's class z residue, or
+#pragma unroll                                      // -huge when its (y, x) is outside
   for (int k = 0; k < 4; ++k) {
     const int row = (wave * 4 + k) * 16 + lrow;
     const int pos = row / NS, s = row % NS;
     const int q = q0 + s;
     const int rz = q / (d * d), ry = (q / d) % d, rx = q % d;
     const int ty = pos / S, tx = pos % S;
-    const int vox = (rz * E + ry + d * ty) * E + rx + d * tx;
-    pofs[k] = (uint32_t)(vox * g.Cs + ((lane & 3) ^ swz(row)) * 8);
+    if constexpr (RAG) {                            // byte offsets for the buffer DMA
+      const int y = ry + d * ty, x = rx + d * tx;
+      const int vox = (rz * g.H + y) * g.W + x;
+      pofs[k] = (uint32_t)(vox * g.Cs + ((lane & 3) ^ swz(row)) * 8) * 2u;
+      rzk[k] = (y < g.H && x < g.W) ? rz : -(1 << 20);
+    } else {
+      const int vox = (rz * E + ry + d * ty) * E + rx + d * tx;
+      pofs[k] = (uint32_t)(vox * g.Cs + ((lane & 3) ^ swz(row)) * 8);
+      rzk[k] = 0;
+    }
   }
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)srcn, 0, RAG ? (int)__builtin_amdgcn_readfirstlane((uint32_t)(svox * g.Cs * 2)) : 0,
+      0x00020000);
   auto issue_plane = [&](int kz, int cc, int slot) {
-    const u16* base = srcn + (int64_t)(tz + kz) * plane_vox * g.Cs + cc * KC;
     char* pb = smem + slot * PLANE;
+    if constexpr (RAG) {
+      constexpr uint32_t OOB = 0x80000000u;         // >= any per-sample volume (ok())
+      const int zp = d * (tz + kz);                 // plane's z offset from the class residue
+      const uint32_t zoff = (uint32_t)(zp * g.H * g.W * g.Cs + cc * KC) * 2u;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      glds16_asm(base + pofs[k], lds_addr_of(pb + (wave * 4 + k) * 1024));
+      for (int k = 0; k < 4; ++k) {
+        const bool ok = rzk[k] >= 0 && rzk[k] + zp < g.D;
+        buf_lds16_asm(ok ? pofs[k] + zoff : OOB, rsx, lds_addr_of(pb + (wave * 4 + k) * 1024));
+      }
+    } else {
+      const u16* base = srcn + (int64_t)(tz + kz) * plane_vox * g.Cs + cc * KC;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        glds16_asm(base + pofs[k], lds_addr_of(pb + (wave * 4 + k) * 1024));
+    }
   };
   // ---- weight DMA: stage (chunk cc, first tap t) into ring slot sl: 3 consecutive taps
   // (one kx row), 16 rows per wave per tap
@@ -210,7 +243,7 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
 
   // stage list: chunk-major, then the valid kz planes, then ky; a stage runs kx = -1, 0, 1.
   // Group u = (chunk, kz) of 3 stages reads plane slot u % 2.
-  const int kz0 = tz == 0 ? 0 : -1, kz1 = tz == S - 1 ? 0 : 1;
+  const int kz0 = tz == 0 ? 0 : -1, kz1 = tz == NZ - 1 ? 0 : 1;
   const int nkz = kz1 - kz0 + 1;
   const int ngrp = g.nchunk * nkz;                  // (chunk, kz) groups
   const int nstage = ngrp * 3;
@@ -293,14 +326,32 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
 
   // ---- epilogue: tile row r = pos * NS + sub; acc[i*2+h][j][e] is row
   // (pos_i * NS + h*16 + lk*4 + e), column wn*64 + j*16 + lr
+  // (RAG: -1 for a row outside the grid)
   auto dst_vox = [&](int row) -> int64_t {
     const int pos = row / NS, s = row % NS;
     const int q = q0 + s;
     const int rz = q / (d * d), ry = (q / d) % d, rx = q % d;
     const int ty = pos / S, tx = pos % S;
+    if constexpr (RAG) {
+      const int z = rz + d * tz, y = ry + d * ty, x = rx + d * tx;
+      if (z >= g.D || y >= g.H || x >= g.W) return -1;
+      return (((int64_t)n * g.D + z) * g.H + y) * g.W + x;
+    }
     return (((int64_t)n * E + rz + d * tz) * E + ry + d * ty) * E + rx + d * tx;
   };
   u16* ctile = reinterpret_cast<u16*>(smem);
+  // RAG: which of this lane's 32 accumulator rows lie inside the grid (bit i*8 + h*4 + e),
+  // computed once in a rolled loop (unrolled, the row tests were hoisted into ~100 VGPRs)
+  uint32_t vmask = 0xffffffffu;
+  if constexpr (RAG) {
+    vmask = 0;
+#pragma unroll 1
+    for (int b = 0; b < 32; ++b) {
+      const int i = b >> 3, h = (b >> 2) & 1, e = b & 3;
+      const int row = (i * S + ((i + wm) & 3)) * NS + h * 16 + lk * 4 + e;
+      if (dst_vox(row) >= 0) vmask |= 1u << b;
+    }
+  }
   float cs[TN], cq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -318,8 +369,10 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
           const int row = pos * NS + h * 16 + lk * 4 + e;
           const float v = acc[i * 2 + h][j][e] + bv;
           ctile[row * (CROW / 2) + col] = f2bf(v);
-          cs[j] += v;
-          cq[j] += v * v;
+          if ((vmask >> (i * 8 + h * 4 + e)) & 1u) {
+            cs[j] += v;
+            cq[j] += v * v;
+          }
         }
     }
   }
@@ -329,7 +382,9 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
   for (int hh = 0; hh < PL * CPR / NTHR; ++hh) {
     const int qd = tid + NTHR * hh;
     const int row = qd / CPR, c8 = qd % CPR;
-    const int64_t o = dst_vox(row) * g.Nd + n0 + c8 * 8;
+    const int64_t dv = dst_vox(row);
+    if (RAG && dv < 0) continue;
+    const int64_t o = dv * g.Nd + n0 + c8 * 8;
     u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) + row * CROW +
                                               c8 * 16);
     if (g.res != nullptr || g.relu) v = epi_res_relu(v, g.res ? g.res + o : nullptr, g.relu);
@@ -354,7 +409,7 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
     }
     __syncthreads();
     if (wm == 0 && lk == 0) {
-      const int mt = gid * S + tz;
+      const int mt = gid * NZ + tz;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = wn * 16 * TN + j * 16 + lr;
@@ -668,8 +723,17 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
   }
 }
 
+// MMAD_LATTICE: 1 (default) where the tiles fill the CUs, 2 at any size, 0 off;
+// mmad_set_kernel_variant("lattice", v) overrides it at run time
+std::atomic<int> g_lattice_mode{-1};
 int lattice_mode() {
-  static const int v = [] { const char* e = getenv("MMAD_LATTICE"); return e ? atoi(e) : 1; }();
+  int v = g_lattice_mode.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("MMAD_LATTICE");
+    int expect = -1;
+    g_lattice_mode.compare_exchange_strong(expect, e ? atoi(e) : 1);
+    v = g_lattice_mode.load(std::memory_order_relaxed);
+  }
   return v;
 }
 
@@ -679,13 +743,42 @@ namespace mmad_lattice {
 
 int64_t tiles(const mmad_patch::Geo& q);
 
+int set_mode(int v) {
+  const int prev = lattice_mode();
+  if (v >= 0) g_lattice_mode.store(v, std::memory_order_relaxed);
+  return prev;
+}
+
+// a 4d^3 grid (every class a full 4^3 sub-lattice) or, with MMAD_LATTICE_RAGGED (default
+// on), a ragged one: same extents in and out, up to 4 x 4 positions per class plane
+static bool exact(const mmad_patch::Geo& q) {
+  const int E = S * q.dd;
+  return q.Ds == E && q.Hs == E && q.Ws == E && q.Dd == E && q.Hd == E && q.Wd == E;
+}
+static int ragged_mode() {
+  static const int v = [] {
+    const char* e = getenv("MMAD_LATTICE_RAGGED");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+static bool ragged(const mmad_patch::Geo& q) {
+  const int d = q.dd;
+  return !exact(q) && q.Ds == q.Dd && q.Hs == q.Hd && q.Ws == q.Wd &&
+         (q.Hs + d - 1) / d <= S && (q.Ws + d - 1) / d <= S &&
+         (int64_t)q.Ds * q.Hs * q.Ws * q.Cs * 2 < (int64_t(1) << 31);
+}
+static int planes(const mmad_patch::Geo& q) {
+  return exact(q) ? S : (q.Ds + q.dd - 1) / q.dd;
+}
+
 bool ok(const mmad_patch::Geo& q) {
   if (lattice_mode() <= 0) return false;
   const int d = q.dd;
   if (q.KD != 3 || q.KH != 3 || q.KW != 3 || q.dh != d || q.dw != d || d < 2) return false;
   if (q.pd != d || q.ph != d || q.pw != d) return false;
   const int E = S * d;
-  if (q.Ds != E || q.Hs != E || q.Ws != E || q.Dd != E || q.Hd != E || q.Wd != E) return false;
+  if (!exact(q) && !(ragged_mode() > 0 && ragged(q))) return false;
   if ((d * d * d) % NS) return false;
   if (q.Cs % KC || q.Nd % 64 || q.Kpad != 27 * q.Cs) return false;
   // 32-bit per-lane DMA offsets (lattice_conv_kernel): one sample's volume, the packed weights
@@ -699,8 +792,8 @@ bool ok(const mmad_patch::Geo& q) {
 }
 
 int64_t tiles(const mmad_patch::Geo& q) {
-  if (mmad_lattice_zp::ok(q)) return mmad_lattice_zp::tiles(q);
-  return (int64_t)q.nb * q.dd * q.dd * q.dd / NS * S;
+  if (exact(q) && mmad_lattice_zp::ok(q)) return mmad_lattice_zp::tiles(q);
+  return (int64_t)q.nb * q.dd * q.dd * q.dd / NS * planes(q);
 }
 
 
@@ -762,11 +855,17 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
 int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias,
         void* dst, float* stats, void* stream) {
   if (!mmad_lattice::ok(q)) return MMAD_EUNSUPPORTED;
-  if (mmad_lattice_zp::ok(q)) return mmad_lattice_zp::fwd(q, src, wp, bias, dst, stats, stream);
+  const bool rag = !exact(q);
+  if (!rag && mmad_lattice_zp::ok(q))
+    return mmad_lattice_zp::fwd(q, src, wp, bias, dst, stats, stream);
   static const bool attr =
-      hipFuncSetAttribute((const void*)lattice_conv_kernel<4>,
+      hipFuncSetAttribute((const void*)lattice_conv_kernel<4, false>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
-      hipFuncSetAttribute((const void*)lattice_conv_kernel<2>,
+      hipFuncSetAttribute((const void*)lattice_conv_kernel<2, false>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
+      hipFuncSetAttribute((const void*)lattice_conv_kernel<4, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
+      hipFuncSetAttribute((const void*)lattice_conv_kernel<2, true>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   if (!attr) return MMAD_EUNSUPPORTED;
   // 128-channel tiles (4 MFMA columns per wave) when they give every CU a block, else 64
@@ -783,15 +882,15 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
     return e ? atoi(e) : 0;
   }();
   g.prio = prio;
-  const int64_t nblk = (int64_t)g.ngroups * S * g.nbn;
-  if (wide)
-    hipLaunchKernelGGL(lattice_conv_kernel<4>, dim3((unsigned)nblk), dim3(NTHR), LDS_BYTES,
-                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                       stats);
-  else
-    hipLaunchKernelGGL(lattice_conv_kernel<2>, dim3((unsigned)nblk), dim3(NTHR), LDS_BYTES,
-                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                       stats);
+  g.D = q.Ds; g.H = q.Hs; g.W = q.Ws;
+  g.nz = planes(q);
+  const int64_t nblk = (int64_t)g.ngroups * g.nz * g.nbn;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(NTHR), LDS_BYTES, as_stream(stream), g,
+                       (const u16*)src, (const u16*)wp, bias, (u16*)dst, stats);
+  };
+  if (wide) rag ? go(lattice_conv_kernel<4, true>) : go(lattice_conv_kernel<4, false>);
+  else rag ? go(lattice_conv_kernel<2, true>) : go(lattice_conv_kernel<2, false>);
   return launch_status();
 }
 

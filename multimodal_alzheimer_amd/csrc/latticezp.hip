@@ -425,6 +425,8 @@ namespace mmad_lattice_zp {
 // (16^3 grids, 64 classes per sample) and enough tiles to give every CU one
 bool ok(const mmad_patch::Geo& q) {
   if (zp_mode() <= 0 || q.dd != 4 || q.Cs % KC || q.Nd % 64) return false;
+  if (q.Ds != 16 || q.Hs != 16 || q.Ws != 16 || q.Dd != 16 || q.Hd != 16 || q.Wd != 16)
+    return false;                                   // 16^3 grids only (full 4^3 sub-lattices)
   if (q.Cs / KC < 2) return false;
   return (int64_t)q.nb * 8 * (q.Nd / 64) >= 256 || zp_mode() == 2;
 }
@@ -465,10 +467,13 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
 }  // namespace mmad_lattice_zp
 
 extern "C" int mmad_set_kernel_variant(const char* name, int value) {
-  if (name != nullptr && std::strcmp(name, "lattice_zp") == 0) {
+  if (name == nullptr) return -1;
+  if (std::strcmp(name, "lattice_zp") == 0) {
     const int prev = zp_mode();
     if (value >= 0) g_zp_mode.store(value, std::memory_order_relaxed);
     return prev;
   }
+  if (std::strcmp(name, "lattice") == 0) return mmad_lattice::set_mode(value);
+  if (std::strcmp(name, "lattice8") == 0) return mmad_lattice8::set_mode(value);
   return -1;
 }

@@ -26,6 +26,7 @@ int fwd(const Geo& g, const void* src, const void* wp, const float* bias, void* 
 // Residue-class conv for dilated 3^3 convs on a 4d^3 grid (latticeconv.hip): same geometry
 // record, packed weights and partial-sum layout as the patch kernel.
 namespace mmad_lattice {
+int set_mode(int v);              // MMAD_LATTICE at run time; returns the previous mode
 bool ok(const mmad_patch::Geo& g);
 int64_t tiles(const mmad_patch::Geo& g);
 int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,
@@ -49,6 +50,7 @@ int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* 
 
 // Residue-class conv for dilation-2 3^3 convs on a 16^3 grid (lattice8.hip, layer3).
 namespace mmad_lattice8 {
+int set_mode(int v);              // MMAD_LATTICE8 at run time; returns the previous mode
 bool ok(const mmad_patch::Geo& g);
 int64_t tiles(const mmad_patch::Geo& g);
 int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,
