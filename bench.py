@@ -159,7 +159,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8)
-    ap.add_argument("--size", type=int, default=128)
+    ap.add_argument("--size", default="128",
+                    help="cubic volume edge, or 'mni' for the reference's own 91x109x91 MNI "
+                         "volumes (pkg/utils/dataloader.py:228-229; secondary line)")
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -174,6 +176,11 @@ def main():
                          "ResNet-10 x2 + MLP head, focal loss, pairs/sec; three: config 5, "
                          "MRI ResNet-34 + PET ResNet-18 + tabular MLP at 160^3, triples/sec")
     args = ap.parse_args()
+    mni = args.size == "mni"
+    args.size = 128 if mni else int(args.size)
+    if mni:
+        args.no_roofline = True           # the probe times the 128^3 dominant kernel
+        args.no_cpu_baseline = True
     if args.workload != "mri":
         args.no_roofline = True         # the probe times config 2's dominant kernel
         args.no_cpu_baseline = True
@@ -212,11 +219,12 @@ def main():
         reducer = GradAllReduce(model.parameters(),
                                 bucket_mb=float(os.environ.get("MMAD_DP_BUCKET_MB", "4")))
     B, S = args.batch, args.size
+    VOL = (91, 109, 91) if mni else (S, S, S)
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)   # this rank's shard
-    batch = {"mri": torch.rand((B, S, S, S), device="cuda", dtype=torch.float64, generator=g),
+    batch = {"mri": torch.rand((B,) + VOL, device="cuda", dtype=torch.float64, generator=g),
              "label": torch.randint(0, 2, (B,), device="cuda", generator=g)}
     if args.workload != "mri":            # z-scored PET (dataloader.py:213-215)
-        batch["pet1451"] = torch.randn((B, S, S, S), device="cuda", dtype=torch.float64,
+        batch["pet1451"] = torch.randn((B,) + VOL, device="cuda", dtype=torch.float64,
                                        generator=g)
     if args.workload == "three":          # 9 tabular features (dataloader.py:306)
         batch["tabular"] = torch.rand((B, 9), device="cuda", dtype=torch.float64, generator=g)
@@ -298,7 +306,7 @@ def main():
         "data": "synthetic uniform[0,1) f64 volumes resident in HBM, random-init weights",
         "config": {"workload": f"BASELINE config 2: Anat_CNN ResNet-10 MRI-only, 1x{S}^3, "
                                f"batch {B}/GPU, weighted CE, Adam, fwd+bwd+step",
-                   "global_batch": B * world, "volume": [1, S, S, S],
+                   "global_batch": B * world, "volume": [1, *VOL],
                    "parallelism": f"dp{world}"},
     }
     if args.workload != "mri":
@@ -311,9 +319,15 @@ def main():
             "unit": unit,
             "config": {"workload": f"{desc}, 2x1x{S}^3 (+9 tabular), batch {B}/GPU, focal "
                                    f"loss gamma 2, Adam, fwd+bwd+step",
-                       "global_batch": B * world, "volume": [1, S, S, S],
+                       "global_batch": B * world, "volume": [1, *VOL],
                        "parallelism": f"dp{world}"}})
-    elif S in FLOP_PER_VOL:
+    if mni:
+        result.update({
+            "metric": "volumes/sec fwd+bwd, 3D-ResNet-10 @91x109x91 (MNI) bf16 (secondary line)",
+            "config": dict(result["config"], workload=(
+                f"Anat_CNN ResNet-10 MRI-only on the reference's MNI volumes 1x91x109x91, "
+                f"batch {B}/GPU, weighted CE, Adam, fwd+bwd+step"))})
+    elif S in FLOP_PER_VOL and args.workload == "mri":
         per_gpu = value / world
         result["step_mfma_frac"] = per_gpu * FLOP_PER_VOL[S] / (
             PEAK_BF16 if cdtype == torch.bfloat16 else PEAK_F32)

@@ -51,8 +51,11 @@ def test_plane_pair_equals_one_plane(ci, co):
     assert torch.equal(got[0], ref[0]), "forward differs"
     assert torch.equal(got[2], ref[2]), "input gradient differs"
     assert torch.equal(got[3], ref[3]), "weight gradient differs"
-    tol = 1e-5 * ref[1].abs() + 1e-6
-    assert ((got[1] - ref[1]).abs() <= tol).all(), "BN partial-sum totals differ"
+    # the totals of the partial sums, grouped into different tile rows: equal to fp32
+    # rounding of the summed magnitudes (the per-channel sum itself may cancel to ~0)
+    y = ref[0].float()
+    mag = torch.stack((y.abs().sum(dim=(0, 2, 3, 4)), (y * y).sum(dim=(0, 2, 3, 4))))
+    assert ((got[1] - ref[1]).abs() <= 1e-5 * mag + 1e-6).all(), "BN partial-sum totals differ"
 
 
 def test_plane_pair_eval_epilogue_residual_relu():
