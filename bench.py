@@ -80,7 +80,7 @@ def dominant_kernel_roofline(events, batch, size, dtype, where="timed region"):
     # dense count runs on the MFMA pipes (achieved / frac use the dense count, as cuDNN /
     # MIOpen report conv FLOPs)
     executed = flops * (10 / 12) ** 3 if s == 16 else flops
-    return {"kernel": f"lattice_conv_kernel layer4.0.conv2 fwd (512->512, 3^3 dil 4, "
+    return {"kernel": f"lattice_zp_kernel layer4.0.conv2 fwd (512->512, 3^3 dil 4, "
                       f"{batch}x{s}^3)",
             "bound": "mfma", "achieved": flops / sec / 1e12, "peak": peak / 1e12,
             "unit": "TFLOP/s", "frac": flops / sec / peak, "traffic": traffic,

@@ -85,7 +85,8 @@ def dispatches(d, name):
 def counter(d, name):
     rows = list(csv.DictReader(open(f"{d}/run_counter_collection.csv")))
     vals = [float(r["Counter_Value"]) for r in rows
-            if ("igemm_kernel" in r["Kernel_Name"] or "lattice_conv_kernel" in r["Kernel_Name"])
+            if any(k in r["Kernel_Name"] for k in ("igemm_kernel", "lattice_conv_kernel",
+                                                   "lattice_zp_kernel"))
             and r["Counter_Name"] == name]
     return vals
 
@@ -96,7 +97,7 @@ def traffic(fetch_dir, write_dir):
     # rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB
     fb = statistics.median(f) * 1024 * 2
     wb = statistics.median(w) * 1024
-    return {"kernel": "lattice_conv_kernel layer4.0.conv2 fwd (bf16, 8x512x16^3, 3^3 dil 4)",
+    return {"kernel": "layer4.0.conv2 fwd residue-class kernel (bf16, 8x512x16^3, 3^3 dil 4)",
             "launches": [len(f), len(w)],
             "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
             "hbm_bytes_per_launch": fb + wb,
