@@ -138,15 +138,26 @@ __device__ __forceinline__ void mma_a(f32x4 (&acc)[NF][TN], const bf16x8 (&a)[NF
 // for the next tap right after the current tap's MFMAs have read it, so one set of A
 // fragments and two sets of B fragments are live, and each refill has the other fragments'
 // MFMAs (and the partner wave) to land behind.
-template <int TN, int WM, int P, int KZ, int KY>
+// `dma` (the stage's LDS-DMA issues) runs after the first tap's fragment reads are issued:
+// the ~60-cycle issue of each DMA then overlaps those reads' latency instead of delaying
+// them behind the barrier.  ZP_EARLY_READS: 1 (default) for the 64-channel form only -- the
+// 128-channel form has no registers to spare for it (256 VGPRs and spills inside the main
+// loop); 2 both forms; 0 neither (barrier -> DMA -> reads).
+#ifndef ZP_EARLY_READS
+#define ZP_EARLY_READS 1
+#endif
+template <int TN, int WM, int P, int KZ, int KY, typename DMA>
 __device__ __forceinline__ void stage_body(f32x4 (&acc)[NF][TN], const char* bsl,
-                                           const char* const (&pl)[3]) {
+                                           const char* const (&pl)[3], DMA&& dma) {
+  constexpr bool EARLY = ZP_EARLY_READS == 2 || (ZP_EARLY_READS == 1 && TN == 2);
   bf16x8 a[NF], b0[TN], b1[TN];
+  if constexpr (!EARLY) dma();
   read_b<TN, -1>(bsl, b0);
   [&]<int... F>(std::integer_sequence<int, F...>) {
     (read_a<WM, P, KZ, KY, -1, F>(pl, a), ...);
   }(std::make_integer_sequence<int, NF>{});
   read_b<TN, 0>(bsl, b1);
+  if constexpr (EARLY) dma();
   [&]<int... F>(std::integer_sequence<int, F...>) {
     ((mma_a<TN, WM, P, KZ, KY, -1, F>(acc, a, b0), read_a<WM, P, KZ, KY, 0, F>(pl, a)), ...);
   }(std::make_integer_sequence<int, NF>{});
@@ -284,22 +295,24 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
           wait_vm_lgkm0<C::WI + PI * PYL>();
         }
         raw_barrier();
-        if constexpr (P == 0) {
-          if constexpr (R == 0) {
-            issue_plane(c, 2);
-            if (more) issue_plane(c + 1, 0);
-          } else if constexpr (R == 6) {
-            if (more) issue_plane(c + 1, 1);
+        auto dma = [&]() {
+          if constexpr (P == 0) {
+            if constexpr (R == 0) {
+              issue_plane(c, 2);
+              if (more) issue_plane(c + 1, 0);
+            } else if constexpr (R == 6) {
+              if (more) issue_plane(c + 1, 1);
+            }
+          } else {
+            if constexpr (R == 0 || R == 3 || R == 6) {
+              if (more) issue_plane(c + 1, R / 3);
+            }
           }
-        } else {
-          if constexpr (R == 0 || R == 3 || R == 6) {
-            if (more) issue_plane(c + 1, R / 3);
-          }
-        }
-        if (s + 2 < nstage) issue_stage_b(s + 2);
+          if (s + 2 < nstage) issue_stage_b(s + 2);
+        };
         int boff = C::RING_OFF + (s % NSTL) * C::BSLOT;
         asm volatile("" : "+s"(boff));              // per-stage base stays opaque (no early
-        stage_body<TN, WM, P, KZ, KY>(acc, smem + boff + b_lane, pl);   // address hoisting)
+        stage_body<TN, WM, P, KZ, KY>(acc, smem + boff + b_lane, pl, dma);   // hoisting)
       };
       stage(std::integral_constant<int, 0>{});
       stage(std::integral_constant<int, 1>{});
