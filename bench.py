@@ -10,8 +10,10 @@ all-reduce (N>1) + Adam; all parameters trainable (lr_pretrained set).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
-At N=1 (config 2) the step is captured once as a HIP graph and replayed (``--eager``
-launches it from Python every step, as the N>1 path does).  Rank 0 prints one JSON line.
+The step is captured once as a HIP graph and replayed (``--eager`` launches it from Python
+every step); under torchrun the graph holds forward + backward, the bucketed RCCL
+all-reduces run eagerly after each replay, then the captured Adam (``--graph`` captures the
+all-reduces too).  Rank 0 prints one JSON line.
 ``roofline`` times the dominant kernel (layer4.0.conv2 forward, the lattice conv) with HIP
 events recorded around each of its launches, on the stream it runs on -- inside the timed
 region when eager, over eager steps just before the capture when graph-replayed;
@@ -166,11 +168,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", action="store_true",
-                    help="replay the step as one captured HIP graph (graph_step.GraphedTrainStep;"
-                         " the default at N=1 on the config-2 workload; under torchrun it "
-                         "captures the RCCL bucket all-reduces too -- opt-in, one-rank checked)")
+                    help="under torchrun: capture the RCCL bucket all-reduces inside the step's "
+                         "graph too (opt-in, one-rank checked); the default graph-replays "
+                         "forward + backward and runs the all-reduces eagerly after it")
     ap.add_argument("--eager", action="store_true",
-                    help="launch every kernel of every step from Python (the N>1 path)")
+                    help="launch every kernel of every step from Python, the all-reduces from "
+                         "the backward's hooks (overlapped with it)")
     ap.add_argument("--workload", default="mri", choices=["mri", "fusion", "three"],
                     help="mri: BASELINE config 2 (the metric); fusion: config 3/4, PET+MRI "
                          "ResNet-10 x2 + MLP head, focal loss, pairs/sec; three: config 5, "
@@ -246,12 +249,17 @@ def main():
                 dp_events.append((e0, e1))
         opt.step()
 
-    # N=1: the whole step (general_step, backward, Adam) is captured once as a HIP graph and
-    # replayed -- the same kernels, bit-identical to eager steps (tests/test_graph_step_gpu.py);
-    # eager, the host needs ~2.9 of the GPU's ~3.5 ms per step to enqueue it, so a slower or
-    # busier host makes the run launch-bound (measured: 1713 vol/s on one box).  N>1 runs
-    # eager: the RCCL all-reduce is launched from autograd hooks.
-    use_graph = args.graph or (not dp and args.workload == "mri" and not args.eager)
+    # The step (general_step, backward, Adam) is captured once as a HIP graph and replayed --
+    # the same kernels, bit-identical to eager steps (tests/test_graph_step_gpu.py); eager,
+    # the host needs ~2.9 of the GPU's ~3.5 ms per step to enqueue it, so a slower or busier
+    # host makes the run launch-bound (measured: 1713 vol/s on one box).  N>1 uses the same
+    # launch mode, so the 1 -> N curve compares like with like: forward + backward replayed
+    # from the graph, then the bucketed RCCL all-reduces issued eagerly (not overlapped with
+    # the backward: ~57 MB of fp32 gradients per step for ResNet-10), then the captured Adam.
+    # --graph captures the all-reduces inside the graph (overlapped; one-rank checked only),
+    # --eager launches them from the backward's hooks (overlapped; host-bound).
+    use_graph = not args.eager and (args.graph or args.workload == "mri")
+    collectives = "inside" if args.graph else "after"
     events = []
     if use_graph:
         if not args.no_roofline:
@@ -267,12 +275,12 @@ def main():
                 step()
             torch.cuda.synchronize()
             volume_ops.FWD_PROBES.clear()
-        # with the RCCL path (explicit --graph only) the bucket all-reduces are captured too
         gstep = GraphedTrainStep(model, opt, batch, warmup=max(1, args.warmup),
-                                 reducer=reducer)
+                                 reducer=reducer, collectives=collectives)
         gstep()
 
         def step(timed=False):
+            gstep.finish_events = dp_events if timed and reducer is not None else None
             gstep()
     else:
         for _ in range(args.warmup):
@@ -332,7 +340,10 @@ def main():
         result["step_mfma_frac"] = per_gpu * FLOP_PER_VOL[S] / (
             PEAK_BF16 if cdtype == torch.bfloat16 else PEAK_F32)
         result["hbm_roofline_frac_m2"] = per_gpu * M2_BYTES_PER_VOL / PEAK_HBM
-    result["config"]["step_launch"] = "hip graph replay" if use_graph else "eager"
+    result["config"]["step_launch"] = (
+        "eager" if not use_graph else "hip graph replay" if reducer is None else
+        "hip graph replay (fwd+bwd) + eager RCCL all-reduce + graph-replayed Adam"
+        if collectives == "after" else "hip graph replay incl. RCCL all-reduce")
     # host time spent enqueueing each step: close to ms_per_step means the run was bound by
     # the host (Python / launch overhead), not by the GPU
     result["host_issue_ms_per_step"] = t_issue / args.steps * 1e3

@@ -111,6 +111,10 @@ class GradAllReduce:
                     p._mmad_grad_view = self._views[p]
             self.flats.append(flat)
         self._hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
+        # defer: the hooks only count; finish() launches every bucket.  Set while a step's
+        # forward + backward is captured without its collectives (graph_step
+        # collectives="after"): a replay runs no Python hooks, so finish() does it all.
+        self.defer = False
         self.reset()
 
     def reset(self):
@@ -120,7 +124,7 @@ class GradAllReduce:
     def _ready(self, p):
         bi = self._owner[p]
         self._pending[bi] -= 1
-        if self._pending[bi] == 0:
+        if self._pending[bi] == 0 and not self.defer:
             self._launch(bi)
 
     def _foreign(self, bi):

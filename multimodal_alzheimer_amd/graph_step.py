@@ -32,12 +32,22 @@ from . import volume_ops
 
 
 class GraphedTrainStep:
-    def __init__(self, model, optimizer, batch, warmup=3, reducer=None):
-        """``reducer``: a data_parallel.GradAllReduce whose bucket all-reduces (launched from
-        the backward's hooks) and ``finish()`` are captured with the step (experimental:
-        bench.py --graph under torchrun; checked at one rank only)."""
+    def __init__(self, model, optimizer, batch, warmup=3, reducer=None, collectives="inside"):
+        """``reducer``: a data_parallel.GradAllReduce.  ``collectives``:
+        * "inside": its bucket all-reduces (launched from the backward's hooks) and
+          ``finish()`` are captured with the step (experimental: bench.py --graph under
+          torchrun; checked at one rank only);
+        * "after": the graph holds forward + backward only (gradients land in the bucket
+          slices); each call replays it, then runs ``finish()`` eagerly -- every bucket's
+          RCCL all-reduce on the side stream, not overlapped with the backward -- then
+          replays the captured optimizer step.  No collective inside a graph; the host
+          issues a handful of calls per step (bench.py's default at N > 1)."""
         self.model, self.optimizer = model, optimizer
         self.reducer = reducer
+        self.after = reducer is not None and collectives == "after"
+        self.finish_events = None            # list: (start, end) events around each finish()
+        if reducer is not None and collectives not in ("inside", "after"):
+            raise ValueError(f"collectives must be 'inside' or 'after', not {collectives!r}")
         self.static = {k: v.clone() if torch.is_tensor(v) else v for k, v in batch.items()}
         dev = next(model.parameters()).device
         for g in optimizer.param_groups:
@@ -52,12 +62,27 @@ class GraphedTrainStep:
         torch.cuda.current_stream().wait_stream(side)
         optimizer.zero_grad(set_to_none=True)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out = model.general_step(self.static, 0, "train")
-            self.out["loss"].backward()
-            if reducer is not None:
-                reducer.finish()
-            optimizer.step()
+        self.opt_graph = None
+        if self.after:
+            reducer.defer = True
+            try:
+                with torch.cuda.graph(self.graph):
+                    self.out = model.general_step(self.static, 0, "train")
+                    self.out["loss"].backward()
+            finally:
+                reducer.defer = False
+            reducer.reset()                  # the capture's hooks only counted
+            reducer.finish()                 # eager: gradients now averaged in place
+            self.opt_graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.opt_graph, pool=self.graph.pool()):
+                optimizer.step()
+        else:
+            with torch.cuda.graph(self.graph):
+                self.out = model.general_step(self.static, 0, "train")
+                self.out["loss"].backward()
+                if reducer is not None:
+                    reducer.finish()
+                optimizer.step()
         # keep the graph-owned output buffers, not their autograd graph: a live grad_fn chain
         # would keep every parameter's AccumulateGrad node (created on the capture stream)
         # alive, and later eager steps would reuse those nodes across streams
@@ -65,9 +90,15 @@ class GraphedTrainStep:
 
     def _eager(self):
         self.optimizer.zero_grad(set_to_none=True)
-        self.model.general_step(self.static, 0, "train")["loss"].backward()
         if self.reducer is not None:
-            self.reducer.finish()
+            self.reducer.defer = self.after
+        try:
+            self.model.general_step(self.static, 0, "train")["loss"].backward()
+            if self.reducer is not None:
+                self.reducer.finish()
+        finally:
+            if self.reducer is not None:
+                self.reducer.defer = False
         self.optimizer.step()
 
     def __call__(self, batch=None):
@@ -79,5 +110,15 @@ class GraphedTrainStep:
                 if torch.is_tensor(v):
                     self.static[k].copy_(v, non_blocking=True)
         self.graph.replay()
+        if self.after:
+            if self.finish_events is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            self.reducer.finish()            # no hook ran in the replay: launches every bucket
+            if self.finish_events is not None:
+                e1.record()
+                self.finish_events.append((e0, e1))
+            self.opt_graph.replay()
         volume_ops._BN_UPDATES[0] += 1     # weights / running stats changed on the device
         return self.out

@@ -187,3 +187,47 @@ def test_capture_after_eager_default_stream_steps():
         assert torch.equal(la, lb)
     for (na, pa), (nb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
         assert torch.equal(pa, pb), na
+
+
+def test_graph_with_allreduce_after_replay_equals_eager():
+    """bench.py's N > 1 launch mode at one RCCL rank: forward + backward replayed from the
+    graph (gradients straight into the bucket slices), the bucketed all-reduces issued
+    eagerly after the replay, then the captured Adam -- bit-identical to plain eager steps
+    of an identical model (at world 1 the average is the gradient itself)."""
+    import torch.distributed as dist
+    from multimodal_alzheimer_amd.data_parallel import GradAllReduce
+    torch.manual_seed(13)
+    a = M.Anat_CNN(_hparams("bf16")).cuda()
+    b = copy.deepcopy(a)
+    batches = [_batch(40 + i) for i in range(3)]
+    warm = 2
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29563", rank=0, world_size=1,
+                            device_id=torch.device("cuda", torch.cuda.current_device()))
+    try:
+        opt_a = a.configure_optimizers()
+        for grp in opt_a.param_groups:
+            grp["capturable"] = True
+            grp["lr"] = torch.tensor(float(grp["lr"]), device="cuda")
+        for _ in range(warm):
+            opt_a.zero_grad(set_to_none=True)
+            a.general_step(batches[0], 0, "train")["loss"].backward()
+            opt_a.step()
+        losses_a = []
+        for i in range(3):
+            opt_a.zero_grad(set_to_none=True)
+            out = a.general_step(batches[i], 0, "train")
+            out["loss"].backward()
+            opt_a.step()
+            losses_a.append(out["loss"].detach().clone())
+        opt_b = b.configure_optimizers()
+        red = GradAllReduce(b.parameters(), bucket_mb=4.0)
+        gs = GraphedTrainStep(b, opt_b, batches[0], warmup=warm, reducer=red, collectives="after")
+        assert gs.opt_graph is not None
+        losses_b = [gs(batches[i])["loss"].clone() for i in range(3)]
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    for la, lb in zip(losses_a, losses_b):
+        assert torch.equal(la, lb)
+    for (na, pa), (nb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(pa, pb), na
