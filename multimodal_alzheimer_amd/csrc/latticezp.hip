@@ -146,6 +146,20 @@ __device__ __forceinline__ void mma_a(f32x4 (&acc)[NF][TN], const bf16x8 (&a)[NF
 #ifndef ZP_EARLY_READS
 #define ZP_EARLY_READS 1
 #endif
+#ifndef ZP_PIPE
+#define ZP_PIPE 1
+#endif
+// ZP_PIN 1: a scheduling barrier after each fragment's (MFMAs, refill) pair keeps the
+// compiler from hoisting the refills (their latency is covered by the other fragments'
+// MFMAs anyway) and so from inflating the live fragment registers into spills
+#ifndef ZP_PIN_MODE
+#define ZP_PIN_MODE 1
+#endif
+#if ZP_PIN_MODE
+#define ZP_PIN() __builtin_amdgcn_sched_barrier(0)
+#else
+#define ZP_PIN() (void)0
+#endif
 template <int TN, int WM, int P, int KZ, int KY, typename DMA>
 __device__ __forceinline__ void stage_body(f32x4 (&acc)[NF][TN], const char* bsl,
                                            const char* const (&pl)[3], DMA&& dma) {
@@ -254,12 +268,13 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
     for (int j = 0; j < TN; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: the first chunk's planes needed before its plane issues (pair 0: planes 0, 1;
-  // pair 1: all three), then the weights of stages 0 and 1
+  // pair 1: all three), then the weights of stages 0 and 1 (and 2 for ZP_PIPE)
   issue_plane(0, 0);
   issue_plane(0, 1);
   if (pair == 1) issue_plane(0, 2);
   issue_stage_b(0);
   issue_stage_b(1);
+  if constexpr (ZP_PIPE) issue_stage_b(2);
 
   // Stage s = 9c + R (R = 3 (kz+1) + ky+1) waits for its weights (issued at stage s - 2);
   // younger are the ops issued at stage s - 1: its planes and the weights of stage s + 1.
@@ -325,9 +340,112 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
       stage(std::integral_constant<int, 8>{});
     }
   };
+  // ZP_PIPE: the stage boundary is one more step of the rolling pipeline.  Stage s's
+  // barrier sits between its kx = 0 and kx = +1 taps: before it each wave waits for the
+  // weights of stage s + 1 (and every LDS read of stage s); after it the DMA group of stage
+  // s goes out (its planes and the weights of stage s + 3 into stage s's weight slot, free
+  // now) and each fragment register, once the kx = +1 MFMAs have read it, is refilled with
+  // stage s + 1's kx = -1 fragment.  The MFMA pipe then runs straight across stage
+  // boundaries: no wave waits on its first fragment reads after a barrier.  A plane first
+  // read by stage t is issued in a DMA group <= t - 3, before the weights of stage t, so the
+  // wait at barrier t - 1 covers it; a slot is refilled in group s only when its last reader
+  // is stage s or earlier (the pair schedules above satisfy both).
+  auto run_pipe = [&](auto wmc, auto pc) {
+    constexpr int WM = decltype(wmc)::value, P = decltype(pc)::value;
+    bf16x8 a[NF], b0[TN], b1[TN];
+    wait_vm_lgkm0<2 * C::WI>();                     // stage 0's weights and chunk 0's planes
+    raw_barrier();
+    {
+      const char* const pl0[3] = {smem + 0 * ZPL + a_lane, smem + 1 * ZPL + a_lane,
+                                  smem + 2 * ZPL + a_lane};
+      read_b<TN, -1>(ring + b_lane, b0);
+      [&]<int... F>(std::integer_sequence<int, F...>) {
+        (read_a<WM, P, -1, -1, -1, F>(pl0, a), ...);
+      }(std::make_integer_sequence<int, NF>{});
+    }
+    // the last chunk is its own instantiation (MORE = false), so that no stage carries a
+    // run-time branch between its MFMAs
+    auto chunk = [&](int c, auto morec) {
+      constexpr bool MORE = decltype(morec)::value;
+      const char* const pl[3] = {smem + ((3 * c + 0) & 3) * ZPL + a_lane,
+                                 smem + ((3 * c + 1) & 3) * ZPL + a_lane,
+                                 smem + ((3 * c + 2) & 3) * ZPL + a_lane};
+      const char* const pln[3] = {smem + ((3 * c + 3) & 3) * ZPL + a_lane,
+                                  smem + ((3 * c + 4) & 3) * ZPL + a_lane,
+                                  smem + ((3 * c + 5) & 3) * ZPL + a_lane};
+      auto stage = [&](auto rc) {
+        constexpr int R = decltype(rc)::value;
+        constexpr int KZ = R / 3 - 1, KY = R % 3 - 1;
+        constexpr int KZN = R < 8 ? (R + 1) / 3 - 1 : -1, KYN = R < 8 ? (R + 1) % 3 - 1 : -1;
+        const int s = 9 * c + R;
+        int boff = C::RING_OFF + (s % NSTL) * C::BSLOT;
+        int bnof = C::RING_OFF + ((s + 1) % NSTL) * C::BSLOT;
+        asm volatile("" : "+s"(boff), "+s"(bnof));  // per-stage bases stay opaque
+        const char* bsl = smem + boff + b_lane;
+        const char* bsn = smem + bnof + b_lane;
+        const char* const (&plx)[3] = R < 8 ? pl : pln;
+        read_b<TN, 0>(bsl, b1);
+        [&]<int... F>(std::integer_sequence<int, F...>) {
+          ((mma_a<TN, WM, P, KZ, KY, -1, F>(acc, a, b0), read_a<WM, P, KZ, KY, 0, F>(pl, a),
+            ZP_PIN()), ...);
+        }(std::make_integer_sequence<int, NF>{});
+        read_b<TN, 1>(bsl, b0);
+        [&]<int... F>(std::integer_sequence<int, F...>) {
+          ((mma_a<TN, WM, P, KZ, KY, 0, F>(acc, a, b1), read_a<WM, P, KZ, KY, 1, F>(pl, a),
+            ZP_PIN()), ...);
+        }(std::make_integer_sequence<int, NF>{});
+        // barrier of stage s: the weights of stage s + 1 issued in group s - 2; younger are
+        // group s - 1's planes and its weights of stage s + 2
+        if constexpr (MORE) {
+          wait_vm_lgkm0<C::WI + PI * (R >= 1 ? planes_at<P, R - 1>() : 0)>();
+        } else if constexpr (R == 8 || R == 7) {
+          wait_vm_lgkm0<0>();
+        } else {
+          wait_vm_lgkm0<C::WI + PI * ((P == 0 && R == 1) ? 1 : 0)>();
+        }
+        raw_barrier();
+        auto dma = [&]() {
+          if constexpr (P == 0) {
+            if constexpr (R == 0) {
+              issue_plane(c, 2);
+              if constexpr (MORE) issue_plane(c + 1, 0);
+            } else if constexpr (R == 6 && MORE) {
+              issue_plane(c + 1, 1);
+            }
+          } else {
+            if constexpr ((R == 0 || R == 3 || R == 6) && MORE) issue_plane(c + 1, R / 3);
+          }
+          if constexpr (MORE || R < 6) issue_stage_b(s + 3);
+        };
+        read_b<TN, -1>(bsn, b1);
+        [&]<int... F>(std::integer_sequence<int, F...>) {
+          ((mma_a<TN, WM, P, KZ, KY, 1, F>(acc, a, b0),
+            read_a<WM, P, KZN, KYN, -1, F>(plx, a), F == 1 ? dma() : void(), ZP_PIN()), ...);
+        }(std::make_integer_sequence<int, NF>{});
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b0[j] = b1[j];
+      };
+      stage(std::integral_constant<int, 0>{});
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
+      stage(std::integral_constant<int, 4>{});
+      stage(std::integral_constant<int, 5>{});
+      stage(std::integral_constant<int, 6>{});
+      stage(std::integral_constant<int, 7>{});
+      stage(std::integral_constant<int, 8>{});
+    };
+    for (int c = 0; c + 1 < g.nchunk; ++c) chunk(c, std::true_type{});
+    chunk(g.nchunk - 1, std::false_type{});
+  };
   auto by_pair = [&](auto wmc) {
-    if (pair == 0) run(wmc, std::integral_constant<int, 0>{});
-    else run(wmc, std::integral_constant<int, 1>{});
+    if constexpr (ZP_PIPE) {
+      if (pair == 0) run_pipe(wmc, std::integral_constant<int, 0>{});
+      else run_pipe(wmc, std::integral_constant<int, 1>{});
+    } else {
+      if (pair == 0) run(wmc, std::integral_constant<int, 0>{});
+      else run(wmc, std::integral_constant<int, 1>{});
+    }
   };
   switch (wm) {                                     // wave-uniform
     case 0: by_pair(std::integral_constant<int, 0>{}); break;
