@@ -47,6 +47,9 @@ constexpr int CROW8 = BN8 * 2 + 16;
 constexpr int EPI8 = PL8 * CROW8 + 3 * 2 * BN8 * 4;
 constexpr int LDS8 = MAIN8 > EPI8 ? MAIN8 : EPI8;
 constexpr int NT8 = 512;
+#ifndef L8_PIPE
+#define L8_PIPE 1
+#endif
 
 struct L8 {
   int nb, Cs, Nd, Kpad, nbn, nchunk;
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: chunk-0 planes, weights of stages 0 and 1
+  // prologue: chunk-0 planes, weights of stages 0 and 1 (L8_PIPE: and 2, in run_pipe)
   for (int p = 0; p < 3; ++p)
     if (p - 1 >= kz0 && p - 1 <= kz1) issue_plane(p, 0);
   for (int s = 0; s < 2 && s < nstage; ++s) {
@@ -293,11 +296,87 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
       stage8<TN, WM, 1>(acc, ring + ((s0 + 2) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
     }
   };
+  // L8_PIPE: stage s's barrier sits between its kx = 0 and kx = +1 MFMAs.  Before it each
+  // wave waits for stage s + 1's weights (issued three stages ahead, in group s - 2) and its
+  // own LDS reads of stage s; after it the DMA group of stage s goes out (weights of stage
+  // s + 3 into stage s's slot, free now, and -- after a kz plane's last stage -- that plane
+  // of the next chunk, first read nspc - 2 >= 4 stages later), then stage s + 1's kx = -1
+  // fragments are read behind stage s's kx = +1 MFMAs: the MFMA pipe runs across barriers.
+  auto run_pipe = [&](auto wmc) {
+    constexpr int WM = decltype(wmc)::value;
+    auto plane_due2 = [&](int s, int& p, int& cc) -> bool {
+      const int c = s / nspc, r = s - c * nspc;
+      if (r % 3 != 2 || c + 1 >= g.nchunk) return false;
+      p = kz0 + r / 3 + 1;
+      cc = c + 1;
+      return true;
+    };
+    if (2 < nstage) {
+      int cc, t;
+      stage_w(2, cc, t);
+      issue_b(cc, t, 2);
+    }
+    if (2 < nstage && nbi == 2) wait_vm_lgkm0<4>();
+    else if (2 < nstage && nbi == 1) wait_vm_lgkm0<2>();
+    else wait_vm_lgkm0<0>();
+    raw_barrier();
+    Fr8<TN> f0, f1;
+    read8<TN, WM, -1, -1>(ring + b_lane, smem + (kz0 + 1) * PLANE8, ao, zp, lhi, f0);
+    int pl_prev = 0;                                // plane instructions of group s - 1
+    auto barrier_dma = [&](int s) {
+      const int younger = (s + 2 < nstage ? nbi : 0) + pl_prev;
+      switch (younger) {
+        case 0: wait_vm_lgkm0<0>(); break;
+        case 1: wait_vm_lgkm0<1>(); break;
+        case 2: wait_vm_lgkm0<2>(); break;
+        case 4: wait_vm_lgkm0<4>(); break;
+        case 5: wait_vm_lgkm0<5>(); break;
+        default: wait_vm_lgkm0<6>(); break;
+      }
+      raw_barrier();
+      if (s + 3 < nstage) {
+        int cc, t;
+        stage_w(s + 3, cc, t);
+        issue_b(cc, t, s % NSL8);
+      }
+      int p, pc;
+      pl_prev = 0;
+      if (plane_due2(s, p, pc)) {
+        issue_plane(p, pc);
+        pl_prev = 4;
+      }
+    };
+    const int ngrp = nstage / 3;
+    for (int g2 = 0; g2 < ngrp; ++g2) {
+      const int kz = kz0 + g2 % nkz, kzn = kz0 + (g2 + 1) % nkz;
+      const char* pl = smem + (kz + 1) * PLANE8;
+      const char* pln = smem + (kzn + 1) * PLANE8;
+      const int s0 = g2 * 3;
+      auto stage = [&](auto kyc, int s, Fr8<TN>& fa, Fr8<TN>& fb) {
+        constexpr int KY = decltype(kyc)::value;
+        constexpr int KYN = KY < 1 ? KY + 1 : -1;
+        int boff = RING8 + (s % NSL8) * BSLOT8, bnof = RING8 + ((s + 1) % NSL8) * BSLOT8;
+        asm volatile("" : "+s"(boff), "+s"(bnof));
+        const char* bsl = smem + boff + b_lane;
+        read8<TN, WM, KY, 0>(bsl, pl, ao, zp, lhi, fb);
+        mma8<TN, WM, KY>(acc, fa);
+        read8<TN, WM, KY, 1>(bsl, pl, ao, zp, lhi, fa);
+        mma8<TN, WM, KY>(acc, fb);
+        barrier_dma(s);
+        read8<TN, WM, KYN, -1>(smem + bnof + b_lane, KY < 1 ? pl : pln, ao, zp, lhi, fb);
+        mma8<TN, WM, KY>(acc, fa);
+      };
+      stage(std::integral_constant<int, -1>{}, s0, f0, f1);
+      stage(std::integral_constant<int, 0>{}, s0 + 1, f1, f0);
+      stage(std::integral_constant<int, 1>{}, s0 + 2, f0, f1);
+      f0 = f1;
+    }
+  };
   switch (wm) {
-    case 0: run(std::integral_constant<int, 0>{}); break;
-    case 1: run(std::integral_constant<int, 1>{}); break;
-    case 2: run(std::integral_constant<int, 2>{}); break;
-    default: run(std::integral_constant<int, 3>{}); break;
+    case 0: L8_PIPE ? run_pipe(std::integral_constant<int, 0>{}) : run(std::integral_constant<int, 0>{}); break;
+    case 1: L8_PIPE ? run_pipe(std::integral_constant<int, 1>{}) : run(std::integral_constant<int, 1>{}); break;
+    case 2: L8_PIPE ? run_pipe(std::integral_constant<int, 2>{}) : run(std::integral_constant<int, 2>{}); break;
+    default: L8_PIPE ? run_pipe(std::integral_constant<int, 3>{}) : run(std::integral_constant<int, 3>{}); break;
   }
   __syncthreads();                                  // patch / ring reused by the epilogue
 

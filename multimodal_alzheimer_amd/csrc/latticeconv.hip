@@ -442,6 +442,9 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
 //  * both operands are m-major images read with transposing ds_read_b64_tr_b16 fragment
 //    reads (as conv.hip's wgrad_kernel); fp32 partial slabs [split][co][tap*Cs + ci] are
 //    summed and transposed by conv.hip's wgrad_reduce_t_kernel.
+#ifndef LW_PIPE
+#define LW_PIPE 1
+#endif
 constexpr int WXROW = 64;                 // X rows: 32 ci x 2 B
 constexpr int WYROW = 128;                // dY rows: 64 co x 2 B
 constexpr int WPLANE = PL * WXROW;        // 32 KiB
@@ -700,11 +703,132 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       stage(std::integral_constant<int, 7>{});
     }
   };
+  // LW_PIPE: the barrier of stage s sits between its two positions' MFMAs.  Stage s reads
+  // its second position's fragments behind the first position's MFMAs, waits for stage
+  // s + 1's dY (and every LDS read of stage s), takes the barrier, issues its DMA group (dY
+  // of stage s + 3 into stage s's slot, free now; X plane o + 2 at a plane's first stage)
+  // and reads stage s + 1's first-position fragments behind its second position's MFMAs:
+  // the MFMA pipe runs across the barrier.  X plane o + 2 is issued 8 stages before its first
+  // reader's barrier and ahead of that barrier's dY, so the same wait covers it.
+  auto run_pipe = [&](auto tgc) {
+    constexpr int TG = decltype(tgc)::value;
+    constexpr int NT = TG == 3 ? 6 : 7;
+    auto yx_on = [](auto kc, auto posc) constexpr {
+      constexpr int K = decltype(kc)::value, POS = decltype(posc)::value;
+      constexpr int t = TG * 7 + K;
+      constexpr int ky = (t / 3) % 3 - 1, kx = t % 3 - 1;
+      constexpr int py = POS / S + ky, px = POS % S + kx;
+      return K < NT && py >= 0 && py < S && px >= 0 && px < S;
+    };
+    auto kread = [&](const char* yimg, auto qc, auto posc, int pb, const bool (&zk)[7], WFr& f) {
+      constexpr int Q = decltype(qc)::value, POS = decltype(posc)::value;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        f.a[i] = __builtin_shufflevector(tr8(yimg + Q * NS * WYROW + ya_lo[i]),
+                                         tr8(yimg + Q * NS * WYROW + ya_hi[i]), 0, 1, 2, 3, 4,
+                                         5, 6, 7);
+      auto one = [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        if constexpr (yx_on(kc, posc)) {
+          constexpr int t = TG * 7 + K;
+          constexpr int dk = (t / 9 - 1) * WPLANE + (((t / 3) % 3 - 1) * S + t % 3 - 1) * NS * WXROW +
+                             POS * NS * WXROW;
+          const char* img = smem + (zk[K] ? pb + dk : WZERO_OFF);
+          f.b[K] = __builtin_shufflevector(tr8(img + xb_lo), tr8(img + xb_hi), 0, 1, 2, 3, 4, 5,
+                                           6, 7);
+        }
+      };
+      one(std::integral_constant<int, 0>{});
+      one(std::integral_constant<int, 1>{});
+      one(std::integral_constant<int, 2>{});
+      one(std::integral_constant<int, 3>{});
+      one(std::integral_constant<int, 4>{});
+      one(std::integral_constant<int, 5>{});
+      one(std::integral_constant<int, 6>{});
+    };
+    auto kmma = [&](const WFr& f, auto posc) {
+      auto one = [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        if constexpr (yx_on(kc, posc)) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i][K] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[K], acc[i][K], 0, 0,
+                                                                0);
+        }
+      };
+      one(std::integral_constant<int, 0>{});
+      one(std::integral_constant<int, 1>{});
+      one(std::integral_constant<int, 2>{});
+      one(std::integral_constant<int, 3>{});
+      one(std::integral_constant<int, 4>{});
+      one(std::integral_constant<int, 5>{});
+      one(std::integral_constant<int, 6>{});
+    };
+    auto zflags = [&](int tz, bool (&zk)[7]) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const int kz = (TG * 7 + k) / 9 - 1;
+        zk[k] = (unsigned)(tz + kz) < (unsigned)S;
+      }
+    };
+    issue_y_at(plane_y0(0), 2, 2);                  // the prologue's third dY stage
+    wait_vm_lgkm0<2>();                             // X planes 0, 1 and dY stage 0
+    raw_barrier();
+    WFr f0, f1;
+    bool zok[7], zn[7];
+    zflags(0, zok);
+    kread(smem + WY_OFF, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0,
+          zok, f0);
+    for (int o = 0; o < nplane_out; ++o) {
+      const int tz = o % S;
+      const bool xnow = o + 2 < nplane_out;         // X plane o + 2 issued at stage 0
+      const bool lastp = o + 1 == nplane_out;
+      const int pbase = tz * WPLANE, pnext = ((o + 1) % S) * WPLANE;
+      zflags(tz, zok);
+      zflags((o + 1) % S, zn);
+      const int64_t y_here = plane_y0(o);
+      const int64_t y_next = lastp ? y_here : plane_y0(o + 1);
+      const int sl0 = (o * 8) % WYSLOTS;
+      auto stage = [&](auto mc) {
+        constexpr int M = decltype(mc)::value;
+        const int sl = (sl0 + M) % WYSLOTS;
+        int yoff = WY_OFF + sl * WYST, ynof = WY_OFF + ((sl + 1) % WYSLOTS) * WYST;
+        asm volatile("" : "+s"(yoff), "+s"(ynof));
+        kread(smem + yoff, std::integral_constant<int, 1>{},
+              std::integral_constant<int, 2 * M + 1>{}, pbase, zok, f1);
+        kmma(f0, std::integral_constant<int, 2 * M>{});
+        // barrier of stage s: dY of stage s + 1 (issued in group s - 2) landed; younger are
+        // group s - 1's dY (stage s + 2) and, after a plane's first stage, its X plane
+        if (M == 1 && xnow) wait_vm_lgkm0<5>();
+        else if (lastp && M >= 6) wait_vm_lgkm0<0>();
+        else wait_vm_lgkm0<1>();
+        raw_barrier();
+        if (M + 3 < 8) issue_y_at(y_here, M + 3, sl);
+        else if (!lastp) issue_y_at(y_next, M - 5, sl);
+        if (M == 0 && xnow) issue_x(o + 2);
+        if constexpr (M < 7)
+          kread(smem + ynof, std::integral_constant<int, 0>{},
+                std::integral_constant<int, 2 * M + 2>{}, pbase, zok, f0);
+        else
+          kread(smem + ynof, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                pnext, zn, f0);
+        kmma(f1, std::integral_constant<int, 2 * M + 1>{});
+      };
+      stage(std::integral_constant<int, 0>{});
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
+      stage(std::integral_constant<int, 4>{});
+      stage(std::integral_constant<int, 5>{});
+      stage(std::integral_constant<int, 6>{});
+      stage(std::integral_constant<int, 7>{});
+    }
+  };
   switch (tg) {                                     // wave-uniform
-    case 0: run(std::integral_constant<int, 0>{}); break;
-    case 1: run(std::integral_constant<int, 1>{}); break;
-    case 2: run(std::integral_constant<int, 2>{}); break;
-    default: run(std::integral_constant<int, 3>{}); break;
+    case 0: LW_PIPE ? run_pipe(std::integral_constant<int, 0>{}) : run(std::integral_constant<int, 0>{}); break;
+    case 1: LW_PIPE ? run_pipe(std::integral_constant<int, 1>{}) : run(std::integral_constant<int, 1>{}); break;
+    case 2: LW_PIPE ? run_pipe(std::integral_constant<int, 2>{}) : run(std::integral_constant<int, 2>{}); break;
+    default: LW_PIPE ? run_pipe(std::integral_constant<int, 3>{}) : run(std::integral_constant<int, 3>{}); break;
   }
 
   // partial slab [split][co][tap * Cs + ci]

@@ -137,6 +137,36 @@ def step(d):
     return "\n".join(out)
 
 
+def stepavg(d, skip=2):
+    """Per-position kernel durations (us) averaged over the complete steps of the trace
+    (the first `skip` steps dropped), in launch order, plus the mean step sum."""
+    rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ends = [i for i, r in enumerate(rows) if "FusedAdam" in r["Kernel_Name"] or
+            "FusedOptimizerTensorListMetadata" in r["Kernel_Name"]]
+    groups, cur = [], [ends[0]]
+    for e in ends[1:]:
+        if e - cur[-1] <= 3:
+            cur.append(e)
+        else:
+            groups.append(cur)
+            cur = [e]
+    groups.append(cur)
+    steps = [rows[a[-1] + 1:b[-1] + 1] for a, b in zip(groups, groups[1:])][skip:]
+    n = min(len(st) for st in steps)
+    steps = [st for st in steps if len(st) == n]
+    out, tot = [], 0.0
+    for i in range(n):
+        us = sum((int(st[i]["End_Timestamp"]) - int(st[i]["Start_Timestamp"])) / 1e3
+                 for st in steps) / len(steps)
+        tot += us
+        r = steps[0][i]
+        out.append(f"{us:8.1f}  g={r['Grid_Size_X']:>8}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']}  "
+                   f"{short(r['Kernel_Name']).split('(')[0][:90]}")
+    out.insert(0, f"steps averaged: {len(steps)}, kernels per step {n}, mean sum {tot:.1f} us")
+    return "\n".join(out)
+
+
 if __name__ == "__main__":
     mode = sys.argv[1]
     if mode == "stats":
@@ -147,5 +177,7 @@ if __name__ == "__main__":
         print(dispatches(sys.argv[2], sys.argv[3]))
     elif mode == "step":
         print(step(sys.argv[2]))
+    elif mode == "stepavg":
+        print(stepavg(sys.argv[2]))
     elif mode == "traffic":
         print(json.dumps(traffic(sys.argv[2], sys.argv[3]), indent=1))
