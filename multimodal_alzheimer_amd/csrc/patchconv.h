@@ -65,3 +65,8 @@ int64_t workspace(const mmad_patch::Geo& g);
 int wgrad(const mmad_patch::Geo& g, const void* x, const void* dy, float* ws, int* splits,
           void* stream);
 }  // namespace mmad_pwgrad
+
+namespace mmad_pool {
+// MMAD_POOL_RUN run-time override (mmad_set_kernel_variant("pool_run", v)); returns the old mode
+int set_run_mode(int v);
+}  // namespace mmad_pool

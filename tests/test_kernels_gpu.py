@@ -250,6 +250,31 @@ def test_bn_relu_maxpool_fused(dtype, training):
     close(bn_b.running_var, rv_r, 1e-5, "running_var")
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 9, 10, 11), (2, 64, 64, 64, 64), (1, 128, 8, 6, 4)],
+                         ids=["odd", "stem", "c128"])
+def test_bnpool_run_kernel_matches_rows_kernel(shape):
+    """The column-carrying stem pool kernel (pool.hip bnpool3s2_fwd_run_kernel) against the
+    per-output rows kernel it replaces: pooled output, argmax-routed input gradient and BN
+    parameter gradients bit-identical (ties on ReLU zeros everywhere)."""
+    n, c = shape[:2]
+    lib = _lib.load()
+    res = {}
+    for mode in (0, 1):
+        bn = _BN(c, 75)
+        bn.training = True
+        y = to_vol(rnd(*shape, seed=74, scale=2.0), torch.bfloat16).requires_grad_(True)
+        prev = lib.mmad_set_kernel_variant(b"pool_run", mode)
+        try:
+            p = V.batchnorm_relu_maxpool(y, bn, None, 3, 2, 1)
+            p.backward(to_vol(rnd(*p.shape, seed=76), torch.bfloat16))
+            torch.cuda.synchronize()
+        finally:
+            lib.mmad_set_kernel_variant(b"pool_run", prev)
+        res[mode] = (p, y.grad, bn.weight.grad, bn.bias.grad)
+    for nm, a, b in zip(("out", "dy", "dgamma", "dbeta"), res[0], res[1]):
+        assert torch.equal(a, b), nm
+
+
 @pytest.mark.parametrize("shape,dil", [((2, 512, 4, 4, 4), 4), ((2, 256, 4, 4, 4), 2),
                                        ((2, 64, 8, 8, 8), 1)])
 def test_conv_bn_relu_chain(shape, dil):
