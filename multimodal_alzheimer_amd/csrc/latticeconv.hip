@@ -709,7 +709,10 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
   // of stage s + 3 into stage s's slot, free now; X plane o + 2 at a plane's first stage)
   // and reads stage s + 1's first-position fragments behind its second position's MFMAs:
   // the MFMA pipe runs across the barrier.  X plane o + 2 is issued 8 stages before its first
-  // reader's barrier and ahead of that barrier's dY, so the same wait covers it.
+  // reader's barrier and ahead of that barrier's dY, so the same wait covers it.  A tap whose
+  // z shift leaves the sub-lattice (first / last plane of a sub group) is skipped by a
+  // wave-uniform branch -- reads and MFMAs -- instead of adding the zero block's products:
+  // the reads run a phase ahead of their MFMAs, so the branches cost no overlap.
   auto run_pipe = [&](auto tgc) {
     constexpr int TG = decltype(tgc)::value;
     constexpr int NT = TG == 3 ? 6 : 7;
@@ -733,9 +736,11 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
           constexpr int t = TG * 7 + K;
           constexpr int dk = (t / 9 - 1) * WPLANE + (((t / 3) % 3 - 1) * S + t % 3 - 1) * NS * WXROW +
                              POS * NS * WXROW;
-          const char* img = smem + (zk[K] ? pb + dk : WZERO_OFF);
-          f.b[K] = __builtin_shufflevector(tr8(img + xb_lo), tr8(img + xb_hi), 0, 1, 2, 3, 4, 5,
-                                           6, 7);
+          if (zk[K]) {                                // wave-uniform: z padding skipped
+            const char* img = smem + pb + dk;
+            f.b[K] = __builtin_shufflevector(tr8(img + xb_lo), tr8(img + xb_hi), 0, 1, 2, 3, 4,
+                                             5, 6, 7);
+          }
         }
       };
       one(std::integral_constant<int, 0>{});
@@ -746,14 +751,16 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       one(std::integral_constant<int, 5>{});
       one(std::integral_constant<int, 6>{});
     };
-    auto kmma = [&](const WFr& f, auto posc) {
+    auto kmma = [&](const WFr& f, auto posc, const bool (&zk)[7]) {
       auto one = [&](auto kc) {
         constexpr int K = decltype(kc)::value;
         if constexpr (yx_on(kc, posc)) {
+          if (zk[K]) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[i][K] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[K], acc[i][K], 0, 0,
-                                                                0);
+            for (int i = 0; i < 4; ++i)
+              acc[i][K] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[K], acc[i][K], 0,
+                                                                  0, 0);
+          }
         }
       };
       one(std::integral_constant<int, 0>{});
@@ -796,7 +803,7 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
         asm volatile("" : "+s"(yoff), "+s"(ynof));
         kread(smem + yoff, std::integral_constant<int, 1>{},
               std::integral_constant<int, 2 * M + 1>{}, pbase, zok, f1);
-        kmma(f0, std::integral_constant<int, 2 * M>{});
+        kmma(f0, std::integral_constant<int, 2 * M>{}, zok);
         // barrier of stage s: dY of stage s + 1 (issued in group s - 2) landed; younger are
         // group s - 1's dY (stage s + 2) and, after a plane's first stage, its X plane
         if (M == 1 && xnow) wait_vm_lgkm0<5>();
@@ -812,7 +819,7 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
         else
           kread(smem + ynof, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
                 pnext, zn, f0);
-        kmma(f1, std::integral_constant<int, 2 * M + 1>{});
+        kmma(f1, std::integral_constant<int, 2 * M + 1>{}, zok);
       };
       stage(std::integral_constant<int, 0>{});
       stage(std::integral_constant<int, 1>{});

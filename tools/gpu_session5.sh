@@ -18,7 +18,7 @@ step() {
 }
 step tests 500 $PYT -s tests/test_lattice_zp_gpu.py tests/test_fullsize_gpu.py tests/test_mni_geometry_gpu.py tests/test_fullsize_oracle_gpu.py tests/test_graph_step_gpu.py "tests/test_kernels_gpu.py::test_bnpool_run_kernel_matches_rows_kernel" "tests/test_kernels_gpu.py::test_bn_relu_maxpool_fused" tests/test_twin_gpu.py
 step bench 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline
-for v in default nopipe lw0 l80; do
+for v in default nopipe; do
   if [ $v = default ]; then LIB=multimodal_alzheimer_amd/libmmad_hip.so; else LIB=variants/$v/libmmad_hip.so; fi
   step prof_$v 200 env MMAD_LIB_PATH=$LIB rocprofv3 --kernel-trace --stats -d $OUT/prof_$v -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline
   python3 tools/prof_summary.py stepavg $OUT/prof_$v > $OUT/step_$v.txt 2>&1; head -1 $OUT/step_$v.txt; grep -E "lattice|patch_conv" $OUT/step_$v.txt | cut -c1-70
