@@ -23,6 +23,16 @@ int fwd(const Geo& g, const void* src, const void* wp, const float* bias, void* 
         float* stats, void* stream);
 }  // namespace mmad_patch
 
+// Persistent z-walking form of the patch conv for 64-channel inputs on grids of 4 x 8 x 8
+// boxes (patchz.hip, layer1): mmad_patch::fwd / tiles route to it when ok().
+namespace mmad_patchz {
+int set_mode(int v);              // MMAD_PATCHZ at run time; returns the previous mode
+bool ok(const mmad_patch::Geo& g);
+int64_t tiles(const mmad_patch::Geo& g);
+int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,
+        float* stats, void* stream);
+}  // namespace mmad_patchz
+
 // Residue-class conv for dilated 3^3 convs on a 4d^3 grid (latticeconv.hip): same geometry
 // record, packed weights and partial-sum layout as the patch kernel.
 namespace mmad_lattice {

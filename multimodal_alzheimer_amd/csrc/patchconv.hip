@@ -394,6 +394,7 @@ bool ok(const Geo& q) {
 }
 
 int64_t tiles(const Geo& q) {
+  if (mmad_patchz::ok(q)) return mmad_patchz::tiles(q);
   const PG g = make_pg(q, tz_for(q));
   return (int64_t)q.nb * g.ntz * g.nty * g.ntx;
 }
@@ -401,6 +402,7 @@ int64_t tiles(const Geo& q) {
 int fwd(const Geo& q, const void* src, const void* wp, const float* bias, void* dst,
         float* stats, void* stream) {
   if (!ok(q)) return MMAD_EUNSUPPORTED;
+  if (mmad_patchz::ok(q)) return mmad_patchz::fwd(q, src, wp, bias, dst, stats, stream);
   const int tz = tz_for(q);
   const PG g = make_pg(q, tz);
   hipStream_t st = as_stream(stream);
