@@ -47,8 +47,11 @@ constexpr int CROW8 = BN8 * 2 + 16;
 constexpr int EPI8 = PL8 * CROW8 + 3 * 2 * BN8 * 4;
 constexpr int LDS8 = MAIN8 > EPI8 ? MAIN8 : EPI8;
 constexpr int NT8 = 512;
+// L8_PIPE (default 0): the pipelined stage loop (run_pipe); measured r03e in the config-2
+// step 1-2 % slower than the barrier-first loop on all four layer3 launches (55.9 / 102.3 /
+// 96.5 / 66.0 us against 54.4 / 100.1 / 94.5 / 64.6) -- kept for A/B, not shipped.
 #ifndef L8_PIPE
-#define L8_PIPE 1
+#define L8_PIPE 0
 #endif
 
 struct L8 {

@@ -442,8 +442,15 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
 //  * both operands are m-major images read with transposing ds_read_b64_tr_b16 fragment
 //    reads (as conv.hip's wgrad_kernel); fp32 partial slabs [split][co][tap*Cs + ci] are
 //    summed and transposed by conv.hip's wgrad_reduce_t_kernel.
+// LW_PIPE (default 0): the pipelined stage loop below (run_pipe); measured r03e in the
+// config-2 step: layer4.0.conv2 wgrad 266.5 us against 241.0 for the barrier-first loop
+// (run), layer4.0.conv1 138.1 against 125.7 -- kept for A/B, not shipped.  LW_ZSKIP (with
+// LW_PIPE): z-padding taps skipped by a uniform branch instead of the zero block.
 #ifndef LW_PIPE
-#define LW_PIPE 1
+#define LW_PIPE 0
+#endif
+#ifndef LW_ZSKIP
+#define LW_ZSKIP 1
 #endif
 constexpr int WXROW = 64;                 // X rows: 32 ci x 2 B
 constexpr int WYROW = 128;                // dY rows: 64 co x 2 B
@@ -736,8 +743,8 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
           constexpr int t = TG * 7 + K;
           constexpr int dk = (t / 9 - 1) * WPLANE + (((t / 3) % 3 - 1) * S + t % 3 - 1) * NS * WXROW +
                              POS * NS * WXROW;
-          if (zk[K]) {                                // wave-uniform: z padding skipped
-            const char* img = smem + pb + dk;
+          if (!LW_ZSKIP || zk[K]) {                    // wave-uniform: z padding skipped
+            const char* img = smem + (zk[K] ? pb + dk : WZERO_OFF);
             f.b[K] = __builtin_shufflevector(tr8(img + xb_lo), tr8(img + xb_hi), 0, 1, 2, 3, 4,
                                              5, 6, 7);
           }
@@ -755,7 +762,7 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       auto one = [&](auto kc) {
         constexpr int K = decltype(kc)::value;
         if constexpr (yx_on(kc, posc)) {
-          if (zk[K]) {
+          if (!LW_ZSKIP || zk[K]) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
               acc[i][K] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[K], acc[i][K], 0,

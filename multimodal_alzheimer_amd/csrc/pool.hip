@@ -762,15 +762,17 @@ bool rows_on() {
   return v;
 }
 
-// MMAD_POOL_RUN: 1 (default) the column-carrying bnpool3s2_fwd_run_kernel for the stem pool
-// (k 3, s 2, p 1, bf16), 0 the per-output rows kernel; mmad_set_kernel_variant("pool_run", v)
+// MMAD_POOL_RUN: 1 the column-carrying bnpool3s2_fwd_run_kernel for the stem pool (k 3, s 2,
+// p 1, bf16), 0 (default) the per-output rows kernel; mmad_set_kernel_variant("pool_run", v).
+// Measured r03e at config 2: 124.5 us against the rows kernel's 110.8 (r03a) -- the run
+// kernel's 2 waves per SIMD do not keep enough loads in flight; kept for A/B.
 std::atomic<int> g_pool_run{-1};
 int pool_run_mode() {
   int v = g_pool_run.load(std::memory_order_relaxed);
   if (v < 0) {
     const char* e = getenv("MMAD_POOL_RUN");
     int expect = -1;
-    g_pool_run.compare_exchange_strong(expect, e ? atoi(e) : 1);
+    g_pool_run.compare_exchange_strong(expect, e ? atoi(e) : 0);
     v = g_pool_run.load(std::memory_order_relaxed);
   }
   return v;

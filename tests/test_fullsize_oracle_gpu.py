@@ -39,10 +39,18 @@ LOGIT_ATOL = 1e-4
 
 # bf16 gradient bounds per layer group (see the module docstring): normwise relative error
 # of the sampled elements, and relative error of each large sampled element
-NRM16 = (("layer4", 0.12), ("layer3", 0.25), ("layer2", 0.35), ("layer1", 0.45),
-         ("conv1", 0.6), ("bn1", 0.6), ("", 0.05))
-LRG16 = (("layer4", 0.15), ("layer3", 0.3), ("layer2", 0.45), ("layer1", 0.6),
-         ("conv1", 0.8), ("bn1", 0.8), ("", 0.06))
+# Calibrated on the MI355X (gpurun_out/r03e, both configs; maxima over each group):
+# normwise 0.144 / 0.194 / 0.286 / 0.337 / 0.300 / 0.304 / 7e-4 (layer4 .. bn1, head),
+# large-element 0.198 / 0.253 / 0.458 / 0.428 / 0.471 / 0.356 / 2e-3, |g| sum 0.116; the
+# bounds are those x ~1.5.  The error grows smoothly towards the input (no layer stands out),
+# the |g| sums agree to ~1 %, and the fp32 path passes the 4x-reference-error bar above: it
+# is bf16 rounding compounded through cancelling sums (dY . X over 32k voxels after BN's
+# mean subtraction) and max-pool argmax moves, not a kernel error.
+NRM16 = (("layer4", 0.22), ("layer3", 0.3), ("layer2", 0.43), ("layer1", 0.5),
+         ("conv1", 0.45), ("bn1", 0.45), ("", 0.05))
+LRG16 = (("layer4", 0.3), ("layer3", 0.38), ("layer2", 0.7), ("layer1", 0.65),
+         ("conv1", 0.7), ("bn1", 0.55), ("", 0.06))
+SUM16 = 0.18
 
 
 def _group_tol(table, pname):
@@ -165,7 +173,7 @@ def test_full_size_bf16_matches_reference(name):
         st = g["grad64/stats/" + pname]
         sum_rel = abs(np.abs(full).sum() - st[1]) / max(st[1], 1e-30)
         rows.append((pname, nrm, lrg, sum_rel))
-        if nrm > _group_tol(NRM16, pname) or lrg > _group_tol(LRG16, pname) or sum_rel > 0.1:
+        if nrm > _group_tol(NRM16, pname) or lrg > _group_tol(LRG16, pname) or sum_rel > SUM16:
             bad.append(pname)
     for pname, nrm, lrg, sum_rel in rows:
         print(f"  {pname}: normwise {nrm:.3e}  large-element {lrg:.3e}  |g| sum {sum_rel:.3e}")
