@@ -157,5 +157,12 @@ static inline int hip_status(hipError_t e) { return e == hipSuccess ? MMAD_OK : 
 static inline int launch_status() { return hip_status(hipGetLastError()); }
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Zero-fill as a kernel (16-byte stores, any 4-byte-aligned size): used instead of
+// hipMemsetAsync on paths that run inside captured HIP graphs -- a captured memset node was
+// not re-executed on replays after the first on this ROCm stack (tools/diag_replay.py),
+// while kernel nodes are.
+__global__ void zero_fill_kernel(uint32_t* __restrict__ p, int64_t words);
+int zero_fill(void* p, int64_t bytes, hipStream_t st);
 static inline bool is_pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 static inline int ilog2(int64_t v) { int r = 0; while ((int64_t(1) << r) < v) ++r; return r; }

@@ -1667,7 +1667,7 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
     // plus that class's GEMM (the 7 empty classes as igemm launches cost ~3x more)
     const int64_t bytes = (int64_t)d->n * d->di * d->hi * d->wi * d->ci *
                           (dtype == MMAD_BF16 ? 2 : 4);
-    const int rc = hip_status(hipMemsetAsync(dx, 0, (size_t)bytes, as_stream(stream)));
+    const int rc = zero_fill(dx, bytes, as_stream(stream));
     if (rc) return rc;
     return run_igemm<DGRAD>(g, dtype, mmax, 1, dy, wpt, nullptr, dx, nullptr, as_stream(stream));
   }
@@ -1814,3 +1814,23 @@ int mmad_conv3d_wgrad_split(const mmad_conv_desc* d, int dtype, const void* x, c
 }
 
 }  // extern "C"
+
+__global__ void zero_fill_kernel(uint32_t* __restrict__ p, int64_t words) {
+  const int64_t n4 = words >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    reinterpret_cast<u32x4*>(p)[i] = u32x4{0u, 0u, 0u, 0u};
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words;
+       i += stride)
+    p[i] = 0u;
+}
+
+int zero_fill(void* p, int64_t bytes, hipStream_t st) {
+  if (bytes <= 0) return MMAD_OK;
+  if (((uintptr_t)p & 15) || (bytes & 3)) return MMAD_EUNSUPPORTED;
+  const int64_t words = bytes / 4;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(words / 4, 256), 4096));
+  hipLaunchKernelGGL(zero_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     (uint32_t*)p, words);
+  return launch_status();
+}

@@ -26,6 +26,8 @@ depends on it:
 * dropout draws its seed on the device (``head_ops.dropout``), so every replay gets a
   fresh mask.
 """
+import os
+
 import torch
 
 from . import volume_ops
@@ -64,17 +66,24 @@ class GraphedTrainStep:
         self.graph = torch.cuda.CUDAGraph()
         self.opt_graph = None
         if self.after:
-            reducer.defer = True
+            reducer.defer = os.environ.get("MMAD_GRAPH_DEBUG", "") != "nodefer"
             try:
                 with torch.cuda.graph(self.graph):
                     self.out = model.general_step(self.static, 0, "train")
                     self.out["loss"].backward()
+                    dbg = os.environ.get("MMAD_GRAPH_DEBUG", "")
+                    if dbg == "join":
+                        torch.cuda.current_stream().wait_stream(
+                            volume_ops.grad_stream(self.static_device()))
+                    elif dbg == "tail":
+                        self._tail = torch.zeros(1, device=self.static_device()).add_(1)
             finally:
                 reducer.defer = False
             reducer.reset()                  # the capture's hooks only counted
             reducer.finish()                 # eager: gradients now averaged in place
             self.opt_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.opt_graph, pool=self.graph.pool()):
+            pool = self.graph.pool() if os.environ.get("MMAD_GRAPH_SHARE_POOL", "1") != "0" else None
+            with torch.cuda.graph(self.opt_graph, pool=pool):
                 optimizer.step()
         else:
             with torch.cuda.graph(self.graph):
@@ -82,11 +91,15 @@ class GraphedTrainStep:
                 self.out["loss"].backward()
                 if reducer is not None:
                     reducer.finish()
-                optimizer.step()
+                if os.environ.get("MMAD_GRAPH_DEBUG", "") != "noopt":
+                    optimizer.step()
         # keep the graph-owned output buffers, not their autograd graph: a live grad_fn chain
         # would keep every parameter's AccumulateGrad node (created on the capture stream)
         # alive, and later eager steps would reuse those nodes across streams
         self.out = {k: v.detach() if torch.is_tensor(v) else v for k, v in self.out.items()}
+
+    def static_device(self):
+        return next(self.model.parameters()).device
 
     def _eager(self):
         self.optimizer.zero_grad(set_to_none=True)

@@ -1,14 +1,34 @@
 """Diagnose GraphedTrainStep(collectives="after") against plain eager steps at one RCCL
-rank: where do model b's parameters leave model a's?  Prints, per step, the gradient and
-parameter mismatches (count of tensors, worst element) after the replay, after finish(),
-and after the optimizer replay, plus an eager-with-reducer control."""
+rank: which parameters' replayed gradients leave the eager ones, under which setup.
+
+  python tools/diag_after.py SCENARIO
+    after       GraphedTrainStep(reducer, collectives="after")  (bench.py's N > 1 mode)
+    after1      the same with one bucket (bucket_mb 1024)
+    inside      GraphedTrainStep(reducer, collectives="inside")
+    noslots     "after" with the reducer's gradient slots disabled (MMAD_DP_GRAD_SLOTS=0)
+    nopool      "after" with the optimizer graph in its own memory pool
+    nofinish    "after" without the eager finish() between the replays
+    join / tail "after" with a grad-stream join / a trivial kernel ending the capture
+    insidenoopt "inside" without the optimizer step in the graph (stepped eagerly)
+    plainnoopt  no reducer, graph = forward + backward only, optimizer stepped eagerly
+Prints per step the gradient mismatches after the replay (count, worst, first names)."""
 import copy
+import os
 import sys
 
 import torch
 import torch.distributed as dist
 
 sys.path.insert(0, ".")
+SCEN = sys.argv[1] if len(sys.argv) > 1 else "after"
+if SCEN == "noslots":
+    os.environ["MMAD_DP_GRAD_SLOTS"] = "0"
+if SCEN == "nopool":
+    os.environ["MMAD_GRAPH_SHARE_POOL"] = "0"
+if SCEN in ("join", "tail", "nodefer"):
+    os.environ["MMAD_GRAPH_DEBUG"] = SCEN
+if SCEN in ("insidenoopt", "plainnoopt"):
+    os.environ["MMAD_GRAPH_DEBUG"] = "noopt"
 import multimodal_alzheimer_amd as M  # noqa: E402
 from multimodal_alzheimer_amd.data_parallel import GradAllReduce  # noqa: E402
 from multimodal_alzheimer_amd.graph_step import GraphedTrainStep  # noqa: E402
@@ -37,8 +57,8 @@ def cmp(tag, a, b, grads=False):
             continue
         if not torch.equal(x, y):
             bad.append(na)
-            worst = max(worst, (x.float() - y.float()).abs().max().item())
-    print(f"{tag}: {len(bad)} differ, worst {worst:.3e}, first {bad[:3]}", flush=True)
+            worst = max(worst, (x.float() - y.float()).abs().nan_to_num(1e38).max().item())
+    print(f"{SCEN} {tag}: {len(bad)} differ, worst {worst:.3e}, {bad[:12]}", flush=True)
 
 
 def main():
@@ -47,58 +67,39 @@ def main():
     torch.manual_seed(13)
     a = M.Anat_CNN(hp()).cuda()
     b = copy.deepcopy(a)
-    c = copy.deepcopy(a)
     bs = [batch(40 + i) for i in range(3)]
     opt_a = a.configure_optimizers()
-    for m, opt in ((a, opt_a),):
-        for grp in opt.param_groups:
-            grp["capturable"] = True
-            grp["lr"] = torch.tensor(float(grp["lr"]), device="cuda")
+    for grp in opt_a.param_groups:
+        grp["capturable"] = True
+        grp["lr"] = torch.tensor(float(grp["lr"]), device="cuda")
     for _ in range(2):
         opt_a.zero_grad(set_to_none=True)
         a.general_step(bs[0], 0, "train")["loss"].backward()
         opt_a.step()
-    # control: eager steps of c with the reducer (defer mode, as the "after" warm-up)
-    opt_c = c.configure_optimizers()
-    for grp in opt_c.param_groups:
-        grp["capturable"] = True
-        grp["lr"] = torch.tensor(float(grp["lr"]), device="cuda")
-    red_c = GradAllReduce(c.parameters(), bucket_mb=4.0)
-    for _ in range(2):
-        opt_c.zero_grad(set_to_none=True)
-        red_c.defer = True
-        c.general_step(bs[0], 0, "train")["loss"].backward()
-        red_c.defer = False
-        red_c.finish()
-        opt_c.step()
-    torch.cuda.synchronize()
-    cmp("control eager+reducer after warm-up", a, c)
-
     opt_b = b.configure_optimizers()
-    red = GradAllReduce(b.parameters(), bucket_mb=4.0)
-    gs = GraphedTrainStep(b, opt_b, bs[0], warmup=2, reducer=red, collectives="after")
+    red = None if SCEN == "plainnoopt" else \
+        GradAllReduce(b.parameters(), bucket_mb=1024.0 if SCEN == "after1" else 4.0)
+    coll = "inside" if SCEN in ("inside", "insidenoopt", "plainnoopt") else "after"
+    gs = GraphedTrainStep(b, opt_b, bs[0], warmup=2, reducer=red, collectives=coll)
     torch.cuda.synchronize()
-    cmp("b after warm-up + capture", a, b)
-    for i in range(3):
+    cmp("after warm-up + capture", a, b)
+    for i in range(2):
         opt_a.zero_grad(set_to_none=True)
-        la = a.general_step(bs[i], 0, "train")["loss"]
-        la.backward()
+        a.general_step(bs[i], 0, "train")["loss"].backward()
         for k, v in bs[i].items():
             gs.static[k].copy_(v)
         gs.graph.replay()
         torch.cuda.synchronize()
-        print(f"step {i}: loss a {la.item():.9g} b {gs.out['loss'].item():.9g}", flush=True)
         cmp(f"step {i} grads after replay", a, b, grads=True)
-        gs.reducer.finish()
-        torch.cuda.synchronize()
-        cmp(f"step {i} grads after finish", a, b, grads=True)
+        if SCEN in ("insidenoopt", "plainnoopt"):
+            opt_b.step()
+        if coll == "after":
+            if SCEN != "nofinish":
+                gs.reducer.finish()
+            gs.opt_graph.replay()
         opt_a.step()
-        gs.opt_graph.replay()
         torch.cuda.synchronize()
         cmp(f"step {i} params after step", a, b)
-        sa = opt_a.state[next(iter(opt_a.state))]
-        sb = opt_b.state[next(iter(opt_b.state))]
-        print(f"   adam step a {sa['step'].item()} b {sb['step'].item()}", flush=True)
     dist.destroy_process_group()
 
 

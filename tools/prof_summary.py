@@ -68,9 +68,10 @@ def dispatches(d, name):
             if name in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # steps in the trace: 13 = 3 warm-up + 10 timed (eager bench); 27 = the graph-mode bench
-    # (3 warm + 10 probed eager steps, 3 capture warm-up steps, 1 + 10 replays)
+    # (3 warm + 10 probed eager steps, 3 capture warm-up steps, 1 + 10 replays); 14 = the
+    # graph-mode bench without the probe (3 warm-up, 1 capture, 10 replays)
     per = next((n for n in (6, 5, 4, 3, 2, 1)
-                if len(rows) % n == 0 and len(rows) // n in (13, 10, 20, 25, 27)), 1)
+                if len(rows) % n == 0 and len(rows) // n in (13, 10, 14, 20, 25, 27)), 1)
     groups = collections.defaultdict(list)
     for i, r in enumerate(rows):
         groups[i % per].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
