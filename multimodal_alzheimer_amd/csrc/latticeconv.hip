@@ -452,6 +452,9 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
 #ifndef LW_ZSKIP
 #define LW_ZSKIP 1
 #endif
+#ifndef LW_TZ
+#define LW_TZ 1
+#endif
 constexpr int WXROW = 64;                 // X rows: 32 ci x 2 B
 constexpr int WYROW = 128;                // dY rows: 64 co x 2 B
 constexpr int WPLANE = PL * WXROW;        // 32 KiB
@@ -616,10 +619,20 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       constexpr int py = POS / S + ky, px = POS % S + kx;
       return K < NT && py >= 0 && py < S && px >= 0 && px < S;
     };
+    // LW_TZ: the plane's z position in its sub group is a compile-time constant too, so a
+    // tap whose z shift leaves the sub-lattice has no reads and no MFMAs either (the plane
+    // loop is unrolled by the 4 planes of a sub group); LW_TZ = 0 reads the zero block and
+    // adds zero products instead
+    auto z_on = [](auto kc, auto tzc) constexpr {
+      constexpr int K = decltype(kc)::value, TZ = decltype(tzc)::value;
+      constexpr int kz = (TG * 7 + K) / 9 - 1;
+      return TZ < 0 || (TZ + kz >= 0 && TZ + kz < S);
+    };
     bool zok[7];
     int pbase = 0;                                  // plane tz's X offset in the ring
-    auto kread = [&](const char* yimg, auto qc, auto posc, WFr& f) {
+    auto kread = [&](const char* yimg, auto qc, auto posc, auto tzc, WFr& f) {
       constexpr int Q = decltype(qc)::value, POS = decltype(posc)::value;
+      constexpr int TZ = decltype(tzc)::value;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         f.a[i] = __builtin_shufflevector(tr8(yimg + Q * NS * WYROW + ya_lo[i]),
@@ -627,11 +640,13 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
                                          5, 6, 7);
       auto one = [&](auto kc) {
         constexpr int K = decltype(kc)::value;
-        if constexpr (yx_on(kc, posc)) {
+        if constexpr (yx_on(kc, posc) && z_on(kc, tzc)) {
           constexpr int t = TG * 7 + K;
           constexpr int dk = (t / 9 - 1) * WPLANE + (((t / 3) % 3 - 1) * S + t % 3 - 1) * NS * WXROW +
                              POS * NS * WXROW;
-          const char* img = smem + (zok[K] ? pbase + dk : WZERO_OFF);
+          const char* img;
+          if constexpr (TZ >= 0) img = smem + TZ * WPLANE + dk;
+          else img = smem + (zok[K] ? pbase + dk : WZERO_OFF);
           f.b[K] = __builtin_shufflevector(tr8(img + xb_lo), tr8(img + xb_hi), 0, 1, 2, 3, 4, 5,
                                            6, 7);
         }
@@ -644,10 +659,10 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       one(std::integral_constant<int, 5>{});
       one(std::integral_constant<int, 6>{});
     };
-    auto kmma = [&](const WFr& f, auto posc) {
+    auto kmma = [&](const WFr& f, auto posc, auto tzc) {
       auto one = [&](auto kc) {
         constexpr int K = decltype(kc)::value;
-        if constexpr (yx_on(kc, posc)) {
+        if constexpr (yx_on(kc, posc) && z_on(kc, tzc)) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             acc[i][K] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[K], acc[i][K], 0, 0,
@@ -663,7 +678,8 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       one(std::integral_constant<int, 6>{});
     };
 
-    for (int o = 0; o < nplane_out; ++o) {
+    // plane o of the block's stream; tzc = its z position in the sub group (-1: run time)
+    auto plane = [&](int o, auto tzc) {
       const int tz = o % S;
       const bool xnow = o + 2 < nplane_out;         // X plane o + 2 issued at stage 0
       pbase = tz * WPLANE;
@@ -694,11 +710,12 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
         asm volatile("" : "+s"(yoff));
         const char* yimg = smem + yoff;
         WFr f0, f1;
-        kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, f0);
+        kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, tzc,
+              f0);
         kread(yimg, std::integral_constant<int, 1>{}, std::integral_constant<int, 2 * M + 1>{},
-              f1);
-        kmma(f0, std::integral_constant<int, 2 * M>{});
-        kmma(f1, std::integral_constant<int, 2 * M + 1>{});
+              tzc, f1);
+        kmma(f0, std::integral_constant<int, 2 * M>{}, tzc);
+        kmma(f1, std::integral_constant<int, 2 * M + 1>{}, tzc);
       };
       stage(std::integral_constant<int, 0>{});
       stage(std::integral_constant<int, 1>{});
@@ -708,6 +725,16 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       stage(std::integral_constant<int, 5>{});
       stage(std::integral_constant<int, 6>{});
       stage(std::integral_constant<int, 7>{});
+    };
+    if constexpr (LW_TZ) {
+      for (int og = 0; og < nplane_out; og += S) {  // a sub group's 4 planes
+        plane(og + 0, std::integral_constant<int, 0>{});
+        plane(og + 1, std::integral_constant<int, 1>{});
+        plane(og + 2, std::integral_constant<int, 2>{});
+        plane(og + 3, std::integral_constant<int, 3>{});
+      }
+    } else {
+      for (int o = 0; o < nplane_out; ++o) plane(o, std::integral_constant<int, -1>{});
     }
   };
   // LW_PIPE: the barrier of stage s sits between its two positions' MFMAs.  Stage s reads
