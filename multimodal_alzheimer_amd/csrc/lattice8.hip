@@ -44,7 +44,7 @@ constexpr int RING8 = 3 * PLANE8;
 constexpr int ZERO8 = RING8 + NSL8 * BSLOT8;
 constexpr int MAIN8 = ZERO8 + RB8;
 constexpr int CROW8 = BN8 * 2 + 16;
-constexpr int EPI8 = PL8 * CROW8 + 3 * 2 * BN8 * 4;
+constexpr int EPI8 = PL8 * CROW8 + 7 * 2 * BN8 * 4;   // + partial sums of up to 7 wave rows
 constexpr int LDS8 = MAIN8 > EPI8 ? MAIN8 : EPI8;
 constexpr int NT8 = 512;
 // L8_PIPE (default 0): the pipelined stage loop (run_pipe); measured r03e in the config-2
@@ -63,31 +63,32 @@ struct L8 {
 
 __device__ __forceinline__ int swz8(int row) { return 3 * ((row >> 3) & 1); }
 
-template <int TN>
+template <int TN, int NFR>
 struct Fr8 {
   bf16x8 b[TN];
-  bf16x8 a[8];
+  bf16x8 a[NFR];
 };
 
-// fragment f of wave row WM: plane row ty = 2*WM + (f >> 2), x pair j = f & 3
-template <int WM, int KY>
+// fragment f of wave row WM (WR plane rows per wave): plane row ty = WR*WM + (f >> 2),
+// x pair j = f & 3
+template <int WM, int KY, int WR>
 __device__ constexpr bool row_ok(int f) {
-  return 2 * WM + (f >> 2) + KY >= 0 && 2 * WM + (f >> 2) + KY < S8;
+  return WR * WM + (f >> 2) + KY >= 0 && WR * WM + (f >> 2) + KY < S8;
 }
 
 // ao: this lane's row offset + chunk for an even (index 0) / odd (1) x shift; zlane: the
 // lane's zero-row address; lhi: lane is the fragment's second x position
-template <int TN, int WM, int KY, int KX>
+template <int TN, int WM, int KY, int KX, int WR>
 __device__ __forceinline__ void read8(const char* bsl, const char* pl, const uint32_t (&ao)[2],
-                                      const char* zp, bool lhi, Fr8<TN>& f) {
+                                      const char* zp, bool lhi, Fr8<TN, 4 * WR>& f) {
 #pragma unroll
   for (int j = 0; j < TN; ++j)
     f.b[j] = *reinterpret_cast<const bf16x8*>(bsl + (KX + 1) * BTAP8 + j * 16 * RB8);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    if (row_ok<WM, KY>(q)) {
+  for (int q = 0; q < 4 * WR; ++q) {
+    if (row_ok<WM, KY, WR>(q)) {
       constexpr int dummy = 0;
-      const int ty = 2 * WM + (q >> 2) + KY + dummy, x0 = 2 * (q & 3) + KX;
+      const int ty = WR * WM + (q >> 2) + KY + dummy, x0 = 2 * (q & 3) + KX;
       const int base = (ty * S8 + x0) * NC * RB8;       // may be -8 rows: lanes redirected
       const char* p = pl + base + ao[KX & 1];
       if (KX == -1 && (q & 3) == 0) p = lhi ? p : zp;
@@ -97,27 +98,28 @@ __device__ __forceinline__ void read8(const char* bsl, const char* pl, const uin
   }
 }
 
-template <int TN, int WM, int KY>
-__device__ __forceinline__ void mma8(f32x4 (&acc)[8][TN], const Fr8<TN>& f) {
+template <int TN, int WM, int KY, int WR>
+__device__ __forceinline__ void mma8(f32x4 (&acc)[4 * WR][TN], const Fr8<TN, 4 * WR>& f) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q)
-    if (row_ok<WM, KY>(q)) {
+  for (int q = 0; q < 4 * WR; ++q)
+    if (row_ok<WM, KY, WR>(q)) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[q], f.b[j], acc[q][j], 0, 0, 0);
     }
 }
 
-template <int TN, int WM, int KY>
-__device__ __forceinline__ void stage8(f32x4 (&acc)[8][TN], const char* bsl, const char* pl,
-                                       const uint32_t (&ao)[2], const char* zp, bool lhi) {
-  Fr8<TN> f0, f1;
-  read8<TN, WM, KY, -1>(bsl, pl, ao, zp, lhi, f0);
-  read8<TN, WM, KY, 0>(bsl, pl, ao, zp, lhi, f1);
-  mma8<TN, WM, KY>(acc, f0);
-  read8<TN, WM, KY, 1>(bsl, pl, ao, zp, lhi, f0);
-  mma8<TN, WM, KY>(acc, f1);
-  mma8<TN, WM, KY>(acc, f0);
+template <int TN, int WM, int KY, int WR>
+__device__ __forceinline__ void stage8(f32x4 (&acc)[4 * WR][TN], const char* bsl,
+                                       const char* pl, const uint32_t (&ao)[2], const char* zp,
+                                       bool lhi) {
+  Fr8<TN, 4 * WR> f0, f1;
+  read8<TN, WM, KY, -1, WR>(bsl, pl, ao, zp, lhi, f0);
+  read8<TN, WM, KY, 0, WR>(bsl, pl, ao, zp, lhi, f1);
+  mma8<TN, WM, KY, WR>(acc, f0);
+  read8<TN, WM, KY, 1, WR>(bsl, pl, ao, zp, lhi, f0);
+  mma8<TN, WM, KY, WR>(acc, f1);
+  mma8<TN, WM, KY, WR>(acc, f0);
 }
 
 // TN = 16-column MFMA tiles per wave: 2 (64-channel tiles) or 1 (32 channels, for layers
@@ -126,7 +128,10 @@ __device__ __forceinline__ void stage8(f32x4 (&acc)[8][TN], const char* bsl, con
 // 91 x 109 x 91 MNI volumes give 12 x 14 x 12 at layer3), as latticeconv.hip's RAG form:
 // the positions / planes a class lacks are LDS-DMA'd as zeros (buffer resource, offset past
 // its end) and skipped in the epilogue.
-template <int TN, bool RAG>
+// WR = plane rows per wave: 2 (4 x 2 waves of 128 rows x 16 TN channels) or 1 (8 waves of
+// 64 rows, one y row each, x 16 TN channels: the same tile width at TN doubled, 4 A + TN B
+// fragment reads per tap instead of 8 + TN / 2 ... for the same MFMAs)
+template <int TN, bool RAG, int WR>
 __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __restrict__ src,
                                                             const u16* __restrict__ wgt,
                                                             const float* __restrict__ bias,
@@ -143,7 +148,9 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   const int t2 = tile / g.nbn;
   const int NZ = RAG ? g.nz : S8;
   const int tz = t2 % NZ, n = t2 / NZ;
-  constexpr int BW = 16 * TN * 2;                  // output channels of this tile
+  constexpr int NFR = 4 * WR;                      // A fragments per wave
+  constexpr int NWM = 8 / WR, NWN = WR;            // wave rows x wave columns
+  constexpr int BW = 16 * TN * NWN;                // output channels of this tile
   const int n0 = nt * BW;
   constexpr int E = 2 * S8;                          // 16
 
@@ -199,17 +206,18 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   };
   // ---- weight DMA: 3 taps x BW rows x 64 B = 6*TN instructions; wave w issues q = w
   // and q = w + 8 (while < 6*TN); instruction q = tap q / (2TN), rows (q % 2TN) * 16 ..
-  constexpr int NQ = 3 * 2 * TN;
+  constexpr int NQ = 3 * BW / 16;
+  constexpr int QB = BW / 16;                      // 16-row weight pieces per tap
   const int nbi = (wave < NQ ? 1 : 0) + (wave + 8 < NQ ? 1 : 0);
   const u16* wq[2];
   int wslot_off[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int q = min(wave + 8 * h, NQ - 1);
-    const int row = (q % (2 * TN)) * 16 + lrow;
+    const int row = (q % QB) * 16 + lrow;
     wq[h] = wgt + (int64_t)(n0 + row) * g.Kpad + ((lane & 3) ^ swz8(row)) * 8 +
-            (q / (2 * TN)) * g.Cs;
-    wslot_off[h] = (q / (2 * TN)) * BTAP8 + (q % (2 * TN)) * 1024;
+            (q / QB) * g.Cs;
+    wslot_off[h] = (q / QB) * BTAP8 + (q % QB) * 1024;
   }
   auto issue_b = [&](int cc, int t, int sl) {
 #pragma unroll
@@ -236,7 +244,7 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
     return true;
   };
 
-  const int wm = wave & 3, wn = wave >> 2;
+  const int wm = wave % NWM, wn = wave / NWM;
   const int lr = lane & 15, lk = lane >> 4;
   const bool lhi = (lr >> 3) != 0;
   uint32_t ao[2];
@@ -244,9 +252,9 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   ao[1] = lr * RB8 + ((lk ^ (3 - swz8(lr))) << 4);   // rows shifted by 8: the other swizzle
   const char* zp = smem + ZERO8 + (lk << 4);
   const uint32_t b_lane = (wn * 16 * TN + lr) * RB8 + ((lk ^ swz8(lr)) << 4);
-  f32x4 acc[8][TN];
+  f32x4 acc[NFR][TN];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < NFR; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -292,11 +300,11 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
       const char* pl = smem + (kz + 1) * PLANE8;
       const int s0 = g2 * 3;
       one_stage(s0);
-      stage8<TN, WM, -1>(acc, ring + (s0 % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
+      stage8<TN, WM, -1, WR>(acc, ring + (s0 % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
       one_stage(s0 + 1);
-      stage8<TN, WM, 0>(acc, ring + ((s0 + 1) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
+      stage8<TN, WM, 0, WR>(acc, ring + ((s0 + 1) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
       one_stage(s0 + 2);
-      stage8<TN, WM, 1>(acc, ring + ((s0 + 2) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
+      stage8<TN, WM, 1, WR>(acc, ring + ((s0 + 2) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
     }
   };
   // L8_PIPE: stage s's barrier sits between its kx = 0 and kx = +1 MFMAs.  Before it each
@@ -323,8 +331,8 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
     else if (2 < nstage && nbi == 1) wait_vm_lgkm0<2>();
     else wait_vm_lgkm0<0>();
     raw_barrier();
-    Fr8<TN> f0, f1;
-    read8<TN, WM, -1, -1>(ring + b_lane, smem + (kz0 + 1) * PLANE8, ao, zp, lhi, f0);
+    Fr8<TN, NFR> f0, f1;
+    read8<TN, WM, -1, -1, WR>(ring + b_lane, smem + (kz0 + 1) * PLANE8, ao, zp, lhi, f0);
     int pl_prev = 0;                                // plane instructions of group s - 1
     auto barrier_dma = [&](int s) {
       const int younger = (s + 2 < nstage ? nbi : 0) + pl_prev;
@@ -355,19 +363,19 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
       const char* pl = smem + (kz + 1) * PLANE8;
       const char* pln = smem + (kzn + 1) * PLANE8;
       const int s0 = g2 * 3;
-      auto stage = [&](auto kyc, int s, Fr8<TN>& fa, Fr8<TN>& fb) {
+      auto stage = [&](auto kyc, int s, Fr8<TN, NFR>& fa, Fr8<TN, NFR>& fb) {
         constexpr int KY = decltype(kyc)::value;
         constexpr int KYN = KY < 1 ? KY + 1 : -1;
         int boff = RING8 + (s % NSL8) * BSLOT8, bnof = RING8 + ((s + 1) % NSL8) * BSLOT8;
         asm volatile("" : "+s"(boff), "+s"(bnof));
         const char* bsl = smem + boff + b_lane;
-        read8<TN, WM, KY, 0>(bsl, pl, ao, zp, lhi, fb);
-        mma8<TN, WM, KY>(acc, fa);
-        read8<TN, WM, KY, 1>(bsl, pl, ao, zp, lhi, fa);
-        mma8<TN, WM, KY>(acc, fb);
+        read8<TN, WM, KY, 0, WR>(bsl, pl, ao, zp, lhi, fb);
+        mma8<TN, WM, KY, WR>(acc, fa);
+        read8<TN, WM, KY, 1, WR>(bsl, pl, ao, zp, lhi, fa);
+        mma8<TN, WM, KY, WR>(acc, fb);
         barrier_dma(s);
-        read8<TN, WM, KYN, -1>(smem + bnof + b_lane, KY < 1 ? pl : pln, ao, zp, lhi, fb);
-        mma8<TN, WM, KY>(acc, fa);
+        read8<TN, WM, KYN, -1, WR>(smem + bnof + b_lane, KY < 1 ? pl : pln, ao, zp, lhi, fb);
+        mma8<TN, WM, KY, WR>(acc, fa);
       };
       stage(std::integral_constant<int, -1>{}, s0, f0, f1);
       stage(std::integral_constant<int, 0>{}, s0 + 1, f1, f0);
@@ -375,16 +383,26 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
       f0 = f1;
     }
   };
-  switch (wm) {
-    case 0: L8_PIPE ? run_pipe(std::integral_constant<int, 0>{}) : run(std::integral_constant<int, 0>{}); break;
-    case 1: L8_PIPE ? run_pipe(std::integral_constant<int, 1>{}) : run(std::integral_constant<int, 1>{}); break;
-    case 2: L8_PIPE ? run_pipe(std::integral_constant<int, 2>{}) : run(std::integral_constant<int, 2>{}); break;
-    default: L8_PIPE ? run_pipe(std::integral_constant<int, 3>{}) : run(std::integral_constant<int, 3>{}); break;
+  auto dispatch = [&](auto wmc) {
+    if constexpr (decltype(wmc)::value < NWM) {
+      if constexpr (L8_PIPE) run_pipe(wmc);
+      else run(wmc);
+    }
+  };
+  switch (wm) {                                     // wave-uniform
+    case 0: dispatch(std::integral_constant<int, 0>{}); break;
+    case 1: dispatch(std::integral_constant<int, 1>{}); break;
+    case 2: dispatch(std::integral_constant<int, 2>{}); break;
+    case 3: dispatch(std::integral_constant<int, 3>{}); break;
+    case 4: dispatch(std::integral_constant<int, 4>{}); break;
+    case 5: dispatch(std::integral_constant<int, 5>{}); break;
+    case 6: dispatch(std::integral_constant<int, 6>{}); break;
+    default: dispatch(std::integral_constant<int, 7>{}); break;
   }
   __syncthreads();                                  // patch / ring reused by the epilogue
 
   // ---- epilogue: acc[q][j][e] is tile row (ty*8 + 2*(q&3))*8 + lk*4 + e with
-  // ty = 2*wm + (q >> 2), column wn*32 + j*16 + lr
+  // ty = WR*wm + (q >> 2), column wn*16*TN + j*16 + lr
   // (RAG: -1 for a row outside the grid)
   auto dst_vox = [&](int row) -> int64_t {
     const int pos = row >> 3, c = row & 7;
@@ -398,14 +416,14 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
            2 * tx;
   };
   u16* ctile = reinterpret_cast<u16*>(smem);
-  // RAG: which of this lane's 32 accumulator rows lie inside the grid (bit q*4 + e)
+  // RAG: which of this lane's 4 NFR accumulator rows lie inside the grid (bit q*4 + e)
   uint32_t vmask = 0xffffffffu;
   if constexpr (RAG) {
     vmask = 0;
 #pragma unroll 1
-    for (int b = 0; b < 32; ++b) {
+    for (int b = 0; b < 4 * NFR; ++b) {
       const int q = b >> 2, e = b & 3;
-      const int row = ((2 * wm + (q >> 2)) * S8 + 2 * (q & 3)) * NC + lk * 4 + e;
+      const int row = ((WR * wm + (q >> 2)) * S8 + 2 * (q & 3)) * NC + lk * 4 + e;
       if (dst_vox(row) >= 0) vmask |= 1u << b;
     }
   }
@@ -417,8 +435,8 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
     const int col = wn * 16 * TN + j * 16 + lr;
     const float bv = bias != nullptr ? bias[n0 + col] : 0.f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int ty = 2 * wm + (q >> 2);
+    for (int q = 0; q < NFR; ++q) {
+      const int ty = WR * wm + (q >> 2);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = (ty * S8 + 2 * (q & 3)) * NC + lk * 4 + e;
@@ -469,7 +487,7 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
       for (int j = 0; j < TN; ++j) {
         const int col = wn * 16 * TN + j * 16 + lr;
         float ss = cs[j], qs = cq[j];
-        for (int w = 1; w < 4; ++w) {              // fixed order: deterministic
+        for (int w = 1; w < NWM; ++w) {            // fixed order: deterministic
           ss += red[(w - 1) * 2 * BW + col];
           qs += red[(w - 1) * 2 * BW + BW + col];
         }
@@ -491,6 +509,16 @@ int lattice8_mode() {
     g_lattice8_mode.compare_exchange_strong(expect, e ? atoi(e) : 1);
     v = g_lattice8_mode.load(std::memory_order_relaxed);
   }
+  return v;
+}
+
+// MMAD_L8_ROWS: plane rows per wave, 1 (default: 64-row wave tiles at twice the columns,
+// fewer A-fragment reads per MFMA) or 2 (128-row wave tiles)
+int l8_rows() {
+  static const int v = [] {
+    const char* e = getenv("MMAD_L8_ROWS");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
   return v;
 }
 
@@ -538,15 +566,19 @@ int64_t tiles(const mmad_patch::Geo& q) { return (int64_t)q.nb * planes8(q); }
 int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias,
         void* dst, float* stats, void* stream) {
   if (!mmad_lattice8::ok(q)) return MMAD_EUNSUPPORTED;
+  auto attr1 = [](const void* k) {
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) ==
+           hipSuccess;
+  };
   static const bool attr =
-      hipFuncSetAttribute((const void*)lattice8_conv_kernel<2, false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) == hipSuccess &&
-      hipFuncSetAttribute((const void*)lattice8_conv_kernel<1, false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) == hipSuccess &&
-      hipFuncSetAttribute((const void*)lattice8_conv_kernel<2, true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) == hipSuccess &&
-      hipFuncSetAttribute((const void*)lattice8_conv_kernel<1, true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS8) == hipSuccess;
+      attr1((const void*)lattice8_conv_kernel<2, false, 2>) &&
+      attr1((const void*)lattice8_conv_kernel<1, false, 2>) &&
+      attr1((const void*)lattice8_conv_kernel<2, true, 2>) &&
+      attr1((const void*)lattice8_conv_kernel<1, true, 2>) &&
+      attr1((const void*)lattice8_conv_kernel<4, false, 1>) &&
+      attr1((const void*)lattice8_conv_kernel<2, false, 1>) &&
+      attr1((const void*)lattice8_conv_kernel<4, true, 1>) &&
+      attr1((const void*)lattice8_conv_kernel<2, true, 1>);
   if (!attr) return MMAD_EUNSUPPORTED;
   const bool rag = !exact8(q);
   const int nz = planes8(q);
@@ -564,8 +596,13 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
     hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(NT8), LDS8, as_stream(stream), g,
                        (const u16*)src, (const u16*)wp, bias, (u16*)dst, stats);
   };
-  if (wide) rag ? go(lattice8_conv_kernel<2, true>) : go(lattice8_conv_kernel<2, false>);
-  else rag ? go(lattice8_conv_kernel<1, true>) : go(lattice8_conv_kernel<1, false>);
+  if (l8_rows() == 1) {                             // one plane row per wave
+    if (wide) rag ? go(lattice8_conv_kernel<4, true, 1>) : go(lattice8_conv_kernel<4, false, 1>);
+    else rag ? go(lattice8_conv_kernel<2, true, 1>) : go(lattice8_conv_kernel<2, false, 1>);
+  } else {                                          // two plane rows per wave
+    if (wide) rag ? go(lattice8_conv_kernel<2, true, 2>) : go(lattice8_conv_kernel<2, false, 2>);
+    else rag ? go(lattice8_conv_kernel<1, true, 2>) : go(lattice8_conv_kernel<1, false, 2>);
+  }
   return launch_status();
 }
 
