@@ -189,7 +189,8 @@ def test_capture_after_eager_default_stream_steps():
         assert torch.equal(pa, pb), na
 
 
-def test_graph_with_allreduce_after_replay_equals_eager():
+@pytest.mark.parametrize("overlap", [False, True], ids=["after_replay", "mid_replay_events"])
+def test_graph_with_allreduce_after_replay_equals_eager(overlap):
     """bench.py's N > 1 launch mode at one RCCL rank: forward + backward replayed from the
     graph (gradients straight into the bucket slices), the bucketed all-reduces issued
     eagerly after the replay, then the captured Adam -- bit-identical to plain eager steps
@@ -201,7 +202,7 @@ def test_graph_with_allreduce_after_replay_equals_eager():
     b = copy.deepcopy(a)
     batches = [_batch(40 + i) for i in range(3)]
     warm = 2
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29563", rank=0, world_size=1,
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{29563 + int(overlap)}", rank=0, world_size=1,
                             device_id=torch.device("cuda", torch.cuda.current_device()))
     try:
         opt_a = a.configure_optimizers()
@@ -221,7 +222,8 @@ def test_graph_with_allreduce_after_replay_equals_eager():
             losses_a.append(out["loss"].detach().clone())
         opt_b = b.configure_optimizers()
         red = GradAllReduce(b.parameters(), bucket_mb=4.0)
-        gs = GraphedTrainStep(b, opt_b, batches[0], warmup=warm, reducer=red, collectives="after")
+        gs = GraphedTrainStep(b, opt_b, batches[0], warmup=warm, reducer=red, collectives="after",
+                              overlap=overlap)
         assert gs.opt_graph is not None
         losses_b = [gs(batches[i])["loss"].clone() for i in range(3)]
         torch.cuda.synchronize()
