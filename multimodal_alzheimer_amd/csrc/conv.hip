@@ -1285,12 +1285,26 @@ int big_cfg() {
   static const int v = [] { const char* e = getenv("MMAD_IGEMM_BIG"); return e ? atoi(e) : 0; }();
   return v;
 }
+int big_min_k() {
+  static const int v = [] { const char* e = getenv("MMAD_IGEMM_BIG_MINK"); return e ? atoi(e) : 1024; }();
+  return v;
+}
+// ring depth of the default (4-wave) tiles: 2, or 3 (MMAD_IGEMM_NST=3: two stages of
+// LDS-DMA in flight, still two blocks per CU at 64 x 128 / 128 x 64 tiles; for the shallow,
+// latency-bound grids such as the stride-2 layer2.0.conv1)
+int igemm_nst() {
+  static const int v = [] { const char* e = getenv("MMAD_IGEMM_NST"); return e ? atoi(e) : 2; }();
+  return v;
+}
 int big_cfg_for(const Geom& g, int dtype, int64_t m_max, int classes) {
   if (dtype != MMAD_BF16) return 0;
   int cfg = big_cfg();
   if (cfg < 0) return 0;                        // MMAD_IGEMM_BIG=-1: 128 x 128 tiles only
-  if (cfg == 0)   // default: 256 x 256 tiles (8 waves) when they give every CU a block
-    return g.Nd % 256 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 256) >= 256 ? 2 : 0;
+  if (cfg == 0)   // default: 256 x 256 tiles (8 waves) when they give every CU a block and
+                  // K is deep enough to amortise their epilogue (the 1x1x1 shortcut, K = 256,
+                  // is epilogue-bound at one block per CU; MMAD_IGEMM_BIG_MINK=0 keeps them)
+    return g.Nd % 256 == 0 && g.K >= big_min_k() &&
+                   cdiv(m_max, 256) * classes * (g.Nd / 256) >= 256 ? 2 : 0;
   if (cfg == 4) return g.Nd % 128 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 128) >= 256 ? 4 : 0;
   if (cfg == 5 || cfg == 6)
     return g.Nd % 256 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 256) >= 256 ? cfg : 0;
@@ -1336,6 +1350,15 @@ int run_igemm_t(const Geom& g, int64_t m_max, int classes, const void* src, cons
     }
   }
   const bool small = igemm_bm(m_max * classes, g) == 64;
+  if constexpr (sizeof(T) == 2) {
+    if (igemm_nst() == 3) {
+      if (bn_of(g) == 64)
+        return small ? launch_igemm_bm<T, 64, MODE, 64, 2, 2, 3>(g, m_max, classes, src, w, bias, dst, stats, st)
+                     : launch_igemm_bm<T, 64, MODE, 128, 2, 2, 3>(g, m_max, classes, src, w, bias, dst, stats, st);
+      return small ? launch_igemm_bm<T, 128, MODE, 64, 2, 2, 3>(g, m_max, classes, src, w, bias, dst, stats, st)
+                   : launch_igemm_bm<T, 128, MODE, 128, 2, 2, 3>(g, m_max, classes, src, w, bias, dst, stats, st);
+    }
+  }
   if (bn_of(g) == 64)
     return small ? launch_igemm_bm<T, 64, MODE, 64>(g, m_max, classes, src, w, bias, dst, stats, st)
                  : launch_igemm_bm<T, 64, MODE, 128>(g, m_max, classes, src, w, bias, dst, stats, st);

@@ -133,8 +133,11 @@ class GradAllReduce:
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             if self.defer and self.record_events:
-                ev = torch.cuda.Event(external=True)
-                ev.record()
+                # an event-record node of the captured graph (torch refuses external
+                # events on ROCm; the C ABI records one with hipEventRecordExternal)
+                from . import _lib as L
+                ev = L.GraphEvent()
+                ev.record(L.stream())
                 self.events[bi] = ev
             if not self.defer:
                 self._launch(bi)
@@ -164,7 +167,8 @@ class GradAllReduce:
             main = torch.cuda.current_stream()
             side = grad_stream(flat.device)
             if after is not None:
-                side.wait_event(after)         # this bucket's gradients, mid-replay
+                from . import _lib as L
+                after.wait(side.cuda_stream)   # this bucket's gradients, mid-replay
             else:
                 side.wait_stream(main)
             with torch.cuda.stream(side):

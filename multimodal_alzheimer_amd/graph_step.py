@@ -71,7 +71,9 @@ class GraphedTrainStep:
         self.opt_graph = None
         if self.after:
             reducer.defer = os.environ.get("MMAD_GRAPH_DEBUG", "") != "nodefer"
-            reducer.record_events = bool(overlap)
+            # (with wgrads on volume_ops' side stream a mid-backward record on the main
+            # stream would not cover them: overlap needs them on the main stream)
+            reducer.record_events = bool(overlap) and not volume_ops.WGRAD_STREAM
             reducer.events = {}
             try:
                 with torch.cuda.graph(self.graph):
