@@ -171,10 +171,6 @@ def main():
                     help="under torchrun: capture the RCCL bucket all-reduces inside the step's "
                          "graph too (opt-in, one-rank checked); the default graph-replays "
                          "forward + backward and runs the all-reduces eagerly after it")
-    ap.add_argument("--no-overlap", action="store_true",
-                    help="N > 1 graph mode: launch the bucket all-reduces only after the whole "
-                         "replayed backward (default: each behind an event its bucket records "
-                         "inside the captured backward, overlapping the rest of it)")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel of every step from Python, the all-reduces from "
                          "the backward's hooks (overlapped with it)")
@@ -258,10 +254,8 @@ def main():
     # the host needs ~2.9 of the GPU's ~3.5 ms per step to enqueue it, so a slower or busier
     # host makes the run launch-bound (measured: 1713 vol/s on one box).  N>1 uses the same
     # launch mode, so the 1 -> N curve compares like with like: forward + backward replayed
-    # from the graph, then the bucketed RCCL all-reduces issued eagerly -- each on the side
-    # stream behind an event its bucket recorded inside the captured backward, so it
-    # overlaps the rest of the replayed backward (--no-overlap: behind the whole replay;
-    # ~57 MB of fp32 gradients per step for ResNet-10) -- then the captured Adam.
+    # from the graph, then the bucketed RCCL all-reduces issued eagerly (not overlapped with
+    # the backward: ~57 MB of fp32 gradients per step for ResNet-10), then the captured Adam.
     # --graph captures the all-reduces inside the graph (overlapped; one-rank checked only),
     # --eager launches them from the backward's hooks (overlapped; host-bound).
     use_graph = not args.eager and (args.graph or args.workload == "mri")
@@ -282,8 +276,7 @@ def main():
             torch.cuda.synchronize()
             volume_ops.FWD_PROBES.clear()
         gstep = GraphedTrainStep(model, opt, batch, warmup=max(1, args.warmup),
-                                 reducer=reducer, collectives=collectives,
-                                 overlap=not args.no_overlap)
+                                 reducer=reducer, collectives=collectives)
         gstep()
 
         def step(timed=False):
@@ -349,9 +342,7 @@ def main():
         result["hbm_roofline_frac_m2"] = per_gpu * M2_BYTES_PER_VOL / PEAK_HBM
     result["config"]["step_launch"] = (
         "eager" if not use_graph else "hip graph replay" if reducer is None else
-        ("hip graph replay (fwd+bwd) + eager RCCL all-reduce" +
-         (" behind the full replay" if args.no_overlap else
-          " behind mid-replay bucket events") + " + graph-replayed Adam")
+        "hip graph replay (fwd+bwd) + eager RCCL all-reduce + graph-replayed Adam"
         if collectives == "after" else "hip graph replay incl. RCCL all-reduce")
     # host time spent enqueueing each step: close to ms_per_step means the run was bound by
     # the host (Python / launch overhead), not by the GPU

@@ -63,15 +63,6 @@ const char* mmad_strerror(int status);
  * Returns the previous value, -1 for an unknown name.  Not thread-safe against concurrent
  * launches. */
 int mmad_set_kernel_variant(const char* name, int value);
-/* Graph-crossing events (no reference counterpart: plumbing for the overlapped gradient
- * all-reduce of a replayed step, multimodal_alzheimer_amd/graph_step.py).  An event
- * recorded with mmad_event_record_external inside a stream capture becomes an event-record
- * node of the graph; eager work on another stream can then wait for that point of a replay
- * (mmad_stream_wait_event).  Timing is disabled on these events. */
-int mmad_event_create(void** ev);
-int mmad_event_record_external(void* ev, void* stream);
-int mmad_stream_wait_event(void* stream, void* ev);
-int mmad_event_destroy(void* ev);
 
 /* ---- 3D convolution as MFMA implicit GEMM --------------------------------------
  * Replaces nn.Conv3d forward/backward: MedicalNet conv1 / BasicBlock / Bottleneck /

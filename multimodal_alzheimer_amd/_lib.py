@@ -138,10 +138,6 @@ _SIGS = {
     "mmad_mean_std": (_i32, [_i32, _vp, _vp, _vp]),
     "mmad_bn_relu_bwd_reduce": (_i32, [_i32, _i64, _i32] + [_vp] * 8),
     "mmad_bn_relu_bwd_apply": (_i32, [_i32, _i64, _i32] + [_vp] * 9),
-    "mmad_event_create": (_i32, [C.POINTER(C.c_void_p)]),
-    "mmad_event_record_external": (_i32, [_vp, _vp]),
-    "mmad_stream_wait_event": (_i32, [_vp, _vp]),
-    "mmad_event_destroy": (_i32, [_vp]),
 }
 EXPORTS = tuple(_SIGS)
 
@@ -215,25 +211,3 @@ def require_device(*tensors):
                             f"(got a tensor on {t.device}); move the model and batch to "
                             "'cuda' -- there is no CPU fallback")
 
-
-class GraphEvent:
-    """A HIP event that may be recorded inside a stream capture (hipEventRecordExternal:
-    an event-record node of the graph) and waited on by eager work on another stream after
-    each replay.  torch.cuda.Event(external=True) is refused on ROCm; HIP supports it."""
-
-    def __init__(self):
-        h = C.c_void_p()
-        call("mmad_event_create", C.byref(h))
-        self._h = h.value
-
-    def record(self, stream_ptr):
-        call("mmad_event_record_external", self._h, stream_ptr)
-
-    def wait(self, stream_ptr):
-        """make ``stream_ptr`` wait for the last execution of the record"""
-        call("mmad_stream_wait_event", stream_ptr, self._h)
-
-    def __del__(self):
-        h, self._h = getattr(self, "_h", None), None
-        if h and _lib is not None:
-            _lib.mmad_event_destroy(h)

@@ -1289,12 +1289,15 @@ int big_min_k() {
   static const int v = [] { const char* e = getenv("MMAD_IGEMM_BIG_MINK"); return e ? atoi(e) : 1024; }();
   return v;
 }
-// ring depth of the default (4-wave) tiles: 2, or 3 (MMAD_IGEMM_NST=3: two stages of
-// LDS-DMA in flight, still two blocks per CU at 64 x 128 / 128 x 64 tiles; for the shallow,
-// latency-bound grids such as the stride-2 layer2.0.conv1)
-int igemm_nst() {
-  static const int v = [] { const char* e = getenv("MMAD_IGEMM_NST"); return e ? atoi(e) : 2; }();
-  return v;
+// ring depth of the default (4-wave) tiles: 3 (two stages of LDS-DMA in flight, still two
+// blocks per CU at 64 x 128 tiles) for strided forward convs, 2 elsewhere.  Measured in the
+// config-2 step (r03s): layer2.0.conv1 fwd 39.3 -> 33.1 us, its 1x1x1 shortcut 8.4 -> 8.2;
+// every stride-1 launch and the parity-class dgrads were slower at 3 (e.g. 57.9 -> 71.6
+// us).  MMAD_IGEMM_NST=2 / 3 forces one depth everywhere (A/B).
+int igemm_nst(const Geom& g, int mode) {
+  static const int v = [] { const char* e = getenv("MMAD_IGEMM_NST"); return e ? atoi(e) : 0; }();
+  if (v) return v;
+  return mode == FWD && (g.sd > 1 || g.sh > 1 || g.sw > 1) ? 3 : 2;
 }
 int big_cfg_for(const Geom& g, int dtype, int64_t m_max, int classes) {
   if (dtype != MMAD_BF16) return 0;
@@ -1351,7 +1354,7 @@ int run_igemm_t(const Geom& g, int64_t m_max, int classes, const void* src, cons
   }
   const bool small = igemm_bm(m_max * classes, g) == 64;
   if constexpr (sizeof(T) == 2) {
-    if (igemm_nst() == 3) {
+    if (igemm_nst(g, MODE) == 3) {
       if (bn_of(g) == 64)
         return small ? launch_igemm_bm<T, 64, MODE, 64, 2, 2, 3>(g, m_max, classes, src, w, bias, dst, stats, st)
                      : launch_igemm_bm<T, 64, MODE, 128, 2, 2, 3>(g, m_max, classes, src, w, bias, dst, stats, st);

@@ -504,38 +504,6 @@ int mmad_mean_std(int n, const float* v, double* out, void* stream) {
 
 int mmad_abi_version(void) { return MMAD_ABI_VERSION; }
 
-// Graph-crossing events (plumbing for graph_step's overlapped all-reduce; torch refuses
-// external events on ROCm, HIP itself supports them): recorded with hipEventRecordExternal
-// inside a stream capture they become event-record nodes of the graph, so eager work on
-// another stream can wait for a point in the middle of a replay.
-int mmad_event_create(void** ev) {
-  if (!ev) return MMAD_ENULL;
-  hipEvent_t e = nullptr;
-  const hipError_t rc = hipEventCreateWithFlags(&e, hipEventDisableTiming);
-  if (rc != hipSuccess) return MMAD_EHIP + (int)rc;
-  *ev = (void*)e;
-  return MMAD_OK;
-}
-
-int mmad_event_record_external(void* ev, void* stream) {
-  if (!ev) return MMAD_ENULL;
-  const hipError_t rc = hipEventRecordWithFlags((hipEvent_t)ev, as_stream(stream),
-                                                hipEventRecordExternal);
-  return rc == hipSuccess ? MMAD_OK : MMAD_EHIP + (int)rc;
-}
-
-int mmad_stream_wait_event(void* stream, void* ev) {
-  if (!ev) return MMAD_ENULL;
-  const hipError_t rc = hipStreamWaitEvent(as_stream(stream), (hipEvent_t)ev, 0);
-  return rc == hipSuccess ? MMAD_OK : MMAD_EHIP + (int)rc;
-}
-
-int mmad_event_destroy(void* ev) {
-  if (!ev) return MMAD_OK;
-  const hipError_t rc = hipEventDestroy((hipEvent_t)ev);
-  return rc == hipSuccess ? MMAD_OK : MMAD_EHIP + (int)rc;
-}
-
 const char* mmad_strerror(int s) {
   switch (s) {
     case MMAD_OK: return "ok";

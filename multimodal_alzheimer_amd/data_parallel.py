@@ -115,13 +115,6 @@ class GradAllReduce:
         # forward + backward is captured without its collectives (graph_step
         # collectives="after"): a replay runs no Python hooks, so finish() does it all.
         self.defer = False
-        # record_events (with defer, while a graph is captured): a completed bucket records
-        # an external event in the backward -- an event-record node of the graph -- so that
-        # after each replay launch_recorded() can start that bucket's all-reduce on the side
-        # stream as soon as the replay has produced its gradients, overlapping the rest of
-        # the replayed backward, with no collective inside the graph
-        self.record_events = False
-        self.events = {}
         self.reset()
 
     def reset(self):
@@ -131,23 +124,8 @@ class GradAllReduce:
     def _ready(self, p):
         bi = self._owner[p]
         self._pending[bi] -= 1
-        if self._pending[bi] == 0:
-            if self.defer and self.record_events:
-                # an event-record node of the captured graph (torch refuses external
-                # events on ROCm; the C ABI records one with hipEventRecordExternal)
-                from . import _lib as L
-                ev = L.GraphEvent()
-                ev.record(L.stream())
-                self.events[bi] = ev
-            if not self.defer:
-                self._launch(bi)
-
-    def launch_recorded(self):
-        """After a graph replay: launch every bucket that recorded an event during the
-        capture, in readiness order, each behind its event (not behind the whole replay)."""
-        for bi, ev in self.events.items():
-            if bi not in self._inflight:
-                self._launch(bi, after=ev)
+        if self._pending[bi] == 0 and not self.defer:
+            self._launch(bi)
 
     def _foreign(self, bi):
         """(grads, views) of the bucket's parameters whose .grad is not their slice."""
@@ -155,7 +133,7 @@ class GradAllReduce:
                  if p.grad.data_ptr() != self._views[p].data_ptr()]
         return [g for g, _ in pairs], [v for _, v in pairs]
 
-    def _launch(self, bi, after=None):
+    def _launch(self, bi):
         flat = self.flats[bi]
         grads, views = self._foreign(bi)
         if flat.is_cuda:
@@ -166,11 +144,7 @@ class GradAllReduce:
             from .volume_ops import grad_stream
             main = torch.cuda.current_stream()
             side = grad_stream(flat.device)
-            if after is not None:
-                from . import _lib as L
-                after.wait(side.cuda_stream)   # this bucket's gradients, mid-replay
-            else:
-                side.wait_stream(main)
+            side.wait_stream(main)
             with torch.cuda.stream(side):
                 if grads:
                     torch._foreach_copy_(views, grads)

@@ -34,8 +34,7 @@ from . import volume_ops
 
 
 class GraphedTrainStep:
-    def __init__(self, model, optimizer, batch, warmup=3, reducer=None, collectives="inside",
-                 overlap=False):
+    def __init__(self, model, optimizer, batch, warmup=3, reducer=None, collectives="inside"):
         """``reducer``: a data_parallel.GradAllReduce.  ``collectives``:
         * "inside": its bucket all-reduces (launched from the backward's hooks) and
           ``finish()`` are captured with the step (experimental: bench.py --graph under
@@ -44,10 +43,7 @@ class GraphedTrainStep:
           slices); each call replays it, then runs ``finish()`` eagerly -- every bucket's
           RCCL all-reduce on the side stream, not overlapped with the backward -- then
           replays the captured optimizer step.  No collective inside a graph; the host
-          issues a handful of calls per step (bench.py's default at N > 1).
-        ``overlap`` (with "after"): each completed bucket records an external event inside
-        the captured backward; after each replay its all-reduce is launched behind that
-        event, so it overlaps the rest of the replayed backward."""
+          issues a handful of calls per step (bench.py's default at N > 1)."""
         self.model, self.optimizer = model, optimizer
         self.reducer = reducer
         self.after = reducer is not None and collectives == "after"
@@ -71,10 +67,6 @@ class GraphedTrainStep:
         self.opt_graph = None
         if self.after:
             reducer.defer = os.environ.get("MMAD_GRAPH_DEBUG", "") != "nodefer"
-            # (with wgrads on volume_ops' side stream a mid-backward record on the main
-            # stream would not cover them: overlap needs them on the main stream)
-            reducer.record_events = bool(overlap) and not volume_ops.WGRAD_STREAM
-            reducer.events = {}
             try:
                 with torch.cuda.graph(self.graph):
                     self.out = model.general_step(self.static, 0, "train")
@@ -87,7 +79,6 @@ class GraphedTrainStep:
                         self._tail = torch.zeros(1, device=self.static_device()).add_(1)
             finally:
                 reducer.defer = False
-                reducer.record_events = False
             reducer.reset()                  # the capture's hooks only counted
             reducer.finish()                 # eager: gradients now averaged in place
             self.opt_graph = torch.cuda.CUDAGraph()
@@ -137,8 +128,7 @@ class GraphedTrainStep:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-            self.reducer.launch_recorded()   # buckets behind their mid-replay events
-            self.reducer.finish()            # the rest: no hook ran in the replay
+            self.reducer.finish()            # no hook ran in the replay: launches every bucket
             if self.finish_events is not None:
                 e1.record()
                 self.finish_events.append((e0, e1))
