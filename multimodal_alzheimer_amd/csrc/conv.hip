@@ -1202,6 +1202,10 @@ bool use_pwgrad(const Geom& g, int dtype) {
   return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
          mmad_pwgrad::ok(patch_geo(g));
 }
+// the parity-sub-patch kernel (s2conv.hip) for the stride-2 3^3 forward (layer2.0.conv1)
+bool use_s2(const Geom& g, int dtype) {
+  return dtype == MMAD_BF16 && mmad_s2::ok(patch_geo(g), g.sd, g.sh, g.sw);
+}
 bool use_lattice_wgrad(const Geom& g, int dtype) {
   return dtype == MMAD_BF16 && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
          mmad_lattice::wgrad_ok(patch_geo(g));
@@ -1613,6 +1617,7 @@ int64_t mmad_conv3d_stats_rows(const mmad_conv_desc* d, int dtype) {
   if (!unfolded(d) && use_lattice(g, dtype)) return mmad_lattice::tiles(patch_geo(g));
   if (!unfolded(d) && use_lattice8(g, dtype)) return mmad_lattice8::tiles(patch_geo(g));
   if (!unfolded(d) && use_patch(g, dtype)) return mmad_patch::tiles(patch_geo(g));
+  if (!unfolded(d) && use_s2(g, dtype)) return mmad_s2::tiles(patch_geo(g));
   return cdiv(g.M, fwd_tile_rows(g, dtype));
 }
 
@@ -1631,6 +1636,8 @@ int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x, const voi
     return mmad_lattice8::fwd(patch_geo(g), x, wp, bias, y, stats, stream);
   if (!unfolded(d) && use_patch(g, dtype))
     return mmad_patch::fwd(patch_geo(g), x, wp, bias, y, stats, stream);
+  if (!unfolded(d) && use_s2(g, dtype))
+    return mmad_s2::fwd(patch_geo(g), g.sd, g.sh, g.sw, x, wp, bias, y, stats, stream);
   return run_igemm<FWD>(g, dtype, g.M, 1, x, wp, bias, y, stats, as_stream(stream));
 }
 
@@ -1659,6 +1666,12 @@ int mmad_conv3d_fwd_ex(const mmad_conv_desc* d, int dtype, const void* x, const 
     q.relu = g.relu;
     return mmad_patch::fwd(q, x, wp, bias, y, stats, stream);
   }
+  if (use_s2(g, dtype)) {
+    mmad_patch::Geo q = patch_geo(g);
+    q.res = res;
+    q.relu = g.relu;
+    return mmad_s2::fwd(q, g.sd, g.sh, g.sw, x, wp, bias, y, stats, stream);
+  }
   return run_igemm<FWD>(g, dtype, g.M, 1, x, wp, bias, y, stats, as_stream(stream));
 }
 
@@ -1684,6 +1697,7 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
     return run_igemm<FWD>(gf, dtype, gf.M, 1, dy, wpt, nullptr, dx, nullptr,
                           as_stream(stream));
   }
+  if (dtype == MMAD_BF16 && mmad_s2::dgrad_ok(d)) return mmad_s2::dgrad(d, dy, wpt, dx, stream);
   const Geom g = dgrad_geom(d, dtype);
   if (!geom_ok(g, dtype)) return MMAD_EUNSUPPORTED;
   // the largest parity class (0,0,0) sizes the grid

@@ -49,6 +49,20 @@ int wgrad(const mmad_patch::Geo& g, const void* x, const void* dy, float* ws, in
           void* stream);
 }  // namespace mmad_lattice
 
+// Stride-2 3^3 conv forward on parity sub-patches (s2conv.hip, layer2.0.conv1: 64 input
+// channels, even input extents, whole 2 x 8 x 8 output boxes); strides passed separately
+// (Geo has none).  One BN partial-sum row per output box.
+namespace mmad_s2 {
+bool ok(const mmad_patch::Geo& g, int sd, int sh, int sw);
+int64_t tiles(const mmad_patch::Geo& g);
+int fwd(const mmad_patch::Geo& g, int sd, int sh, int sw, const void* src, const void* wp,
+        const float* bias, void* dst, float* stats, void* stream);
+// its input gradient (64 ci, 128 co, bf16; dgrad-packed weights [ci][tap][co]): all 8
+// stride-parity classes of dX from one dY patch per block
+bool dgrad_ok(const mmad_conv_desc* d);
+int dgrad(const mmad_conv_desc* d, const void* dy, const void* wpt, void* dx, void* stream);
+}  // namespace mmad_s2
+
 // Plane-pair form of the residue-class conv for d = 4 (latticezp.hip): two z-planes of 16
 // subs per tile, one wave per SIMD; mmad_lattice::fwd / tiles route to it when ok().
 namespace mmad_lattice_zp {

@@ -53,8 +53,10 @@ def test_host_side_shape_queries(lib):
     assert (d.do_, d.ho, d.wo) == (16, 16, 16)
     assert lib.mmad_conv_packed_elems(d, _lib.BF16, 0) == 128 * 27 * 64
     assert lib.mmad_conv_packed_elems(d, _lib.BF16, 1) == 64 * 27 * 128
-    # one BN partial row per output tile: 128-voxel tiles, or 64 for grids under 512 tiles
-    assert lib.mmad_conv3d_stats_rows(d, _lib.BF16) == 8 * 16 ** 3 // 64
+    # one BN partial row per output tile: the stride-2 sub-patch kernel's 2 x 8 x 8 boxes in
+    # bf16; the implicit GEMM's 64-voxel tiles (grids under 512 tiles of 128) in fp32
+    assert lib.mmad_conv3d_stats_rows(d, _lib.BF16) == 8 * 16 ** 3 // 128
+    assert lib.mmad_conv3d_stats_rows(d, _lib.F32) == 8 * 16 ** 3 // 64
     assert lib.mmad_conv3d_wgrad_workspace(d, _lib.BF16) > 0
     stem = conv_desc((8, 1, 128, 128, 128), (64, 1, 7, 7, 7), (2, 2, 2), (3, 3, 3), (1, 1, 1))
     assert lib.mmad_conv_unfolded_elems(stem) == 8 * 128 * 128 * 64 * 8

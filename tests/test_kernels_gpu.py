@@ -34,6 +34,9 @@ CONV_CASES = [
     (2, 1, 20, 18, 22, 64, 7, 2, 3, 1, False),     # MedicalNet stem (unfolded path)
     (2, 64, 8, 10, 6, 64, 3, 1, 1, 1, False),      # layer1
     (2, 64, 9, 8, 10, 128, 3, 2, 1, 1, False),     # layer2.0.conv1 (stride 2)
+    (2, 64, 16, 16, 16, 128, 3, 2, 1, 1, False),   # stride 2: sub-patch fwd and all-class dgrad
+    (1, 64, 8, 16, 16, 64, 3, 2, 1, 1, True),      # stride 2, sub-patch fwd (64 co), bias
+    (1, 64, 4, 32, 16, 256, 3, 2, 1, 1, True),     # stride 2, sub-patch fwd: 2 co tiles, bias
     (2, 128, 6, 9, 10, 128, 3, 1, 1, 1, False),    # layer2 conv2 (patch kernel, 2 ci chunks)
     (1, 64, 13, 17, 9, 128, 3, 1, 1, 1, True),     # ragged boxes + bias (patch kernel)
     (2, 128, 6, 7, 5, 256, 3, 1, 2, 2, False),     # layer3 (dilation 2)

@@ -223,9 +223,11 @@ def test_two_backbone_fusion_and_three_branch_run():
     assert torch.isfinite(o5["loss"])
 
 
-def test_eval_fused_blocks_match_unfused():
+@pytest.mark.parametrize("size", [32, 64])
+def test_eval_fused_blocks_match_unfused(size):
     """Eval-mode BasicBlocks (BN folded into the conv, residual + ReLU in the epilogue) vs
-    the training-style op sequence on the same trained weights and running statistics."""
+    the training-style op sequence on the same trained weights and running statistics.
+    At 64^3 layer2.0.conv1 (16^3 -> 8^3) runs the stride-2 sub-patch kernel's epilogue."""
     from multimodal_alzheimer_amd import medicalnet
     for precision, tol in ((torch.float32, 2e-5), (torch.bfloat16, 3e-2)):
         torch.manual_seed(3)
@@ -233,7 +235,7 @@ def test_eval_fused_blocks_match_unfused():
         m = M.Anat_CNN(h)
         M.layers.set_compute_dtype(m, precision)
         m = m.to(DEV)
-        batch = {"mri": torch.rand((2, 32, 32, 32), dtype=torch.float64, device=DEV),
+        batch = {"mri": torch.rand((2, size, size, size), dtype=torch.float64, device=DEV),
                  "label": torch.tensor([0, 1], device=DEV)}
         opt = m.configure_optimizers()
         for _ in range(3):                       # non-trivial running statistics
