@@ -1294,14 +1294,15 @@ int big_min_k() {
   return v;
 }
 // ring depth of the default (4-wave) tiles: 3 (two stages of LDS-DMA in flight, still two
-// blocks per CU at 64 x 128 tiles) for strided forward convs, 2 elsewhere.  Measured in the
-// config-2 step (r03s): layer2.0.conv1 fwd 39.3 -> 33.1 us, its 1x1x1 shortcut 8.4 -> 8.2;
+// blocks per CU at 64 x 128 tiles) for strided forward convs with taps (those the stride-2
+// sub-patch kernel does not take: fp32, ragged grids), 2 elsewhere.  Measured in the
+// config-2 step (r03s): layer2.0.conv1 fwd 39.3 -> 33.1 us;
 // every stride-1 launch and the parity-class dgrads were slower at 3 (e.g. 57.9 -> 71.6
 // us).  MMAD_IGEMM_NST=2 / 3 forces one depth everywhere (A/B).
 int igemm_nst(const Geom& g, int mode) {
   static const int v = [] { const char* e = getenv("MMAD_IGEMM_NST"); return e ? atoi(e) : 0; }();
   if (v) return v;
-  return mode == FWD && (g.sd > 1 || g.sh > 1 || g.sw > 1) ? 3 : 2;
+  return mode == FWD && g.taps > 1 && (g.sd > 1 || g.sh > 1 || g.sw > 1) ? 3 : 2;
 }
 int big_cfg_for(const Geom& g, int dtype, int64_t m_max, int classes) {
   if (dtype != MMAD_BF16) return 0;
