@@ -267,7 +267,12 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
     issue_b(cc, t, s);
   }
   int pl_at[2] = {0, 0};                            // plane instructions issued at s-1, s-2
-  auto one_stage = [&](int s) {
+  // Stage bookkeeping kept incrementally (no run-time division in the loop: stage_w /
+  // plane_due divide by nspc, and a scalar division is a ~30-instruction sequence that ran
+  // twice per stage): the weights issued at stage s are those of stage s + 2 = (wc, wr) =
+  // divmod(s + 2, nspc); the plane check looks at stage s - 1 = (pcn, prn).
+  int wc = 2 / nspc, wr = 2 % nspc, pcn = 0, prn = -1;
+  auto one_stage = [&](int s, int slot_next) {
     // B(s) landed; younger: B(s+1) and any plane issued after B(s) (stages s-1, s-2)
     const int younger = (s + 1 < nstage ? nbi : 0) + pl_at[0] + pl_at[1];
     switch (younger) {
@@ -281,31 +286,31 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
     raw_barrier();
     pl_at[1] = pl_at[0];
     pl_at[0] = 0;
-    if (s + 2 < nstage) {
-      int cc, t;
-      stage_w(s + 2, cc, t);
-      issue_b(cc, t, (s + 2) % NSL8);
-    }
-    int p, pc;
-    if (plane_due(s, p, pc)) {
-      issue_plane(p, pc);
+    if (s + 2 < nstage)                             // wr < 9: constant-divisor arithmetic
+      issue_b(wc, (kz0 + wr / 3 + 1) * 9 + (wr % 3) * 3, slot_next);
+    if (++wr == nspc) { wr = 0; ++wc; }
+    if (prn >= 0 && prn % 3 == 2 && pcn + 1 < g.nchunk) {
+      issue_plane(kz0 + prn / 3 + 1, pcn + 1);
       pl_at[0] = 4;
     }
+    if (++prn == nspc) { prn = 0; ++pcn; }
   };
   auto run = [&](auto wmc) {
     constexpr int WM = decltype(wmc)::value;
-    const int ngrp = nstage / 3;
-    for (int g2 = 0; g2 < ngrp; ++g2) {
-      const int kz = kz0 + g2 % nkz;
-      const char* pl = smem + (kz + 1) * PLANE8;
-      const int s0 = g2 * 3;
-      one_stage(s0);
-      stage8<TN, WM, -1, WR>(acc, ring + (s0 % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
-      one_stage(s0 + 1);
-      stage8<TN, WM, 0, WR>(acc, ring + ((s0 + 1) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
-      one_stage(s0 + 2);
-      stage8<TN, WM, 1, WR>(acc, ring + ((s0 + 2) % NSL8) * BSLOT8 + b_lane, pl, ao, zp, lhi);
-    }
+    // stage s0 = 3 * group: its three stages use weight slots 0, 1, 2 (NSL8 = 3) and issue
+    // the weights of stages s0 + 2 .. s0 + 4 into slots 2, 0, 1
+    static_assert(NSL8 == 3, "slot pattern");
+    int s0 = 0;
+    for (int c = 0; c < g.nchunk; ++c)
+      for (int kzi = 0; kzi < nkz; ++kzi, s0 += 3) {
+        const char* pl = smem + (kz0 + kzi + 1) * PLANE8;
+        one_stage(s0, 2);
+        stage8<TN, WM, -1, WR>(acc, ring + 0 * BSLOT8 + b_lane, pl, ao, zp, lhi);
+        one_stage(s0 + 1, 0);
+        stage8<TN, WM, 0, WR>(acc, ring + 1 * BSLOT8 + b_lane, pl, ao, zp, lhi);
+        one_stage(s0 + 2, 1);
+        stage8<TN, WM, 1, WR>(acc, ring + 2 * BSLOT8 + b_lane, pl, ao, zp, lhi);
+      }
   };
   // L8_PIPE: stage s's barrier sits between its kx = 0 and kx = +1 MFMAs.  Before it each
   // wave waits for stage s + 1's weights (issued three stages ahead, in group s - 2) and its
