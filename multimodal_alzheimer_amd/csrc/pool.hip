@@ -756,23 +756,126 @@ __global__ void gap_bwd_kernel(int n, int64_t S, int C, float inv, const float* 
   }
 }
 
+// k = 3, stride 2, pad 1, bf16 (the MedicalNet stem pool, BN + ReLU fused): a block owns
+// one output row (n, oh) of a z segment and walks it along z.  The 3 x 3 (y, x) max of input
+// plane p is computed once and serves both outputs that read the plane (od = p / 2 and
+// (p + 1) / 2): per output 18 window elements are loaded and transformed instead of 27 (the
+// rows kernel ran VALU-bound: r03y counters, 85 % of its cycles issuing VALU).  Keys and tie
+// order as bnpool3_fwd_one_bf16 (value << 16 | 31 - window index, the index composed as
+// plane part + 9 * kd, windows clipped at the borders), so out / argmax / ymax are
+// bit-identical to the rows kernel's.  Thread = (output x, 8-channel vector).
+struct PlaneMax {
+  uint32_t key[8], rb[8];
+};
+__device__ __forceinline__ void plane_max(const PoolG& g, const u16* __restrict__ yp, int y0,
+                                          int x0, int c0, const f32x2* sc2, const f32x2* sh2,
+                                          PlaneMax& m) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { m.key[e] = 0; m.rb[e] = 0; }
+  u32x4 raw[9];
+  uint32_t tag[9];
+#pragma unroll
+  for (int w = 0; w < 9; ++w) {
+    const int yc = min(max(y0 + w / 3, 0), g.hi - 1), xc = min(max(x0 + w % 3, 0), g.wi - 1);
+    tag[w] = 31 - 18 - ((yc - y0) * 3 + (xc - x0));     // kd = 2 part; + 9 (2 - kd) later
+    raw[w] = *reinterpret_cast<const u32x4*>(yp + ((int64_t)yc * g.wi + xc) * g.c + c0);
+  }
+#pragma unroll
+  for (int w = 0; w < 9; ++w) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t word = raw[w][q];
+      const f32x2 a = {__uint_as_float(word << 16), __uint_as_float(word & 0xffff0000u)};
+      const f32x2 sv = __builtin_elementwise_fma(a, sc2[q], sh2[q]);
+      const s16x2 v = __builtin_elementwise_max(
+          __builtin_bit_cast(s16x2, __builtin_convertvector(sv, bf16x2)), (s16x2){0, 0});
+      const uint32_t pk = __builtin_bit_cast(uint32_t, v);
+      const uint32_t k0 = (pk << 16) | tag[w], k1 = (pk & 0xffff0000u) | tag[w];
+      if (k0 > m.key[2 * q]) { m.key[2 * q] = k0; m.rb[2 * q] = word; }
+      if (k1 > m.key[2 * q + 1]) { m.key[2 * q + 1] = k1; m.rb[2 * q + 1] = word; }
+    }
+  }
+}
+__device__ __forceinline__ void zmerge(PlaneMax& best, const PlaneMax& m, uint32_t add) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t k = m.key[e] + add;
+    if (k > best.key[e]) { best.key[e] = k; best.rb[e] = m.rb[e]; }
+  }
+}
+
+__global__ __launch_bounds__(256) void bnpool3s2_fwd_zwalk_kernel(
+    PoolG g, int cv_shift, int ods, const u16* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, u16* __restrict__ out, uint8_t* __restrict__ am,
+    u16* __restrict__ ymax) {
+  const int cvn = 1 << cv_shift;
+  const int ow = threadIdx.x >> cv_shift, c0 = (threadIdx.x & (cvn - 1)) * 8;
+  if (ow >= g.wo) return;                          // (no barrier in this kernel)
+  const int oh = blockIdx.y;
+  const int64_t nb = blockIdx.z;
+  const int od0 = blockIdx.x * ods, od1 = min(g.do_, od0 + ods);
+  f32x2 sc2[4], sh2[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    sc2[q] = (f32x2){scale[c0 + 2 * q], scale[c0 + 2 * q + 1]};
+    sh2[q] = (f32x2){shift[c0 + 2 * q], shift[c0 + 2 * q + 1]};
+  }
+  const int y0 = 2 * oh - 1, x0 = 2 * ow - 1;
+  const int64_t plane = (int64_t)g.hi * g.wi * g.c;
+  const u16* __restrict__ yn = y + nb * g.di * plane;
+  PlaneMax prev;                                   // plane 2 od - 1 (the previous od's last)
+  bool prev_ok = 2 * od0 - 1 >= 0;
+  if (prev_ok) plane_max(g, yn + (2 * od0 - 1) * plane, y0, x0, c0, sc2, sh2, prev);
+  for (int od = od0; od < od1; ++od) {
+    PlaneMax a, b;
+    plane_max(g, yn + (2 * od) * plane, y0, x0, c0, sc2, sh2, a);
+    const bool b_ok = 2 * od + 1 < g.di;
+    if (b_ok) plane_max(g, yn + (2 * od + 1) * plane, y0, x0, c0, sc2, sh2, b);
+    PlaneMax best;                                 // kd = 1: always inside the volume
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best.key[e] = a.key[e] + 9; best.rb[e] = a.rb[e]; }
+    if (prev_ok) zmerge(best, prev, 18);           // kd = 0
+    if (b_ok) zmerge(best, b, 0);                  // kd = 2
+    const int64_t ovox = ((nb * g.do_ + od) * g.ho + oh) * g.wo + ow;
+    u32x4 o, r;
+    uint64_t packed = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      o[q] = (best.key[2 * q] >> 16) | (best.key[2 * q + 1] & 0xffff0000u);
+      r[q] = (best.rb[2 * q] & 0xffffu) | (best.rb[2 * q + 1] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t vb = best.key[e] >> 16;
+      const bool pos = vb != 0 && vb <= 0x7f80u;
+      packed |= (uint64_t)((31 - (best.key[e] & 31)) | (pos ? 0x80 : 0)) << (8 * e);
+    }
+    *reinterpret_cast<u32x4*>(out + ovox * g.c + c0) = o;
+    *reinterpret_cast<u32x4*>(ymax + ovox * g.c + c0) = r;
+    *reinterpret_cast<uint64_t*>(am + ovox * g.c + c0) = packed;
+    prev = b;
+    prev_ok = b_ok;
+  }
+}
+
 // MMAD_POOL_ROWS=0 keeps the grid-stride fused pool kernels (A/B switch)
 bool rows_on() {
   static const bool v = [] { const char* e = getenv("MMAD_POOL_ROWS"); return !e || atoi(e) != 0; }();
   return v;
 }
 
-// MMAD_POOL_RUN: 1 the column-carrying bnpool3s2_fwd_run_kernel for the stem pool (k 3, s 2,
-// p 1, bf16), 0 (default) the per-output rows kernel; mmad_set_kernel_variant("pool_run", v).
-// Measured r03e at config 2: 124.5 us against the rows kernel's 110.8 (r03a) -- the run
-// kernel's 2 waves per SIMD do not keep enough loads in flight; kept for A/B.
+// MMAD_POOL_RUN: 2 (default) the z-walking bnpool3s2_fwd_zwalk_kernel for the stem pool (k 3,
+// s 2, p 1, bf16), 1 the column-carrying bnpool3s2_fwd_run_kernel, 0 the per-output rows
+// kernel; mmad_set_kernel_variant("pool_run", v).  Measured r03e at config 2: run kernel
+// 124.5 us against the rows kernel's 110.8 (r03a) -- its 2 waves per SIMD do not keep enough
+// loads in flight; kept for A/B.
 std::atomic<int> g_pool_run{-1};
 int pool_run_mode() {
   int v = g_pool_run.load(std::memory_order_relaxed);
   if (v < 0) {
     const char* e = getenv("MMAD_POOL_RUN");
     int expect = -1;
-    g_pool_run.compare_exchange_strong(expect, e ? atoi(e) : 0);
+    g_pool_run.compare_exchange_strong(expect, e ? atoi(e) : 2);
     v = g_pool_run.load(std::memory_order_relaxed);
   }
   return v;
@@ -823,8 +926,18 @@ int bnpool_fwd(const PoolG& g, const void* y, const float* scale, const float* s
   const int64_t vox = (int64_t)g.n * g.do_ * g.ho * g.wo;
   const int cv = g.c / VEC;
   if constexpr (sizeof(T) == 2) {
+    if (g.c % VEC == 0 && g.k == 3 && g.s == 2 && g.p == 1 && is_pow2(cv) &&
+        pool_run_mode() == 2 && cv * g.wo <= 256 && g.ho < 65536 && g.n < 65536) {
+      // z segments of 4 outputs (one extra plane each): >= 8 blocks per CU at the stem
+      const int ods = 4;
+      hipLaunchKernelGGL(bnpool3s2_fwd_zwalk_kernel,
+                         dim3((unsigned)cdiv(g.do_, ods), (unsigned)g.ho, (unsigned)g.n),
+                         dim3(256), 0, st, g, ilog2(cv), ods, (const u16*)y, scale, shift,
+                         (u16*)out, am, (u16*)ymax);
+      return launch_status();
+    }
     if (g.c % VEC == 0 && g.k == 3 && g.s == 2 && g.p == 1 && is_pow2(cv) && cv <= 64 &&
-        pool_run_mode() > 0 && (int64_t)g.n * g.do_ < 65536 && g.wo >= 2) {
+        pool_run_mode() == 1 && (int64_t)g.n * g.do_ < 65536 && g.wo >= 2) {
       const int cvs = ilog2(cv), rows = 256 >> (cvs + 1);
       hipLaunchKernelGGL(bnpool3s2_fwd_run_kernel,
                          dim3((unsigned)cdiv(g.ho, rows), (unsigned)(g.n * g.do_)), dim3(256), 0,

@@ -256,13 +256,13 @@ def test_bn_relu_maxpool_fused(dtype, training):
 @pytest.mark.parametrize("shape", [(2, 64, 9, 10, 11), (2, 64, 64, 64, 64), (1, 128, 8, 6, 4)],
                          ids=["odd", "stem", "c128"])
 def test_bnpool_run_kernel_matches_rows_kernel(shape):
-    """The column-carrying stem pool kernel (pool.hip bnpool3s2_fwd_run_kernel) against the
-    per-output rows kernel it replaces: pooled output, argmax-routed input gradient and BN
-    parameter gradients bit-identical (ties on ReLU zeros everywhere)."""
+    """The column-carrying (pool_run 1) and z-walking (2, the default) stem pool kernels of
+    pool.hip against the per-output rows kernel (0): pooled output, argmax-routed input
+    gradient and BN parameter gradients bit-identical (ties on ReLU zeros everywhere)."""
     n, c = shape[:2]
     lib = _lib.load()
     res = {}
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         bn = _BN(c, 75)
         bn.training = True
         y = to_vol(rnd(*shape, seed=74, scale=2.0), torch.bfloat16).requires_grad_(True)
@@ -274,8 +274,9 @@ def test_bnpool_run_kernel_matches_rows_kernel(shape):
         finally:
             lib.mmad_set_kernel_variant(b"pool_run", prev)
         res[mode] = (p, y.grad, bn.weight.grad, bn.bias.grad)
-    for nm, a, b in zip(("out", "dy", "dgamma", "dbeta"), res[0], res[1]):
-        assert torch.equal(a, b), nm
+    for mode in (1, 2):
+        for nm, a, b in zip(("out", "dy", "dgamma", "dbeta"), res[0], res[mode]):
+            assert torch.equal(a, b), (mode, nm)
 
 
 @pytest.mark.parametrize("shape,dil", [((2, 512, 4, 4, 4), 4), ((2, 256, 4, 4, 4), 2),
