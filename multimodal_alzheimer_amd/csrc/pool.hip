@@ -804,7 +804,13 @@ __device__ __forceinline__ void zmerge(PlaneMax& best, const PlaneMax& m, uint32
   }
 }
 
-__global__ __launch_bounds__(256) void bnpool3s2_fwd_zwalk_kernel(
+#ifndef POOL_ZW_WAVES
+#define POOL_ZW_WAVES 1
+#endif
+#ifndef POOL_ZW_ODS
+#define POOL_ZW_ODS 4
+#endif
+__global__ __launch_bounds__(256, POOL_ZW_WAVES) void bnpool3s2_fwd_zwalk_kernel(
     PoolG g, int cv_shift, int ods, const u16* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, u16* __restrict__ out, uint8_t* __restrict__ am,
     u16* __restrict__ ymax) {
@@ -929,7 +935,7 @@ int bnpool_fwd(const PoolG& g, const void* y, const float* scale, const float* s
     if (g.c % VEC == 0 && g.k == 3 && g.s == 2 && g.p == 1 && is_pow2(cv) &&
         pool_run_mode() == 2 && cv * g.wo <= 256 && g.ho < 65536 && g.n < 65536) {
       // z segments of 4 outputs (one extra plane each): >= 8 blocks per CU at the stem
-      const int ods = 4;
+      const int ods = POOL_ZW_ODS;
       hipLaunchKernelGGL(bnpool3s2_fwd_zwalk_kernel,
                          dim3((unsigned)cdiv(g.do_, ods), (unsigned)g.ho, (unsigned)g.n),
                          dim3(256), 0, st, g, ilog2(cv), ods, (const u16*)y, scale, shift,
