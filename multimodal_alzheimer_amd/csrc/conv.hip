@@ -1619,6 +1619,7 @@ int64_t mmad_conv3d_stats_rows(const mmad_conv_desc* d, int dtype) {
   if (!unfolded(d) && use_lattice8(g, dtype)) return mmad_lattice8::tiles(patch_geo(g));
   if (!unfolded(d) && use_patch(g, dtype)) return mmad_patch::tiles(patch_geo(g));
   if (!unfolded(d) && use_s2(g, dtype)) return mmad_s2::tiles(patch_geo(g));
+  if (mmad_pw::fwd_ok(d, dtype)) return mmad_pw::fwd_tiles(d);
   return cdiv(g.M, fwd_tile_rows(g, dtype));
 }
 
@@ -1639,6 +1640,7 @@ int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x, const voi
     return mmad_patch::fwd(patch_geo(g), x, wp, bias, y, stats, stream);
   if (!unfolded(d) && use_s2(g, dtype))
     return mmad_s2::fwd(patch_geo(g), g.sd, g.sh, g.sw, x, wp, bias, y, stats, stream);
+  if (mmad_pw::fwd_ok(d, dtype)) return mmad_pw::fwd(d, x, wp, bias, y, stats, stream);
   return run_igemm<FWD>(g, dtype, g.M, 1, x, wp, bias, y, stats, as_stream(stream));
 }
 

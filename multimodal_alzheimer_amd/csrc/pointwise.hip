@@ -13,6 +13,11 @@
 // as 16-byte channel vectors.  The step has two such launches (layer4: 32768 x 256 x 512,
 // layer3: 32768 x 128 x 256 at batch 8): bandwidth-bound on the dY read (M x K x 2 bytes).
 // Replaces the hipBLASLt GEMM used before round 3 (Cijk_* kernels, 18.8 / 10.8 us).
+//
+// The same GEMM form serves the shortcut's forward (round 3): Y[m][co] = sum_ci X[m][ci] *
+// W[co][ci] with the forward-packed weights [co][ci] as the B rows, N tiles of 256 columns
+// in blockIdx.y, and the BN partial sums of the fp32 accumulators written per 128-row tile
+// (the implicit GEMM ran this K = 128 / 256 GEMM latency-bound: 31.4 / 17.6 us).
 #include <cstdlib>
 
 #include "common.h"
@@ -38,20 +43,26 @@ struct PC {
   static constexpr int CROW = BN * 2 + 16;
   static constexpr int EPI = TM * CROW;
   static constexpr int MAIN = NST * SLOT;
-  static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
+  static constexpr int LDS = MAIN > EPI + 2 * BN * 4 ? MAIN : EPI + 2 * BN * 4;
 };
 
 __device__ __forceinline__ int swz8(int row) { return row & 7; }
 
+// C[m][n0 + n] = sum_k A[m][k] * B[n0 + n][k]; ldc = the output row length (all N tiles);
+// stats (forward): [m tile][2][ldc] sums of C and C^2 over the tile's 128 rows
 template <int BN>
 __global__ __launch_bounds__(NTHR) void pw_dgrad_kernel(int K, const u16* __restrict__ dy,
                                                         const u16* __restrict__ wd,
-                                                        u16* __restrict__ dx) {
+                                                        u16* __restrict__ dx, int ldc,
+                                                        float* __restrict__ stats,
+                                                        const float* __restrict__ bias) {
   using C = PC<BN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t m0 = (int64_t)blockIdx.x * TM;
+  const int n0 = (int)blockIdx.y * BN;
+  wd += (int64_t)n0 * K;
   const int nstage = K / KS;
 
   // DMA instruction q = wave + NW h: rows 8q .. 8q + 7 of the stage image (A rows first,
@@ -113,6 +124,14 @@ __global__ __launch_bounds__(NTHR) void pw_dgrad_kernel(int K, const u16* __rest
   __syncthreads();                                  // ring reused by the epilogue
 
   // acc[i][j][e]: row wm*64 + i*16 + lk*4 + e, column wn*16*TN + j*16 + lr
+  if (bias != nullptr) {
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) {
+      const float bv = bias[n0 + wn * 16 * C::TN + j * 16 + lr];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] += f32x4{bv, bv, bv, bv};
+    }
+  }
   u16* ctile = reinterpret_cast<u16*>(smem);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -124,13 +143,53 @@ __global__ __launch_bounds__(NTHR) void pw_dgrad_kernel(int K, const u16* __rest
         const int col = wn * 16 * C::TN + j * 16 + lr;
         ctile[row * (C::CROW / 2) + col] = f2bf(acc[i][j][e]);
       }
-  __syncthreads();
+  if (stats != nullptr) {
+    // per column: this wave's 64 rows (i, e, then the 4 lk groups by shuffles), then the two
+    // row halves (wm) in fixed order through LDS past the C tile: deterministic
+    float* red = reinterpret_cast<float*>(smem + C::EPI);
+    float cs[C::TN], cq[C::TN];
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) {
+      cs[j] = 0.f;
+      cq[j] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          cs[j] += acc[i][j][e];
+          cq[j] += acc[i][j][e] * acc[i][j][e];
+        }
+      cs[j] += __shfl_xor(cs[j], 16, 64);
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 16, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+    }
+    if (wm == 1 && lk == 0) {
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) {
+        const int col = wn * 16 * C::TN + j * 16 + lr;
+        red[col] = cs[j];
+        red[BN + col] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && lk == 0) {
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) {
+        const int col = wn * 16 * C::TN + j * 16 + lr;
+        stats[((int64_t)blockIdx.x * 2) * ldc + n0 + col] = cs[j] + red[col];
+        stats[((int64_t)blockIdx.x * 2 + 1) * ldc + n0 + col] = cq[j] + red[BN + col];
+      }
+    }
+  } else {
+    __syncthreads();
+  }
   constexpr int CPR = BN / 8;                       // 16-byte vectors per row
 #pragma unroll
   for (int hh = 0; hh < TM * CPR / NTHR; ++hh) {
     const int qd = tid + NTHR * hh;
     const int row = qd / CPR, c8 = qd % CPR;
-    *reinterpret_cast<u32x4*>(dx + (m0 + row) * BN + c8 * 8) =
+    *reinterpret_cast<u32x4*>(dx + (m0 + row) * ldc + n0 + c8 * 8) =
         *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) + row * C::CROW +
                                         c8 * 16);
   }
@@ -168,10 +227,36 @@ int dgrad(const mmad_conv_desc* d, const void* dy, const void* wpt, void* dx, vo
   const dim3 grid((unsigned)(m / TM));
   if (d->ci == 256)
     hipLaunchKernelGGL(pw_dgrad_kernel<256>, grid, dim3(NTHR), PC<256>::LDS, as_stream(stream),
-                       d->co, (const u16*)dy, (const u16*)wpt, (u16*)dx);
+                       d->co, (const u16*)dy, (const u16*)wpt, (u16*)dx, 256, nullptr, nullptr);
   else
     hipLaunchKernelGGL(pw_dgrad_kernel<128>, grid, dim3(NTHR), PC<128>::LDS, as_stream(stream),
-                       d->co, (const u16*)dy, (const u16*)wpt, (u16*)dx);
+                       d->co, (const u16*)dy, (const u16*)wpt, (u16*)dx, 128, nullptr, nullptr);
+  return launch_status();
+}
+
+bool fwd_ok(const mmad_conv_desc* d, int dtype) {
+  if (!pw_on() || dtype != MMAD_BF16) return false;
+  if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->sd != 1 || d->sh != 1 || d->sw != 1) return false;
+  if (d->pd || d->ph || d->pw || d->ci % KS || d->co % 256) return false;
+  if (d->di != d->do_ || d->hi != d->ho || d->wi != d->wo) return false;
+  const int64_t m = (int64_t)d->n * d->di * d->hi * d->wi;
+  return m % TM == 0 && m / TM < (int64_t(1) << 31) && m * d->co < (int64_t(1) << 40);
+}
+
+int64_t fwd_tiles(const mmad_conv_desc* d) {
+  return (int64_t)d->n * d->di * d->hi * d->wi / TM;
+}
+
+int fwd(const mmad_conv_desc* d, const void* x, const void* wp, const float* bias, void* y,
+        float* stats, void* stream) {
+  static const bool attr =
+      hipFuncSetAttribute((const void*)pw_dgrad_kernel<256>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, PC<256>::LDS) == hipSuccess;
+  if (!attr) return MMAD_EUNSUPPORTED;
+  const int64_t m = (int64_t)d->n * d->di * d->hi * d->wi;
+  const dim3 grid((unsigned)(m / TM), (unsigned)(d->co / 256));
+  hipLaunchKernelGGL(pw_dgrad_kernel<256>, grid, dim3(NTHR), PC<256>::LDS, as_stream(stream),
+                     d->ci, (const u16*)x, (const u16*)wp, (u16*)y, d->co, stats, bias);
   return launch_status();
 }
 

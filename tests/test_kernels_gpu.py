@@ -43,6 +43,8 @@ CONV_CASES = [
     (1, 256, 6, 6, 6, 512, 3, 1, 4, 4, False),     # layer4 (dilation 4)
     (2, 64, 9, 8, 10, 128, 1, 2, 0, 1, False),     # shortcut B, stride 2
     (2, 128, 5, 6, 7, 256, 1, 1, 0, 1, False),     # shortcut B, stride 1
+    (2, 128, 8, 8, 8, 256, 1, 1, 0, 1, False),     # shortcut B, stride 1: pointwise GEMM fwd
+    (1, 256, 8, 4, 8, 512, 1, 1, 0, 1, True),      # pointwise GEMM fwd: 2 column tiles, bias
     (2, 1, 12, 11, 13, 8, 5, 1, 2, 1, True),       # Small_PET_CNN conv 1 (k5 'same')
     (2, 1, 9, 10, 8, 16, 7, 1, 3, 1, True),        # Small_PET_CNN conv 1 (k7 'same')
     (2, 8, 10, 9, 11, 16, 5, 1, 2, 1, True),       # Small_PET_CNN conv 2
