@@ -6,14 +6,16 @@
 #include "../../include/mmad.h"
 
 namespace mmad_pw {
-// true for bf16 1x1x1 stride-1 unpadded convs with ci in {128, 256}, co % 64 == 0 and a
-// voxel count that is a multiple of 128 (layer3 / layer4 shortcuts at batch 8)
+// true for bf16 1x1x1 unpadded convs of stride 1 or 2 with ci in {64, 128, 256}, co % 64 == 0
+// and an output voxel count that is a multiple of 128 (the layer2 / 3 / 4 shortcuts at batch 8)
 bool ok(const mmad_conv_desc* d, int dtype);
-// dX = dY . W over the dgrad-packed weights [ci][co]
+// dX = dY . W over the dgrad-packed weights [ci][co]; stride 2: the GEMM rows land on the
+// all-even voxels and the block writes the zeros of the rest of each 2x2x2 cell
 int dgrad(const mmad_conv_desc* d, const void* dy, const void* wpt, void* dx, void* stream);
-// the same GEMM as the forward of a bf16 1x1x1 stride-1 conv with co % 256 == 0 and ci % 64
-// == 0 (layer3 / layer4 shortcuts): Y = X . W^T over the forward-packed weights [co][ci], BN
-// partial sums one row per 128 voxels (fwd_tiles rows)
+// the same GEMM as the forward of a bf16 1x1x1 conv of stride 1 or 2 with co % 256 == 0 or
+// co == 128, ci % 64 == 0 (the layer2 / 3 / 4 shortcuts): Y = X . W^T over the forward-packed
+// weights [co][ci] (stride 2: the A rows gathered from the all-even input voxels), BN partial
+// sums one row per 128 output voxels (fwd_tiles rows)
 bool fwd_ok(const mmad_conv_desc* d, int dtype);
 int64_t fwd_tiles(const mmad_conv_desc* d);
 int fwd(const mmad_conv_desc* d, const void* x, const void* wp, const float* bias, void* y,

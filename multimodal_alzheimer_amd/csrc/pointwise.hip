@@ -48,14 +48,33 @@ struct PC {
 
 __device__ __forceinline__ int swz8(int row) { return row & 7; }
 
+// stride-2 1x1x1 geometry (the layer2 shortcut): output grid Do x Ho x Wo, input Di x Hi x Wi
+struct PwS2 {
+  int Do, Ho, Wo, Di, Hi, Wi;
+};
+// the input voxel a stride-2 1x1x1 conv's output row m reads
+__device__ __forceinline__ int64_t s2_src(const PwS2& q, int64_t m) {
+  const int ox = (int)(m % q.Wo);
+  int64_t t = m / q.Wo;
+  const int oy = (int)(t % q.Ho);
+  t /= q.Ho;
+  const int oz = (int)(t % q.Do);
+  const int64_t n = t / q.Do;
+  return ((n * q.Di + 2 * oz) * q.Hi + 2 * oy) * q.Wi + 2 * ox;
+}
+
 // C[m][n0 + n] = sum_k A[m][k] * B[n0 + n][k]; ldc = the output row length (all N tiles);
-// stats (forward): [m tile][2][ldc] sums of C and C^2 over the tile's 128 rows
-template <int BN>
+// stats (forward): [m tile][2][ldc] sums of C and C^2 over the tile's 128 rows.
+// MODE 1 (stride-2 forward): A row m is the input voxel s2_src(m).  MODE 2 (stride-2 input
+// gradient): C row m is dX voxel s2_src(m), and the block also writes the zeros of the other
+// 7 voxels of each 2x2x2 cell (inside the volume), so dX needs no separate fill.
+template <int BN, int MODE = 0>
 __global__ __launch_bounds__(NTHR) void pw_dgrad_kernel(int K, const u16* __restrict__ dy,
                                                         const u16* __restrict__ wd,
                                                         u16* __restrict__ dx, int ldc,
                                                         float* __restrict__ stats,
-                                                        const float* __restrict__ bias) {
+                                                        const float* __restrict__ bias,
+                                                        PwS2 s2) {
   using C = PC<BN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -74,7 +93,8 @@ __global__ __launch_bounds__(NTHR) void pw_dgrad_kernel(int K, const u16* __rest
     const int q = wave + NW * h;
     const int row = q * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ swz8(row);
-    srcp[h] = row < TM ? dy + (m0 + row) * K + ch * 8 : wd + (int64_t)(row - TM) * K + ch * 8;
+    const int64_t arow = MODE == 1 ? s2_src(s2, m0 + row) : m0 + row;
+    srcp[h] = row < TM ? dy + arow * K + ch * 8 : wd + (int64_t)(row - TM) * K + ch * 8;
     lofs[h] = q * 1024;
   }
   auto issue = [&](int s) {
@@ -189,9 +209,25 @@ __global__ __launch_bounds__(NTHR) void pw_dgrad_kernel(int K, const u16* __rest
   for (int hh = 0; hh < TM * CPR / NTHR; ++hh) {
     const int qd = tid + NTHR * hh;
     const int row = qd / CPR, c8 = qd % CPR;
-    *reinterpret_cast<u32x4*>(dx + (m0 + row) * ldc + n0 + c8 * 8) =
-        *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) + row * C::CROW +
-                                        c8 * 16);
+    const u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
+                                                    row * C::CROW + c8 * 16);
+    if constexpr (MODE == 2) {
+      const int64_t dv = s2_src(s2, m0 + row);
+      const int64_t m = m0 + row;
+      const int ox = (int)(m % s2.Wo), oy = (int)((m / s2.Wo) % s2.Ho),
+                oz = (int)((m / ((int64_t)s2.Wo * s2.Ho)) % s2.Do);
+#pragma unroll
+      for (int cell = 0; cell < 8; ++cell) {
+        const int a = cell >> 2, b = (cell >> 1) & 1, c = cell & 1;
+        if (2 * oz + a < s2.Di && 2 * oy + b < s2.Hi && 2 * ox + c < s2.Wi) {
+          const int64_t o = dv + ((int64_t)a * s2.Hi + b) * s2.Wi + c;
+          *reinterpret_cast<u32x4*>(dx + o * ldc + n0 + c8 * 8) =
+              cell == 0 ? v : u32x4{0u, 0u, 0u, 0u};
+        }
+      }
+    } else {
+      *reinterpret_cast<u32x4*>(dx + (m0 + row) * ldc + n0 + c8 * 8) = v;
+    }
   }
 }
 
@@ -207,57 +243,88 @@ bool pw_on() {
 
 namespace mmad_pw {
 
+namespace {
+bool s2_geom(const mmad_conv_desc* d) {
+  return d->sd == 2 && d->sh == 2 && d->sw == 2 &&
+         (d->di == 2 * d->do_ || d->di == 2 * d->do_ - 1) &&
+         (d->hi == 2 * d->ho || d->hi == 2 * d->ho - 1) &&
+         (d->wi == 2 * d->wo || d->wi == 2 * d->wo - 1);
+}
+bool stride1_geom(const mmad_conv_desc* d) {
+  return d->sd == 1 && d->sh == 1 && d->sw == 1 && d->di == d->do_ && d->hi == d->ho &&
+         d->wi == d->wo;
+}
+PwS2 s2_of(const mmad_conv_desc* d) {
+  return PwS2{d->do_, d->ho, d->wo, d->di, d->hi, d->wi};
+}
+template <int BN, int MODE>
+int launch(dim3 grid, int K, const void* a, const void* b, void* c, int ldc, float* stats,
+           const float* bias, PwS2 q, void* stream) {
+  static const bool attr = hipFuncSetAttribute((const void*)pw_dgrad_kernel<BN, MODE>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               PC<BN>::LDS) == hipSuccess;
+  if (!attr) return MMAD_EUNSUPPORTED;
+  hipLaunchKernelGGL((pw_dgrad_kernel<BN, MODE>), grid, dim3(NTHR), PC<BN>::LDS,
+                     as_stream(stream), K, (const u16*)a, (const u16*)b, (u16*)c, ldc, stats, bias,
+                     q);
+  return launch_status();
+}
+}  // namespace
+
 bool ok(const mmad_conv_desc* d, int dtype) {
   if (!pw_on() || dtype != MMAD_BF16) return false;
-  if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->sd != 1 || d->sh != 1 || d->sw != 1) return false;
-  if (d->pd || d->ph || d->pw || d->co % KS || (d->ci != 128 && d->ci != 256)) return false;
-  if (d->di != d->do_ || d->hi != d->ho || d->wi != d->wo) return false;
-  const int64_t m = (int64_t)d->n * d->di * d->hi * d->wi;
-  return m % TM == 0 && m * d->co < (int64_t(1) << 40);
+  if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw) return false;
+  if (!stride1_geom(d) && !s2_geom(d)) return false;
+  if (d->co % KS || (d->ci != 64 && d->ci != 128 && d->ci != 256)) return false;
+  const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;       // dY rows
+  const int64_t mi = (int64_t)d->n * d->di * d->hi * d->wi;
+  return m % TM == 0 && mi * d->ci < (int64_t(1) << 40) && m * d->co < (int64_t(1) << 40);
 }
 
 int dgrad(const mmad_conv_desc* d, const void* dy, const void* wpt, void* dx, void* stream) {
-  static const bool attr =
-      hipFuncSetAttribute((const void*)pw_dgrad_kernel<128>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, PC<128>::LDS) == hipSuccess &&
-      hipFuncSetAttribute((const void*)pw_dgrad_kernel<256>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, PC<256>::LDS) == hipSuccess;
-  if (!attr) return MMAD_EUNSUPPORTED;
-  const int64_t m = (int64_t)d->n * d->di * d->hi * d->wi;
+  if (!ok(d, MMAD_BF16)) return MMAD_EUNSUPPORTED;
+  const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
   const dim3 grid((unsigned)(m / TM));
-  if (d->ci == 256)
-    hipLaunchKernelGGL(pw_dgrad_kernel<256>, grid, dim3(NTHR), PC<256>::LDS, as_stream(stream),
-                       d->co, (const u16*)dy, (const u16*)wpt, (u16*)dx, 256, nullptr, nullptr);
-  else
-    hipLaunchKernelGGL(pw_dgrad_kernel<128>, grid, dim3(NTHR), PC<128>::LDS, as_stream(stream),
-                       d->co, (const u16*)dy, (const u16*)wpt, (u16*)dx, 128, nullptr, nullptr);
-  return launch_status();
+  const PwS2 q = s2_of(d);
+  if (s2_geom(d)) {
+    if (d->ci == 256) return launch<256, 2>(grid, d->co, dy, wpt, dx, 256, nullptr, nullptr, q, stream);
+    if (d->ci == 128) return launch<128, 2>(grid, d->co, dy, wpt, dx, 128, nullptr, nullptr, q, stream);
+    return launch<64, 2>(grid, d->co, dy, wpt, dx, 64, nullptr, nullptr, q, stream);
+  }
+  if (d->ci == 256) return launch<256, 0>(grid, d->co, dy, wpt, dx, 256, nullptr, nullptr, q, stream);
+  if (d->ci == 128) return launch<128, 0>(grid, d->co, dy, wpt, dx, 128, nullptr, nullptr, q, stream);
+  return launch<64, 0>(grid, d->co, dy, wpt, dx, 64, nullptr, nullptr, q, stream);
 }
 
 bool fwd_ok(const mmad_conv_desc* d, int dtype) {
   if (!pw_on() || dtype != MMAD_BF16) return false;
-  if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->sd != 1 || d->sh != 1 || d->sw != 1) return false;
-  if (d->pd || d->ph || d->pw || d->ci % KS || d->co % 256) return false;
-  if (d->di != d->do_ || d->hi != d->ho || d->wi != d->wo) return false;
-  const int64_t m = (int64_t)d->n * d->di * d->hi * d->wi;
-  return m % TM == 0 && m / TM < (int64_t(1) << 31) && m * d->co < (int64_t(1) << 40);
+  if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw) return false;
+  if (!stride1_geom(d) && !s2_geom(d)) return false;
+  if (d->ci % KS || (d->co % 256 && d->co != 128)) return false;
+  const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
+  const int64_t mi = (int64_t)d->n * d->di * d->hi * d->wi;
+  return m % TM == 0 && m / TM < (int64_t(1) << 31) && m * d->co < (int64_t(1) << 40) &&
+         mi * d->ci < (int64_t(1) << 40);
 }
 
 int64_t fwd_tiles(const mmad_conv_desc* d) {
-  return (int64_t)d->n * d->di * d->hi * d->wi / TM;
+  return (int64_t)d->n * d->do_ * d->ho * d->wo / TM;
 }
 
 int fwd(const mmad_conv_desc* d, const void* x, const void* wp, const float* bias, void* y,
         float* stats, void* stream) {
-  static const bool attr =
-      hipFuncSetAttribute((const void*)pw_dgrad_kernel<256>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, PC<256>::LDS) == hipSuccess;
-  if (!attr) return MMAD_EUNSUPPORTED;
-  const int64_t m = (int64_t)d->n * d->di * d->hi * d->wi;
+  if (!fwd_ok(d, MMAD_BF16)) return MMAD_EUNSUPPORTED;
+  const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
+  const PwS2 q = s2_of(d);
+  const bool s2 = s2_geom(d);
+  if (d->co == 128) {
+    const dim3 grid((unsigned)(m / TM), 1);
+    return s2 ? launch<128, 1>(grid, d->ci, x, wp, y, 128, stats, bias, q, stream)
+              : launch<128, 0>(grid, d->ci, x, wp, y, 128, stats, bias, q, stream);
+  }
   const dim3 grid((unsigned)(m / TM), (unsigned)(d->co / 256));
-  hipLaunchKernelGGL(pw_dgrad_kernel<256>, grid, dim3(NTHR), PC<256>::LDS, as_stream(stream),
-                     d->ci, (const u16*)x, (const u16*)wp, (u16*)y, d->co, stats, bias);
-  return launch_status();
+  return s2 ? launch<256, 1>(grid, d->ci, x, wp, y, d->co, stats, bias, q, stream)
+            : launch<256, 0>(grid, d->ci, x, wp, y, d->co, stats, bias, q, stream);
 }
 
 }  // namespace mmad_pw

@@ -42,6 +42,8 @@ CONV_CASES = [
     (2, 128, 6, 7, 5, 256, 3, 1, 2, 2, False),     # layer3 (dilation 2)
     (1, 256, 6, 6, 6, 512, 3, 1, 4, 4, False),     # layer4 (dilation 4)
     (2, 64, 9, 8, 10, 128, 1, 2, 0, 1, False),     # shortcut B, stride 2
+    (2, 64, 16, 16, 16, 128, 1, 2, 0, 1, False),   # stride 2, pointwise GEMM fwd / cell dgrad
+    (1, 64, 15, 16, 31, 128, 1, 2, 0, 1, True),    # same, odd input extents (clipped cells)
     (2, 128, 5, 6, 7, 256, 1, 1, 0, 1, False),     # shortcut B, stride 1
     (2, 128, 8, 8, 8, 256, 1, 1, 0, 1, False),     # shortcut B, stride 1: pointwise GEMM fwd
     (1, 256, 8, 4, 8, 512, 1, 1, 0, 1, True),      # pointwise GEMM fwd: 2 column tiles, bias
