@@ -1256,6 +1256,9 @@ WSplit wgrad_split(const Geom& g, int dtype) {
   }
   static const int force = [] { const char* e = getenv("MMAD_WGRAD_SPLITS"); return e ? atoi(e) : 0; }();
   if (force > 0) want = std::min<int64_t>(force, max_split);
+  // 1x1x1 convs (the shortcuts): MMAD_WGRAD_1X1_SPLITS overrides the model's count (A/B)
+  static const int force1 = [] { const char* e = getenv("MMAD_WGRAD_1X1_SPLITS"); return e ? atoi(e) : 0; }();
+  if (force1 > 0 && g.taps == 1) want = std::min<int64_t>(force1, max_split);
   s.m_per_split = (int)(cdiv(cdiv(g.M, want), WBK) * WBK);
   s.splits = (int)cdiv(g.M, s.m_per_split);
   return s;
@@ -1415,10 +1418,17 @@ int launch_wgrad_k(const Geom& g, const WSplit& sp, const void* x, const void* d
   return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, false>(g, sp, x, dy, ws, st);
 }
 
+// MMAD_WGRAD_1X1_NST: ring depth of the 1x1x1 (shortcut) weight gradients, 2 (default) or 3
+int wgrad_1x1_nst() {
+  static const int v = [] { const char* e = getenv("MMAD_WGRAD_1X1_NST"); return e ? atoi(e) : 2; }();
+  return v;
+}
+
 template <typename T, int BMW>
 int launch_wgrad(const Geom& g, const WSplit& sp, const void* x, const void* dy, float* ws,
                  hipStream_t st) {
   // ring depth 2: deeper rings (3, 4) cost blocks per CU and measured 10-30 % slower
+  if (g.taps == 1 && wgrad_1x1_nst() == 3) return launch_wgrad_k<T, BMW, 32, 3>(g, sp, x, dy, ws, st);
   return launch_wgrad_k<T, BMW, 32, 2>(g, sp, x, dy, ws, st);
 }
 
