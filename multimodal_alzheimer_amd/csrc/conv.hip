@@ -1418,9 +1418,11 @@ int launch_wgrad_k(const Geom& g, const WSplit& sp, const void* x, const void* d
   return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, false>(g, sp, x, dy, ws, st);
 }
 
-// MMAD_WGRAD_1X1_NST: ring depth of the 1x1x1 (shortcut) weight gradients, 2 (default) or 3
+// ring depth of the 1x1x1 (shortcut) weight gradients: 3 (two stages in flight; measured r03zf
+// layer4 / 3 / 2 downsample wgrad 26.2 / 13.1 / 11.4 -> 26.0 / 12.1 / 10.1 us), or 2
+// (MMAD_WGRAD_1X1_NST=2, the depth of every other wgrad)
 int wgrad_1x1_nst() {
-  static const int v = [] { const char* e = getenv("MMAD_WGRAD_1X1_NST"); return e ? atoi(e) : 2; }();
+  static const int v = [] { const char* e = getenv("MMAD_WGRAD_1X1_NST"); return e ? atoi(e) : 3; }();
   return v;
 }
 
