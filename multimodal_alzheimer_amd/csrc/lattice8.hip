@@ -8,16 +8,16 @@
 // the same for layer4's 4^3 sub-lattices).  Here a tile is one sample's 8 classes over one
 // whole z-plane of the sub-lattice: 64 positions x 8 classes = 512 GEMM rows
 // (position-major), so the tile needs no y/x halo -- a y or x shift that leaves the plane
-// is padding -- and only the three input planes tz-1..tz+1 (32 input channels each chunk,
-// 96 KiB) sit in LDS as the patch.  Per tap only the weights stream (64 output channels x
-// 32 input channels = 4 KiB; 3 taps = one stage; 3-slot ring, two stages in flight).
+// is padding.  A stage is one input plane tz+kz (32 input channels, 32 KiB) and its 9 taps'
+// weights (64 output channels x 32 input channels = 4 KiB a tap), double-buffered: the next
+// stage's plane and weights load during this stage's MFMAs (L8_STAGE9=0 keeps the older
+// loop: the three planes tz-1..tz+1 resident, 3-tap weight stages on a 3-slot ring).
 //  * a 16-row MFMA fragment is 2 x-neighbouring positions x 8 classes: a y shift out of
 //    the plane drops the whole fragment (compile-time per wave row, skipped); an x shift
 //    out of the plane drops half the lanes, which then read a zero row (one select);
 //  * 8 waves = 4 x 2 wave tiles of 128 rows (two y rows of the plane) x 32 channels;
-//  * the loop walks (chunk, kz, ky) stages with kx = -1, 0, 1 inside, the next tap's
-//    fragment reads in flight during each tap's MFMAs; patch planes for the next chunk are
-//    reloaded as soon as the current chunk's last stage on them has run;
+//  * the loop walks (chunk, kz) stages with ky, kx = -1, 0, 1 inside, the next tap's
+//    fragment reads in flight during each tap's MFMAs, one barrier per stage;
 //  * epilogue as the implicit GEMM: bias, BN partial sums (one row per tile), optional
 //    residual + ReLU, bf16 tile transposed through LDS into 16-byte channel stores.
 #include <atomic>
@@ -37,10 +37,19 @@ constexpr int KC8 = RB8 / 2;
 constexpr int PLANE8 = PL8 * RB8;          // 32 KiB
 constexpr int BN8 = 64;                    // output channels per tile
 constexpr int BTAP8 = BN8 * RB8;           // 4 KiB
-constexpr int TPS8 = 3;
-constexpr int BSLOT8 = TPS8 * BTAP8;       // 12 KiB
-constexpr int NSL8 = 3;
-constexpr int RING8 = 3 * PLANE8;
+// L8_STAGE9 (default 1): a stage is a whole kz plane of 9 taps (3 ky rows x 3 kx), streamed
+// with its input plane through a 2-slot plane ring and a 2-slot weight ring (36 KiB a slot),
+// so a tile runs nchunk * nkz stages with one barrier each instead of three times as many.
+// Measured r03l8s9 in the config-2 step: the four layer3 launches 52.1 / 91.7 / 88.0 / 59.1
+// us (3-tap stages, L8_STAGE9=0) -> 47.2 / 81.2 / 76.0 / 47.1 us
+#ifndef L8_STAGE9
+#define L8_STAGE9 1
+#endif
+constexpr int TPS8 = L8_STAGE9 ? 9 : 3;
+constexpr int BSLOT8 = TPS8 * BTAP8;       // 12 KiB (36 KiB for 9-tap stages)
+constexpr int NSL8 = L8_STAGE9 ? 2 : 3;
+constexpr int NPL8 = L8_STAGE9 ? 2 : 3;    // plane slots
+constexpr int RING8 = NPL8 * PLANE8;
 constexpr int ZERO8 = RING8 + NSL8 * BSLOT8;
 constexpr int MAIN8 = ZERO8 + RB8;
 constexpr int CROW8 = BN8 * 2 + 16;
@@ -185,11 +194,12 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   [[maybe_unused]] const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(src + (int64_t)n * svox * g.Cs), 0,
       RAG ? (int)__builtin_amdgcn_readfirstlane((uint32_t)(svox * g.Cs * 2)) : 0, 0x00020000);
-  auto issue_plane = [&](int p, int cc) {
+  // input plane tz - 1 + zr (zr = kz + 1) of channel chunk cc into plane slot p
+  auto issue_plane_at = [&](int p, int zr, int cc) {
     char* pb = smem + p * PLANE8;
     if constexpr (RAG) {
       constexpr uint32_t OOB = 0x80000000u;         // >= any per-sample volume (ok())
-      const int zp = 2 * (tz - 1 + p);
+      const int zp = 2 * (tz - 1 + zr);
       const uint32_t zoff = (uint32_t)(zp * g.H * g.W * g.Cs + cc * KC8) * 2u;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -197,13 +207,14 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
         buf_lds16_asm(ok ? pofs[k] + zoff : OOB, rsx, lds_addr_of(pb + (wave * 4 + k) * 1024));
       }
     } else {
-      const int64_t zoff = (int64_t)2 * (tz - 1 + p) * E * E;
+      const int64_t zoff = (int64_t)2 * (tz - 1 + zr) * E * E;
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         glds16_asm(src + (pvox[k] + zoff) * g.Cs + cc * KC8 + pch[k] * 8,
                    lds_addr_of(pb + (wave * 4 + k) * 1024));
     }
   };
+  auto issue_plane = [&](int p, int cc) { issue_plane_at(p, p, cc); };
   // ---- weight DMA: 3 taps x BW rows x 64 B = 6*TN instructions; wave w issues q = w
   // and q = w + 8 (while < 6*TN); instruction q = tap q / (2TN), rows (q % 2TN) * 16 ..
   constexpr int NQ = 3 * BW / 16;
@@ -219,6 +230,19 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
             (q / QB) * g.Cs;
     wslot_off[h] = (q / QB) * BTAP8 + (q % QB) * 1024;
   }
+  // 9-tap stage weights (L8_STAGE9): taps t0 .. t0 + 8 of chunk cc into slot sl; 9 * BW / 16
+  // instructions, WI9 per wave (surplus ones repeat the last: the same bytes, same place)
+  constexpr int NQ9 = 9 * BW / 16, WI9 = (NQ9 + 7) / 8;
+  auto issue_b9 = [&](int cc, int t0, int sl) {
+#pragma unroll
+    for (int h = 0; h < WI9; ++h) {
+      const int q = min(wave + 8 * h, NQ9 - 1);
+      const int row = (q % QB) * 16 + lrow;
+      const u16* src9 = wgt + (int64_t)(n0 + row) * g.Kpad + ((lane & 3) ^ swz8(row)) * 8 +
+                        (t0 + q / QB) * g.Cs + cc * KC8;
+      glds16_asm(src9, lds_addr_of(ring + sl * BSLOT8 + (q / QB) * BTAP8 + (q % QB) * 1024));
+    }
+  };
   auto issue_b = [&](int cc, int t, int sl) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -258,10 +282,12 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: chunk-0 planes, weights of stages 0 and 1 (L8_PIPE: and 2, in run_pipe)
+  // prologue: chunk-0 planes, weights of stages 0 and 1 (L8_PIPE: and 2, in run_pipe;
+  // L8_STAGE9: stage 0's plane and weights, in run9)
+  if (!L8_STAGE9)
   for (int p = 0; p < 3; ++p)
     if (p - 1 >= kz0 && p - 1 <= kz1) issue_plane(p, 0);
-  for (int s = 0; s < 2 && s < nstage; ++s) {
+  for (int s = 0; s < 2 && s < nstage && !L8_STAGE9; ++s) {
     int cc, t;
     stage_w(s, cc, t);
     issue_b(cc, t, s);
@@ -388,9 +414,35 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
       f0 = f1;
     }
   };
+  // L8_STAGE9: stage e = (chunk c, kz): plane e and its 9 taps' weights land in slot e & 1,
+  // issued at the top of stage e - 1 (after its barrier, when slot (e - 1) & 1 = (e + 1) & 1
+  // has been read by every wave), so the top of stage e waits for everything issued
+  auto run9 = [&](auto wmc) {
+    constexpr int WM = decltype(wmc)::value;
+    const int n9 = g.nchunk * nkz;
+    issue_plane_at(0, kz0 + 1, 0);
+    issue_b9(0, (kz0 + 1) * 9, 0);
+    int e = 0;
+    for (int c = 0; c < g.nchunk; ++c)
+      for (int kzi = 0; kzi < nkz; ++kzi, ++e) {
+        wait_vm_lgkm0<0>();
+        raw_barrier();
+        if (e + 1 < n9) {
+          const int c1 = kzi + 1 < nkz ? c : c + 1, kz1 = kz0 + (kzi + 1 < nkz ? kzi + 1 : 0);
+          issue_plane_at((e + 1) & 1, kz1 + 1, c1);
+          issue_b9(c1, (kz1 + 1) * 9, (e + 1) & 1);
+        }
+        const char* pl = smem + (e & 1) * PLANE8;
+        const char* bs = ring + (e & 1) * BSLOT8 + b_lane;
+        stage8<TN, WM, -1, WR>(acc, bs, pl, ao, zp, lhi);
+        stage8<TN, WM, 0, WR>(acc, bs + 3 * BTAP8, pl, ao, zp, lhi);
+        stage8<TN, WM, 1, WR>(acc, bs + 6 * BTAP8, pl, ao, zp, lhi);
+      }
+  };
   auto dispatch = [&](auto wmc) {
     if constexpr (decltype(wmc)::value < NWM) {
-      if constexpr (L8_PIPE) run_pipe(wmc);
+      if constexpr (L8_STAGE9) run9(wmc);
+      else if constexpr (L8_PIPE) run_pipe(wmc);
       else run(wmc);
     }
   };
