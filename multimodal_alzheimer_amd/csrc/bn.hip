@@ -328,13 +328,22 @@ __device__ __forceinline__ void finalize_body(int C, int64_t count, int nparts,
                                               float* scale_out, float* shift_out, int64_t* nbt,
                                               double* sm) {
   const int c = blockIdx.x * FC + (threadIdx.x % FC);
+  // the per-channel operands are loaded before the partial sums, so their memory round trip
+  // overlaps the sum's instead of following it (this kernel is latency-bound)
+  const bool own = threadIdx.x < FC && c < C;
+  float gm = 1.f, bt = 0.f, rm = 0.f, rv = 0.f;
+  if (own) {
+    if (gamma) gm = gamma[c];
+    if (beta) bt = beta[c];
+    if (running_mean != nullptr) { rm = running_mean[c]; rv = running_var[c]; }
+  }
   double S, Q;
   if (training) {
     sum_parts(c, C, nparts, parts, sm, S, Q);
   } else {
     S = Q = 0.0;
   }
-  if (threadIdx.x >= FC || c >= C) return;
+  if (!own) return;
   double mean, var;
   if (training) {
     mean = S / (double)count;
@@ -343,15 +352,14 @@ __device__ __forceinline__ void finalize_body(int C, int64_t count, int nparts,
     if (running_mean != nullptr) {
       if (nbt != nullptr && c == 0) *nbt += 1;
       const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
-      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
-      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+      running_mean[c] = (float)((1.0 - momentum) * rm + momentum * mean);
+      running_var[c] = (float)((1.0 - momentum) * rv + momentum * unb);
     }
   } else {
-    mean = running_mean[c];
-    var = running_var[c];
+    mean = rm;
+    var = rv;
   }
   const float is = (float)(1.0 / sqrt(var + (double)eps));
-  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
   if (mean_out) mean_out[c] = (float)mean;
   if (invstd_out) invstd_out[c] = is;
   if (scale_out) scale_out[c] = gm * is;
@@ -402,12 +410,18 @@ __device__ __forceinline__ void bwd_finalize(int C, int64_t count, int nparts,
                                              const float* invstd, int training, float* dgamma,
                                              float* dbeta, float* coef, double* sm) {
   const int c = blockIdx.x * FC + (threadIdx.x % FC);
+  const bool own = threadIdx.x < FC && c < C;
+  float gm = 1.f, is = 0.f;                      // loaded ahead of the partial sums
+  if (own) {
+    if (gamma) gm = gamma[c];
+    is = invstd[c];
+  }
   double S, Q;
   sum_parts(c, C, nparts, parts, sm, S, Q);
-  if (threadIdx.x >= FC || c >= C) return;
+  if (!own) return;
   if (dbeta) dbeta[c] = (float)S;
   if (dgamma) dgamma[c] = (float)Q;
-  const double k0 = (double)(gamma ? gamma[c] : 1.f) * invstd[c];
+  const double k0 = (double)gm * is;
   coef[c] = (float)k0;
   coef[C + c] = training ? (float)(k0 * S / (double)count) : 0.f;
   coef[2 * C + c] = training ? (float)(k0 * Q / (double)count) : 0.f;

@@ -31,19 +31,33 @@ namespace {
 constexpr int PW_KC = 32;                        // input channels per block
 constexpr int PW_TY = 8;                         // output rows per y tile
 constexpr int PW_XW = 32;                        // voxels per row (one K step)
-constexpr int PW_XR = PW_XW + 2;                 // x positions per image row group
 constexpr int PW_YR = PW_TY + 2;                 // y rows per plane image
-constexpr int PW_XROWS = PW_YR * PW_XR;          // 340 image rows of 64 B
-constexpr int PW_XDMA = (PW_XROWS + 15) / 16;    // 22 DMA instructions (16 rows each)
-constexpr int PW_XSLOT = PW_XDMA * 1024;
 constexpr int PW_XSLOTS = 4;
 constexpr int PW_YROW = 128;                     // dY rows: 64 co x 2 B
 constexpr int PW_YST = 2 * PW_XW * PW_YROW;      // 8 KiB: 2 K steps per stage
 constexpr int PW_YSLOTS = 3;
-constexpr int PW_Y_OFF = PW_XSLOTS * PW_XSLOT;
-constexpr int PW_LDS = PW_Y_OFF + PW_YSLOTS * PW_YST;
 constexpr int PW_NTHR = 512;
 constexpr uint32_t PW_OOB = 0x80000000u;
+// LAT = false: the 32-wide volume (layer1); a K step is one 32-voxel row and an image row
+// group holds its 34 x positions (x = -1 .. 32).
+// LAT = true: the residue-class form for layer3's dilation-2 convs (16^3 grid, 8 classes of
+// 8^3 sub-lattices, pkg/models/mri_models/anat_cnn.py:29-31): a K step is one sub-lattice
+// row (z', y') of the 4 classes (ry, rx) of one rz, as 4 segments of 8 voxels (x' = 0..7),
+// and an image row group holds 4 x 10 positions (x' = -1 .. 8 per segment, the pads zero
+// rows).  The transposing fragment reads cover 8 K rows per 16-lane group, i.e. exactly one
+// segment, so a tap's kx shift stays a per-lane constant plus an immediate and the layer1
+// loop runs unchanged; a split is (sample, rz, z range) and taps whose y shift leaves the
+// sub-lattice are skipped at compile time (the y tile is the whole 8-row sub-lattice).
+template <bool LAT>
+struct PWC {
+  static constexpr int XR = LAT ? 40 : PW_XW + 2;            // image positions per y row
+  static constexpr int XROWS = PW_YR * XR;                   // 400 / 340 rows of 64 B
+  static constexpr int XDMA = (XROWS + 15) / 16;             // 25 / 22 DMA instructions
+  static constexpr int XSLOT = XDMA * 1024;
+  static constexpr int Y_OFF = PW_XSLOTS * XSLOT;
+  static constexpr int LDS = Y_OFF + PW_YSLOTS * PW_YST;
+  static constexpr int NXMAX = (XDMA + 7) / 8;               // X DMA instructions per wave
+};
 
 struct PWG {
   int nb, Cs, Nd, D, H, K;
@@ -52,9 +66,12 @@ struct PWG {
 
 __device__ __forceinline__ int pw_wsz128(int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); }
 
+template <bool LAT>
 __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __restrict__ x,
                                                          const u16* __restrict__ dy,
                                                          float* __restrict__ ws) {
+  using C = PWC<LAT>;
+  constexpr int XR = C::XR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -65,11 +82,13 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
   const int cot = tile % nco, t2 = tile / nco;
   const int cit = t2 % nci, split = t2 / nci;
-  const int nyt = g.H / PW_TY, nzr = g.D / g.zr;
+  // split = (n, y tile, z range); LAT: (n, rz, z range), rz the class group
+  const int nyt = LAT ? 2 : g.H / PW_TY, nzr = (LAT ? 8 : g.D) / g.zr;
   const int zi = split % nzr, yt = (split / nzr) % nyt, n = split / (nzr * nyt);
-  const int co0 = cot * 64, ci0 = cit * PW_KC, y0 = yt * PW_TY, z0 = zi * g.zr;
+  const int rz = LAT ? yt : 0;
+  const int co0 = cot * 64, ci0 = cit * PW_KC, y0 = LAT ? 0 : yt * PW_TY, z0 = zi * g.zr;
 
-  const int64_t vox = (int64_t)g.D * g.H * PW_XW;
+  const int64_t vox = LAT ? (int64_t)16 * 16 * 16 : (int64_t)g.D * g.H * PW_XW;
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(x + n * vox * g.Cs), 0, (int)__builtin_amdgcn_readfirstlane((int)(vox * g.Cs * 2)),
       0x00020000);
@@ -83,29 +102,48 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   // wraps past the resource; iz = D lands past it: zeros either way)
   // (the lane offsets are recomputed per plane: a few VALU per DMA; held in registers they
   // were spilled by the MFMA loop and reloaded behind a full vmcnt drain)
-  const int nx = wave + 16 < PW_XDMA ? 3 : 2;
+  const int nx = wave + 8 * (C::NXMAX - 1) < C::XDMA ? C::NXMAX : C::NXMAX - 1;
   auto xoff = [&](int h) -> uint32_t {
     const int q = wave + 8 * h, row = 16 * q + (lane >> 2);
-    const int yv = y0 - 1 + row / PW_XR, xv = row % PW_XR - 1;
-    const bool ok = row < PW_XROWS && (unsigned)yv < (unsigned)g.H &&
-                    (unsigned)xv < (unsigned)PW_XW;
-    return ok ? (uint32_t)(((yv * PW_XW + xv) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
+    if constexpr (LAT) {
+      // image row = (y' + 1) * 40 + segment * 10 + x' + 1; segment = class (ry, rx)
+      const int yv = row / XR - 1, ps = row % XR, sg = ps / 10, xv = ps % 10 - 1;
+      const bool ok = row < C::XROWS && (unsigned)yv < 8u && (unsigned)xv < 8u;
+      const int vy = (sg >> 1) + 2 * yv, vx = (sg & 1) + 2 * xv;
+      return ok ? (uint32_t)(((vy * 16 + vx) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
+    } else {
+      const int yv = y0 - 1 + row / XR, xv = row % XR - 1;
+      const bool ok = row < C::XROWS && (unsigned)yv < (unsigned)g.H &&
+                      (unsigned)xv < (unsigned)PW_XW;
+      return ok ? (uint32_t)(((yv * PW_XW + xv) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
+    }
   };
-  const uint32_t xplane = (uint32_t)(g.H * PW_XW * g.Cs * 2);
-  auto issue_x = [&](int e) {                    // stream entry e = input plane z0 - 1 + e
-    const uint32_t pz = (uint32_t)(z0 - 1 + e) * xplane;
-    const uint32_t slot = smem_l + (uint32_t)((e % PW_XSLOTS) * PW_XSLOT);
+  const uint32_t xplane = LAT ? (uint32_t)(16 * 16 * g.Cs * 2) : (uint32_t)(g.H * PW_XW * g.Cs * 2);
+  // (rz: LAT's class group, 0 or 1)
+  auto issue_x = [&](int e, int rz) {            // stream entry e = input plane z0 - 1 + e
+    const uint32_t slot = smem_l + (uint32_t)((e % PW_XSLOTS) * C::XSLOT);
+    const int zp = z0 - 1 + e;
+    // LAT: sub-lattice plane z' -> grid plane rz + 2 z'; planes outside it read as zeros
+    const bool zin = !LAT || (unsigned)zp < 8u;
+    const uint32_t pz = LAT ? (uint32_t)(rz + 2 * zp) * xplane : (uint32_t)zp * xplane;
 #pragma unroll
-    for (int h = 0; h < 3; ++h)
-      if (h < nx) buf_lds16_asm(xoff(h) + pz, rsx, slot + (uint32_t)((wave + 8 * h) * 1024));
+    for (int h = 0; h < C::NXMAX; ++h)
+      if (h < nx)
+        buf_lds16_asm(zin ? xoff(h) + pz : PW_OOB, rsx, slot + (uint32_t)((wave + 8 * h) * 1024));
   };
   // dY stage (output plane o, rows 2M, 2M + 1): image row r = q * 32 + x, one instruction
   // per wave of 8 rows x 128 B, chunk-swizzled for the transposing reads
   const int yr = wave * 8 + (lane >> 3);
-  const uint32_t ylane = (uint32_t)((yr * g.Nd + co0 + ((lane & 7) ^ pw_wsz128(yr)) * 8) * 2);
-  auto issue_y = [&](int o, int m, int sl) {
-    const uint32_t base = (uint32_t)(((z0 + o) * g.H + y0 + 2 * m) * PW_XW) * (uint32_t)g.Nd * 2;
-    buf_lds16_asm(base + ylane, rsy, smem_l + (uint32_t)(PW_Y_OFF + sl * PW_YST + wave * 1024));
+  // LAT: image row q * 32 + segment * 8 + x' = voxel (ry + 2 (y' + q), rx + 2 x') of the plane
+  const int yvox = LAT ? ((((yr >> 3) & 3) >> 1) + 2 * (yr >> 5)) * 16 + (((yr >> 3) & 3) & 1) +
+                             2 * (yr & 7)
+                       : yr;
+  const uint32_t ylane = (uint32_t)((yvox * g.Nd + co0 + ((lane & 7) ^ pw_wsz128(yr)) * 8) * 2);
+  auto issue_y = [&](int o, int m, int sl, int rz) {
+    const uint32_t base =
+        LAT ? (uint32_t)(((rz + 2 * (z0 + o)) * 16 + 4 * m) * 16) * (uint32_t)g.Nd * 2
+            : (uint32_t)(((z0 + o) * g.H + y0 + 2 * m) * PW_XW) * (uint32_t)g.Nd * 2;
+    buf_lds16_asm(base + ylane, rsy, smem_l + (uint32_t)(C::Y_OFF + sl * PW_YST + wave * 1024));
   };
 
   const int cf = wave & 1, tg = wave >> 1;
@@ -120,7 +158,8 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
     ya_hi[i] = (uint32_t)((rsel + 4) * PW_YROW + (((col >> 3) ^ pw_wsz128(rsel + 4)) << 4) +
                           (col & 7) * 2);
   }
-  const uint32_t xb = (uint32_t)(rsel * 64 + cf * 32 + 8 * p4);
+  // (LAT: the 16-lane group lk reads segment lk, whose image positions start at 10 lk)
+  const uint32_t xb = (uint32_t)((LAT ? 10 * lk + q4 : rsel) * 64 + cf * 32 + 8 * p4);
   f32x4 acc[4][7];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -130,12 +169,15 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   auto tr8 = [](const char* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p);
   };
-  // prologue: stream entries 0..2 (planes z0-1..z0+1), dY stages 0 and 1
-  issue_x(0);
-  issue_x(1);
-  issue_x(2);
-  issue_y(0, 0, 0);
-  issue_y(0, 1, 1);
+  // prologue (per rz group): stream entries 0..2 (planes z0-1..z0+1), dY stages 0 and 1
+  auto prologue = [&](int rz) {
+    issue_x(0, rz);
+    issue_x(1, rz);
+    issue_x(2, rz);
+    issue_y(0, 0, 0, rz);
+    issue_y(0, 1, 1, rz);
+  };
+  prologue(rz);
   const int nstage = g.zr * 4;
 
   struct PFr { bf16x8 a[4], b[7]; };
@@ -146,6 +188,10 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
     // (asm move) so the compiler cannot hoist one base per (tap, row) out of the plane loop
     // (30 live VGPRs, spilled); every read is then base + an immediate offset
     const char* xbase[3];
+    // LAT: tap t at output row YL reads sub-lattice row YL + ky - 1: inside it?
+    auto y_on = [](int t, int yl) constexpr {
+      return !LAT || ((unsigned)(yl + (t / 3) % 3 - 1) < 8u);
+    };
     // one K step = output row YL of the current plane (compile time)
     auto kread = [&](const char* yimg, auto qc, auto ylc, PFr& f) {
       constexpr int Q = decltype(qc)::value, YL = decltype(ylc)::value;
@@ -156,10 +202,10 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
                                          4, 5, 6, 7);
       auto one = [&](auto kc) {
         constexpr int K = decltype(kc)::value;
-        if constexpr (K < NT) {
+        if constexpr (K < NT && y_on(TG * 7 + K, YL)) {
           constexpr int t = TG * 7 + K;
           constexpr int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;   // 0..2 (shift + 1)
-          constexpr int r0 = (YL + ky) * PW_XR + kx;
+          constexpr int r0 = (YL + ky) * XR + kx;
           const char* img = xbase[kz] + r0 * 64;
           f.b[K] = __builtin_shufflevector(tr8(img), tr8(img + 4 * 64), 0, 1, 2, 3, 4, 5, 6, 7);
         }
@@ -172,10 +218,11 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
       one(std::integral_constant<int, 5>{});
       one(std::integral_constant<int, 6>{});
     };
-    auto kmma = [&](const PFr& f) {
+    auto kmma = [&](const PFr& f, auto ylc) {
+      constexpr int YL = decltype(ylc)::value;
       auto one = [&](auto kc) {
         constexpr int K = decltype(kc)::value;
-        if constexpr (K < NT) {
+        if constexpr (K < NT && y_on(TG * 7 + K, YL)) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             acc[i][K] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[K], acc[i][K], 0, 0,
@@ -194,7 +241,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
     for (int o = 0; o < g.zr; ++o) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        uint32_t b = (uint32_t)(((o + j) % PW_XSLOTS) * PW_XSLOT) + xb;
+        uint32_t b = (uint32_t)(((o + j) % PW_XSLOTS) * C::XSLOT) + xb;
         asm volatile("v_mov_b32 %0, %1" : "=v"(b) : "v"(b));
         xbase[j] = smem + b;
       }
@@ -207,25 +254,26 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
         if (s + 1 >= nstage) {
           wait_vm_lgkm0<0>();
         } else if ((M == 1 || M == 2) && xnext) {
-          if (nx == 3) wait_vm_lgkm0<4>();
+          if (nx == 4) wait_vm_lgkm0<5>();
+          else if (nx == 3) wait_vm_lgkm0<4>();
           else wait_vm_lgkm0<3>();
         } else {
           wait_vm_lgkm0<1>();
         }
         raw_barrier();
-        if (s + 2 < nstage) issue_y((s + 2) / 4, (s + 2) % 4, (s + 2) % PW_YSLOTS);
-        if (M == 0 && xnext) issue_x(o + 3);
+        if (s + 2 < nstage) issue_y((s + 2) / 4, (s + 2) % 4, (s + 2) % PW_YSLOTS, rz);
+        if (M == 0 && xnext) issue_x(o + 3, rz);
         // (opaque, defined after the barrier: otherwise the dY fragment addresses of all four
         // stages are computed at the plane start and held -- 64 VGPRs, spilled)
-        int yoff = PW_Y_OFF + (s % PW_YSLOTS) * PW_YST;
+        int yoff = C::Y_OFF + (s % PW_YSLOTS) * PW_YST;
         asm volatile("" : "+s"(yoff));
         const char* yimg = smem + yoff;
         PFr f0, f1;
         kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, f0);
         kread(yimg, std::integral_constant<int, 1>{}, std::integral_constant<int, 2 * M + 1>{},
               f1);
-        kmma(f0);
-        kmma(f1);
+        kmma(f0, std::integral_constant<int, 2 * M>{});
+        kmma(f1, std::integral_constant<int, 2 * M + 1>{});
       };
       stage(std::integral_constant<int, 0>{});
       stage(std::integral_constant<int, 1>{});
@@ -256,7 +304,8 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   }
 }
 
-// MMAD_PWGRAD=0 routes these convs back to the row-gather wgrad_kernel (A/B switch)
+// MMAD_PWGRAD=0 routes these convs back to the row-gather wgrad_kernel (A/B switch);
+// MMAD_PWGRAD_LAT=0 keeps layer3's dilation-2 convs there
 bool pw_on() {
   static const bool v = [] {
     const char* e = getenv("MMAD_PWGRAD");
@@ -264,9 +313,30 @@ bool pw_on() {
   }();
   return v;
 }
+bool lat_on() {
+  static const bool v = [] {
+    const char* e = getenv("MMAD_PWGRAD_LAT");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return v;
+}
+
+// the residue-class form: 3^3 dilation 2, padding 2, stride 1 on a 16^3 grid (8^3 classes)
+bool lat_geo(const mmad_patch::Geo& q) {
+  return q.KD == 3 && q.KH == 3 && q.KW == 3 && q.dd == 2 && q.dh == 2 && q.dw == 2 &&
+         q.pd == 2 && q.ph == 2 && q.pw == 2 && q.Ds == 16 && q.Hs == 16 && q.Ws == 16 &&
+         q.Dd == 16 && q.Hd == 16 && q.Wd == 16;
+}
 
 // output planes per split: the largest divisor of D (>= 4) that still gives >= 256 blocks
+// (LAT: of the 8-plane sub-lattice, down to 2)
 int pw_zr(const mmad_patch::Geo& q) {
+  if (lat_geo(q)) {
+    const int64_t base = (int64_t)q.nb * 2 * (q.Cs / PW_KC) * (q.Nd / 64);
+    int zr = 8;
+    while (zr > 2 && base * (8 / zr) < 256) zr /= 2;
+    return zr;
+  }
   const int64_t base = (int64_t)q.nb * (q.Hd / PW_TY) * (q.Cs / PW_KC) * (q.Nd / 64);
   int zr = q.Dd;
   while (zr > 4 && zr % 2 == 0 && base * (q.Dd / zr) < 256) zr /= 2;
@@ -279,16 +349,19 @@ namespace mmad_pwgrad {
 
 bool ok(const mmad_patch::Geo& q) {
   if (!pw_on()) return false;
+  if (q.Cs % PW_KC || q.Nd % 64 || q.Kpad != 27 * q.Cs) return false;
+  if (lat_geo(q)) return lat_on() && (int64_t)4096 * std::max(q.Cs, q.Nd) * 2 < (int64_t(1) << 30);
   if (q.KD != 3 || q.KH != 3 || q.KW != 3 || q.dd != 1 || q.dh != 1 || q.dw != 1) return false;
   if (q.pd != 1 || q.ph != 1 || q.pw != 1) return false;
   if (q.Ds != q.Dd || q.Hs != q.Hd || q.Ws != q.Wd || q.Wd != PW_XW) return false;
-  if (q.Hd % PW_TY || q.Dd < 4 || q.Cs % PW_KC || q.Nd % 64 || q.Kpad != 27 * q.Cs) return false;
+  if (q.Hd % PW_TY || q.Dd < 4) return false;
   if ((int64_t)q.Dd * q.Hd * PW_XW * std::max(q.Cs, q.Nd) * 2 >= (int64_t(1) << 30)) return false;
   const int zr = pw_zr(q);
   return q.Dd % zr == 0 && zr >= 2;
 }
 
 int64_t splits(const mmad_patch::Geo& q) {
+  if (lat_geo(q)) return (int64_t)q.nb * 2 * (8 / pw_zr(q));
   return (int64_t)q.nb * (q.Hd / PW_TY) * (q.Dd / pw_zr(q));
 }
 
@@ -299,17 +372,24 @@ int64_t workspace(const mmad_patch::Geo& q) {
 int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, int* nsplit,
           void* stream) {
   if (!mmad_pwgrad::ok(q)) return MMAD_EUNSUPPORTED;
-  static const bool attr = hipFuncSetAttribute((const void*)pwgrad_kernel,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               PW_LDS) == hipSuccess;
+  static const bool attr =
+      hipFuncSetAttribute((const void*)pwgrad_kernel<false>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, PWC<false>::LDS) == hipSuccess &&
+      hipFuncSetAttribute((const void*)pwgrad_kernel<true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, PWC<true>::LDS) == hipSuccess;
   if (!attr) return MMAD_EUNSUPPORTED;
+  const bool lat = lat_geo(q);
   PWG g{};
   g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.D = q.Dd; g.H = q.Hd; g.K = 27 * q.Cs;
   g.zr = pw_zr(q);
   const int64_t sp = mmad_pwgrad::splits(q);
   const int64_t nblk = sp * (q.Cs / PW_KC) * (q.Nd / 64);
-  hipLaunchKernelGGL(pwgrad_kernel, dim3((unsigned)nblk), dim3(PW_NTHR), PW_LDS,
-                     as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  if (lat)
+    hipLaunchKernelGGL(pwgrad_kernel<true>, dim3((unsigned)nblk), dim3(PW_NTHR), PWC<true>::LDS,
+                       as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  else
+    hipLaunchKernelGGL(pwgrad_kernel<false>, dim3((unsigned)nblk), dim3(PW_NTHR),
+                       PWC<false>::LDS, as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
   *nsplit = (int)sp;
   return launch_status();
 }

@@ -40,6 +40,8 @@ CONV_CASES = [
     (2, 128, 6, 9, 10, 128, 3, 1, 1, 1, False),    # layer2 conv2 (patch kernel, 2 ci chunks)
     (1, 64, 13, 17, 9, 128, 3, 1, 1, 1, True),     # ragged boxes + bias (patch kernel)
     (2, 128, 6, 7, 5, 256, 3, 1, 2, 2, False),     # layer3 (dilation 2)
+    (1, 128, 16, 16, 16, 256, 3, 1, 2, 2, False),  # layer3 at 16^3: residue-class patch wgrad
+    (2, 64, 16, 16, 16, 64, 3, 1, 2, 2, True),     # same, 2 ci chunks, one co tile, bias
     (1, 256, 6, 6, 6, 512, 3, 1, 4, 4, False),     # layer4 (dilation 4)
     (2, 64, 9, 8, 10, 128, 1, 2, 0, 1, False),     # shortcut B, stride 2
     (2, 64, 16, 16, 16, 128, 1, 2, 0, 1, False),   # stride 2, pointwise GEMM fwd / cell dgrad
