@@ -48,11 +48,18 @@ constexpr uint32_t PW_OOB = 0x80000000u;
 // segment, so a tap's kx shift stays a per-lane constant plus an immediate and the layer1
 // loop runs unchanged; a split is (sample, rz, z range) and taps whose y shift leaves the
 // sub-lattice are skipped at compile time (the y tile is the whole 8-row sub-lattice).
-template <bool LAT>
+// W16 (MODE 2): 16-wide volumes (layer2's stride-1 conv on the 16^3 grid): a K step is two
+// consecutive 16-voxel rows (y, y + 1) of one plane, as 2 segments of 16 (the 16-lane groups
+// lk = 0, 1 read segment 0, lk = 2, 3 segment 1); the y tile is the whole 16-row plane and an
+// image row group holds 18 x positions (x = -1 .. 16), 18 rows of them.
+// MODE: 0 the 32-wide form, 1 LAT, 2 W16
+template <int MODE>
 struct PWC {
-  static constexpr int XR = LAT ? 40 : PW_XW + 2;            // image positions per y row
-  static constexpr int XROWS = PW_YR * XR;                   // 400 / 340 rows of 64 B
-  static constexpr int XDMA = (XROWS + 15) / 16;             // 25 / 22 DMA instructions
+  static constexpr bool LAT = MODE == 1, W16 = MODE == 2;
+  static constexpr int XR = LAT ? 40 : W16 ? 18 : PW_XW + 2;  // image positions per y row
+  static constexpr int YRI = W16 ? 18 : PW_YR;               // image y rows
+  static constexpr int XROWS = YRI * XR;                     // 400 / 324 / 340 rows of 64 B
+  static constexpr int XDMA = (XROWS + 15) / 16;             // 25 / 21 / 22 DMA instructions
   static constexpr int XSLOT = XDMA * 1024;
   static constexpr int Y_OFF = PW_XSLOTS * XSLOT;
   static constexpr int LDS = Y_OFF + PW_YSLOTS * PW_YST;
@@ -66,11 +73,12 @@ struct PWG {
 
 __device__ __forceinline__ int pw_wsz128(int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); }
 
-template <bool LAT>
+template <int MODE>
 __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __restrict__ x,
                                                          const u16* __restrict__ dy,
                                                          float* __restrict__ ws) {
-  using C = PWC<LAT>;
+  using C = PWC<MODE>;
+  constexpr bool LAT = C::LAT, W16 = C::W16;
   constexpr int XR = C::XR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -83,12 +91,13 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   const int cot = tile % nco, t2 = tile / nco;
   const int cit = t2 % nci, split = t2 / nci;
   // split = (n, y tile, z range); LAT: (n, rz, z range), rz the class group
-  const int nyt = LAT ? 2 : g.H / PW_TY, nzr = (LAT ? 8 : g.D) / g.zr;
+  const int nyt = LAT ? 2 : W16 ? 1 : g.H / PW_TY, nzr = (LAT ? 8 : g.D) / g.zr;
   const int zi = split % nzr, yt = (split / nzr) % nyt, n = split / (nzr * nyt);
   const int rz = LAT ? yt : 0;
-  const int co0 = cot * 64, ci0 = cit * PW_KC, y0 = LAT ? 0 : yt * PW_TY, z0 = zi * g.zr;
+  const int co0 = cot * 64, ci0 = cit * PW_KC, y0 = LAT || W16 ? 0 : yt * PW_TY, z0 = zi * g.zr;
+  constexpr int VW = LAT || W16 ? 16 : PW_XW;      // voxels per volume row
 
-  const int64_t vox = LAT ? (int64_t)16 * 16 * 16 : (int64_t)g.D * g.H * PW_XW;
+  const int64_t vox = LAT ? (int64_t)16 * 16 * 16 : (int64_t)g.D * g.H * VW;
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(x + n * vox * g.Cs), 0, (int)__builtin_amdgcn_readfirstlane((int)(vox * g.Cs * 2)),
       0x00020000);
@@ -111,6 +120,10 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
       const bool ok = row < C::XROWS && (unsigned)yv < 8u && (unsigned)xv < 8u;
       const int vy = (sg >> 1) + 2 * yv, vx = (sg & 1) + 2 * xv;
       return ok ? (uint32_t)(((vy * 16 + vx) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
+    } else if constexpr (W16) {
+      const int yv = row / XR - 1, xv = row % XR - 1;
+      const bool ok = row < C::XROWS && (unsigned)yv < (unsigned)g.H && (unsigned)xv < 16u;
+      return ok ? (uint32_t)(((yv * 16 + xv) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
     } else {
       const int yv = y0 - 1 + row / XR, xv = row % XR - 1;
       const bool ok = row < C::XROWS && (unsigned)yv < (unsigned)g.H &&
@@ -118,7 +131,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
       return ok ? (uint32_t)(((yv * PW_XW + xv) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
     }
   };
-  const uint32_t xplane = LAT ? (uint32_t)(16 * 16 * g.Cs * 2) : (uint32_t)(g.H * PW_XW * g.Cs * 2);
+  const uint32_t xplane = LAT ? (uint32_t)(16 * 16 * g.Cs * 2) : (uint32_t)(g.H * VW * g.Cs * 2);
   // (rz: LAT's class group, 0 or 1)
   auto issue_x = [&](int e, int rz) {            // stream entry e = input plane z0 - 1 + e
     const uint32_t slot = smem_l + (uint32_t)((e % PW_XSLOTS) * C::XSLOT);
@@ -142,6 +155,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   auto issue_y = [&](int o, int m, int sl, int rz) {
     const uint32_t base =
         LAT ? (uint32_t)(((rz + 2 * (z0 + o)) * 16 + 4 * m) * 16) * (uint32_t)g.Nd * 2
+        : W16 ? (uint32_t)(((z0 + o) * g.H + 4 * m) * 16) * (uint32_t)g.Nd * 2
             : (uint32_t)(((z0 + o) * g.H + y0 + 2 * m) * PW_XW) * (uint32_t)g.Nd * 2;
     buf_lds16_asm(base + ylane, rsy, smem_l + (uint32_t)(C::Y_OFF + sl * PW_YST + wave * 1024));
   };
@@ -159,7 +173,10 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
                           (col & 7) * 2);
   }
   // (LAT: the 16-lane group lk reads segment lk, whose image positions start at 10 lk)
-  const uint32_t xb = (uint32_t)((LAT ? 10 * lk + q4 : rsel) * 64 + cf * 32 + 8 * p4);
+  // (W16: groups lk = 0, 1 read x 0-7, 8-15 of segment 0 -- image row y -- and lk = 2, 3 those
+  // of segment 1, one image row group (18 positions) further)
+  const uint32_t xb = (uint32_t)((LAT ? 10 * lk + q4 : W16 ? 18 * (lk >> 1) + 8 * (lk & 1) + q4 : rsel) *
+                                     64 + cf * 32 + 8 * p4);
   f32x4 acc[4][7];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -205,7 +222,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
         if constexpr (K < NT && y_on(TG * 7 + K, YL)) {
           constexpr int t = TG * 7 + K;
           constexpr int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;   // 0..2 (shift + 1)
-          constexpr int r0 = (YL + ky) * XR + kx;
+          constexpr int r0 = ((W16 ? 2 : 1) * YL + ky) * XR + kx;
           const char* img = xbase[kz] + r0 * 64;
           f.b[K] = __builtin_shufflevector(tr8(img), tr8(img + 4 * 64), 0, 1, 2, 3, 4, 5, 6, 7);
         }
@@ -321,6 +338,21 @@ bool lat_on() {
   return v;
 }
 
+// MMAD_PWGRAD_W16=1 moves the 16-wide stride-1 convs off the row-gather wgrad_kernel
+// (default off until measured)
+bool w16_on() {
+  static const bool v = [] {
+    const char* e = getenv("MMAD_PWGRAD_W16");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  return v;
+}
+// the 16-wide form: dense 3^3, padding 1, stride 1 on volumes 16 voxels wide and high
+bool w16_geo(const mmad_patch::Geo& q) {
+  return q.KD == 3 && q.KH == 3 && q.KW == 3 && q.dd == 1 && q.dh == 1 && q.dw == 1 &&
+         q.pd == 1 && q.ph == 1 && q.pw == 1 && q.Ds == q.Dd && q.Hs == q.Hd && q.Ws == q.Wd &&
+         q.Wd == 16 && q.Hd == 16 && q.Dd >= 4;
+}
 // the residue-class form: 3^3 dilation 2, padding 2, stride 1 on a 16^3 grid (8^3 classes)
 bool lat_geo(const mmad_patch::Geo& q) {
   return q.KD == 3 && q.KH == 3 && q.KW == 3 && q.dd == 2 && q.dh == 2 && q.dw == 2 &&
@@ -337,7 +369,8 @@ int pw_zr(const mmad_patch::Geo& q) {
     while (zr > 2 && base * (8 / zr) < 256) zr /= 2;
     return zr;
   }
-  const int64_t base = (int64_t)q.nb * (q.Hd / PW_TY) * (q.Cs / PW_KC) * (q.Nd / 64);
+  const int64_t base =
+      (int64_t)q.nb * (w16_geo(q) ? 1 : q.Hd / PW_TY) * (q.Cs / PW_KC) * (q.Nd / 64);
   int zr = q.Dd;
   while (zr > 4 && zr % 2 == 0 && base * (q.Dd / zr) < 256) zr /= 2;
   return zr;
@@ -351,6 +384,12 @@ bool ok(const mmad_patch::Geo& q) {
   if (!pw_on()) return false;
   if (q.Cs % PW_KC || q.Nd % 64 || q.Kpad != 27 * q.Cs) return false;
   if (lat_geo(q)) return lat_on() && (int64_t)4096 * std::max(q.Cs, q.Nd) * 2 < (int64_t(1) << 30);
+  if (w16_geo(q)) {
+    if (!w16_on() || (int64_t)q.Dd * 256 * std::max(q.Cs, q.Nd) * 2 >= (int64_t(1) << 30))
+      return false;
+    const int zr = pw_zr(q);
+    return q.Dd % zr == 0 && zr >= 2;
+  }
   if (q.KD != 3 || q.KH != 3 || q.KW != 3 || q.dd != 1 || q.dh != 1 || q.dw != 1) return false;
   if (q.pd != 1 || q.ph != 1 || q.pw != 1) return false;
   if (q.Ds != q.Dd || q.Hs != q.Hd || q.Ws != q.Wd || q.Wd != PW_XW) return false;
@@ -362,6 +401,7 @@ bool ok(const mmad_patch::Geo& q) {
 
 int64_t splits(const mmad_patch::Geo& q) {
   if (lat_geo(q)) return (int64_t)q.nb * 2 * (8 / pw_zr(q));
+  if (w16_geo(q)) return (int64_t)q.nb * (q.Dd / pw_zr(q));
   return (int64_t)q.nb * (q.Hd / PW_TY) * (q.Dd / pw_zr(q));
 }
 
@@ -373,23 +413,28 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
           void* stream) {
   if (!mmad_pwgrad::ok(q)) return MMAD_EUNSUPPORTED;
   static const bool attr =
-      hipFuncSetAttribute((const void*)pwgrad_kernel<false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, PWC<false>::LDS) == hipSuccess &&
-      hipFuncSetAttribute((const void*)pwgrad_kernel<true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, PWC<true>::LDS) == hipSuccess;
+      hipFuncSetAttribute((const void*)pwgrad_kernel<0>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, PWC<0>::LDS) == hipSuccess &&
+      hipFuncSetAttribute((const void*)pwgrad_kernel<1>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, PWC<1>::LDS) == hipSuccess &&
+      hipFuncSetAttribute((const void*)pwgrad_kernel<2>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, PWC<2>::LDS) == hipSuccess;
   if (!attr) return MMAD_EUNSUPPORTED;
-  const bool lat = lat_geo(q);
+  const int mode = lat_geo(q) ? 1 : w16_geo(q) ? 2 : 0;
   PWG g{};
   g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.D = q.Dd; g.H = q.Hd; g.K = 27 * q.Cs;
   g.zr = pw_zr(q);
   const int64_t sp = mmad_pwgrad::splits(q);
   const int64_t nblk = sp * (q.Cs / PW_KC) * (q.Nd / 64);
-  if (lat)
-    hipLaunchKernelGGL(pwgrad_kernel<true>, dim3((unsigned)nblk), dim3(PW_NTHR), PWC<true>::LDS,
+  if (mode == 1)
+    hipLaunchKernelGGL(pwgrad_kernel<1>, dim3((unsigned)nblk), dim3(PW_NTHR), PWC<1>::LDS,
+                       as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  else if (mode == 2)
+    hipLaunchKernelGGL(pwgrad_kernel<2>, dim3((unsigned)nblk), dim3(PW_NTHR), PWC<2>::LDS,
                        as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
   else
-    hipLaunchKernelGGL(pwgrad_kernel<false>, dim3((unsigned)nblk), dim3(PW_NTHR),
-                       PWC<false>::LDS, as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+    hipLaunchKernelGGL(pwgrad_kernel<0>, dim3((unsigned)nblk), dim3(PW_NTHR), PWC<0>::LDS,
+                       as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
   *nsplit = (int)sp;
   return launch_status();
 }

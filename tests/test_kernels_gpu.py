@@ -54,6 +54,8 @@ CONV_CASES = [
     (2, 8, 10, 9, 11, 16, 5, 1, 2, 1, True),       # Small_PET_CNN conv 2
     (2, 32, 6, 5, 7, 64, 3, 1, 1, 1, True),        # Small_PET_CNN conv 4
     (1, 32, 4, 8, 32, 64, 3, 1, 1, 1, False),      # 32-wide: patch wgrad, one split
+    (2, 128, 8, 16, 16, 128, 3, 1, 1, 1, False),   # 16-wide: patch wgrad (2-row K steps)
+    (1, 64, 6, 16, 16, 64, 3, 1, 1, 1, True),      # 16-wide: one z split of 6 planes, bias
     (2, 64, 6, 16, 32, 128, 3, 1, 1, 1, True),     # 32-wide: patch wgrad, 2 co tiles, bias
 ]
 
