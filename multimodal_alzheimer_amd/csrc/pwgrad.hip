@@ -69,6 +69,7 @@ struct PWC {
 struct PWG {
   int nb, Cs, Nd, D, H, K;
   int zr;                                        // output planes per split
+  int ng;                                        // LAT: class groups (rz) per block, 1 or 2
 };
 
 __device__ __forceinline__ int pw_wsz128(int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); }
@@ -90,10 +91,11 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
   const int cot = tile % nco, t2 = tile / nco;
   const int cit = t2 % nci, split = t2 / nci;
-  // split = (n, y tile, z range); LAT: (n, rz, z range), rz the class group
-  const int nyt = LAT ? 2 : W16 ? 1 : g.H / PW_TY, nzr = (LAT ? 8 : g.D) / g.zr;
+  // split = (n, y tile, z range); LAT: (n, rz, z range), rz the class group (or, with
+  // g.ng = 2, (n, z range): the block walks both groups as one stream)
+  const int nyt = LAT ? 2 / g.ng : W16 ? 1 : g.H / PW_TY, nzr = (LAT ? 8 : g.D) / g.zr;
   const int zi = split % nzr, yt = (split / nzr) % nyt, n = split / (nzr * nyt);
-  const int rz = LAT ? yt : 0;
+  const int rz = LAT ? yt : 0;                    // (first) class group
   const int co0 = cot * 64, ci0 = cit * PW_KC, y0 = LAT || W16 ? 0 : yt * PW_TY, z0 = zi * g.zr;
   constexpr int VW = LAT || W16 ? 16 : PW_XW;      // voxels per volume row
 
@@ -132,9 +134,15 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
     }
   };
   const uint32_t xplane = LAT ? (uint32_t)(16 * 16 * g.Cs * 2) : (uint32_t)(g.H * VW * g.Cs * 2);
-  // (rz: LAT's class group, 0 or 1)
+  // (rz: LAT's class group, 0 or 1).  With two groups per block the stream is both groups'
+  // entries back to back: entry e = g (zr + 2) + e', e' = input plane z0 - 1 + e' of group g
+  const int gstride = g.zr + 2;
   auto issue_x = [&](int e, int rz) {            // stream entry e = input plane z0 - 1 + e
     const uint32_t slot = smem_l + (uint32_t)((e % PW_XSLOTS) * C::XSLOT);
+    if (LAT && e >= gstride) {
+      e -= gstride;
+      rz += 1;
+    }
     const int zp = z0 - 1 + e;
     // LAT: sub-lattice plane z' -> grid plane rz + 2 z'; planes outside it read as zeros
     const bool zin = !LAT || (unsigned)zp < 8u;
@@ -195,7 +203,8 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
     issue_y(0, 1, 1, rz);
   };
   prologue(rz);
-  const int nstage = g.zr * 4;
+  const int ng = LAT ? g.ng : 1;
+  const int nstage = ng * g.zr * 4;
 
   struct PFr { bf16x8 a[4], b[7]; };
   auto run = [&](auto tgc) {
@@ -255,20 +264,31 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
       one(std::integral_constant<int, 6>{});
     };
 #pragma unroll 1
-    for (int o = 0; o < g.zr; ++o) {
+    for (int o = 0; o < ng * g.zr; ++o) {
+      // v: this plane's stream position (the second group's planes sit 2 entries on)
+      const bool second = o >= g.zr;
+      const int v = o + (second ? 2 : 0);
+      if (LAT && o == g.zr) {
+        // between the groups: every wave is done with the first group's last plane, whose
+        // slots take the second group's entries 1 and 2 (entry 0 went out a plane earlier)
+        raw_barrier();
+        issue_x(v + 1, rz);
+        issue_x(v + 2, rz);
+      }
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        uint32_t b = (uint32_t)(((o + j) % PW_XSLOTS) * C::XSLOT) + xb;
+        uint32_t b = (uint32_t)(((v + j) % PW_XSLOTS) * C::XSLOT) + xb;
         asm volatile("v_mov_b32 %0, %1" : "=v"(b) : "v"(b));
         xbase[j] = smem + b;
       }
-      const bool xnext = o + 3 <= g.zr + 1;      // stream entry o + 3 exists
+      const bool xnext = v + 3 < ng * gstride;   // stream entry v + 3 exists
       auto stage = [&](auto mc) {
         constexpr int M = decltype(mc)::value;
         const int s = o * 4 + M;
         // dY(s) landed (and at M = 0 the planes of o, issued a plane earlier); younger: dY(s+1)
         // and, at stages 1 and 2, the X plane issued at stage 0 right after stage 2's dY
-        if (s + 1 >= nstage) {
+        // (the second group's first stage: everything, its entries 1 and 2 included)
+        if (s + 1 >= nstage || (LAT && M == 0 && o == g.zr)) {
           wait_vm_lgkm0<0>();
         } else if ((M == 1 || M == 2) && xnext) {
           if (nx == 4) wait_vm_lgkm0<5>();
@@ -278,8 +298,11 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
           wait_vm_lgkm0<1>();
         }
         raw_barrier();
-        if (s + 2 < nstage) issue_y((s + 2) / 4, (s + 2) % 4, (s + 2) % PW_YSLOTS, rz);
-        if (M == 0 && xnext) issue_x(o + 3, rz);
+        if (s + 2 < nstage) {
+          const int p2 = (s + 2) / 4, g2 = p2 >= g.zr ? 1 : 0;
+          issue_y(p2 - g2 * g.zr, (s + 2) % 4, (s + 2) % PW_YSLOTS, rz + g2);
+        }
+        if (M == 0 && xnext) issue_x(v + 3, rz);
         // (opaque, defined after the barrier: otherwise the dY fragment addresses of all four
         // stages are computed at the plane start and held -- 64 VGPRs, spilled)
         int yoff = C::Y_OFF + (s % PW_YSLOTS) * PW_YST;
@@ -360,11 +383,23 @@ bool lat_geo(const mmad_patch::Geo& q) {
          q.Dd == 16 && q.Hd == 16 && q.Wd == 16;
 }
 
+// LAT: both class groups in one block (half the partial slabs) when that still gives >= 256
+// blocks over whole sub-lattices (MMAD_PWGRAD_LAT_NG=1 keeps one group per block; r03ng:
+// layer3.0.conv2 wgrad 90.5 + 20.0 us reduce -> 84.5 + 11.5)
+int lat_ng(const mmad_patch::Geo& q) {
+  static const int force1 = [] {
+    const char* e = getenv("MMAD_PWGRAD_LAT_NG");
+    return e != nullptr && atoi(e) == 1;
+  }();
+  if (!lat_geo(q) || force1) return 1;
+  return (int64_t)q.nb * (q.Cs / PW_KC) * (q.Nd / 64) >= 256 ? 2 : 1;
+}
+
 // output planes per split: the largest divisor of D (>= 4) that still gives >= 256 blocks
 // (LAT: of the 8-plane sub-lattice, down to 2)
 int pw_zr(const mmad_patch::Geo& q) {
   if (lat_geo(q)) {
-    const int64_t base = (int64_t)q.nb * 2 * (q.Cs / PW_KC) * (q.Nd / 64);
+    const int64_t base = (int64_t)q.nb * (2 / lat_ng(q)) * (q.Cs / PW_KC) * (q.Nd / 64);
     int zr = 8;
     while (zr > 2 && base * (8 / zr) < 256) zr /= 2;
     return zr;
@@ -400,7 +435,7 @@ bool ok(const mmad_patch::Geo& q) {
 }
 
 int64_t splits(const mmad_patch::Geo& q) {
-  if (lat_geo(q)) return (int64_t)q.nb * 2 * (8 / pw_zr(q));
+  if (lat_geo(q)) return (int64_t)q.nb * (2 / lat_ng(q)) * (8 / pw_zr(q));
   if (w16_geo(q)) return (int64_t)q.nb * (q.Dd / pw_zr(q));
   return (int64_t)q.nb * (q.Hd / PW_TY) * (q.Dd / pw_zr(q));
 }
@@ -424,6 +459,7 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
   PWG g{};
   g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.D = q.Dd; g.H = q.Hd; g.K = 27 * q.Cs;
   g.zr = pw_zr(q);
+  g.ng = lat_ng(q);
   const int64_t sp = mmad_pwgrad::splits(q);
   const int64_t nblk = sp * (q.Cs / PW_KC) * (q.Nd / 64);
   if (mode == 1)
