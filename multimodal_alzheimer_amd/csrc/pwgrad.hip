@@ -46,7 +46,8 @@ constexpr uint32_t PW_OOB = 0x80000000u;
 // and an image row group holds 4 x 10 positions (x' = -1 .. 8 per segment, the pads zero
 // rows).  The transposing fragment reads cover 8 K rows per 16-lane group, i.e. exactly one
 // segment, so a tap's kx shift stays a per-lane constant plus an immediate and the layer1
-// loop runs unchanged; a split is (sample, rz, z range) and taps whose y shift leaves the
+// loop runs unchanged; a split is (sample, rz, z range) -- or (sample, z range) with both rz
+// groups walked as one plane stream (g.ng = 2) -- and taps whose y shift leaves the
 // sub-lattice are skipped at compile time (the y tile is the whole 8-row sub-lattice).
 // W16 (MODE 2): 16-wide volumes (layer2's stride-1 conv on the 16^3 grid): a K step is two
 // consecutive 16-voxel rows (y, y + 1) of one plane, as 2 segments of 16 (the 16-lane groups
