@@ -1050,7 +1050,10 @@ __global__ void unfold_w_kernel(const TI* __restrict__ x, TO* __restrict__ xu, i
 // Same, UNF_RB input rows per block staged through LDS (Wi <= UNF_MAXW): the rows are one
 // contiguous span, read with one coalesced load per element instead of one strided load
 // per (output, tap); the taps then come from LDS.
-constexpr int UNF_RB = 8, UNF_MAXW = 256;
+#ifndef UNF_RB_V
+#define UNF_RB_V 8
+#endif
+constexpr int UNF_RB = UNF_RB_V, UNF_MAXW = 256;
 template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void unfold_w_rows_kernel(const TI* __restrict__ x,
                                                             TO* __restrict__ xu, int64_t rows,
