@@ -840,6 +840,77 @@ __global__ __launch_bounds__(256) void wgrad_reduce_t_kernel(const float* __rest
     out[l] = tile[(l / taps) * (taps + 1) + l % taps];
 }
 
+// Same sum and layout for grids of few (co, channel-slice) blocks (the 64-channel layer1 and
+// layer2 shapes: 64-128 blocks for 128-69 slabs, ~3.5 TB/s): blockIdx.z takes a group of
+// taps, and each (tap, 4-channel) position's slabs are split over SP thread groups whose
+// partial sums are added in a fixed order (deterministic; the order differs from
+// wgrad_reduce_t_kernel's single chain only in fp32 rounding).
+__global__ __launch_bounds__(256) void wgrad_reduce_tz_kernel(const float* __restrict__ ws,
+                                                              float* __restrict__ dw, int splits,
+                                                              int Nd, int K, int Cs, int taps,
+                                                              int tper) {
+  __shared__ f32x4 part[256];
+  __shared__ float tile[64 * 33];
+  const int ct = min(64, Cs);
+  const int q4 = ct / 4;
+  const int co = blockIdx.y, c0 = blockIdx.x * ct;
+  const int t0 = blockIdx.z * tper, nt = min(taps - t0, tper);
+  const int P = nt * q4;                         // (tap, 4-channel) positions of this block
+  const int SP = max(1, 256 / max(P, 1));        // slab groups per position
+  const int pos = threadIdx.x % P, sg = threadIdx.x / P;
+  const int64_t total = (int64_t)Nd * K;
+  if (nt <= 0) return;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  const int e4 = pos % q4, tl = pos / q4;
+  if (sg < SP) {
+    const int per = (splits + SP - 1) / SP;
+    const int sp0 = sg * per, sp1 = min(splits, sp0 + per);
+    const float* base = ws + (int64_t)co * K + c0 + e4 * 4 + (int64_t)(t0 + tl) * Cs;
+#pragma unroll 8
+    for (int sp = sp0; sp < sp1; ++sp) s += *reinterpret_cast<const f32x4*>(base + sp * total);
+    part[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < P) {
+    f32x4 a = part[threadIdx.x];
+    for (int g2 = 1; g2 < SP; ++g2) a += part[g2 * P + threadIdx.x];   // fixed order
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tile[(e4 * 4 + q) * (tper + 1) + tl] = a[q];
+  }
+  __syncthreads();
+  // dW[co][c][t0 .. t0 + nt): runs of nt taps per channel
+  float* out = dw + ((int64_t)co * Cs + c0) * taps + t0;
+  for (int l = threadIdx.x; l < ct * nt; l += 256) {
+    const int c = l / nt, t = l % nt;
+    out[(int64_t)c * taps + t] = tile[c * (tper + 1) + t];
+  }
+}
+
+// the transposing reduce: wgrad_reduce_t_kernel when its (channel slice, co) grid fills the
+// CUs, else wgrad_reduce_tz_kernel over tap groups (MMAD_REDUCE_TZ=0 keeps the former;
+// r03tz: layer1 16.4 / 16.2 -> 10.6 / 10.3 us, layer2.0.conv1 13.9 -> 11.5)
+int launch_reduce_t(const float* ws, float* dw, int splits, int Nd, int K, int Cs, int taps,
+                    hipStream_t st) {
+  static const bool tz_on = [] {
+    const char* e = getenv("MMAD_REDUCE_TZ");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  const int64_t blocks = (int64_t)cdiv(Cs, 64) * Nd;
+  const int ct = std::min(64, Cs);
+  if (tz_on && blocks < 256 && taps <= 32 && ct % 4 == 0) {
+    int gz = (int)std::min<int64_t>(taps, cdiv(256, blocks));
+    int tper = (int)cdiv(taps, gz);
+    while (tper * (ct / 4) > 256) ++gz, tper = (int)cdiv(taps, gz);
+    gz = (int)cdiv(taps, tper);
+    hipLaunchKernelGGL(wgrad_reduce_tz_kernel, dim3((unsigned)cdiv(Cs, 64), (unsigned)Nd, gz),
+                       dim3(256), 0, st, ws, dw, splits, Nd, K, Cs, taps, tper);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)cdiv(Cs, 64), (unsigned)Nd),
+                       dim3(256), 0, st, ws, dw, splits, Nd, K, Cs, taps);
+  }
+  return launch_status();
+}
+
 // ---- weight packing / input unfolding -------------------------------------------------
 template <typename T>
 __global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ wp, int rows,
@@ -1810,10 +1881,7 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
              : mmad_lattice::wgrad(patch_geo(g), x, dy, (float*)workspace, &splits, stream);
     if (rc) return rc;
     if (rst != st && (rc = fork_stream(st, rst))) return rc;
-    hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)cdiv(g.Cs, 64), (unsigned)g.Nd),
-                       dim3(256), 0, rst, (const float*)workspace, dw, splits, g.Nd, g.K, g.Cs,
-                       g.taps);
-    rc = launch_status();
+    rc = launch_reduce_t((const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.taps, rst);
     if (rc) return rc;
     if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, rstream);
     return MMAD_OK;
@@ -1835,11 +1903,10 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
   const int64_t total = (int64_t)g.Nd * g.K;
   // (the transposing reduce writes whole [ci][taps] runs of dW; scattered 4-byte dW stores
   // from an element-wise reduce cost ~2x in partial-line writes)
-  if (!unfolded(d) && g.taps > 1 && g.taps <= 32)
-    hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)cdiv(g.Cs, 64), (unsigned)g.Nd),
-                       dim3(256), 0, rst, (const float*)workspace, dw, sp.splits, g.Nd, g.K,
-                       g.Cs, g.taps);
-  else if (sp.splits >= 8)
+  if (!unfolded(d) && g.taps > 1 && g.taps <= 32) {
+    rc = launch_reduce_t((const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.taps, rst);
+    if (rc) return rc;
+  } else if (sp.splits >= 8)
     hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
                        rst, (const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.cs_shift,
                        g.taps, unfolded(d) ? d->kw : 0, 1);
