@@ -10,10 +10,13 @@ all-reduce (N>1) + Adam; all parameters trainable (lr_pretrained set).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
-The step is captured once as a HIP graph and replayed (``--eager`` launches it from Python
-every step); under torchrun the graph holds forward + backward, the bucketed RCCL
-all-reduces run eagerly after each replay, then the captured Adam (``--graph`` captures the
-all-reduces too).  Rank 0 prints one JSON line.
+The step is captured once as HIP graphs and replayed (``--eager`` launches it from Python
+every step).  Under torchrun the backward is captured as four graphs split at the backbone
+stages (head + layer4 | layer3 | layer2 | layer1 + stem, graph_step "staged"): after each
+replay that stage's gradient bucket is all-reduced over RCCL on a side stream while the
+next stage's graph runs, then the captured Adam (``--after``: one forward + backward graph,
+every all-reduce after it; ``--graph``: the all-reduces captured inside the step graph).
+Rank 0 prints one JSON line.
 ``roofline`` times the dominant kernel (layer4.0.conv2 forward, the lattice conv) with HIP
 events recorded around each of its launches, on the stream it runs on -- inside the timed
 region when eager, over eager steps just before the capture when graph-replayed;
@@ -33,7 +36,8 @@ sys.path.insert(0, REPO)
 
 import multimodal_alzheimer_amd as M  # noqa: E402
 from multimodal_alzheimer_amd import _lib, volume_ops  # noqa: E402
-from multimodal_alzheimer_amd.graph_step import GraphedTrainStep  # noqa: E402
+from multimodal_alzheimer_amd.graph_step import (GraphedTrainStep,  # noqa: E402
+                                                  backward_stages)
 from multimodal_alzheimer_amd.data_parallel import (GradAllReduce,  # noqa: E402
                                                     broadcast_module_state)
 
@@ -169,8 +173,12 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", action="store_true",
                     help="under torchrun: capture the RCCL bucket all-reduces inside the step's "
-                         "graph too (opt-in, one-rank checked); the default graph-replays "
-                         "forward + backward and runs the all-reduces eagerly after it")
+                         "graph too (opt-in, one-rank checked)")
+    ap.add_argument("--after", action="store_true",
+                    help="under torchrun: one forward + backward graph, every bucket "
+                         "all-reduced after it (not overlapped); the default replays the "
+                         "backward in four stage graphs and overlaps each stage's all-reduce "
+                         "with the next")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel of every step from Python, the all-reduces from "
                          "the backward's hooks (overlapped with it)")
@@ -213,14 +221,22 @@ def main():
         model = M.All_Modalities_Fusion(dict(hparams(args.precision), fl_gamma=2,
                                              resnet_depth_mri=34, resnet_depth_pet=18)).cuda()
     opt = model.configure_optimizers()
-    # 4 MiB buckets: layer4's big weights still go in early (each its own bucket, launched
-    # while backward continues), and the bucket launched last -- stem + layer1, ready only
-    # when backward ends, so its all-reduce is not hidden -- stays ~1 MB instead of ~15 MB
+    use_graph = not args.eager and (args.graph or args.workload in ("mri", "fusion"))
+    collectives = "inside" if args.graph else "after" if args.after else "staged"
+    # staged (default): one bucket per backward stage -- head + layer4 (~43 MB for
+    # ResNet-10, overlapped by the three later stages), layer3, layer2, layer1 + stem (~1 MB,
+    # the only one not hidden).  Otherwise 4 MiB buckets in reverse order: eager, layer4's
+    # big weights go in early (launched from the hooks while backward continues) and the
+    # bucket launched last stays ~1 MB instead of ~15 MB.
     reducer = None
     if dp:
         broadcast_module_state(model)          # identical replicas, as DDP
-        reducer = GradAllReduce(model.parameters(),
-                                bucket_mb=float(os.environ.get("MMAD_DP_BUCKET_MB", "4")))
+        if use_graph and collectives == "staged":
+            reducer = GradAllReduce(model.parameters(), bucket_mb=None,
+                                    stages=backward_stages(model)[1])
+        else:
+            reducer = GradAllReduce(model.parameters(),
+                                    bucket_mb=float(os.environ.get("MMAD_DP_BUCKET_MB", "4")))
     B, S = args.batch, args.size
     VOL = (91, 109, 91) if mni else (S, S, S)
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)   # this rank's shard
@@ -249,17 +265,14 @@ def main():
                 dp_events.append((e0, e1))
         opt.step()
 
-    # The step (general_step, backward, Adam) is captured once as a HIP graph and replayed --
+    # The step (general_step, backward, Adam) is captured once as HIP graphs and replayed --
     # the same kernels, bit-identical to eager steps (tests/test_graph_step_gpu.py); eager,
     # the host needs ~2.9 of the GPU's ~3.5 ms per step to enqueue it, so a slower or busier
-    # host makes the run launch-bound (measured: 1713 vol/s on one box).  N>1 uses the same
-    # launch mode, so the 1 -> N curve compares like with like: forward + backward replayed
-    # from the graph, then the bucketed RCCL all-reduces issued eagerly (not overlapped with
-    # the backward: ~57 MB of fp32 gradients per step for ResNet-10), then the captured Adam.
-    # --graph captures the all-reduces inside the graph (overlapped; one-rank checked only),
-    # --eager launches them from the backward's hooks (overlapped; host-bound).
-    use_graph = not args.eager and (args.graph or args.workload == "mri")
-    collectives = "inside" if args.graph else "after"
+    # host makes the run launch-bound (measured: 1713 vol/s on one box).  N>1 replays the
+    # same kernels with the backward split into stage graphs, each stage's RCCL all-reduce
+    # overlapping the next stage (tests/test_dp_graph_world2_gpu.py); --after issues every
+    # all-reduce after the backward, --graph captures them inside the graph (one-rank
+    # checked only), --eager launches them from the backward's hooks (host-bound).
     events = []
     if use_graph:
         if not args.no_roofline:
@@ -343,7 +356,10 @@ def main():
     result["config"]["step_launch"] = (
         "eager" if not use_graph else "hip graph replay" if reducer is None else
         "hip graph replay (fwd+bwd) + eager RCCL all-reduce + graph-replayed Adam"
-        if collectives == "after" else "hip graph replay incl. RCCL all-reduce")
+        if collectives == "after" else
+        "hip graph replay: fwd + 4 backward-stage graphs, each stage's RCCL all-reduce "
+        "overlapping the next, graph-replayed Adam" if collectives == "staged" else
+        "hip graph replay incl. RCCL all-reduce")
     # host time spent enqueueing each step: close to ms_per_step means the run was bound by
     # the host (Python / launch overhead), not by the GPU
     result["host_issue_ms_per_step"] = t_issue / args.steps * 1e3

@@ -56,8 +56,9 @@ const char* mmad_strerror(int status);
 /* Kernel-variant switch (the run-time twin of the MMAD_* environment A/B switches; no
  * reference counterpart): "lattice_zp" = 1 plane-pair residue-class conv (default), 0 the
  * one-plane form, 2 plane-pair at any size; "lattice" / "lattice8" = 1 residue-class convs
- * where their tiles fill the CUs (default), 2 at any size, 0 off; "pool_run" = 1 the
- * column-carrying stem pool forward, 0 the per-output form (default); "patchz" = 1 the
+ * where their tiles fill the CUs (default), 2 at any size, 0 off; "pool_run" = the stem
+ * BN+ReLU+max-pool forward: 2 the z-walking kernel (default), 1 the column-carrying kernel,
+ * 0 the per-output rows kernel; "patchz" = 1 the
  * persistent z-walking layer1 conv where its work items fill the CUs (default), 2 at any
  * size, 0 the per-box patch conv.  value < 0 only queries.
  * Returns the previous value, -1 for an unknown name.  Not thread-safe against concurrent

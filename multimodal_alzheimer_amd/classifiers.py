@@ -307,6 +307,11 @@ class MergedAdam(torch.optim.Adam):
 
     def state_dict(self):
         sd = super().state_dict()
+        for g in sd["param_groups"]:
+            # a captured step's 0-d device lr (graph_step) is saved as the plain float the
+            # reference's torch 1.13 Adam keeps (it feeds lr straight into addcdiv_'s value)
+            if torch.is_tensor(g.get("lr")):
+                g["lr"] = float(g["lr"])
         if len(self._ref_groups) == len(self.param_groups):
             return sd                      # nothing was merged: the layouts coincide
         idx, gidx = self._merged_index()

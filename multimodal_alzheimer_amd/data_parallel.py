@@ -7,10 +7,12 @@ only exchange per step is the gradient all-reduce:
 
 * ``shard_indices`` -- DistributedSampler-style sharding of the sample-pair index list
   (seeded shuffle per epoch, equal shard sizes by padding with wrap-around samples);
-* ``GradAllReduce`` -- gradient buckets (~32 MiB, reverse registration order so the
-  last layers' gradients, ready first in backward, go first) all-reduced asynchronously
-  from post-accumulate-grad hooks while backward continues; ``finish()`` waits, averages
-  and writes the reduced gradients back.
+* ``GradAllReduce`` -- gradient buckets (``bucket_mb``, reverse registration order so the
+  last layers' gradients, ready first in backward, go first; or one bucket per backward
+  stage, ``stages=``) all-reduced asynchronously -- from post-accumulate-grad hooks while an
+  eager backward continues, or per stage between the replayed backward graphs
+  (graph_step ``collectives="staged"``); ``finish()`` waits, averages and writes the
+  reduced gradients back.
 
 BN batch statistics are per replica (each rank normalises its own shard, as DDP without
 SyncBatchNorm).  The running statistics: DDP's default ``broadcast_buffers=True`` copies
@@ -41,6 +43,28 @@ def shard_indices(n_samples, rank, world, epoch=0, shuffle=True, seed=15):
     return order[rank:total:world]
 
 
+class ShardSampler(torch.utils.data.Sampler):
+    """This rank's shard of a dataset's samples -- for ``dataset.MultiModalDataset`` the
+    merged PET/MRI/tabular pairs and triples -- as a DataLoader sampler
+    (DistributedSampler semantics via ``shard_indices``); ``set_epoch`` reshuffles."""
+
+    def __init__(self, dataset, rank=None, world=None, shuffle=True, seed=15):
+        self.n = len(dataset)
+        self.rank = dist.get_rank() if rank is None else rank
+        self.world = dist.get_world_size() if world is None else world
+        self.shuffle, self.seed, self.epoch = shuffle, seed, 0
+
+    def set_epoch(self, epoch):
+        self.epoch = epoch
+
+    def __iter__(self):
+        return iter(shard_indices(self.n, self.rank, self.world, self.epoch, self.shuffle,
+                                  self.seed))
+
+    def __len__(self):
+        return -(-self.n // self.world)
+
+
 def broadcast_module_state(module, src=0, group=None, buffers_only=False):
     """Every rank takes rank ``src``'s parameters and buffers (BN running statistics,
     num_batches_tracked), as DDP does at construction; ``buffers_only`` re-syncs just the
@@ -65,25 +89,48 @@ def _aligned(numel, elsize):
     return -(-numel // step) * step
 
 
+def _split(params, cap):
+    out, cur, size = [], [], 0
+    for p in params:
+        cur.append(p)
+        size += p.numel() * p.element_size()
+        if size >= cap:
+            out.append(cur)
+            cur, size = [], 0
+    if cur:
+        out.append(cur)
+    return out
+
+
 class GradAllReduce:
-    def __init__(self, params, bucket_mb=32.0, group=None):
+    def __init__(self, params, bucket_mb=32.0, group=None, stages=None):
+        """``stages``: optional list of parameter lists in the order backward completes them
+        (graph_step.backward_stages); each stage is cut into buckets of ``bucket_mb``
+        (``None``: one bucket per stage) and ``launch_stage(k)`` starts stage k's buckets.
+        Without it the parameters are bucketed in reverse registration order."""
         self.group = group
         self.world = dist.get_world_size(group)
         # RCCL averages in the collective itself (ncclAvg); gloo has no AVG: sum, then scale
         self._avg = dist.get_backend(group) == "nccl"
         self._op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
         self.params = [p for p in params if p.requires_grad]
-        cap = int(bucket_mb * (1 << 20))
-        self.buckets = []
-        cur, size = [], 0
-        for p in reversed(self.params):          # backward produces the last layers first
-            cur.append(p)
-            size += p.numel() * p.element_size()
-            if size >= cap:
-                self.buckets.append(cur)
-                cur, size = [], 0
-        if cur:
-            self.buckets.append(cur)
+        cap = float("inf") if bucket_mb is None else int(bucket_mb * (1 << 20))
+        self.stage_buckets = None
+        if stages is None:
+            # backward produces the last layers first
+            self.buckets = _split(list(reversed(self.params)), cap)
+        else:
+            mine = set(self.params)
+            staged = [[p for p in st if p in mine] for st in stages]
+            seen = [p for st in staged for p in st]
+            if len(seen) != len(set(seen)) or set(seen) != mine:
+                raise ValueError("stages must partition the trainable parameters")
+            self.buckets, self.stage_buckets = [], []
+            for st in staged:
+                bs = _split(st, cap) if st else []
+                self.stage_buckets.append(list(range(len(self.buckets),
+                                                     len(self.buckets) + len(bs))))
+                self.buckets += bs
         self._owner = {}
         for bi, b in enumerate(self.buckets):
             for p in b:
@@ -135,6 +182,9 @@ class GradAllReduce:
 
     def _launch(self, bi):
         flat = self.flats[bi]
+        for p in self.buckets[bi]:
+            if p.grad is None:                   # unused this step: contributes zeros
+                p.grad = torch.zeros_like(p)
         grads, views = self._foreign(bi)
         if flat.is_cuda:
             # conv weight gradients may come from volume_ops' side stream (the backward
@@ -155,14 +205,19 @@ class GradAllReduce:
             work = dist.all_reduce(flat, op=self._op, group=self.group, async_op=True)
         self._inflight[bi] = work
 
+    def launch_stage(self, k):
+        """Start the all-reduce of backward stage k's buckets (their gradients are complete
+        on the current stream): on the side stream, overlapping whatever the current stream
+        runs next."""
+        for bi in self.stage_buckets[k]:
+            if bi not in self._inflight:
+                self._launch(bi)
+
     def finish(self):
         """Wait for every bucket (launching any whose grads never all arrived), then
         make every parameter's grad the mean over ranks."""
         for bi, b in enumerate(self.buckets):
             if bi not in self._inflight:
-                for p in b:
-                    if p.grad is None:
-                        p.grad = torch.zeros_like(p)
                 self._launch(bi)
         if self.params and self.params[0].is_cuda:
             from .volume_ops import grad_stream

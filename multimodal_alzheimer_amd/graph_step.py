@@ -1,4 +1,4 @@
-"""One training step captured as a HIP graph and replayed.
+"""One training step captured as HIP graphs and replayed.
 
 The eager step (``general_step`` -> ``loss.backward()`` -> ``optimizer.step()``, what
 Lightning's automatic optimisation runs per batch, anat_cnn.py:99-109 + :111-136) issues
@@ -12,7 +12,27 @@ buffer (``step(batch)`` copies the new batch into it), no host reads of device v
 the step, the optimizer made capturable (set here), gradients produced inside the graph
 (``zero_grad(set_to_none=True)`` before capture).  Warm-up iterations run eagerly on a side
 stream first, as torch requires, so the model takes ``warmup`` optimizer steps before the
-first replay.  Not combined with the RCCL gradient all-reduce (data_parallel) here.
+first replay.
+
+With a data-parallel gradient all-reduce (``reducer``, data_parallel.GradAllReduce) there
+are three ways to place the RCCL collectives (``collectives=``):
+
+* ``"staged"`` (bench.py's default at N > 1): the backward is split at backbone stage
+  boundaries (``backward_stages``: head + layer4 | layer3 | layer2 | layer1 + stem of every
+  MedicalNet ResNet in the model) and each part is captured as its own graph
+  (``StagedBackward``: ``torch.autograd.grad`` from the previous boundary's gradients to
+  the next boundary's tensors and this stage's parameters).  Each call replays graph 0
+  (forward + first backward stage), starts that stage's bucket all-reduce on the side
+  stream (after the main stream's work so far), replays graph 1 on the main stream while
+  the collective runs, and so on; then ``finish()`` (main waits for the side stream) and
+  the captured Adam.  Only the last stage's ~1 MB bucket is not overlapped.  The ordering
+  guarantee is plain stream order: a bucket's collective is enqueued on the side stream
+  behind an event recorded on the main stream after the graph that produced it.
+* ``"after"``: one graph holds forward + backward; each call replays it, runs
+  ``finish()`` eagerly -- every bucket's all-reduce on the side stream, not overlapped with
+  the backward -- then replays the captured optimizer step.
+* ``"inside"``: the bucket all-reduces (launched from the backward's hooks) and
+  ``finish()`` are captured with the step (experimental; bench.py --graph).
 
 What a replay changes without running Python is made visible to the host-side state that
 depends on it:
@@ -26,36 +46,150 @@ depends on it:
 * dropout draws its seed on the device (``head_ops.dropout``), so every replay gets a
   fresh mask.
 """
-import os
-
 import torch
 
 from . import volume_ops
 
+COLLECTIVES = ("staged", "after", "inside")
+DEFAULT_CUTS = ("layer4", "layer3", "layer2")
+
+
+def backward_stages(model, cuts=DEFAULT_CUTS):
+    """Split ``model``'s backward at the inputs of the named stages of every MedicalNet
+    ResNet inside it (``cuts`` in backward order).  Returns ``(boundaries, params)``:
+    ``boundaries[k]`` = the modules whose forward input closes stage k (k < S - 1), and
+    ``params[k]`` = the trainable parameters whose gradients stage k completes:
+    stage 0 = everything downstream of the first cut (the heads, fusion MLP, any branch
+    that is not a ResNet, the cut stage itself), stage k = the k-th cut stage of each
+    ResNet, the last stage = what precedes the last cut (stem + earlier stages).
+    Returns ``([], [all params])`` when the model has no ResNet."""
+    from .medicalnet import ResNet
+    nets = [m for m in model.modules() if isinstance(m, ResNet)]
+    trainable = [p for p in model.parameters() if p.requires_grad]
+    if not nets or not cuts:
+        return [], [trainable]
+    order = ("conv1", "bn1", "layer1", "layer2", "layer3", "layer4")
+    pos = [order.index(c) for c in cuts]
+    if pos != sorted(pos, reverse=True) or len(set(pos)) != len(pos):
+        raise ValueError(f"cuts must name distinct stages in backward order, got {cuts}")
+    stage_of = {}
+    for net in nets:
+        for i, name in enumerate(order):
+            # stage of module ``name``: the number of cuts at or before it, counted from
+            # the back (a module at or after cuts[0] is in stage 0)
+            k = sum(1 for p in pos if i < p)
+            for p in getattr(net, name).parameters():
+                stage_of[p] = k
+    params = [[] for _ in range(len(cuts) + 1)]
+    for p in trainable:
+        params[stage_of.get(p, 0)].append(p)
+    boundaries = [[getattr(net, c) for net in nets] for c in cuts]
+    return boundaries, params
+
+
+class StagedBackward:
+    """The backward of one step as S consecutive parts (``backward_stages``), so that each
+    part can be captured as its own graph and the gradients it completes handed to the
+    all-reduce while the next part runs.
+
+    ``arm()`` registers forward pre-hooks on the boundary modules that record each
+    boundary's input tensor and its twin alias (volume_ops "twin outputs": a residual
+    block reads its input through two aliases, both outputs of the producer's autograd
+    node).  ``run(k, loss)`` computes stage k with ``torch.autograd.grad`` -- the gradients
+    of the next boundary's tensors are CAPTURED at the producer's node (the node itself
+    runs in the next stage) -- and assigns this stage's parameter gradients as ``.grad``
+    (a weight gradient written into its data-parallel bucket slice stays that slice).
+    Same kernels, same order as one ``loss.backward()``."""
+
+    def __init__(self, boundaries, params):
+        self.boundaries, self.params = boundaries, params
+        self.n = len(params)
+        self._rec = [[] for _ in boundaries]
+        self._grads = None
+        self._hooks = []
+
+    def arm(self):
+        self.disarm()
+        self._rec = [[] for _ in self.boundaries]
+        for k, mods in enumerate(self.boundaries):
+            for m in mods:
+                self._hooks.append(m.register_forward_pre_hook(self._recorder(k)))
+
+    def disarm(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+    def _recorder(self, k):
+        def hook(_mod, args):
+            x = args[0]
+            self._rec[k].append(x)
+            alias = volume_ops._TWINS.get(id(x))
+            if alias is not None and alias._base is x:
+                self._rec[k].append(alias)
+        return hook
+
+    def run(self, k, loss=None):
+        if k == 0:
+            roots, grads = [loss], None
+        else:
+            roots, grads = self._grads
+        nxt = [t for t in self._rec[k] if t.requires_grad] if k < self.n - 1 else []
+        ps = self.params[k]
+        if not nxt and not ps:
+            self._grads = ([], [])
+            return
+        if not roots:
+            raise RuntimeError(f"backward stage {k}: no gradient reached its boundary")
+        out = torch.autograd.grad(roots, nxt + ps, grads, allow_unused=True)
+        for p, g in zip(ps, out[len(nxt):]):
+            if g is None:
+                continue
+            if p.grad is None:
+                p.grad = g
+            else:
+                p.grad.add_(g)
+        keep = [(t, g) for t, g in zip(nxt, out[:len(nxt)]) if g is not None]
+        self._grads = ([t for t, _ in keep], [g for _, g in keep])
+        if k == self.n - 1:
+            self.release()
+
+    def release(self):
+        self._grads = None
+        self._rec = [[] for _ in self.boundaries]
+
+    def run_all(self, loss):
+        """every stage in order (eager use; ``arm()`` must have been active during the
+        forward that produced ``loss``)"""
+        for k in range(self.n):
+            self.run(k, loss)
+
 
 class GraphedTrainStep:
-    def __init__(self, model, optimizer, batch, warmup=3, reducer=None, collectives="inside"):
-        """``reducer``: a data_parallel.GradAllReduce.  ``collectives``:
-        * "inside": its bucket all-reduces (launched from the backward's hooks) and
-          ``finish()`` are captured with the step (experimental: bench.py --graph under
-          torchrun; checked at one rank only);
-        * "after": the graph holds forward + backward only (gradients land in the bucket
-          slices); each call replays it, then runs ``finish()`` eagerly -- every bucket's
-          RCCL all-reduce on the side stream, not overlapped with the backward -- then
-          replays the captured optimizer step.  No collective inside a graph; the host
-          issues a handful of calls per step (bench.py's default at N > 1)."""
+    def __init__(self, model, optimizer, batch, warmup=3, reducer=None, collectives="inside",
+                 cuts=DEFAULT_CUTS):
+        """``reducer``: a data_parallel.GradAllReduce (for ``collectives="staged"`` built
+        with ``stages=backward_stages(model, cuts)[1]``).  ``collectives``: see the module
+        docstring."""
         self.model, self.optimizer = model, optimizer
         self.reducer = reducer
-        self.after = reducer is not None and collectives == "after"
+        if reducer is not None and collectives not in COLLECTIVES:
+            raise ValueError(f"collectives must be one of {COLLECTIVES}, not {collectives!r}")
+        self.mode = collectives if reducer is not None else None
         self.finish_events = None            # list: (start, end) events around each finish()
-        if reducer is not None and collectives not in ("inside", "after"):
-            raise ValueError(f"collectives must be 'inside' or 'after', not {collectives!r}")
         self.static = {k: v.clone() if torch.is_tensor(v) else v for k, v in batch.items()}
         dev = next(model.parameters()).device
         for g in optimizer.param_groups:
             g["capturable"] = True
             if not torch.is_tensor(g["lr"]):
                 g["lr"] = torch.tensor(float(g["lr"]), dtype=torch.float32, device=dev)
+        staged = None
+        if self.mode == "staged":
+            bounds, params = backward_stages(model, cuts)
+            staged = StagedBackward(bounds, params)
+            if reducer.stage_buckets is None or len(reducer.stage_buckets) != staged.n:
+                raise ValueError("collectives='staged' needs GradAllReduce(stages=...) built "
+                                 "from backward_stages(model, cuts)")
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -63,55 +197,59 @@ class GraphedTrainStep:
                 self._eager()
         torch.cuda.current_stream().wait_stream(side)
         optimizer.zero_grad(set_to_none=True)
-        self.graph = torch.cuda.CUDAGraph()
+        self.graphs = []
         self.opt_graph = None
-        if self.after:
-            reducer.defer = os.environ.get("MMAD_GRAPH_DEBUG", "") != "nodefer"
+        if self.mode in ("staged", "after"):
+            reducer.defer = True             # the capture's hooks (if any) only count
             try:
-                with torch.cuda.graph(self.graph):
-                    self.out = model.general_step(self.static, 0, "train")
-                    self.out["loss"].backward()
-                    dbg = os.environ.get("MMAD_GRAPH_DEBUG", "")
-                    if dbg == "join":
-                        torch.cuda.current_stream().wait_stream(
-                            volume_ops.grad_stream(self.static_device()))
-                    elif dbg == "tail":
-                        self._tail = torch.zeros(1, device=self.static_device()).add_(1)
+                if self.mode == "after":
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        self.out = model.general_step(self.static, 0, "train")
+                        self.out["loss"].backward()
+                    self.graphs.append(g)
+                else:
+                    staged.arm()
+                    try:
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g):
+                            self.out = model.general_step(self.static, 0, "train")
+                            staged.run(0, self.out["loss"])
+                    finally:
+                        staged.disarm()
+                    self.graphs.append(g)
+                    for k in range(1, staged.n):
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, pool=self.graphs[0].pool()):
+                            staged.run(k)
+                        self.graphs.append(g)
             finally:
                 reducer.defer = False
-            reducer.reset()                  # the capture's hooks only counted
+            reducer.reset()
             reducer.finish()                 # eager: gradients now averaged in place
             self.opt_graph = torch.cuda.CUDAGraph()
-            pool = self.graph.pool() if os.environ.get("MMAD_GRAPH_SHARE_POOL", "1") != "0" else None
-            with torch.cuda.graph(self.opt_graph, pool=pool):
+            with torch.cuda.graph(self.opt_graph, pool=self.graphs[0].pool()):
                 optimizer.step()
         else:
-            with torch.cuda.graph(self.graph):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
                 self.out = model.general_step(self.static, 0, "train")
                 self.out["loss"].backward()
                 if reducer is not None:
                     reducer.finish()
-                if os.environ.get("MMAD_GRAPH_DEBUG", "") != "noopt":
-                    optimizer.step()
+                optimizer.step()
+            self.graphs.append(g)
+        self.graph = self.graphs[0]
         # keep the graph-owned output buffers, not their autograd graph: a live grad_fn chain
         # would keep every parameter's AccumulateGrad node (created on the capture stream)
         # alive, and later eager steps would reuse those nodes across streams
         self.out = {k: v.detach() if torch.is_tensor(v) else v for k, v in self.out.items()}
 
-    def static_device(self):
-        return next(self.model.parameters()).device
-
     def _eager(self):
         self.optimizer.zero_grad(set_to_none=True)
+        self.model.general_step(self.static, 0, "train")["loss"].backward()
         if self.reducer is not None:
-            self.reducer.defer = self.after
-        try:
-            self.model.general_step(self.static, 0, "train")["loss"].backward()
-            if self.reducer is not None:
-                self.reducer.finish()
-        finally:
-            if self.reducer is not None:
-                self.reducer.defer = False
+            self.reducer.finish()
         self.optimizer.step()
 
     def __call__(self, batch=None):
@@ -122,13 +260,18 @@ class GraphedTrainStep:
             for k, v in batch.items():
                 if torch.is_tensor(v):
                     self.static[k].copy_(v, non_blocking=True)
-        self.graph.replay()
-        if self.after:
+        if self.mode is None or self.mode == "inside":
+            self.graph.replay()
+        else:
+            for k, g in enumerate(self.graphs):
+                g.replay()
+                if self.mode == "staged":
+                    self.reducer.launch_stage(k)   # overlaps the next graph's replay
             if self.finish_events is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-            self.reducer.finish()            # no hook ran in the replay: launches every bucket
+            self.reducer.finish()            # launches what is left, main waits, copies back
             if self.finish_events is not None:
                 e1.record()
                 self.finish_events.append((e0, e1))

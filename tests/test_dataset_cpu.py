@@ -1,0 +1,148 @@
+"""The multimodal sample table (dataset.MultiModalDataset / merge_modalities) against the
+reference class itself: tests/golden/merge_golden.json holds MultiModalDataset's merged
+table and label distribution (pkg/utils/dataloader.py:63-156, 323-344) for 8 settings
+(2 and 3 modalities in several orders, binary / 3-class, 0 / 90 / 180 / 365-day windows,
+one single-modality table), built in this container from tests/golden/merge_samples.csv
+by tests/golden/make_merge_golden.py.  Bit-exact: IDs, labels, paths, tabular values,
+min_time / max_time, row order.  Plus the NIfTI reader, __getitem__ and the shard sampler
+over the merged samples."""
+import json
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from multimodal_alzheimer_amd import nifti
+from multimodal_alzheimer_amd.data_parallel import ShardSampler, shard_indices
+from multimodal_alzheimer_amd.dataset import MultiModalDataset
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CSV = os.path.join(GOLDEN, "merge_samples.csv")
+with open(os.path.join(GOLDEN, "merge_golden.json")) as _f:
+    FIX = json.load(_f)
+
+
+def _val(v):
+    if v is None or (isinstance(v, float) and np.isnan(v)):
+        return None
+    if isinstance(v, pd.Timestamp):
+        return v.strftime("%Y-%m-%d")
+    if isinstance(v, (np.integer, int)) and not isinstance(v, bool):
+        return float(v)
+    if isinstance(v, (np.floating, float)):
+        return float(v)
+    return str(v)
+
+
+def _record(ds):
+    return {"columns": [str(c) for c in ds.columns],
+            "rows": [[_val(v) for v in row] for row in ds.itertuples(index=False, name=None)]}
+
+
+@pytest.mark.parametrize("case", range(len(FIX["settings"])),
+                         ids=[f"{'+'.join(s['modalities'])}-{s['binary_classification']}-"
+                              f"{s['days_threshold']}d" for s in FIX["settings"]])
+def test_merged_table_matches_reference(case):
+    s = FIX["settings"][case]
+    d = MultiModalDataset(CSV, binary_classification=s["binary_classification"],
+                          modalities=s["modalities"], days_threshold=s["days_threshold"])
+    assert len(d) == s["len"]
+    got = _record(d.ds)
+    assert got["columns"] == s["table"]["columns"]
+    for i, (a, b) in enumerate(zip(got["rows"], s["table"]["rows"])):
+        assert a == b, (i, a, b)
+    assert len(got["rows"]) == len(s["table"]["rows"])
+    if "label_distribution_error" in s:
+        with pytest.raises(KeyError):
+            d.get_label_distribution()
+    else:
+        counts, counts_n = d.get_label_distribution()
+        exp = [np.nan if v is None else v for v in s["counts"]]
+        np.testing.assert_array_equal(counts.double().numpy(), np.array(exp))
+        exp = [np.nan if v is None else v for v in s["counts_normalized"]]
+        np.testing.assert_array_equal(counts_n.double().numpy(), np.array(exp))
+
+
+def test_fixture_exercises_the_merge_rules():
+    """the fixture covers what the merge decides: pairs and triples, matches dropped by
+    the window, several matches per base row, groups partly null in a column"""
+    lens = {tuple(s["modalities"]) + (s["days_threshold"],): s["len"] for s in FIX["settings"]}
+    assert lens[("pet1451", "t1w", "tabular", 180)] > 0
+    assert lens[("tabular", "pet1451", "t1w", 365)] > lens[("pet1451", "t1w", "tabular", 180)]
+    table = pd.read_csv(CSV)
+    both = table["path_anat"].notna() & table["AGE"].notna()
+    assert both.any()                                   # rows carrying two modalities
+    s = next(x for x in FIX["settings"] if x["modalities"] == ["t1w", "pet1451"])
+    ids = [r[s["table"]["columns"].index("path_anat")] for r in s["table"]["rows"]]
+    assert len(ids) > len(set(ids))                     # a base row with several matches
+
+
+def test_nifti_reader_round_trip(tmp_path):
+    rng = np.random.RandomState(0)
+    for dtype, ext, slope, inter in ((np.float32, ".nii", 1.0, 0.0), (np.int16, ".nii.gz", 0.5, 3.0),
+                                     (np.uint8, ".nii.gz", 0.0, 0.0), (np.float64, ".nii", 1.0, 0.0)):
+        a = (rng.rand(5, 6, 7) * 100).astype(dtype)
+        p = str(tmp_path / f"v_{np.dtype(dtype).name}{ext}")
+        nifti.save(p, a, slope, inter)
+        got = nifti.load(p)
+        assert got.dtype == np.float64 and got.shape == (5, 6, 7)
+        exp = a.astype(np.float64)
+        if slope not in (0.0, 1.0) or inter != 0.0:
+            exp = exp * slope + inter
+        np.testing.assert_array_equal(got, exp)
+        raw = open(p, "rb").read()
+        if ext == ".nii":                       # x fastest on disk (Fortran order)
+            first = np.frombuffer(raw, dtype=dtype, count=2, offset=352)
+            np.testing.assert_array_equal(first, a[:2, 0, 0])
+    with pytest.raises(ValueError):
+        bad = tmp_path / "bad.nii"
+        bad.write_bytes(b"\x00" * 400)
+        nifti.load(str(bad))
+
+
+def test_getitem_reads_volumes_and_tabular(tmp_path):
+    """__getitem__ of a merged PET + MRI + tabular triple: raw float64 volumes from the
+    NIfTI files, the MRI mask for per-scan normalisation, the reference's 9 tabular
+    features (dataloader.py:294-306, 'whole_brain' read from PTEDUCAT as there)."""
+    rng = np.random.RandomState(1)
+    pet, mri, mask = rng.rand(4, 5, 6), rng.rand(4, 5, 6) * 9, (rng.rand(4, 5, 6) > 0.3)
+    paths = {k: str(tmp_path / f"{k}.nii.gz") for k in ("pet", "mri", "mask")}
+    nifti.save(paths["pet"], pet)
+    nifti.save(paths["mri"], mri.astype(np.float32))
+    nifti.save(paths["mask"], mask.astype(np.uint8))
+    feats = {"Ventricles": 1.0, "Hippocampus": 2.0, "WholeBrain": 3.0, "Entorhinal": 4.0,
+             "Fusiform": 5.0, "MidTemp": 6.0, "ICV": 7.0, "AGE": 70.5, "PTEDUCAT": 16.0}
+    rows = [{"ID": "sub-1", "ses": "2018-01-01", "path_pet1451": paths["pet"], "label": "MCI"},
+            {"ID": "sub-1", "ses": "2018-02-01", "path_anat": paths["mri"],
+             "path_anat_mask": paths["mask"], "label": "MCI"},
+            dict({"ID": "sub-1", "ses": "2018-03-01", "label": "MCI"}, **feats)]
+    csv = tmp_path / "t.csv"
+    pd.DataFrame(rows).to_csv(csv)
+    d = MultiModalDataset(str(csv), modalities=["pet1451", "t1w", "tabular"],
+                          normalize_mri={"per_scan_norm": "min_max"})
+    assert len(d) == 1
+    item = d[0]
+    assert set(item) == {"pet1451", "mri", "mri_mask", "tabular", "label"}
+    np.testing.assert_array_equal(item["pet1451"].numpy(), pet)
+    np.testing.assert_array_equal(item["mri"].numpy(), mri.astype(np.float32).astype(np.float64))
+    np.testing.assert_array_equal(item["mri_mask"].numpy(), mask.astype(np.float64))
+    assert item["tabular"].tolist() == [70.5, 16.0, 1.0, 2.0, 16.0, 4.0, 5.0, 6.0, 7.0]
+    assert item["label"].item() == 1
+    assert d.ds["min_time"][0] == pd.Timestamp("2018-01-01")
+    assert d.ds["max_time"][0] == pd.Timestamp("2018-03-01")
+
+
+def test_shard_sampler_covers_the_merged_samples():
+    d = MultiModalDataset(CSV, modalities=["pet1451", "t1w"], days_threshold=180)
+    n = len(d)
+    shards = [list(ShardSampler(d, rank=r, world=4)) for r in range(4)]
+    assert all(len(s) == -(-n // 4) for s in shards)
+    assert set(i for s in shards for i in s) == set(range(n))
+    assert shards[0] == shard_indices(n, 0, 4)
+    smp = ShardSampler(d, rank=1, world=4)
+    smp.set_epoch(1)
+    assert list(smp) == shard_indices(n, 1, 4, epoch=1)
+    loader = torch.utils.data.DataLoader(torch.arange(n), batch_size=4, sampler=smp)
+    assert sorted(torch.cat(list(loader)).tolist()) == sorted(shard_indices(n, 1, 4, epoch=1))

@@ -189,19 +189,23 @@ def test_capture_after_eager_default_stream_steps():
         assert torch.equal(pa, pb), na
 
 
-def test_graph_with_allreduce_after_replay_equals_eager():
-    """bench.py's N > 1 launch mode at one RCCL rank: forward + backward replayed from the
-    graph (gradients straight into the bucket slices), the bucketed all-reduces issued
-    eagerly after the replay, then the captured Adam -- bit-identical to plain eager steps
-    of an identical model (at world 1 the average is the gradient itself)."""
+@pytest.mark.parametrize("mode", ["staged", "after"])
+def test_graph_with_allreduce_replay_equals_eager(mode):
+    """bench.py's N > 1 launch modes at one RCCL rank: "staged" (the default: the backward
+    replayed as four stage graphs, each stage's bucket all-reduced on the side stream while
+    the next replays) and "after" (forward + backward in one graph, the bucketed all-reduces
+    issued after it), then the captured Adam -- bit-identical to plain eager steps of an
+    identical model (at world 1 the average is the gradient itself)."""
     import torch.distributed as dist
     from multimodal_alzheimer_amd.data_parallel import GradAllReduce
+    from multimodal_alzheimer_amd.graph_step import backward_stages
     torch.manual_seed(13)
     a = M.Anat_CNN(_hparams("bf16")).cuda()
     b = copy.deepcopy(a)
     batches = [_batch(40 + i) for i in range(3)]
     warm = 2
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29563", rank=0, world_size=1,
+    port = 29563 + (mode == "after")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", torch.cuda.current_device()))
     try:
         opt_a = a.configure_optimizers()
@@ -220,9 +224,13 @@ def test_graph_with_allreduce_after_replay_equals_eager():
             opt_a.step()
             losses_a.append(out["loss"].detach().clone())
         opt_b = b.configure_optimizers()
-        red = GradAllReduce(b.parameters(), bucket_mb=4.0)
-        gs = GraphedTrainStep(b, opt_b, batches[0], warmup=warm, reducer=red, collectives="after")
+        if mode == "staged":
+            red = GradAllReduce(b.parameters(), bucket_mb=None, stages=backward_stages(b)[1])
+        else:
+            red = GradAllReduce(b.parameters(), bucket_mb=4.0)
+        gs = GraphedTrainStep(b, opt_b, batches[0], warmup=warm, reducer=red, collectives=mode)
         assert gs.opt_graph is not None
+        assert len(gs.graphs) == (4 if mode == "staged" else 1)
         losses_b = [gs(batches[i])["loss"].clone() for i in range(3)]
         torch.cuda.synchronize()
     finally:

@@ -144,6 +144,34 @@ def test_resume_keeps_optimizer_implementation_and_device_lr():
         [h["lr_pretrained"] * 0.25, h["lr"] * 0.25]), rel=1e-6)     # fp32 lr tensors
 
 
+def test_tensor_lr_saved_as_float_and_loads_into_reference_adam(tmp_path):
+    """A checkpoint saved while GraphedTrainStep's device-resident lr tensors are installed
+    writes plain float lrs in the reference layout: torch's own Adam (the reference's) loads
+    it from a file and steps with it; resuming back keeps the tensor object."""
+    h = G.anat_hparams(10)
+    m = M.Anat_CNN(h)
+    opt = m.configure_optimizers()
+    lr_tensors = []
+    for g in opt.param_groups:
+        g["lr"] = torch.tensor(float(g["lr"]) * 0.5)
+        lr_tensors.append(g["lr"])
+    _fake_grads(m.parameters(), 4)
+    opt.step()
+    path = tmp_path / "opt.pt"
+    torch.save(opt.state_dict(), path)
+    sd = torch.load(path, weights_only=True)
+    assert all(type(g["lr"]) is float for g in sd["param_groups"])
+    ref = copy.deepcopy(m)
+    ref_opt = torch.optim.Adam(_ref_groups_anat(ref, h), weight_decay=h["l2_reg"])
+    ref_opt.load_state_dict(sd)
+    lrs = sorted({g["lr"] for g in ref_opt.param_groups})
+    assert lrs == pytest.approx(sorted([h["lr_pretrained"] * 0.5, h["lr"] * 0.5]), rel=1e-6)
+    _fake_grads(ref.parameters(), 5)
+    ref_opt.step()
+    opt.load_state_dict(copy.deepcopy(ref_opt.state_dict()))
+    assert all(g["lr"] is t for g, t in zip(opt.param_groups, lr_tensors))
+
+
 def test_plateau_scheduler_state_round_trips_reference_layout():
     """ReduceLROnPlateau on the merged optimizer saves min_lrs / _last_lr per reference
     group, so the reference's torch scheduler (one entry per per-tensor group) resumes from
