@@ -191,11 +191,18 @@ __global__ __launch_bounds__(NTHR) void patchz_conv_kernel(PZ g, const u16* __re
     for (int j = 0; j < 4; ++j) B[j] = *reinterpret_cast<const bf16x8*>(pb + j * 16 * RB);
   };
   auto mma = [&](const bf16x8 (&A)[2], const bf16x8 (&B)[4]) __attribute__((always_inline)) {
+#ifdef PZ_NO_MMA   // timing skeleton (tools): fragments consumed, no MFMA
+#pragma unroll
+    for (int i = 0; i < 2; ++i) asm volatile("" ::"v"(A[i]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(B[j]));
+#else
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
+#endif
   };
 
   // ---- epilogue of box i (output planes zs + 4i .. + 3).  No vmcnt drain here: the next
@@ -211,6 +218,13 @@ __global__ __launch_bounds__(NTHR) void patchz_conv_kernel(PZ g, const u16* __re
   }                                             // any DMA, not in an epilogue
   const int64_t nbase = (int64_t)n * g.D;
   auto epilogue = [&](int i) __attribute__((always_inline)) {
+#ifdef PZ_NO_EPI   // timing skeleton (tools): accumulators consumed, nothing stored
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[a][j]));
+    return;
+#endif
     const int z0 = zs + 4 * i;
     u16* ctile = reinterpret_cast<u16*>(smem + STG_OFF);
     float cs[4], cq[4];
@@ -330,7 +344,9 @@ __global__ __launch_bounds__(NTHR) void patchz_conv_kernel(PZ g, const u16* __re
         } else {
           wait_vm_lgkm0<Y>();
         }
+#ifndef PZ_NO_BAR   // timing skeleton (tools): no per-tap barrier (races; timing only)
         raw_barrier();
+#endif
         if constexpr (NEXT && planes_at(T) == 2) {
           issue_plane(q0 + 6);
           issue_plane(q0 + 7);

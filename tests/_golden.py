@@ -70,6 +70,17 @@ def load_prng_weights(model, seed):
             sd[k].copy_(torch.from_numpy(v))
 
 
+def load_fixture_weights(model, g):
+    """A fixture's weights: the prng tensors of its seed, then (full-size cases) the
+    discriminating final Linear the generator recorded (make_golden.mixed_head)."""
+    load_prng_weights(model, int(g["seed"]))
+    if "head_prefix" in g:
+        params = dict(model.named_parameters())
+        with torch.no_grad():
+            params[str(g["head_prefix"]) + "weight"].copy_(torch.from_numpy(g["head_weight"]))
+            params[str(g["head_prefix"]) + "bias"].copy_(torch.from_numpy(g["head_bias"]))
+
+
 # name -> (hparams-builder, kind, batch seed, keys); weights seed = fixture 'seed'
 CASES = {
     "anat_r10_32": (lambda: anat_hparams(10), "anat", 12, ("mri",)),

@@ -445,6 +445,63 @@ def _live_seed(build, batch, seed):
 FULL = (8, 128, 128, 128)          # BASELINE configs 2 and 3: batch 8 of 1 x 128^3
 
 
+def mixed_head(model, head, prefix, batch, out):
+    """Make a full-size case discriminating.  With random weights the pooled 512-d features
+    of different volumes are nearly parallel, so every sample gets the same argmax (and the
+    head's closing ReLU, anat_cnn.py:76-77, zeroed all eval rows of the round-3 fixture).
+    The final Linear (``head``, parameters ``prefix`` + weight / bias) is replaced by
+    w0 = beta p, w1 = -beta p, with p the leading principal direction of the train-mode
+    features across the batch taken orthogonal to their mean, beta scaling the logit spread
+    to ~2, and a bias that puts the decision threshold at the median sample (train argmax
+    split across the batch) and keeps every train logit positive (so every eval row has a
+    positive entry).  The replaced tensors are recorded in the fixture (``head_prefix``,
+    ``head_weight``, ``head_bias``); the tests load them after the prng weights.  The
+    model's state (BN running statistics) is restored after the probes, and eval is probed
+    first, on the fresh statistics, as run_full_case evaluates."""
+    feats = {}
+    hook = head.register_forward_hook(
+        lambda mod, inp, o: feats.__setitem__("x", inp[0].detach().double()))
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        model.eval()
+        model.general_step(batch, 0, "val")
+        fe = feats["x"]
+        model.train()
+        model.general_step(batch, 0, "train")
+        ft = feats["x"]
+    hook.remove()
+    model.load_state_dict(sd)
+    model.train()
+    mean = ft.mean(0)
+    eps = ft - mean
+    u = mean / mean.norm()
+    p = torch.linalg.svd(eps, full_matrices=False).Vh[0]
+    p = p - (p @ u) * u
+    p = p / p.norm()
+    proj = ft @ p
+    beta = 1.0 / float((proj - proj.mean()).abs().max())
+    w = torch.stack([beta * p, -beta * p])
+    d = (ft @ (w[0] - w[1])).sort().values
+    n = d.numel()
+    delta = -float(d[n // 2 - 1] + d[n // 2]) / 2            # b0 - b1
+    margin = float((d + delta).abs().min())
+    z = ft @ w.t()
+    need = max(float(-(z[:, 0] + delta / 2).min()), float(-(z[:, 1] - delta / 2).min()))
+    c = need + 0.25
+    bias = torch.tensor([c + delta / 2, c - delta / 2], dtype=torch.float32)
+    with torch.no_grad():
+        head.weight.copy_(w.float())
+        head.bias.copy_(bias)
+    ze = fe @ w.t() + bias.double()
+    out["head_prefix"] = np.array(prefix)
+    out["head_weight"] = head.weight.detach().numpy().copy()
+    out["head_bias"] = bias.numpy()
+    out["head_margin"] = np.array(margin)
+    print(f"  mixed head: bias {bias.tolist()}, train argmax margin {margin:.3e}, "
+          f"train logits {(z + torch.tensor([delta / 2 + c, c - delta / 2])).tolist()}, "
+          f"eval logits {ze.tolist()}")
+
+
 @case
 def anat_r10_128():
     """BASELINE config 2 at its full size: Anat_CNN ResNet-10, 8 x 1 x 128^3, weighted CE
@@ -452,10 +509,11 @@ def anat_r10_128():
     from pkg.models.mri_models.anat_cnn import Anat_CNN
     batch = batch_for(FULL, 2, 1301)
     torch.manual_seed(0)
-    seed = _live_seed(lambda: Anat_CNN(anat_hparams(10)), batch, 1300)
+    seed = 1300
     m = Anat_CNN(anat_hparams(10))
     load_prng_weights(m, seed)
     out = {"seed": np.array(seed), "shape": np.array(FULL)}
+    mixed_head(m, m.model.conv_seg[-2], "model.conv_seg.2.", batch, out)
     run_full_case(m, models_ref.AnatCNNRef(anat_hparams(10)), batch,
                   lambda b: (b["mri"].unsqueeze(1).double(),), out)
     return out
@@ -486,6 +544,28 @@ def pair_r10_128():
     run_full_case(m, ref64, batch_for(FULL, 2, 1401, keys=("pet1451", "mri")),
                   lambda b: (b["pet1451"].unsqueeze(1).double(), b["mri"].unsqueeze(1).double()),
                   out)
+    return out
+
+
+PET160 = (2, 160, 160, 160)        # BASELINE config 5's volume size
+
+
+@case
+def pet_r18_160():
+    """BASELINE config 5's PET branch at its full size: the reference's own PET_CNN_ResNet
+    with depth 18 (pet_resnet_cnn.py:12-138; MedicalNet from the restatement), 2 x 1 x 160^3,
+    focal loss gamma 2.  Its layer3 / layer4 run on 20^3 grids (10- and 5-wide dilated
+    sub-lattices), the route the config-5 bench takes."""
+    from pkg.models.pet_models.pet_resnet_cnn import PET_CNN_ResNet
+    h = anat_hparams(18, fl_gamma=2)
+    batch = batch_for(PET160, 2, 1501, keys=("pet1451",))
+    torch.manual_seed(0)
+    m = PET_CNN_ResNet(h)
+    load_prng_weights(m, 1500)
+    out = {"seed": np.array(1500), "shape": np.array(PET160)}
+    mixed_head(m, m.model.conv_seg[-2], "model.conv_seg.2.", batch, out)
+    run_full_case(m, models_ref.PETResNetRef(h), batch,
+                  lambda b: (b["pet1451"].unsqueeze(1).double(),), out)
     return out
 
 

@@ -129,10 +129,12 @@ def test_graphed_dp_world2_fusion(tmp_path, mode):
     for r in range(2):
         assert all(res[r]["same_loss"]), (r, res[r]["same_loss"])
         assert not res[r]["diff"], (r, res[r]["diff"][:5])
-    for k in res[0]["pre"]:                       # replicas stay identical
+    for k in res[0]["pre"]:
+        if "running" in k or "num_batches" in k:
+            continue                              # BN statistics are per replica
+        # the parameters stay identical across replicas (averaged gradients, same Adam)
         assert torch.equal(res[0]["pre"][k], res[1]["pre"][k]), k
-        assert torch.equal(res[0]["final"][k], res[1]["final"][k]) or "running" in k \
-            or "num_batches" in k, k
+        assert torch.equal(res[0]["final"][k], res[1]["final"][k]), k
 
     import multimodal_alzheimer_amd as M
     per = []

@@ -99,16 +99,21 @@ def test_bootstrap_metric_oracle_vs_sklearn(seed, n, c):
         assert abs(metrics_ref.mcc(cm) - matthews_corrcoef(y[m].numpy(), pred[m].numpy())) < 1e-12
 
 
-@pytest.mark.parametrize("name", ["anat_r10_128", "pair_r10_128"])
+@pytest.mark.parametrize("name", ["anat_r10_128", "pair_r10_128", "pet_r18_160"])
 def test_oracle_matches_reference_full_size(name):
-    """BASELINE configs 2 / 3 at full size (8 x 1 x 128^3): the oracle's fp32 train-mode
-    forward reproduces the reference's logits and loss; the fixture's float64 logits (the
-    exact answer the GPU tests measure against) sit within fp32 rounding of them."""
+    """BASELINE configs 2 / 3 at full size (8 x 1 x 128^3) and config 5's PET branch
+    (PET_CNN_ResNet-18, 2 x 1 x 160^3): the oracle's fp32 train-mode forward reproduces the
+    reference's logits and loss; the fixture's float64 logits (the exact answer the GPU
+    tests measure against) sit within fp32 rounding of them."""
     g = G.load(name)
     if name == "anat_r10_128":
         m = models_ref.AnatCNNRef(G.anat_hparams(10))
         batch = G.batch_for(tuple(g["shape"]), 2, 1301)
         inp = (batch["mri"].unsqueeze(1).float(),)
+    elif name == "pet_r18_160":
+        m = models_ref.PETResNetRef(G.anat_hparams(18, fl_gamma=2))
+        batch = G.batch_for(tuple(g["shape"]), 2, 1501, ("pet1451",))
+        inp = (batch["pet1451"].unsqueeze(1).float(),)
     else:
         h = G.anat_hparams(10, fl_gamma=2)
         st = dict(h, linear_out=[], conv_out=[], filter_size=[])
@@ -117,7 +122,7 @@ def test_oracle_matches_reference_full_size(name):
         batch = G.batch_for(tuple(g["shape"]), 2, 1401, ("pet1451", "mri"))
         inp = (batch["pet1451"].unsqueeze(1).float(), batch["mri"].unsqueeze(1).float())
     assert list(m.state_dict().keys()) == list(g["state_dict_keys"])
-    G.load_prng_weights(m, int(g["seed"]))
+    G.load_fixture_weights(m, g)
     m.train()
     with torch.no_grad():
         y = m(*inp).double()
@@ -126,3 +131,6 @@ def test_oracle_matches_reference_full_size(name):
     np.testing.assert_allclose(loss, g["train_loss"], rtol=1e-6)
     assert np.abs(g["train_logits64"] - g["train_logits"]).max() <= 1e-5
     assert (g["train_logits64"].argmax(1) == g["train_logits"].argmax(1)).all()
+    if "head_prefix" in g:               # the discriminating head: mixed classes, live rows
+        assert len(set(g["train_logits"].argmax(1).tolist())) == 2
+        assert (g["eval_logits"] > 0).any(axis=1).all()

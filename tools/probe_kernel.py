@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--op", default="wgrad", choices=["fwd", "dgrad", "wgrad"])
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--time", action="store_true",
+                    help="print the median launch time (HIP events) instead of only running")
     a = ap.parse_args()
     ci, co, s, k, st, p, dl = LAYERS[a.layer]
     dtype = torch.bfloat16
@@ -50,22 +52,32 @@ def main():
             memory_format=torch.channels_last_3d)
     y = torch.randn((a.batch, co, d.do_, d.ho, d.wo), device="cuda", dtype=dtype).contiguous(
         memory_format=torch.channels_last_3d)
+    wp = volume_ops.pack_weight(d, dt, w, dtype, a.op == "dgrad") if a.op != "wgrad" else None
+    if a.op == "wgrad":
+        wsp = torch.empty((lib.mmad_conv3d_wgrad_workspace(d, dt) + 3) // 4, device="cuda")
+        dw = torch.empty(ws, device="cuda")
+    times = []
     for _ in range(a.reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         if a.op == "fwd":
-            wp = volume_ops.pack_weight(d, dt, w, dtype, False)
             _lib.call("mmad_conv3d_fwd", d, dt, _lib.ptr(x), _lib.ptr(wp), None, _lib.ptr(y),
                       None, _lib.stream())
         elif a.op == "dgrad":
-            wp = volume_ops.pack_weight(d, dt, w, dtype, True)
             _lib.call("mmad_conv3d_dgrad", d, dt, _lib.ptr(y), _lib.ptr(wp), _lib.ptr(x),
                       _lib.stream())
         else:
-            wsp = torch.empty((lib.mmad_conv3d_wgrad_workspace(d, dt) + 3) // 4, device="cuda")
-            dw = torch.empty(ws, device="cuda")
             _lib.call("mmad_conv3d_wgrad", d, dt, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dw), None,
                       _lib.ptr(wsp), _lib.stream())
+        e1.record()
+        times.append((e0, e1))
     torch.cuda.synchronize()
-    print("ok", a.layer, a.op, a.reps)
+    if a.time:
+        ts = sorted(x.elapsed_time(y) * 1e3 for x, y in times[1:])
+        print(f"{a.layer} {a.op} median {ts[len(ts) // 2]:.1f} us (min {ts[0]:.1f}, "
+              f"{len(ts)} reps, lib {os.environ.get('MMAD_LIB_PATH', 'default')})")
+    else:
+        print("ok", a.layer, a.op, a.reps)
 
 
 if __name__ == "__main__":
