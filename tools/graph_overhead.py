@@ -1,0 +1,42 @@
+"""Wall time per tiny dependent kernel inside a replayed HIP graph (what an extra BN finalize /
+head launch costs the captured step): N back-to-back single-block kernels captured in a
+graph, replayed, timed with HIP events; also N launches of a 4096-block elementwise kernel.
+
+    python tools/graph_overhead.py
+"""
+import torch
+
+
+def run(n, numel, reps=20):
+    x = torch.zeros(numel, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            x.add_(1.0)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            x.add_(1.0)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def main():
+    for numel in (256, 1 << 20):
+        t1 = run(1, numel)
+        t100 = run(100, numel)
+        print(f"numel {numel}: graph of 1 kernel {t1:.1f} us, of 100 kernels {t100:.1f} us -> "
+              f"{(t100 - t1) / 99:.2f} us per extra dependent kernel")
+
+
+if __name__ == "__main__":
+    main()
