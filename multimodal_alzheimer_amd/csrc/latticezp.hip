@@ -49,7 +49,12 @@ constexpr int KC = RBL / 2;
 constexpr int ZPL = PP * RBL;             // 16 KiB per plane
 constexpr int NPS = 4;                    // plane ring slots
 constexpr int TPS = 3;                    // taps per stage
-constexpr int NSTL = 3;                   // weight ring slots (two stages in flight)
+// weight ring slots: the pipelined loop keeps NSTL - 1 stages of weights in flight behind
+// the one being read (ZP_NSTL 4 fills the LDS exactly: 4 planes + 4 weight stages)
+#ifndef ZP_NSTL
+#define ZP_NSTL 3
+#endif
+constexpr int NSTL = ZP_NSTL;
 constexpr int NTHR = 512;
 constexpr int NW = NTHR / 64;
 constexpr int ROWS = 2 * PP;              // tile rows: 512
@@ -190,6 +195,28 @@ template <int P, int R>
 __device__ constexpr int planes_at() {
   return P == 0 ? (R == 0 ? 2 : R == 6 ? 1 : 0) : (R == 0 || R == 3 || R == 6 ? 1 : 0);
 }
+__host__ __device__ constexpr int planes_at_rt(int p, int r) {
+  return p == 0 ? (r == 0 ? 2 : r == 6 ? 1 : 0) : (r == 0 || r == 3 || r == 6 ? 1 : 0);
+}
+// VMEM ops of DMA group rg (issued after stage rg's barrier) of a chunk with / without a
+// successor (pipelined loop): the weights of stage rg + NSTL (while one exists) + planes
+__host__ __device__ constexpr int zp_group_ops(int p, int rg, bool more, int wi, int pi) {
+  const int pl = more ? planes_at_rt(p, rg) : ((p == 0 && rg == 0) ? 1 : 0);
+  return ((more || rg + NSTL < 9) ? wi : 0) + pi * pl;
+}
+// at stage R's barrier each wave waits for the weights of stage R + 1; younger than them are
+// the DMA groups of the NSTL - 2 stages before R (in the first chunk, where those do not
+// exist, the prologue's weights of the later stages)
+__host__ __device__ constexpr int zp_younger(int p, int r, bool more, bool first, int wi, int pi) {
+  int n = 0;
+  for (int d = 1; d <= NSTL - 2; ++d) {
+    const int g = r - d;
+    if (g >= 0) n += zp_group_ops(p, g, more, wi, pi);
+    else if (first) n += wi;
+    else n += zp_group_ops(p, g + 9, true, wi, pi);
+  }
+  return n;
+}
 
 template <int TN>
 __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __restrict__ src, const u16* __restrict__ wgt,
@@ -286,7 +313,8 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
   if (pair == 1) issue_plane(0, 2);
   issue_stage_b(0);
   issue_stage_b(1);
-  if constexpr (ZP_PIPE) issue_stage_b(2);
+  if constexpr (ZP_PIPE)
+    for (int t = 2; t < NSTL; ++t) issue_stage_b(t);
 
   // Stage s = 9c + R (R = 3 (kz+1) + ky+1) waits for its weights (issued at stage s - 2);
   // younger are the ops issued at stage s - 1: its planes and the weights of stage s + 1.
@@ -365,7 +393,7 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
   auto run_pipe = [&](auto wmc, auto pc) {
     constexpr int WM = decltype(wmc)::value, P = decltype(pc)::value;
     bf16x8 a[NF], b0[TN], b1[TN];
-    wait_vm_lgkm0<2 * C::WI>();                     // stage 0's weights and chunk 0's planes
+    wait_vm_lgkm0<(NSTL - 1) * C::WI>();            // stage 0's weights and chunk 0's planes
     raw_barrier();
     {
       const char* const pl0[3] = {smem + 0 * ZPL + a_lane, smem + 1 * ZPL + a_lane,
@@ -406,14 +434,17 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
           ((mma_a<TN, WM, P, KZ, KY, 0, F>(acc, a, b1), read_a<WM, P, KZ, KY, 1, F>(pl, a),
             ZP_PIN()), ...);
         }(std::make_integer_sequence<int, NF>{});
-        // barrier of stage s: the weights of stage s + 1 issued in group s - 2; younger are
-        // group s - 1's planes and its weights of stage s + 2
-        if constexpr (MORE) {
-          wait_vm_lgkm0<C::WI + PI * (R >= 1 ? planes_at<P, R - 1>() : 0)>();
-        } else if constexpr (R == 8 || R == 7) {
-          wait_vm_lgkm0<0>();
-        } else {
-          wait_vm_lgkm0<C::WI + PI * ((P == 0 && R == 1) ? 1 : 0)>();
+        // barrier of stage s: the weights of stage s + 1 (issued in group s + 1 - NSTL, or in
+        // the prologue); younger are the groups of the NSTL - 2 stages before s
+        {
+          constexpr int YF = zp_younger(P, R, MORE, true, C::WI, PI);
+          constexpr int YO = zp_younger(P, R, MORE, false, C::WI, PI);
+          if constexpr (YF == YO) {
+            wait_vm_lgkm0<YO>();
+          } else {
+            if (c == 0) wait_vm_lgkm0<YF>();
+            else wait_vm_lgkm0<YO>();
+          }
         }
         raw_barrier();
         auto dma = [&]() {
@@ -427,7 +458,7 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
           } else {
             if constexpr ((R == 0 || R == 3 || R == 6) && MORE) issue_plane(c + 1, R / 3);
           }
-          if constexpr (MORE || R < 6) issue_stage_b(s + 3);
+          if constexpr (MORE || R + NSTL < 9) issue_stage_b(s + NSTL);
         };
         read_b<TN, -1>(bsn, b1);
         [&]<int... F>(std::integer_sequence<int, F...>) {
@@ -622,5 +653,6 @@ extern "C" int mmad_set_kernel_variant(const char* name, int value) {
   if (std::strcmp(name, "lattice8") == 0) return mmad_lattice8::set_mode(value);
   if (std::strcmp(name, "pool_run") == 0) return mmad_pool::set_run_mode(value);
   if (std::strcmp(name, "patchz") == 0) return mmad_patchz::set_mode(value);
+  if (std::strcmp(name, "patchz_bs") == 0) return mmad_patchz::set_bs_mode(value);
   return -1;
 }

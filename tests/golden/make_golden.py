@@ -451,7 +451,8 @@ def mixed_head(model, head, prefix, batch, out):
     head's closing ReLU, anat_cnn.py:76-77, zeroed all eval rows of the round-3 fixture).
     The final Linear (``head``, parameters ``prefix`` + weight / bias) is replaced by
     w0 = beta p, w1 = -beta p, with p the leading principal direction of the train-mode
-    features across the batch taken orthogonal to their mean, beta scaling the logit spread
+    features across the batch taken orthogonal to the mean train and eval features, beta
+    scaling the logit spread
     to ~2, and a bias that puts the decision threshold at the median sample (train argmax
     split across the batch) and keeps every train logit positive (so every eval row has a
     positive entry).  The replaced tensors are recorded in the fixture (``head_prefix``,
@@ -474,9 +475,12 @@ def mixed_head(model, head, prefix, batch, out):
     model.train()
     mean = ft.mean(0)
     eps = ft - mean
-    u = mean / mean.norm()
     p = torch.linalg.svd(eps, full_matrices=False).Vh[0]
-    p = p - (p @ u) * u
+    # orthogonal to the mean train AND eval features, so neither mode's common part
+    # reaches the logits (eval runs on the fresh running statistics: large features)
+    for v in (mean, fe.mean(0)):
+        u = v / v.norm()
+        p = p - (p @ u) * u
     p = p / p.norm()
     proj = ft @ p
     beta = 1.0 / float((proj - proj.mean()).abs().max())

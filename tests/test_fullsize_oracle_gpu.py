@@ -196,18 +196,44 @@ def _ref_conv(x, w, s, p, d):
     return rc(x, w, s, p, d)
 
 
+def _ref_dw(x, gy, k, s, p, d, planes=2):
+    """dW = sum over output voxels of gY x im2col(X), as fp32 GEMMs over chunks of output
+    z-planes (K <= a few 10^4 voxels each) summed in float64: a weight-gradient reference
+    whose own summation error is far below the kernel's (one fp32 GEMM over all 2^21
+    voxels of the stem is not)."""
+    import torch.nn.functional as F
+    n, c = x.shape[:2]
+    co = gy.shape[1]
+    span = (k - 1) * d + 1
+    u = F.pad(x.float(), (p,) * 6)
+    out = torch.zeros((co, c * k ** 3), dtype=torch.float64, device=x.device)
+    do = gy.shape[2]
+    for z0 in range(0, do, planes):
+        z1 = min(do, z0 + planes)
+        ub = u[:, :, z0 * s:(z1 - 1) * s + span]
+        for dim in (2, 3, 4):
+            ub = ub.unfold(dim, span, s)
+        ub = ub[..., ::d, ::d, ::d]
+        cols = ub.permute(0, 2, 3, 4, 1, 5, 6, 7).reshape(-1, c * k ** 3)
+        g = gy[:, :, z0:z1].float().permute(0, 2, 3, 4, 1).reshape(-1, co)
+        out += (g.t() @ cols).double()
+    return out.view(co, c, k, k, k)
+
+
 @pytest.mark.parametrize("name", ["anat_r10_128", "pet_r18_160"], ids=["config2", "config5_pet"])
 def test_full_size_bf16_every_conv_in_situ(name):
     """The per-kernel bar at the benched size on the step's REAL operands: the bf16 step of
     the fixture's model runs with every conv's input, output, output gradient and input
     gradient recorded, and each conv (stem, patchz / patch, s2conv / s2dgrad, pointwise,
     lattice8, lattice_zp, pwgrad, lattice wgrad: whatever the dispatch picked) is checked
-    against a plain fp32 PyTorch conv (im2col + matmul) of the SAME bf16 operands -- its
-    own error only, not the chain's compounded bf16 drift the model-level test bounds:
+    against a plain PyTorch conv (fp32 im2col + matmul; the weight gradient as fp32 GEMMs over
+    two output planes at a time summed in float64) of the SAME bf16 operands -- its own
+    error only, not the chain's compounded bf16 drift the model-level test bounds:
       y, dX (bf16): |err| <= 2^-7 |ref| + 1e-3 max|ref|   (one bf16 rounding + fp32 sums)
-      dW (fp32):    |err| <= 1e-3 |ref| + 2e-5 (|X|.|gY|) + 1e-6 max|ref|
-    (|X|.|gY| = the same contraction over absolute values: the fp32 summation error scale of
-    a weight gradient that cancels over 2^18-2^21 voxels)."""
+      dW (fp32):    |err| <= 1e-3 |ref| + 1e-4 (|X|.|gY|) + 1e-6 max|ref|
+    (|X|.|gY| = the same contraction over absolute values: the scale of a weight gradient's
+    fp32 summation error, since dW cancels heavily -- BN's backward makes gY zero-mean per
+    channel -- over 2^15 .. 2^21 voxels)."""
     from multimodal_alzheimer_amd import layers as Lyr
     g, m, batch = _build(name, "bf16")
     recs = {}
@@ -229,42 +255,45 @@ def test_full_size_bf16_every_conv_in_situ(name):
     res["loss"].backward()
     torch.cuda.synchronize()
     convs = dict(m.named_modules())
-    checked = []
+    checked, bad = [], []
+    D = torch.float64
     for cname, rec in recs.items():
         conv = convs[cname]
         st, p, d = conv._stride3()[0], conv._pads()[0], conv._dilation3()[0]
+        k = conv.kernel_size[0]
         x = rec["x"]
-        xr = (x.float().to(torch.bfloat16).float() if x.dtype != torch.bfloat16 else x.float())
+        xr = (x.float().to(torch.bfloat16) if x.dtype != torch.bfloat16 else x).float()
         xr = xr.detach().requires_grad_(x.requires_grad)
         wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
         yr = _ref_conv(xr, wr, st, p, d)
         assert "gy" in rec, cname
         gy = rec["gy"].float()
         yr.backward(gy)
-        # |X| . |gY| per weight: the dW contraction over absolute values
-        xa = xr.detach().abs()
-        wa = torch.zeros_like(wr).requires_grad_(True)
-        ya = _ref_conv(xa, wa, st, p, d)
-        ya.backward(gy.abs())
-        absdw = wa.grad
-        for got, ref, rel, absf, what in ((rec["y"], yr, 2 ** -7, 1e-3, "y"),
-                                          (rec.get("dx"), xr.grad, 2 ** -7, 1e-3, "dX")):
+        dwr = _ref_dw(xr.detach(), gy, k, st, p, d)
+        absdw = _ref_dw(xr.detach().abs(), gy.abs(), k, st, p, d)
+        line = [cname]
+        for got, ref, what in ((rec["y"], yr, "y"), (rec.get("dx"), xr.grad, "dX")):
             if got is None or ref is None:
                 continue
-            got, ref = got.float(), ref.detach().float()
+            got, ref = got.to(D), ref.detach()
             err = (got - ref).abs()
-            bound = rel * ref.abs() + absf * ref.abs().max()
-            bad = int((err > bound).sum())
-            assert bad == 0, f"{cname} {what}: {bad} elements beyond the bound, " \
-                             f"max|err| {err.max().item():.3e} / max|ref| {ref.abs().max().item():.3e}"
-        dw, dwr = conv.weight.grad.float(), wr.grad.float()
+            nbad = int((err > 2 ** -7 * ref.abs() + 1e-3 * ref.abs().max()).sum())
+            line.append(f"{what} err/max {err.max().item() / ref.abs().max().item():.2e}"
+                        f"{' BAD ' + str(nbad) if nbad else ''}")
+            if nbad:
+                bad.append((cname, what))
+        dw = conv.weight.grad.to(D)
         err = (dw - dwr).abs()
-        bound = 1e-3 * dwr.abs() + 2e-5 * absdw + 1e-6 * dwr.abs().max()
-        bad = int((err > bound).sum())
-        assert bad == 0, f"{cname} dW: {bad} elements beyond the bound, max|err| " \
-                         f"{err.max().item():.3e} / max|ref| {dwr.abs().max().item():.3e}"
+        nbad = int((err > 1e-3 * dwr.abs() + 1e-4 * absdw + 1e-6 * dwr.abs().max()).sum())
+        line.append(f"dW err/max {err.max().item() / dwr.abs().max().item():.2e} "
+                    f"err/abs {(err / absdw.clamp_min(1e-30)).max().item():.2e}"
+                    f"{' BAD ' + str(nbad) if nbad else ''}")
+        if nbad:
+            bad.append((cname, "dW"))
+        print("  ".join(line))
         checked.append(cname)
-        del yr, ya, xr, wr, wa
+        del yr, xr, wr, dwr, absdw
         torch.cuda.empty_cache()
-    print(f"{name}: {len(checked)} convs checked in situ: {checked}")
+    print(f"{name}: {len(checked)} convs checked in situ")
     assert len(checked) >= (12 if name == "anat_r10_128" else 20)
+    assert not bad, bad
