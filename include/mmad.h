@@ -60,7 +60,7 @@ const char* mmad_strerror(int status);
  * BN+ReLU+max-pool forward: 2 the z-walking kernel (default), 1 the column-carrying kernel,
  * 0 the per-output rows kernel; "patchz" = 1 the
  * persistent z-walking layer1 conv where its work items fill the CUs (default), 2 at any
- * size, 0 the per-box patch conv; "patchz_bs" = 1 its weight-stationary form (default), 0
+ * size, 0 the per-box patch conv; "patchz_bs" = 1 its weight-stationary form, 0 (default)
  * the weight-streaming form.  value < 0 only queries.
  * Returns the previous value, -1 for an unknown name.  Not thread-safe against concurrent
  * launches. */

@@ -646,7 +646,7 @@ int patchz_mode() {
   return v;
 }
 
-// MMAD_PATCHZ_BS: 1 (default) the weight-stationary kernel, 0 the weight-streaming one;
+// MMAD_PATCHZ_BS: 1 the weight-stationary kernel, 0 (default) the weight-streaming one;
 // mmad_set_kernel_variant("patchz_bs", v) at run time
 std::atomic<int> g_bs_mode{-1};
 int bs_mode() {
@@ -654,7 +654,7 @@ int bs_mode() {
   if (v < 0) {
     const char* e = getenv("MMAD_PATCHZ_BS");
     int expect = -1;
-    g_bs_mode.compare_exchange_strong(expect, e ? atoi(e) : 1);
+    g_bs_mode.compare_exchange_strong(expect, e ? atoi(e) : 0);
     v = g_bs_mode.load(std::memory_order_relaxed);
   }
   return v;
