@@ -71,9 +71,15 @@ def load_prng_weights(model, seed):
 
 
 def load_fixture_weights(model, g):
-    """A fixture's weights: the prng tensors of its seed, then (full-size cases) the
-    discriminating final Linear the generator recorded (make_golden.mixed_head)."""
+    """A fixture's weights: the prng tensors of its seed, then (full-size cases) the BN
+    running statistics and the discriminating final Linear the generator recorded
+    (make_golden.calibrate_bn / mixed_head)."""
     load_prng_weights(model, int(g["seed"]))
+    bufs = dict(model.named_buffers())
+    with torch.no_grad():
+        for k in g:
+            if k.startswith("init_buf/"):
+                bufs[k[len("init_buf/"):]].copy_(torch.from_numpy(g[k]))
     if "head_prefix" in g:
         params = dict(model.named_parameters())
         with torch.no_grad():

@@ -445,6 +445,27 @@ def _live_seed(build, batch, seed):
 FULL = (8, 128, 128, 128)          # BASELINE configs 2 and 3: batch 8 of 1 x 128^3
 
 
+def calibrate_bn(model, batch, out):
+    """BN running statistics = this batch's statistics (one train-mode forward with a
+    cumulative average), so eval mode normalises like train mode instead of running a
+    fresh network un-normalised (whose pooled features are huge and nearly parallel);
+    num_batches_tracked back to 0.  Recorded as ``init_buf/<name>``; the tests load them."""
+    bns = [m for m in model.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)]
+    with torch.no_grad():
+        saved = [b.momentum for b in bns]
+        for b in bns:
+            b.momentum = None
+            b.reset_running_stats()
+        model.train()
+        model.general_step(batch, 0, "train")
+        for b, mo in zip(bns, saved):
+            b.momentum = mo
+            b.num_batches_tracked.zero_()
+    for name, b in model.named_buffers():
+        if "running" in name:
+            out[f"init_buf/{name}"] = b.detach().numpy().copy()
+
+
 def mixed_head(model, head, prefix, batch, out):
     """Make a full-size case discriminating.  With random weights the pooled 512-d features
     of different volumes are nearly parallel, so every sample gets the same argmax (and the
@@ -517,6 +538,7 @@ def anat_r10_128():
     m = Anat_CNN(anat_hparams(10))
     load_prng_weights(m, seed)
     out = {"seed": np.array(seed), "shape": np.array(FULL)}
+    calibrate_bn(m, batch, out)
     mixed_head(m, m.model.conv_seg[-2], "model.conv_seg.2.", batch, out)
     run_full_case(m, models_ref.AnatCNNRef(anat_hparams(10)), batch,
                   lambda b: (b["mri"].unsqueeze(1).double(),), out)
@@ -567,6 +589,7 @@ def pet_r18_160():
     m = PET_CNN_ResNet(h)
     load_prng_weights(m, 1500)
     out = {"seed": np.array(1500), "shape": np.array(PET160)}
+    calibrate_bn(m, batch, out)
     mixed_head(m, m.model.conv_seg[-2], "model.conv_seg.2.", batch, out)
     run_full_case(m, models_ref.PETResNetRef(h), batch,
                   lambda b: (b["pet1451"].unsqueeze(1).double(),), out)
