@@ -11,11 +11,19 @@ all-reduce (N>1) + Adam; all parameters trainable (lr_pretrained set).
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
 The step is captured once as HIP graphs and replayed (``--eager`` launches it from Python
-every step).  Under torchrun the backward is captured as four graphs split at the backbone
-stages (head + layer4 | layer3 | layer2 | layer1 + stem, graph_step "staged"): after each
-replay that stage's gradient bucket is all-reduced over RCCL on a side stream while the
-next stage's graph runs, then the captured Adam (``--after``: one forward + backward graph,
-every all-reduce after it; ``--graph``: the all-reduces captured inside the step graph).
+every step).  Under torchrun (``--collectives``):
+  * ``staged``: the backward captured as four graphs split at the backbone stages (head +
+    layer4 | layer3 | layer2 | layer1 + stem, graph_step "staged"); after each replay that
+    stage's gradient bucket is all-reduced over RCCL on a side stream while the next
+    stage's graph runs, then the captured Adam;
+  * ``staged1``: the same with one cut (head + layer4 + layer3 | the rest): one boundary,
+    ~4 MB left exposed;
+  * ``after``: one forward + backward graph, every all-reduce after it;
+  * ``auto`` (default): each of the three is captured in turn and timed over a few replays
+    during warm-up (max over ranks), and the fastest is kept -- overlap pays only while the
+    RCCL kernels' CUs cost the backward less than the all-reduce it hides, which depends on
+    the node (tools/spin_contention.py: 16 CUs held through a step cost ~0.5 ms);
+  * ``inside`` (``--graph``): the all-reduces captured inside the step graph.
 Rank 0 prints one JSON line.
 ``roofline`` times the dominant kernel (layer4.0.conv2 forward, the lattice conv) with HIP
 events recorded around each of its launches, on the stream it runs on -- inside the timed
@@ -36,8 +44,8 @@ sys.path.insert(0, REPO)
 
 import multimodal_alzheimer_amd as M  # noqa: E402
 from multimodal_alzheimer_amd import _lib, volume_ops  # noqa: E402
-from multimodal_alzheimer_amd.graph_step import (GraphedTrainStep,  # noqa: E402
-                                                  backward_stages)
+from multimodal_alzheimer_amd.graph_step import (DEFAULT_CUTS,  # noqa: E402
+                                                  GraphedTrainStep, backward_stages)
 from multimodal_alzheimer_amd.data_parallel import (GradAllReduce,  # noqa: E402
                                                     broadcast_module_state)
 
@@ -47,6 +55,9 @@ M2_BYTES_PER_VOL = 1.163e9               # unfused eager byte model (SURVEY.md 8
 PEAK_BF16 = 2.5e15                       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32 = 157.3e12
 PEAK_HBM = 8.0e12
+# --collectives modes with a graph_step form: (graph_step collectives, backward cuts)
+DP_MODES = {"staged": ("staged", DEFAULT_CUTS), "staged1": ("staged", ("layer3",)),
+            "after": ("after", DEFAULT_CUTS)}
 
 
 def hparams(precision):
@@ -171,14 +182,11 @@ def main():
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--graph", action="store_true",
-                    help="under torchrun: capture the RCCL bucket all-reduces inside the step's "
-                         "graph too (opt-in, one-rank checked)")
-    ap.add_argument("--after", action="store_true",
-                    help="under torchrun: one forward + backward graph, every bucket "
-                         "all-reduced after it (not overlapped); the default replays the "
-                         "backward in four stage graphs and overlaps each stage's all-reduce "
-                         "with the next")
+    ap.add_argument("--collectives", default="auto", choices=list(DP_MODES) + ["auto", "inside"],
+                    help="under torchrun: how the gradient all-reduce meets the replayed step "
+                         "(module docstring); auto probes staged / staged1 / after")
+    ap.add_argument("--graph", action="store_true", help="= --collectives inside")
+    ap.add_argument("--after", action="store_true", help="= --collectives after")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel of every step from Python, the all-reduces from "
                          "the backward's hooks (overlapped with it)")
@@ -222,21 +230,26 @@ def main():
                                              resnet_depth_mri=34, resnet_depth_pet=18)).cuda()
     opt = model.configure_optimizers()
     use_graph = not args.eager and (args.graph or args.workload in ("mri", "fusion"))
-    collectives = "inside" if args.graph else "after" if args.after else "staged"
-    # staged (default): one bucket per backward stage -- head + layer4 (~43 MB for
-    # ResNet-10, overlapped by the three later stages), layer3, layer2, layer1 + stem (~1 MB,
-    # the only one not hidden).  Otherwise 4 MiB buckets in reverse order: eager, layer4's
-    # big weights go in early (launched from the hooks while backward continues) and the
-    # bucket launched last stays ~1 MB instead of ~15 MB.
+    mode = "inside" if args.graph else "after" if args.after else args.collectives
+    if not use_graph:
+        mode = "eager"
+
+    def make_reducer(m):
+        # staged: one bucket per backward stage -- for ResNet-10 head + layer4 (~43 MB,
+        # overlapped by the later stages) ... layer1 + stem (~1 MB, the only one not hidden).
+        # Otherwise 4 MiB buckets in reverse order: eager, layer4's big weights go in early
+        # (launched from the hooks while backward continues) and the bucket launched last
+        # stays ~1 MB instead of ~15 MB.
+        if m in DP_MODES and DP_MODES[m][0] == "staged":
+            return GradAllReduce(model.parameters(), bucket_mb=None,
+                                 stages=backward_stages(model, DP_MODES[m][1])[1])
+        return GradAllReduce(model.parameters(),
+                             bucket_mb=float(os.environ.get("MMAD_DP_BUCKET_MB", "4")))
+
     reducer = None
     if dp:
         broadcast_module_state(model)          # identical replicas, as DDP
-        if use_graph and collectives == "staged":
-            reducer = GradAllReduce(model.parameters(), bucket_mb=None,
-                                    stages=backward_stages(model)[1])
-        else:
-            reducer = GradAllReduce(model.parameters(),
-                                    bucket_mb=float(os.environ.get("MMAD_DP_BUCKET_MB", "4")))
+        reducer = make_reducer("staged" if mode == "auto" else mode)
     B, S = args.batch, args.size
     VOL = (91, 109, 91) if mni else (S, S, S)
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)   # this rank's shard
@@ -288,8 +301,34 @@ def main():
                 step()
             torch.cuda.synchronize()
             volume_ops.FWD_PROBES.clear()
+        probe = {}
+        if dp and mode == "auto":
+            # capture each candidate in turn, time a few replays (max over ranks), drop it;
+            # every rank sees the same times, so every rank picks the same mode
+            reducer.remove()
+            for cand in DP_MODES:
+                red = make_reducer(cand)
+                gs = GraphedTrainStep(model, opt, batch, warmup=1, reducer=red,
+                                      collectives=DP_MODES[cand][0], cuts=DP_MODES[cand][1])
+                gs()
+                torch.cuda.synchronize()
+                dist.barrier()
+                t = time.perf_counter()
+                for _ in range(10):
+                    gs()
+                torch.cuda.synchronize()
+                dist.barrier()
+                el = torch.tensor([time.perf_counter() - t], device="cuda", dtype=torch.float64)
+                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                probe[cand] = el.item() / 10 * 1e3
+                red.remove()
+                del gs, red
+                torch.cuda.synchronize()
+            mode = min(probe, key=probe.get)
+            reducer = make_reducer(mode)
+        gmode, cuts = DP_MODES.get(mode, (mode, DEFAULT_CUTS)) if dp else ("inside", DEFAULT_CUTS)
         gstep = GraphedTrainStep(model, opt, batch, warmup=max(1, args.warmup),
-                                 reducer=reducer, collectives=collectives)
+                                 reducer=reducer, collectives=gmode, cuts=cuts)
         gstep()
 
         def step(timed=False):
@@ -356,10 +395,10 @@ def main():
     result["config"]["step_launch"] = (
         "eager" if not use_graph else "hip graph replay" if reducer is None else
         "hip graph replay (fwd+bwd) + eager RCCL all-reduce + graph-replayed Adam"
-        if collectives == "after" else
-        "hip graph replay: fwd + 4 backward-stage graphs, each stage's RCCL all-reduce "
-        "overlapping the next, graph-replayed Adam" if collectives == "staged" else
-        "hip graph replay incl. RCCL all-reduce")
+        if mode == "after" else
+        f"hip graph replay: fwd + {len(DP_MODES[mode][1]) + 1} backward-stage graphs, each "
+        f"stage's RCCL all-reduce overlapping the next, graph-replayed Adam"
+        if mode in DP_MODES else "hip graph replay incl. RCCL all-reduce")
     # host time spent enqueueing each step: close to ms_per_step means the run was bound by
     # the host (Python / launch overhead), not by the GPU
     result["host_issue_ms_per_step"] = t_issue / args.steps * 1e3
@@ -368,7 +407,9 @@ def main():
         # all-reduce that backward did not hide (plus the copies of non-slot gradients)
         result["dp"] = {"buckets_mb": [round(f.numel() * 4 / 2 ** 20, 2) for f in reducer.flats],
                         "exposed_allreduce_ms": sum(a.elapsed_time(b) for a, b in dp_events)
-                        / len(dp_events), "backend": "rccl"}
+                        / len(dp_events), "backend": "rccl", "collectives": mode}
+        if use_graph and probe:
+            result["dp"]["auto_probe_ms_per_step"] = {k: round(v, 4) for k, v in probe.items()}
     if rank == 0 and not args.no_roofline:
         result["roofline"] = dominant_kernel_roofline(
             events, B, S, cdtype,

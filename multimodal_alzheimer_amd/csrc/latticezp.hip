@@ -50,9 +50,11 @@ constexpr int ZPL = PP * RBL;             // 16 KiB per plane
 constexpr int NPS = 4;                    // plane ring slots
 constexpr int TPS = 3;                    // taps per stage
 // weight ring slots: the pipelined loop keeps NSTL - 1 stages of weights in flight behind
-// the one being read (ZP_NSTL 4 fills the LDS exactly: 4 planes + 4 weight stages)
+// the one being read.  4 (the default since round 4: +0.8 % on the config-2 step against 3,
+// four interleaved bench runs, gpurun_out/r04e) fills the LDS exactly at TN 4: 4 planes + 4
+// weight stages = 160 KiB
 #ifndef ZP_NSTL
-#define ZP_NSTL 3
+#define ZP_NSTL 4
 #endif
 constexpr int NSTL = ZP_NSTL;
 constexpr int NTHR = 512;

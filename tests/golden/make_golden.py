@@ -471,15 +471,18 @@ def mixed_head(model, head, prefix, batch, out):
     of different volumes are nearly parallel, so every sample gets the same argmax (and the
     head's closing ReLU, anat_cnn.py:76-77, zeroed all eval rows of the round-3 fixture).
     The final Linear (``head``, parameters ``prefix`` + weight / bias) is replaced by
-    w0 = beta p, w1 = -beta p, with p the leading principal direction of the train-mode
-    features across the batch taken orthogonal to the mean train and eval features, beta
-    scaling the logit spread
-    to ~2, and a bias that puts the decision threshold at the median sample (train argmax
-    split across the batch) and keeps every train logit positive (so every eval row has a
-    positive entry).  The replaced tensors are recorded in the fixture (``head_prefix``,
-    ``head_weight``, ``head_bias``); the tests load them after the prng weights.  The
-    model's state (BN running statistics) is restored after the probes, and eval is probed
-    first, on the fresh statistics, as run_full_case evaluates."""
+    w0 = p / 2, w1 = -p / 2 and a bias, with p the least-norm direction that puts each
+    sample's train logit difference z0 - z1 at a chosen target t_b while staying orthogonal
+    to the mean train and eval features (so neither mode's common part reaches the logits).
+    Targets: the argmax is split across the batch, and the per-sample loss gradients
+    (p0 - y0, sign fixed by the label) do not cancel: samples of one class sit confidently
+    on their side (|t| ~ 3, small gradient), those of the other weakly (|t| ~ 0.4, large
+    gradient) -- a symmetric split makes every weight gradient a difference of two nearly
+    equal per-sample terms, which is what a bf16 check cannot resolve.  The bias keeps every
+    train logit positive (every eval row has a positive entry).  The replaced tensors are
+    recorded in the fixture (``head_prefix``, ``head_weight``, ``head_bias``); the tests load
+    them after the prng weights.  The model's state (BN running statistics) is restored after
+    the probes, and eval is probed first, as run_full_case evaluates."""
     feats = {}
     hook = head.register_forward_hook(
         lambda mod, inp, o: feats.__setitem__("x", inp[0].detach().double()))
@@ -494,22 +497,24 @@ def mixed_head(model, head, prefix, batch, out):
     hook.remove()
     model.load_state_dict(sd)
     model.train()
+    labels = batch["label"].numpy()
+    n = ft.shape[0]
+    jit = np.linspace(-0.1, 0.1, n)
+    t = np.empty(n)
+    if labels.min() != labels.max():
+        # label 0 confidently right (z0 - z1 = +3), label 1 weakly right (-0.4)
+        t[:] = np.where(labels == 0, 3.0, -0.4) + jit
+    else:
+        # one class only: half confidently right, half weakly wrong (same gradient sign)
+        s = 1.0 if labels[0] == 0 else -1.0
+        t[:] = s * np.where(np.arange(n) % 2 == 0, 3.0, -0.4) + jit
+    tb = torch.from_numpy(t)
     mean = ft.mean(0)
-    eps = ft - mean
-    p = torch.linalg.svd(eps, full_matrices=False).Vh[0]
-    # orthogonal to the mean train AND eval features, so neither mode's common part
-    # reaches the logits (eval runs on the fresh running statistics: large features)
-    for v in (mean, fe.mean(0)):
-        u = v / v.norm()
-        p = p - (p @ u) * u
-    p = p / p.norm()
-    proj = ft @ p
-    beta = 1.0 / float((proj - proj.mean()).abs().max())
-    w = torch.stack([beta * p, -beta * p])
-    d = (ft @ (w[0] - w[1])).sort().values
-    n = d.numel()
-    delta = -float(d[n // 2 - 1] + d[n // 2]) / 2            # b0 - b1
-    margin = float((d + delta).abs().min())
+    A = torch.cat([ft - mean, mean[None], fe.mean(0)[None]])
+    rhs = torch.cat([tb - tb.mean(), torch.zeros(2, dtype=torch.float64)])
+    p = torch.linalg.pinv(A) @ rhs
+    w = torch.stack([p / 2, -p / 2])
+    delta = float(tb.mean())                                     # b0 - b1
     z = ft @ w.t()
     need = max(float(-(z[:, 0] + delta / 2).min()), float(-(z[:, 1] - delta / 2).min()))
     c = need + 0.25
@@ -517,13 +522,15 @@ def mixed_head(model, head, prefix, batch, out):
     with torch.no_grad():
         head.weight.copy_(w.float())
         head.bias.copy_(bias)
+    zt = z + bias.double()
+    margin = float((zt[:, 0] - zt[:, 1]).abs().min())
     ze = fe @ w.t() + bias.double()
     out["head_prefix"] = np.array(prefix)
     out["head_weight"] = head.weight.detach().numpy().copy()
     out["head_bias"] = bias.numpy()
     out["head_margin"] = np.array(margin)
-    print(f"  mixed head: bias {bias.tolist()}, train argmax margin {margin:.3e}, "
-          f"train logits {(z + torch.tensor([delta / 2 + c, c - delta / 2])).tolist()}, "
+    print(f"  mixed head: labels {labels.tolist()}, |p| {float(p.norm()):.3e}, bias "
+          f"{bias.tolist()}, train argmax margin {margin:.3e}, train logits {zt.tolist()}, "
           f"eval logits {ze.tolist()}")
 
 
