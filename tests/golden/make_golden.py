@@ -143,7 +143,9 @@ def run_full_case(model, ref64, batch, inputs, out):
     general_step + backward of the reference code in fp32 (gradients at sampled elements,
     running statistics in full), then the same train step in float64 on the oracle
     restatement loaded with the same weights -- the exact answer the GPU tests measure both
-    the reference's fp32 error and their own against."""
+    the reference's fp32 error and their own against.  Between the two, the reference's
+    train step again under CPU autocast bf16 (``grad16/``, ``train_logits16``): the
+    reference's own bf16 error, which bounds the GPU bf16 test."""
     sd0 = {k: v.clone() for k, v in model.state_dict().items()}
     model.eval()
     with torch.no_grad():
@@ -159,6 +161,19 @@ def run_full_case(model, ref64, batch, inputs, out):
             summarize("buf/", name, b, out)
     out["state_dict_keys"] = np.array(list(model.state_dict().keys()))
     del res
+    model.zero_grad(set_to_none=True)
+    # the reference's own bf16 path (Lightning precision "bf16" = autocast around the step,
+    # backward outside it), on CPU: its error against float64 is the yardstick of the GPU
+    # bf16 test (a bf16 step cannot be closer to float64 than rounding allows)
+    model.load_state_dict(sd0)
+    model.train()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        r16 = model.general_step(batch, 0, "train")
+    r16["loss"].backward()
+    out["train_logits16"] = r16["outputs"].detach().float().numpy()
+    out["train_loss16"] = np.array(r16["loss"].item())
+    record_samples("grad16/", model, out)
+    del r16
     model.zero_grad(set_to_none=True)
     ref64.load_state_dict(sd0)
     ref64 = ref64.double().train()

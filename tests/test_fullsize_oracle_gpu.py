@@ -21,15 +21,19 @@ Bars:
     channel may exceed it, up to 25 %: a ReLU mask flip, see _assert_f64_bar), and the
     full-tensor |g| sums and norms within 2e-3 of the reference's.
   * bf16 HIP path (the kernels the bench launches: stem, patch, lattice, lattice8, pwgrad,
-    fused pool): logits within 3e-2 of max(1, |logit|) of float64 (bf16 operands, 2^-8 unit
-    roundoff compounded through 10 convolutions; measured ~5e-3), argmax exact wherever the
-    float64 top-2 margin exceeds twice that bound, loss within 3e-2 relative; running
-    statistics within 2e-2 of each tensor's max; gradients against float64, per tensor: the
-    normwise relative error of the sampled elements within NRM16[group], and every LARGE
-    sampled element (|g| >= half the tensor's max) within LRG16[group] of its own value.
-    bf16 rounding noise compounds along the backward chain (each dgrad re-rounds to bf16)
-    and the stem's gradient also crosses the 3^3 max-pool, where rounding the stem output
-    moves some pooled maxima to neighbouring voxels -- so the bounds grow towards the input.
+    fused pool) against float64, with the REFERENCE's own bf16 path as the yardstick: the
+    fixture also holds the reference's train step under CPU autocast bf16 (Lightning's
+    precision "bf16"), whose error against float64 is what bf16 storage costs.  Logits within
+    3e-2 of max(1, |logit|) and within 2x the reference's bf16 logit error (+5e-3), argmax
+    exact wherever the float64 top-2 margin exceeds twice the bound, loss within 3e-2
+    relative; running statistics within 2e-2 of each tensor's max; per gradient tensor, the
+    normwise relative error of the sampled elements, the relative error of every LARGE
+    sampled element (|g| >= half the tensor's max) and the |g|-sum error each within 2x the
+    reference's bf16 error of the same quantity + 0.02 (+0.05 for the large elements).
+    bf16 rounding noise compounds along the backward chain (each dgrad re-rounds to bf16) and
+    through BN's cancelling sums and the stem's max-pool argmax moves, so both paths' errors
+    grow towards the input (ResNet-18 at 160^3: ~0.4 normwise at layer1 for both); the
+    strict per-kernel bar is test_full_size_bf16_every_conv_in_situ below.
 """
 import numpy as np
 import pytest
@@ -43,28 +47,16 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 LOGIT_ATOL = 1e-4
 
-# bf16 gradient bounds per layer group (see the module docstring): normwise relative error
-# of the sampled elements, and relative error of each large sampled element
-# Calibrated on the MI355X (gpurun_out/r03e, both configs; maxima over each group):
-# normwise 0.144 / 0.194 / 0.286 / 0.337 / 0.300 / 0.304 / 7e-4 (layer4 .. bn1, head),
-# large-element 0.198 / 0.253 / 0.458 / 0.428 / 0.471 / 0.356 / 2e-3, |g| sum 0.116; the
-# bounds are those x ~1.5.  The error grows smoothly towards the input (no layer stands out),
-# the |g| sums agree to ~1 %, and the fp32 path passes the 4x-reference-error bar above: it
-# is bf16 rounding compounded through cancelling sums (dY . X over 32k voxels after BN's
-# mean subtraction) and max-pool argmax moves, not a kernel error.
-NRM16 = (("layer4", 0.22), ("layer3", 0.3), ("layer2", 0.43), ("layer1", 0.5),
-         ("conv1", 0.45), ("bn1", 0.45), ("", 0.05))
-LRG16 = (("layer4", 0.3), ("layer3", 0.38), ("layer2", 0.7), ("layer1", 0.65),
-         ("conv1", 0.7), ("bn1", 0.55), ("", 0.06))
-SUM16 = 0.18
+# bf16 bars relative to the reference's own bf16 error (module docstring)
+REF16_X, REF16_ABS, REF16_LRG_ABS = 2.0, 0.02, 0.05
 
 
-def _group_tol(table, pname):
-    tail = pname.split("model.")[-1]
-    for pre, tol in table:
-        if tail.startswith(pre):
-            return tol
-    return table[-1][1]
+def _errs(got, ex, full_abs_sum, exact_abs_sum):
+    """normwise, large-element and |g|-sum relative errors of sampled gradient elements"""
+    nrm = np.linalg.norm(got - ex) / max(np.linalg.norm(ex), 1e-30)
+    big = np.abs(ex) >= 0.5 * np.abs(ex).max()
+    lrg = float((np.abs(got - ex)[big] / np.abs(ex)[big]).max()) if big.any() else 0.0
+    return nrm, lrg, abs(full_abs_sum - exact_abs_sum) / max(exact_abs_sum, 1e-30)
 
 
 # fixture -> (model builder, batch keys, batch seed)
@@ -138,7 +130,7 @@ def test_full_size_fp32_matches_reference(name):
             f"{pname}: max err {err.max():.3e} vs bound {bound:.3e} (reference fp32 {e_ref:.3e})"
         st = g["grad/stats/" + pname]
         got = np.array([np.abs(full).sum(), np.sqrt((full * full).sum())])
-        np.testing.assert_allclose(got, st[1:], rtol=2e-3, err_msg=pname)
+        np.testing.assert_allclose(got, st[1:], rtol=2e-3, atol=1e-6 * gscale, err_msg=pname)
         n += 1
     assert n >= 20
 
@@ -148,9 +140,11 @@ def test_full_size_bf16_matches_reference(name):
     """The benched bf16 kernels at the benched size against the same reference fixture."""
     g, m, ev, tr, loss = _run(name, "bf16")
     exact = g["train_logits64"]
-    bound = 3e-2 * max(1.0, np.abs(exact).max())
+    e16 = np.abs(g["train_logits16"] - exact).max()
+    bound = min(3e-2 * max(1.0, np.abs(exact).max()), REF16_X * e16 + 5e-3)
     err = np.abs(tr - exact).max()
-    print(f"{name} bf16 logits max|err| vs f64 {err:.3e} (bound {bound:.3e})")
+    print(f"{name} bf16 logits max|err| vs f64 {err:.3e} (reference bf16 {e16:.3e}, "
+          f"bound {bound:.3e})")
     assert err <= bound
     top2 = np.sort(exact, axis=1)[:, ::-1]
     decided = (top2[:, 0] - top2[:, 1]) > 2 * bound
@@ -168,26 +162,28 @@ def test_full_size_bf16_matches_reference(name):
             e = np.abs(bufs[pname].double().cpu().numpy().ravel()[: ref.size] - ref).max()
             assert e <= 2e-2 * max(np.abs(ref).max(), 1e-3), (key, e)
     params = dict(m.named_parameters())
-    rows, bad = [], []
+    rows, bad, ratios = [], [], []
     for key in g:
         if not key.startswith("grad64/samp/"):
             continue
         pname = key[len("grad64/samp/"):]
         full = params[pname].grad.detach().double().cpu().numpy().ravel()
-        ours = full[prng.sample_index(pname, full.size)]
-        ex = g[key]
-        nrm = np.linalg.norm(ours - ex) / max(np.linalg.norm(ex), 1e-30)
-        big = np.abs(ex) >= 0.5 * np.abs(ex).max()
-        lrg = float((np.abs(ours - ex)[big] / np.abs(ex)[big]).max()) if big.any() else 0.0
-        st = g["grad64/stats/" + pname]
-        sum_rel = abs(np.abs(full).sum() - st[1]) / max(st[1], 1e-30)
-        rows.append((pname, nrm, lrg, sum_rel))
-        if nrm > _group_tol(NRM16, pname) or lrg > _group_tol(LRG16, pname) or sum_rel > SUM16:
+        ex, st = g[key], g["grad64/stats/" + pname]
+        ours = _errs(full[prng.sample_index(pname, full.size)], ex, np.abs(full).sum(), st[1])
+        ref = _errs(g["grad16/samp/" + pname], ex, g["grad16/stats/" + pname][1], st[1])
+        lim = (REF16_X * ref[0] + REF16_ABS, REF16_X * ref[1] + REF16_LRG_ABS,
+               REF16_X * ref[2] + REF16_ABS)
+        rows.append((pname, ours, ref))
+        ratios.append(ours[0] / max(ref[0], 1e-12))
+        if any(o > b for o, b in zip(ours, lim)):
             bad.append(pname)
-    for pname, nrm, lrg, sum_rel in rows:
-        print(f"  {pname}: normwise {nrm:.3e}  large-element {lrg:.3e}  |g| sum {sum_rel:.3e}")
+    for pname, ours, ref in rows:
+        print(f"  {pname}: normwise {ours[0]:.3e} (ref bf16 {ref[0]:.3e})  large-element "
+              f"{ours[1]:.3e} ({ref[1]:.3e})  |g| sum {ours[2]:.3e} ({ref[2]:.3e})")
+    print(f"  median normwise ratio ours / reference bf16: {np.median(ratios):.3f}")
     assert len(rows) >= 20
-    assert not bad, f"bf16 gradients beyond the group bounds: {bad}"
+    assert not bad, f"bf16 gradients beyond 2x the reference's bf16 error: {bad}"
+    assert np.median(ratios) <= 1.25, np.median(ratios)
 
 
 def _ref_conv(x, w, s, p, d):

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--op", default="wgrad", choices=["fwd", "dgrad", "wgrad"])
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--stats", action="store_true", help="fwd: BN partial sums too")
+    ap.add_argument("--relu", action="store_true",
+                    help="operands ReLU'd (about half zeros, like a post-BN activation)")
     ap.add_argument("--time", action="store_true",
                     help="print the median launch time (HIP events) instead of only running")
     a = ap.parse_args()
@@ -52,6 +55,13 @@ def main():
             memory_format=torch.channels_last_3d)
     y = torch.randn((a.batch, co, d.do_, d.ho, d.wo), device="cuda", dtype=dtype).contiguous(
         memory_format=torch.channels_last_3d)
+    if a.relu:
+        x.relu_()
+        y.relu_()
+    st = None
+    if a.stats and a.op == "fwd":
+        rows = lib.mmad_conv3d_stats_rows(d, dt)
+        st = torch.empty((rows, 2, co), device="cuda")
     wp = volume_ops.pack_weight(d, dt, w, dtype, a.op == "dgrad") if a.op != "wgrad" else None
     if a.op == "wgrad":
         wsp = torch.empty((lib.mmad_conv3d_wgrad_workspace(d, dt) + 3) // 4, device="cuda")
@@ -62,7 +72,7 @@ def main():
         e0.record()
         if a.op == "fwd":
             _lib.call("mmad_conv3d_fwd", d, dt, _lib.ptr(x), _lib.ptr(wp), None, _lib.ptr(y),
-                      None, _lib.stream())
+                      None if st is None else _lib.ptr(st), _lib.stream())
         elif a.op == "dgrad":
             _lib.call("mmad_conv3d_dgrad", d, dt, _lib.ptr(y), _lib.ptr(wp), _lib.ptr(x),
                       _lib.stream())
@@ -74,7 +84,8 @@ def main():
     torch.cuda.synchronize()
     if a.time:
         ts = sorted(x.elapsed_time(y) * 1e3 for x, y in times[1:])
-        print(f"{a.layer} {a.op} median {ts[len(ts) // 2]:.1f} us (min {ts[0]:.1f}, "
+        print(f"{a.layer} {a.op}{' stats' if st is not None else ''}"
+              f"{' relu' if a.relu else ''} median {ts[len(ts) // 2]:.1f} us (min {ts[0]:.1f}, "
               f"{len(ts)} reps, lib {os.environ.get('MMAD_LIB_PATH', 'default')})")
     else:
         print("ok", a.layer, a.op, a.reps)
