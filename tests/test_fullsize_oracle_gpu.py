@@ -29,7 +29,9 @@ Bars:
     relative; running statistics within 2e-2 of each tensor's max; per gradient tensor, the
     normwise relative error of the sampled elements, the relative error of every LARGE
     sampled element (|g| >= half the tensor's max) and the |g|-sum error each within 2x the
-    reference's bf16 error of the same quantity + 0.02 (+0.05 for the large elements).
+    reference's bf16 error of the same quantity + 0.02 (+0.05 for the large elements, + a
+    quarter of the reference's normwise error for the sum), and the median over tensors of
+    our normwise error / the reference's at most 1.25 (measured 0.95-1.01).
     bf16 rounding noise compounds along the backward chain (each dgrad re-rounds to bf16) and
     through BN's cancelling sums and the stem's max-pool argmax moves, so both paths' errors
     grow towards the input (ResNet-18 at 160^3: ~0.4 normwise at layer1 for both); the
@@ -171,8 +173,11 @@ def test_full_size_bf16_matches_reference(name):
         ex, st = g[key], g["grad64/stats/" + pname]
         ours = _errs(full[prng.sample_index(pname, full.size)], ex, np.abs(full).sum(), st[1])
         ref = _errs(g["grad16/samp/" + pname], ex, g["grad16/stats/" + pname][1], st[1])
+        # (a |g| sum over 64..512 BN channels fluctuates with the per-element noise: the
+        # reference's own sum error can be small by chance, so a quarter of its normwise
+        # error is allowed on top)
         lim = (REF16_X * ref[0] + REF16_ABS, REF16_X * ref[1] + REF16_LRG_ABS,
-               REF16_X * ref[2] + REF16_ABS)
+               REF16_X * ref[2] + 0.25 * ref[0] + REF16_ABS)
         rows.append((pname, ours, ref))
         ratios.append(ours[0] / max(ref[0], 1e-12))
         if any(o > b for o, b in zip(ours, lim)):
