@@ -243,6 +243,10 @@ def main():
         if m in DP_MODES and DP_MODES[m][0] == "staged":
             return GradAllReduce(model.parameters(), bucket_mb=None,
                                  stages=backward_stages(model, DP_MODES[m][1])[1])
+        if m == "after":
+            # every bucket is reduced on the main stream after the backward graph: one bucket,
+            # one collective (no overlap to gain from splitting)
+            return GradAllReduce(model.parameters(), bucket_mb=None)
         return GradAllReduce(model.parameters(),
                              bucket_mb=float(os.environ.get("MMAD_DP_BUCKET_MB", "4")))
 

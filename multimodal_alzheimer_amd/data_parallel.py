@@ -11,8 +11,9 @@ only exchange per step is the gradient all-reduce:
   last layers' gradients, ready first in backward, go first; or one bucket per backward
   stage, ``stages=``) all-reduced asynchronously -- from post-accumulate-grad hooks while an
   eager backward continues, or per stage between the replayed backward graphs
-  (graph_step ``collectives="staged"``); ``finish()`` waits, averages and writes the
-  reduced gradients back.
+  (graph_step ``collectives="staged"``); ``finish()`` reduces what is left on the current
+  stream (synchronous collective: no cross-stream hop), waits for the rest, averages and
+  writes the reduced gradients back.
 
 BN batch statistics are per replica (each rank normalises its own shard, as DDP without
 SyncBatchNorm).  The running statistics: DDP's default ``broadcast_buffers=True`` copies
@@ -162,6 +163,12 @@ class GradAllReduce:
         # forward + backward is captured without its collectives (graph_step
         # collectives="after"): a replay runs no Python hooks, so finish() does it all.
         self.defer = False
+        # buckets still unlaunched when finish() runs (the last backward stage's; every
+        # bucket in collectives="after") are all-reduced synchronously on the current stream:
+        # a blocking ProcessGroupNCCL collective runs on the caller's stream, an async one on
+        # the group's internal stream behind two cross-stream waits (tools/ar_latency.py, one
+        # RCCL rank: 17 vs 37 us per critical-path all-reduce)
+        self.inline_tail = True
         self.reset()
 
     def reset(self):
@@ -180,12 +187,20 @@ class GradAllReduce:
                  if p.grad.data_ptr() != self._views[p].data_ptr()]
         return [g for g, _ in pairs], [v for _, v in pairs]
 
-    def _launch(self, bi):
+    def _launch(self, bi, inline=False):
         flat = self.flats[bi]
         for p in self.buckets[bi]:
             if p.grad is None:                   # unused this step: contributes zeros
                 p.grad = torch.zeros_like(p)
         grads, views = self._foreign(bi)
+        if inline:
+            if grads:
+                torch._foreach_copy_(views, grads)
+            dist.all_reduce(flat, op=self._op, group=self.group)
+            if not self._avg:
+                flat.div_(self.world)
+            self._inflight[bi] = None            # done (on the current stream)
+            return
         if flat.is_cuda:
             # conv weight gradients may come from volume_ops' side stream (the backward
             # pass joins it only at its end): gather and reduce there, after the main
@@ -216,16 +231,19 @@ class GradAllReduce:
     def finish(self):
         """Wait for every bucket (launching any whose grads never all arrived), then
         make every parameter's grad the mean over ranks."""
+        cuda = bool(self.params) and self.params[0].is_cuda
+        inline = self.inline_tail and not (cuda and torch.cuda.is_current_stream_capturing())
         for bi, b in enumerate(self.buckets):
             if bi not in self._inflight:
-                self._launch(bi)
-        if self.params and self.params[0].is_cuda:
+                self._launch(bi, inline=inline)
+        if cuda and any(w is not None for w in self._inflight.values()):
             from .volume_ops import grad_stream
             torch.cuda.current_stream().wait_stream(grad_stream(self.params[0].device))
         for bi, work in sorted(self._inflight.items()):
-            work.wait()
-            if not self._avg:
-                self.flats[bi].div_(self.world)
+            if work is not None:
+                work.wait()
+                if not self._avg:
+                    self.flats[bi].div_(self.world)
             grads, views = self._foreign(bi)
             if grads:
                 # one multi-tensor launch per bucket, not one copy kernel per parameter

@@ -51,6 +51,10 @@ import torch
 from . import volume_ops
 
 COLLECTIVES = ("staged", "after", "inside")
+# Captures check only this thread's calls: ProcessGroupNCCL's watchdog thread polls the events
+# of collectives issued before a capture (hipEventQuery), which "global" mode turns into a
+# capture error that aborts the process (seen when a blocking all-reduce ran just before one)
+_CAPTURE_MODE = "thread_local"
 DEFAULT_CUTS = ("layer4", "layer3", "layer2")
 
 
@@ -204,7 +208,7 @@ class GraphedTrainStep:
             try:
                 if self.mode == "after":
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g):
+                    with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                         self.out = model.general_step(self.static, 0, "train")
                         self.out["loss"].backward()
                     self.graphs.append(g)
@@ -212,7 +216,7 @@ class GraphedTrainStep:
                     staged.arm()
                     try:
                         g = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(g):
+                        with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                             self.out = model.general_step(self.static, 0, "train")
                             staged.run(0, self.out["loss"])
                     finally:
@@ -220,7 +224,8 @@ class GraphedTrainStep:
                     self.graphs.append(g)
                     for k in range(1, staged.n):
                         g = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(g, pool=self.graphs[0].pool()):
+                        with torch.cuda.graph(g, pool=self.graphs[0].pool(),
+                                              capture_error_mode=_CAPTURE_MODE):
                             staged.run(k)
                         self.graphs.append(g)
             finally:
@@ -228,11 +233,12 @@ class GraphedTrainStep:
             reducer.reset()
             reducer.finish()                 # eager: gradients now averaged in place
             self.opt_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.opt_graph, pool=self.graphs[0].pool()):
+            with torch.cuda.graph(self.opt_graph, pool=self.graphs[0].pool(),
+                                  capture_error_mode=_CAPTURE_MODE):
                 optimizer.step()
         else:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                 self.out = model.general_step(self.static, 0, "train")
                 self.out["loss"].backward()
                 if reducer is not None:
@@ -263,15 +269,18 @@ class GraphedTrainStep:
         if self.mode is None or self.mode == "inside":
             self.graph.replay()
         else:
+            last = len(self.graphs) - 1
             for k, g in enumerate(self.graphs):
                 g.replay()
-                if self.mode == "staged":
+                if self.mode == "staged" and k < last:
                     self.reducer.launch_stage(k)   # overlaps the next graph's replay
             if self.finish_events is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-            self.reducer.finish()            # launches what is left, main waits, copies back
+            # the last stage's buckets (nothing left to overlap them with) are reduced by
+            # finish() on the main stream; then main waits for the side stream, copies back
+            self.reducer.finish()
             if self.finish_events is not None:
                 e1.record()
                 self.finish_events.append((e0, e1))
