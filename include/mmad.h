@@ -144,6 +144,20 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
 int mmad_conv3d_wgrad_split(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,
                             float* dw, float* dbias, void* workspace, void* stream,
                             void* reduce_stream);
+/* MedicalNet stem (Cin 1, 7^3, stride 2, pad 3; the descriptor mmad_conv_unfold_input
+ * takes) straight from the raw volume (n, 1, D, H, W) in `in_dtype` MMAD_F64 (as the
+ * reference DataLoader delivers it, dataloader.py:213-277 -> anat_cnn.py:29) or MMAD_F32,
+ * bf16 compute: the kernels unfold each input row in registers, so no unfolded copy is
+ * written or read.  Results are bit-identical to unfold + mmad_conv3d_fwd / _wgrad.
+ * mmad_stem_raw_ok: 1 when this path applies (even W <= 128, bf16, the stem geometry). */
+int mmad_stem_raw_ok(const mmad_conv_desc* d, int in_dtype, int dtype);
+int mmad_conv3d_fwd_raw(const mmad_conv_desc* d, int in_dtype, const void* x, int dtype,
+                        const void* w_packed, const float* bias, void* y, float* stats,
+                        void* stream);
+/* reduce_stream may be NULL (everything on stream); see mmad_conv3d_wgrad_split */
+int mmad_conv3d_wgrad_raw(const mmad_conv_desc* d, int in_dtype, const void* x, int dtype,
+                          const void* dy, float* dw, float* dbias, void* workspace,
+                          void* stream, void* reduce_stream);
 
 /* ---- BatchNorm3d / BatchNorm1d (+ fused ReLU and residual add) -------------------
  * Replaces nn.BatchNorm3d/1d + nn.ReLU + the residual `out += residual; relu`

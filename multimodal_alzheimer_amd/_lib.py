@@ -77,6 +77,9 @@ _SIGS = {
     "mmad_conv3d_wgrad_workspace": (_i64, [_P, _i32]),
     "mmad_conv3d_wgrad": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_conv3d_wgrad_split": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_stem_raw_ok": (_i32, [_P, _i32, _i32]),
+    "mmad_conv3d_fwd_raw": (_i32, [_P, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_conv3d_wgrad_raw": (_i32, [_P, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_bn_stats_parts": (_i64, [_i64, _i32]),
     "mmad_bn_stats": (_i32, [_i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_bn_parts_fold": (_i32, [_i32, _i32, _vp, _i32, _vp, _vp]),

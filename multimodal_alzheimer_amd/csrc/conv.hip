@@ -1845,7 +1845,8 @@ int fork_stream(hipStream_t st, hipStream_t rst) {
 // gradient) on `rst` -- a second stream lets the memory-bound reduction overlap the
 // latency-bound BN backward kernels that follow on `st`
 int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* dy, float* dw,
-                 float* dbias, void* workspace, hipStream_t st, hipStream_t rst) {
+                 float* dbias, void* workspace, hipStream_t st, hipStream_t rst,
+                 int raw_dtype = -1) {
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!x || !dy || !dw || !workspace) return MMAD_ENULL;
@@ -1856,8 +1857,11 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
   int rc;
   // (1x1x1 weight gradients stay here: hipBLASLt's heuristic offers no split-K algorithm
   // for K = all voxels at this size and its single-pass one ran 5x slower than wgrad_kernel)
-  if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on() && g.K == 392) {
-    rc = mmad_stem::wgrad(d, x, dy, (float*)workspace, stream);
+  if (raw_dtype >= 0 && !(unfolded(d) && mmad_stem::fwd_ok(d, dtype) && g.K == 392))
+    return MMAD_EUNSUPPORTED;                    // raw input: the stem kernel or nothing
+  if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && (stem_kernel_on() || raw_dtype >= 0) &&
+      g.K == 392) {
+    rc = mmad_stem::wgrad(d, x, dy, (float*)workspace, stream, raw_dtype);
     if (rc) return rc;
     if (rst != st && (rc = fork_stream(st, rst))) return rc;
     // (one slab per block: sum 16-slab groups in place first, so no thread walks them all)
@@ -1936,6 +1940,30 @@ int mmad_conv3d_wgrad_split(const mmad_conv_desc* d, int dtype, const void* x, c
   if (!reduce_stream) return MMAD_ENULL;
   return conv3d_wgrad(d, dtype, x, dy, dw, dbias, workspace, as_stream(stream),
                       as_stream(reduce_stream));
+}
+
+int mmad_stem_raw_ok(const mmad_conv_desc* d, int in_dtype, int dtype) {
+  if (!desc_ok(d) || !unfolded(d) || dtype != MMAD_BF16 || !stem_kernel_on()) return 0;
+  return mmad_stem::fwd_ok(d, dtype) && mmad_stem::raw_ok(d, in_dtype) ? 1 : 0;
+}
+
+int mmad_conv3d_fwd_raw(const mmad_conv_desc* d, int in_dtype, const void* x, int dtype,
+                        const void* w_packed, const float* bias, void* y, float* stats,
+                        void* stream) {
+  if (!desc_ok(d)) return MMAD_EBADSHAPE;
+  if (!x || !w_packed || !y) return MMAD_ENULL;
+  if (!mmad_stem_raw_ok(d, in_dtype, dtype)) return MMAD_EUNSUPPORTED;
+  return mmad_stem::fwd(d, x, w_packed, bias, y, stats, stream, in_dtype);
+}
+
+int mmad_conv3d_wgrad_raw(const mmad_conv_desc* d, int in_dtype, const void* x, int dtype,
+                          const void* dy, float* dw, float* dbias, void* workspace,
+                          void* stream, void* reduce_stream) {
+  if (!desc_ok(d)) return MMAD_EBADSHAPE;
+  if (!mmad_stem_raw_ok(d, in_dtype, dtype)) return MMAD_EUNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  return conv3d_wgrad(d, dtype, x, dy, dw, dbias, workspace, st,
+                      reduce_stream ? as_stream(reduce_stream) : st, in_dtype);
 }
 
 }  // extern "C"

@@ -16,6 +16,8 @@
 // writes the 128 x 64 bf16 output tile as 16-byte vectors and one row of BN partial sums,
 // exactly like the implicit-GEMM epilogue, so the BN that follows is unchanged.  The MFMA
 // runs transposed (channels x voxels) so each lane stores 4 adjacent channels directly.
+#include <type_traits>
+
 #include "common.h"
 #include "stem.h"
 
@@ -41,7 +43,51 @@ struct StemG {
   int rzf;                        // forward ring planes: KD + 2*SD (two z-steps ahead)
   int nyb, nzc, zsteps;           // y-pairs, z-chunks, z-steps per block
   int ring_off, c_off, red_off;   // LDS offsets (bytes)
+  int wi;                         // raw input width (raw-input forms)
 };
+
+// ---- raw-input rows (round 4) -----------------------------------------------------------
+// The stem kernels below can read the sample's raw volume (f64 as the DataLoader delivers it,
+// or f32) instead of the W-unfolded copy mmad_conv_unfold_input writes: a row of 2*64 input
+// values is one 16-byte (f64) / 8-byte (f32) load per lane (lane l holds x[2l], x[2l+1]), and
+// the unfolded 16-byte row of output column l -- taps kw 0..6 at x[2l-3 .. 2l+3] and a zero
+// eighth -- is assembled from lanes l-2 .. l+1 with three DPP wave shifts, then written to the
+// same LDS row the DMA would have filled.  Same bf16 values (f64 -> f32 -> bf16, as the
+// unfold kernel rounds), so the results are bit-identical; the unfold kernel's 134 MB write
+// and the kernels' re-read of it disappear.  Needs stride 2, pad 3, kw 7 along W, even Wi.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <typename TI>
+using RawV = std::conditional_t<sizeof(TI) == 8, u32x4, u32x2>;
+
+template <typename TI>
+__device__ __forceinline__ RawV<TI> raw_row_load(__amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+  if constexpr (sizeof(TI) == 8) return __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0);
+  else return __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, 0);
+}
+
+// the unfolded row of output column `lane` (zero past wo) into LDS at `dst` + lane * 16;
+// every lane of the wave must run it (cross-lane reads)
+template <typename TI>
+__device__ __forceinline__ void raw_row_commit(RawV<TI> v, int lane, int wo, char* dst) {
+  float a, b;
+  if constexpr (sizeof(TI) == 8) {
+    a = (float)__builtin_bit_cast(double, ((uint64_t)v[1] << 32) | v[0]);
+    b = (float)__builtin_bit_cast(double, ((uint64_t)v[3] << 32) | v[2]);
+  } else {
+    a = __uint_as_float(v[0]);
+    b = __uint_as_float(v[1]);
+  }
+  // neighbours by DPP wave shifts (VALU: no LDS-queue traffic, so no lgkmcnt wait that would
+  // drain the MFMA fragment reads in flight); lanes shifted in from outside the wave read 0
+  const int me = (int)pack_bf16x2(a, b);                      // x[2l], x[2l+1]
+  const uint32_t l1 = (uint32_t)__builtin_amdgcn_update_dpp(0, me, 0x138, 0xf, 0xf, true);
+  const uint32_t l2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)l1, 0x138, 0xf, 0xf, true);
+  const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, me, 0x130, 0xf, 0xf, true);
+  const uint32_t m = (uint32_t)me;
+  u32x4 w{(l2 >> 16) | (l1 << 16), (l1 >> 16) | (m << 16), (m >> 16) | (r1 << 16), r1 >> 16};
+  if (lane >= wo) w = u32x4{0u, 0u, 0u, 0u};
+  *reinterpret_cast<u32x4*>(dst + lane * 16) = w;
+}
 
 template <int KD, int KH, int SD, int SH>
 __global__ __launch_bounds__(320) void stem_fwd_kernel(StemG g, const u16* __restrict__ U,
@@ -261,13 +307,15 @@ constexpr int STQ = 4;                     // output stores (16 B) per wave per 
 constexpr uint32_t OOBQ = 0x40000000u;     // masked-lane store offset (past any resource)
 constexpr size_t LDSQ = (size_t)RZQ * PLQ + ROWB + 4 * 2 * CO * sizeof(float);
 
-template <bool BIAS>
-__global__ __launch_bounds__(512) void stem_fwdq_kernel(StemG g, const u16* __restrict__ U,
+template <bool BIAS, typename TI>
+__global__ __launch_bounds__(512) void stem_fwdq_kernel(StemG g, const TI* __restrict__ U,
                                                         const u16* __restrict__ wp,
                                                         const float* __restrict__ bias,
                                                         u16* __restrict__ y,
                                                         float* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr bool RAW = sizeof(TI) != 2;          // raw volume rows (else the unfolded U)
+  constexpr int RZ = RZQ;                        // ring planes
   char* ring = smem;
   float* red = reinterpret_cast<float*>(smem + RZQ * PLQ + ROWB);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -285,9 +333,37 @@ __global__ __launch_bounds__(512) void stem_fwdq_kernel(StemG g, const u16* __re
   // Padding rows read past the end of a buffer resource over this sample's U
   // (the range check returns zeros without touching memory: a shared zero buffer would put
   // every block's padding reads on one L2 channel)
+  const int64_t srow = RAW ? g.wi : (int64_t)g.wo * 8;         // elements per input row
   const __amdgpu_buffer_rsrc_t rsu = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(U + (int64_t)nb * g.di * g.hi * g.wo * 8), 0,
-      (int)__builtin_amdgcn_readfirstlane(g.di * g.hi * g.wo * 16), 0x00020000);
+      (void*)(U + (int64_t)nb * g.di * g.hi * srow), 0,
+      (int)__builtin_amdgcn_readfirstlane((int)(g.di * g.hi * srow * (int64_t)sizeof(TI))),
+      0x00020000);
+  // raw form: this lane's offset of row (zi, t), OOBQ for padding rows / lanes past Wi
+  auto raw_off = [&](int zi, int t) __attribute__((always_inline)) {
+    const int yi = ybase + t;
+    const bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi &&
+                    2 * lane < g.wi;
+    return ok ? (uint32_t)(((zi * g.hi + yi) * g.wi + 2 * lane) * (int)sizeof(TI)) : OOBQ;
+  };
+  // raw form: the 2 new planes of z-step ozn (26 rows, <= DMAQ per wave) into registers, and
+  // later into their ring rows
+  auto raw_step_load = [&](int ozn, RawV<TI> (&r)[DMAQ]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < DMAQ; ++h) {
+      const int f = wave + NWQ * h;
+      if (f < 2 * YINQ)
+        r[h] = raw_row_load<TI>(rsu, raw_off(ozn * 2 - g.pd + 5 + f / YINQ, f % YINQ));
+    }
+  };
+  auto raw_step_commit = [&](int ozn, const RawV<TI> (&r)[DMAQ]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < DMAQ; ++h) {
+      const int f = wave + NWQ * h;
+      if (f < 2 * YINQ)
+        raw_row_commit<TI>(r[h], lane, g.wo,
+                           smem + ((ozn * 2 + 5 + f / YINQ) % RZ) * PLQ + (f % YINQ) * ROWB);
+    }
+  };
   auto load_row = [&](int zi, int slot, int t) __attribute__((always_inline)) {
     const int yi = ybase + t;
     bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi && lane < g.wo;
@@ -327,14 +403,41 @@ __global__ __launch_bounds__(512) void stem_fwdq_kernel(StemG g, const u16* __re
   };
 
   // prologue: the 7 planes of the first z-step, then the next step's 2
+  if constexpr (RAW) {
+    // (registers, once, 4 rows at a time) the first step's planes; the next step's raw rows
+    // into staging
+#pragma unroll
+    for (int h0 = 0; h0 < PROQ; h0 += 4) {
+      RawV<TI> pr[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int f = wave + NWQ * (h0 + h);
+        if (f < 7 * YINQ) pr[h] = raw_row_load<TI>(rsu, raw_off(oz0 * 2 - g.pd + f / YINQ, f % YINQ));
+      }
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int f = wave + NWQ * (h0 + h);
+        if (f < 7 * YINQ)
+          raw_row_commit<TI>(pr[h], lane, g.wo,
+                             smem + ((oz0 * 2 + f / YINQ) % RZ) * PLQ + (f % YINQ) * ROWB);
+      }
+    }
+    if (oz0 + 1 < oz1) {
+      RawV<TI> r1[DMAQ];
+      raw_step_load(oz0 + 1, r1);
+      raw_step_commit(oz0 + 1, r1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  } else {
 #pragma unroll 1
-  for (int h = 0; h < PROQ; ++h) {
-    const int f = wave + NWQ * h, kd = f / YINQ;
-    if (f < 7 * YINQ) load_row(oz0 * 2 - g.pd + kd, (oz0 * 2 + kd) % RZQ, f % YINQ);
+    for (int h = 0; h < PROQ; ++h) {
+      const int f = wave + NWQ * h, kd = f / YINQ;
+      if (f < 7 * YINQ) load_row(oz0 * 2 - g.pd + kd, (oz0 * 2 + kd) % RZQ, f % YINQ);
+    }
+    dummy_stores();
+    load_step(oz0 + 1);
+    dummy_stores();
   }
-  dummy_stores();
-  load_step(oz0 + 1);
-  dummy_stores();
 
   const int lr = lane & 15, lk = lane >> 4;
   const int yl = wave & 3, ch = wave >> 2;
@@ -404,15 +507,25 @@ __global__ __launch_bounds__(512) void stem_fwdq_kernel(StemG g, const u16* __re
 
   // z-step oz into C while the epilogue of step oz-1 (P) drains
   auto zstep = [&](f32x4 (&C)[4][2], f32x4 (&P)[4][2], int oz) __attribute__((always_inline)) {
-    wait_planes(oz);                               // planes of oz landed (all waves' ...)
-    raw_barrier();                                 // ... and step oz-1's reads are done
-    load_step(oz + 2);
+    RawV<TI> rn[DMAQ];
+    if constexpr (RAW) {
+      // this wave's ring writes of step oz-1 (the planes of oz + 1) are done; the barrier
+      // makes everyone's visible.  Then the raw rows of oz + 2 (two steps ahead, as the DMA
+      // form) into registers: they land while the MFMAs of oz run
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+      if (oz + 2 < oz1) raw_step_load(oz + 2, rn);
+    } else {
+      wait_planes(oz);                             // planes of oz landed (all waves' ...)
+      raw_barrier();                               // ... and step oz-1's reads are done
+      load_step(oz + 2);
+    }
     const bool plive = oz > oz0;
     const uint32_t psoff = plive ? (uint32_t)((oz - 1) * plane_out) : OOBQ;
-    const int sb = (oz * 2) % RZQ;
+    const int sb = (oz * 2) % RZ;
     auto pbk = [&](int k) __attribute__((always_inline)) {
       const int sl = sb + k;
-      return (uint32_t)((sl >= RZQ ? sl - RZQ : sl) * PLQ);
+      return (uint32_t)((sl >= RZ ? sl - RZ : sl) * PLQ);
     };
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -455,6 +568,12 @@ __global__ __launch_bounds__(512) void stem_fwdq_kernel(StemG g, const u16* __re
       // alone, the scheduler serialises every read behind the MFMAs that consume it)
       __builtin_amdgcn_sched_barrier(0);
     }
+    // raw form: staging is free again (this wave's reads of it are done): the raw rows of
+    // oz + 2, unfolded into the ring during the next step
+    // raw form: the planes of oz + 2 into their ring slots (last read by step oz - 1, next
+    // by step oz + 2)
+    if constexpr (RAW)
+      if (oz + 2 < oz1) raw_step_commit(oz + 2, rn);
   };
   f32x4 acc0[4][2], acc1[4][2];
 #pragma unroll
@@ -663,8 +782,8 @@ __global__ __launch_bounds__(512) void stem_wgrad_kernel(StemG g, const u16* __r
 // shared zero buffer and no per-row range checks), and every LDS fragment read is a
 // per-z-step base register plus an immediate.  The next K-step's fragments are read ahead
 // of the current MFMAs (fenced, so the scheduler keeps them there).
-template <int KD, int KH, int SD, int SH>
-__global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const u16* __restrict__ U,
+template <int KD, int KH, int SD, int SH, typename TI>
+__global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const TI* __restrict__ U,
                                                           const u16* __restrict__ dy,
                                                           float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -684,14 +803,18 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const u16* __
   const int oz1 = min(g.do_, oz0 + g.zsteps);
   const int ybase = yb * YT * SH - g.ph;
   const uint32_t ring_l = lds_addr_of(smem), dyr_l = ring_l + (uint32_t)g.ring_off;
+  constexpr bool RAW = sizeof(TI) != 2;          // raw volume rows (else the unfolded U)
 
+  const int64_t srow = RAW ? g.wi : (int64_t)g.wo * 8;         // elements per input row
   const __amdgpu_buffer_rsrc_t rsu = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(U + (int64_t)nb * g.di * g.hi * g.wo * 8), 0,
-      (int)__builtin_amdgcn_readfirstlane(g.di * g.hi * g.wo * 16), 0x00020000);
+      (void*)(U + (int64_t)nb * g.di * g.hi * srow), 0,
+      (int)__builtin_amdgcn_readfirstlane((int)(g.di * g.hi * srow * (int64_t)sizeof(TI))),
+      0x00020000);
   const __amdgpu_buffer_rsrc_t rsd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(dy + (int64_t)nb * g.do_ * g.ho * g.wo * CO), 0,
       (int)__builtin_amdgcn_readfirstlane(g.do_ * g.ho * g.wo * CO * 2), 0x00020000);
-  const uint32_t ustep = (uint32_t)(SD * g.hi * g.wo * 16), dstep = (uint32_t)(g.ho * g.wo * CO * 2);
+  const uint32_t ustep = (uint32_t)(SD * g.hi * srow * (int64_t)sizeof(TI));
+  const uint32_t dstep = (uint32_t)(g.ho * g.wo * CO * 2);
 
   // this wave's DMA slots h: f = wave + 8h; U rows of the step's SD new planes (f < RSTEP),
   // then the 16 dY pieces (8 rows x 128 B each, chunk-swizzled for the transposing reads)
@@ -702,7 +825,9 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const u16* __
     voff[h] = OOB;
     if (f < RSTEP) {
       const int kd = KD - SD + f / YIN, yi = ybase + f % YIN;
-      if ((unsigned)yi < (unsigned)g.hi && lane < g.wo)
+      if (RAW && (unsigned)yi < (unsigned)g.hi && 2 * lane < g.wi)
+        voff[h] = (uint32_t)((((kd - g.pd) * g.hi + yi) * g.wi + 2 * lane) * (int)sizeof(TI));
+      else if (!RAW && (unsigned)yi < (unsigned)g.hi && lane < g.wo)
         voff[h] = (uint32_t)((((kd - g.pd) * g.hi + yi) * g.wo + lane) * 16);
     } else if (f < RSTEP + 16) {
       const int row = (f - RSTEP) * 8 + (lane >> 3);
@@ -711,7 +836,10 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const u16* __
       if (x < g.wo && yy < g.ho) voff[h] = (uint32_t)(((yy * g.wo + x) * CO + ch * 8) * 2);
     }
   }
-  auto load_step = [&](int ozn) __attribute__((always_inline)) {
+  // raw form: this wave's U rows of the next step in registers (issued with its dY DMAs),
+  // unfolded into the ring at the end of the current step
+  RawV<TI> rv[NH];
+  auto raw_commit_step = [&](int ozn) __attribute__((always_inline)) {
     int sbn = (ozn * SD) % g.rz;
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
@@ -719,8 +847,24 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const u16* __
       if (f < RSTEP) {
         int slot = sbn + KD - SD + f / YIN;
         slot -= slot >= g.rz ? g.rz : 0;
-        buf_lds16_asm(voff[h] + (uint32_t)ozn * ustep, rsu,
-                      ring_l + (uint32_t)((slot * YIN + f % YIN) * ROWB_W));
+        raw_row_commit<TI>(rv[h], lane, g.wo, smem + (slot * YIN + f % YIN) * ROWB_W);
+      }
+    }
+  };
+  auto load_step = [&](int ozn, bool urows = true) __attribute__((always_inline)) {
+    int sbn = (ozn * SD) % g.rz;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int f = wave + 8 * h;
+      if (f < RSTEP) {
+        int slot = sbn + KD - SD + f / YIN;
+        slot -= slot >= g.rz ? g.rz : 0;
+        if constexpr (RAW) {
+          if (urows) rv[h] = raw_row_load<TI>(rsu, voff[h] + (uint32_t)ozn * ustep);
+        } else {
+          buf_lds16_asm(voff[h] + (uint32_t)ozn * ustep, rsu,
+                        ring_l + (uint32_t)((slot * YIN + f % YIN) * ROWB_W));
+        }
       } else if (f < RSTEP + 16) {
         buf_lds16_asm(voff[h] + (uint32_t)ozn * dstep, rsd,
                       dyr_l + (uint32_t)((ozn & 1) * DYB + (f - RSTEP) * 1024));
@@ -729,15 +873,41 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const u16* __
   };
   if (oz0 < oz1) {
     // prologue: the first step's KD - SD older planes (generic addressing, once)
+    if constexpr (RAW) {
+      // (registers, once) all KD planes of the first step; then its dY tile and the next
+      // step's raw rows into staging
+      constexpr int NPR = (KD * YIN + 7) / 8;
+      RawV<TI> pr[NPR];
+#pragma unroll
+      for (int h = 0; h < NPR; ++h) {
+        const int f = wave + 8 * h;
+        if (f < KD * YIN) {
+          const int kd = f / YIN, zi = oz0 * SD - g.pd + kd, yi = ybase + f % YIN;
+          const bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi &&
+                          2 * lane < g.wi;
+          pr[h] = raw_row_load<TI>(
+              rsu, ok ? (uint32_t)(((zi * g.hi + yi) * g.wi + 2 * lane) * (int)sizeof(TI)) : OOB);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < NPR; ++h) {
+        const int f = wave + 8 * h;
+        if (f < KD * YIN)
+          raw_row_commit<TI>(pr[h], lane, g.wo,
+                             smem + (((oz0 * SD + f / YIN) % g.rz) * YIN + f % YIN) * ROWB_W);
+      }
+      load_step(oz0, false);                     // (its dY tile; its U rows are in)
+    } else {
 #pragma unroll 1
-    for (int f = wave; f < (KD - SD) * YIN; f += 8) {
-      const int kd = f / YIN, zi = oz0 * SD - g.pd + kd, yi = ybase + f % YIN;
-      const bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi &&
-                      lane < g.wo;
-      buf_lds16_asm(ok ? (uint32_t)(((zi * g.hi + yi) * g.wo + lane) * 16) : OOB, rsu,
-                    ring_l + (uint32_t)((((oz0 * SD + kd) % g.rz) * YIN + f % YIN) * ROWB_W));
+      for (int f = wave; f < (KD - SD) * YIN; f += 8) {
+        const int kd = f / YIN, zi = oz0 * SD - g.pd + kd, yi = ybase + f % YIN;
+        const bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi &&
+                        lane < g.wo;
+        buf_lds16_asm(ok ? (uint32_t)(((zi * g.hi + yi) * g.wo + lane) * 16) : OOB, rsu,
+                      ring_l + (uint32_t)((((oz0 * SD + kd) % g.rz) * YIN + f % YIN) * ROWB_W));
+      }
+      load_step(oz0);
     }
-    load_step(oz0);
   }
 
   // compute wave w: channels [32*(w&1), +32), k columns [112*(w>>1), +112) = 14 taps
@@ -768,11 +938,16 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const u16* __
 
 #pragma unroll 1
   for (int oz = oz0; oz < oz1; ++oz) {
-    wait_vm_lgkm0<0>();                            // this wave's DMAs for oz landed
+    // this wave's DMAs for oz landed.  (Raw form: as the builtin, which the compiler's wait
+    // bookkeeping sees -- after the opaque asm form it still counted the previous step's
+    // register loads as pending and put a vmcnt(0) before every new one.)
+    if constexpr (RAW) __builtin_amdgcn_s_waitcnt(0);
+    else wait_vm_lgkm0<0>();
     raw_barrier();                                 // ... and everyone's; step oz-1 done
 #ifndef STEMW_NO_DMA
     if (oz + 1 < oz1) load_step(oz + 1);          // lands while the MFMAs of oz run
 #endif
+
     const int sbase = (oz * SD) % g.rz;
     const char* dyt = smem + g.ring_off + (oz & 1) * DYB;
     const char* pl[7];
@@ -814,6 +989,10 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const u16* __
                                                               acc[i][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
+    // raw form: the next step's U rows into their ring slots (free during step oz; read
+    // after the loop-top wait + barrier)
+    if constexpr (RAW)
+      if (oz + 1 < oz1) raw_commit_step(oz + 1);
   }
   // this block's partial slab: ws[bid][co][k], k < 392
   float* out = ws + (int64_t)bid * CO * WK;
@@ -855,6 +1034,7 @@ bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds, bool 
   if (d->dd != 1 || d->dh != 1 || d->dw != 1 || d->wo > XW || d->wo < 1) return false;
   g = StemG{};
   g.n = d->n; g.di = d->di; g.hi = d->hi; g.wo = d->wo; g.do_ = d->do_; g.ho = d->ho;
+  g.wi = d->wi;
   g.sd = d->sd; g.sh = d->sh; g.pd = d->pd; g.ph = d->ph;
   const int ntap = d->kd * d->kh;
   g.kpad = (int)cdiv(ntap * 8, 64) * 64;        // as mmad_conv_pack_weight (mode 2)
@@ -889,6 +1069,19 @@ bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds, bool 
 
 namespace mmad_stem {
 
+bool raw_ok(const mmad_conv_desc* d, int in_dtype) {
+  StemG g;
+  int blocks;
+  size_t lds;
+  if (in_dtype != MMAD_F64) return false;         // (16-byte raw rows: f64 only)
+  if (d->kw != 7 || d->sw != 2 || d->pw != 3 || d->dw != 1 || d->wi % 2 || d->wi > 2 * XW)
+    return false;
+  if (!quad_on() || !geom_for(d, g, blocks, lds, true)) return false;
+  // 32-bit buffer offsets over one sample's volume
+  return (int64_t)d->di * d->hi * d->wi * 8 < (int64_t(1) << 30) &&
+         (int64_t)d->do_ * d->ho * d->wo * CO * 2 < (int64_t(1) << 30);
+}
+
 bool fwd_ok(const mmad_conv_desc* d, int dtype) {
   StemG g;
   int blocks;
@@ -913,26 +1106,33 @@ int64_t wgrad_blocks(const mmad_conv_desc* d) {
   return blocks;
 }
 
-int wgrad(const mmad_conv_desc* d, const void* x_unf, const void* dy, float* ws, void* stream) {
+int wgrad(const mmad_conv_desc* d, const void* x_unf, const void* dy, float* ws, void* stream,
+          int in_dtype) {
   StemG g;
   int blocks;
   size_t lds;
   if (!geom_for(d, g, blocks, lds)) return MMAD_EUNSUPPORTED;
+  if (in_dtype >= 0 && !raw_ok(d, in_dtype)) return MMAD_EUNSUPPORTED;
   // LDS: U plane ring, then two dY tiles
   g.ring_off = g.rz * g.yin * ROWB_W;
   const size_t wl = (size_t)g.ring_off + 2 * YT * XW * CO * 2;
-  static const bool ok = hipFuncSetAttribute((const void*)stem_wgrad_kernel<7, 7, 2, 2>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             160 * 1024) == hipSuccess &&
-                         hipFuncSetAttribute((const void*)stem_wgrad2_kernel<7, 7, 2, 2>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             160 * 1024) == hipSuccess;
+  auto attr = [](const void* k) {
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==
+           hipSuccess;
+  };
+  static const bool ok = attr((const void*)stem_wgrad_kernel<7, 7, 2, 2>) &&
+                         attr((const void*)stem_wgrad2_kernel<7, 7, 2, 2, u16>) &&
+                         attr((const void*)stem_wgrad2_kernel<7, 7, 2, 2, double>);
   if (!ok || wl > 160 * 1024) return MMAD_EUNSUPPORTED;
   // (the hoisted form's buffer offsets are 32-bit)
   const bool small = (int64_t)g.di * g.hi * g.wo * 16 < (int64_t(1) << 30) &&
                      (int64_t)g.do_ * g.ho * g.wo * CO * 2 < (int64_t(1) << 30);
-  if (wg2_on() && small)
-    hipLaunchKernelGGL((stem_wgrad2_kernel<7, 7, 2, 2>), dim3((unsigned)blocks), dim3(512), wl,
+  if (in_dtype == MMAD_F64)
+    hipLaunchKernelGGL((stem_wgrad2_kernel<7, 7, 2, 2, double>), dim3((unsigned)blocks),
+                       dim3(512), wl, as_stream(stream), g, (const double*)x_unf, (const u16*)dy,
+                       ws);
+  else if (wg2_on() && small)
+    hipLaunchKernelGGL((stem_wgrad2_kernel<7, 7, 2, 2, u16>), dim3((unsigned)blocks), dim3(512), wl,
                        as_stream(stream), g, (const u16*)x_unf, (const u16*)dy, ws);
   else
     hipLaunchKernelGGL((stem_wgrad_kernel<7, 7, 2, 2>), dim3((unsigned)blocks), dim3(512), wl,
@@ -940,28 +1140,38 @@ int wgrad(const mmad_conv_desc* d, const void* x_unf, const void* dy, float* ws,
   return launch_status();
 }
 
+template <typename TI>
+int launch_fwdq(const StemG& g, int blocks, const void* x, const void* w_packed,
+                const float* bias, void* y, float* stats, void* stream) {
+  constexpr size_t lds = LDSQ;
+  static const bool okq =
+      hipFuncSetAttribute((const void*)stem_fwdq_kernel<false, TI>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess &&
+      hipFuncSetAttribute((const void*)stem_fwdq_kernel<true, TI>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  if (!okq) return MMAD_EUNSUPPORTED;
+  if (bias != nullptr)
+    hipLaunchKernelGGL((stem_fwdq_kernel<true, TI>), dim3((unsigned)blocks), dim3(512), lds,
+                       as_stream(stream), g, (const TI*)x, (const u16*)w_packed, bias, (u16*)y,
+                       stats);
+  else
+    hipLaunchKernelGGL((stem_fwdq_kernel<false, TI>), dim3((unsigned)blocks), dim3(512), lds,
+                       as_stream(stream), g, (const TI*)x, (const u16*)w_packed, bias, (u16*)y,
+                       stats);
+  return launch_status();
+}
+
 int fwd(const mmad_conv_desc* d, const void* x_unf, const void* w_packed, const float* bias,
-        void* y, float* stats, void* stream) {
+        void* y, float* stats, void* stream, int in_dtype) {
   StemG g;
   int blocks;
   size_t lds;
-  if (quad_on() && geom_for(d, g, blocks, lds, true)) {
-    static const bool okq =
-        hipFuncSetAttribute((const void*)stem_fwdq_kernel<false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, LDSQ) == hipSuccess &&
-        hipFuncSetAttribute((const void*)stem_fwdq_kernel<true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, LDSQ) == hipSuccess;
-    if (!okq) return MMAD_EUNSUPPORTED;
-    if (bias != nullptr)
-      hipLaunchKernelGGL(stem_fwdq_kernel<true>, dim3((unsigned)blocks), dim3(512), LDSQ,
-                         as_stream(stream), g, (const u16*)x_unf, (const u16*)w_packed, bias,
-                         (u16*)y, stats);
-    else
-      hipLaunchKernelGGL(stem_fwdq_kernel<false>, dim3((unsigned)blocks), dim3(512), LDSQ,
-                         as_stream(stream), g, (const u16*)x_unf, (const u16*)w_packed, bias,
-                         (u16*)y, stats);
-    return launch_status();
+  if (in_dtype >= 0) {
+    if (!raw_ok(d, in_dtype) || !geom_for(d, g, blocks, lds, true)) return MMAD_EUNSUPPORTED;
+    return launch_fwdq<double>(g, blocks, x_unf, w_packed, bias, y, stats, stream);
   }
+  if (quad_on() && geom_for(d, g, blocks, lds, true))
+    return launch_fwdq<u16>(g, blocks, x_unf, w_packed, bias, y, stats, stream);
   if (!geom_for(d, g, blocks, lds)) return MMAD_EUNSUPPORTED;
   static const bool ok = hipFuncSetAttribute((const void*)stem_fwd_kernel<7, 7, 2, 2>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -91,6 +91,9 @@ WGRAD_STREAM = os.environ.get("MMAD_WGRAD_STREAM", "0") == "1"
 # (2148-2167 vs 2196-2205 vol/s, interleaved on one MI355X): the reduction blocks wait for
 # CU slots behind the one-block-per-CU conv kernels and then delay the next one.  Off.
 REDUCE_STREAM = os.environ.get("MMAD_REDUCE_STREAM", "0") == "1"
+# MMAD_STEM_RAW=0: the Cin-1 stem reads the W-unfolded copy written by
+# mmad_conv_unfold_input instead of the raw volume (A/B switch; mmad_conv3d_fwd_raw)
+STEM_RAW = os.environ.get("MMAD_STEM_RAW", "1") != "0"
 _SIDE = {}
 _JOIN_PENDING = set()
 
@@ -315,6 +318,7 @@ class _Conv3dFn(torch.autograd.Function):
         lib = L.load()
         ctx.ci_real = d.ci
         wsrc = weight
+        ctx.raw = None
         if isinstance(x, StackedVolumes) or (d.ci > 1 and d.ci % 8):
             # Cin in 2..7 (early fusion): channel-padded operand and weight (fusion.hip);
             # the zero lanes contribute exact zeros
@@ -335,9 +339,15 @@ class _Conv3dFn(torch.autograd.Function):
                 raise L.MMADError("conv3d: gradient w.r.t. a 1-channel raw input volume "
                                   "is not supported (the input never needs one)")
             xc = x.contiguous()
-            src = torch.empty(lib.mmad_conv_unfolded_elems(d), dtype=cdtype, device=x.device)
-            L.call("mmad_conv_unfold_input", d, L.dtype_code(xc.dtype), L.ptr(xc), dt,
-                   L.ptr(src), L.stream())
+            in_dt = L.dtype_code(xc.dtype)
+            if STEM_RAW and lib.mmad_stem_raw_ok(d, in_dt, dt) == 1:
+                # the stem kernels unfold the raw volume's rows themselves (no unfolded copy)
+                src, ctx.raw = xc, in_dt
+            else:
+                src = torch.empty(lib.mmad_conv_unfolded_elems(d), dtype=cdtype,
+                                  device=x.device)
+                L.call("mmad_conv_unfold_input", d, in_dt, L.ptr(xc), dt, L.ptr(src),
+                       L.stream())
         else:
             _check_vol(x, cdtype)
             src = x
@@ -354,8 +364,12 @@ class _Conv3dFn(torch.autograd.Function):
         if probe is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        L.call("mmad_conv3d_fwd", d, dt, L.ptr(src), L.ptr(wp), L.ptr(b), L.ptr(y),
-               L.ptr(stats), L.stream())
+        if ctx.raw is not None:
+            L.call("mmad_conv3d_fwd_raw", d, ctx.raw, L.ptr(src), dt, L.ptr(wp), L.ptr(b),
+                   L.ptr(y), L.ptr(stats), L.stream())
+        else:
+            L.call("mmad_conv3d_fwd", d, dt, L.ptr(src), L.ptr(wp), L.ptr(b), L.ptr(y),
+                   L.ptr(stats), L.stream())
         if probe is not None:
             e1.record()
             probe.append((e0, e1))
@@ -427,7 +441,18 @@ def _wgrad(ctx, d, dt, src, gy, weight, wparam=None, rside=None):
     db = torch.empty(d.co, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
     # a dW that autograd will not adopt as-is (an existing .grad it is added into, or the
     # channel-padded copy cut below) is read on the main stream: no split then
-    if rside is not None and not padded and (wparam is None or wparam.grad is None):
+    raw = getattr(ctx, "raw", None)
+    if raw is not None:
+        # the raw stem input (see _Conv3dFn.forward); slab reduction on rside when given
+        split = rside is not None and (wparam is None or wparam.grad is None)
+        L.call("mmad_conv3d_wgrad_raw", d, raw, L.ptr(src), dt, L.ptr(gy), L.ptr(dw),
+               L.ptr(db), L.ptr(ws), L.stream(), rside.cuda_stream if split else None)
+        if split:
+            for t in (ws, gy, dw, db):
+                if t is not None:
+                    t.record_stream(rside)
+            _queue_join(torch.cuda.current_stream(), rside)
+    elif rside is not None and not padded and (wparam is None or wparam.grad is None):
         L.call("mmad_conv3d_wgrad_split", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db),
                L.ptr(ws), L.stream(), rside.cuda_stream)
         # what the side stream reads or writes stays allocated until it has run; dW (and
