@@ -634,256 +634,6 @@ __global__ __launch_bounds__(NTHR) void patchz_bs_kernel(PZ g, const u16* __rest
   box(g.tps - 1, std::false_type{});
 }
 
-// ---- weight-stationary form, 32x32 tiles, one wave per SIMD (round 4, patchz_bs 2) -------
-// The 8-wave stationary form above needs one 1-KiB A-fragment read per 16x16x32 MFMA, as
-// many LDS cycles as MFMA cycles.  Here 4 waves (one per SIMD) each hold 32 output channels
-// x 32 input channels of all 27 taps as 32x32x16 B operands (54 x 16 B per lane) and the
-// 256 x 32 accumulators of the box (8 32x32 tiles, 128 registers); one A read (32 rows x 16
-// channels) feeds one 32-cycle MFMA: LDS at half the MFMA rate.  Wave (cb, kh): channels
-// 32 cb .., K half kh; the halves meet in the epilogue (kh = 0 finalises rows 0..127, kh = 1
-// rows 128..255).  Planes as above, 4 DMA pieces per wave per plane, and a swizzle that keeps
-// the 32-row fragment reads conflict-free: LDS chunk slot = source chunk ^ ((4 py + px / 2) & 7)
-// for image row (py, px).
-constexpr int H_NTHR = 256, H_NW = 4;
-constexpr int H_NA = 8;                          // A fragments in flight
-constexpr int H_STEPS = TAPS * 2 * 8;            // (tap, K16 step, fragment)
-constexpr int H_XB = 256 * CROW;                 // exchange / staging region
-constexpr int H_RED = RING_OFF;
-constexpr int H_XOFF = H_RED + 2 * 64 * 4;
-constexpr int H_LDS = H_XOFF + H_XB;
-static_assert(H_LDS <= 160 * 1024, "LDS budget");
-constexpr int H_EPI_ST = 8;                      // output stores per wave per box
-constexpr int H_STATS_ST = 2;
-
-__device__ __forceinline__ int h_swz(int py, int px) { return (4 * py + (px >> 1)) & 7; }
-
-__global__ __launch_bounds__(H_NTHR) void patchz_h_kernel(PZ g, const u16* __restrict__ src,
-                                                          const u16* __restrict__ wgt,
-                                                          const float* __restrict__ bias,
-                                                          u16* __restrict__ dst,
-                                                          float* __restrict__ stats) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-  const int item = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  int t1 = item;
-  const int seg = t1 % g.nseg;
-  t1 /= g.nseg;
-  const int nt = t1 % g.nbn;
-  t1 /= g.nbn;
-  const int bx = t1 % g.ntx;
-  t1 /= g.ntx;
-  const int by = t1 % g.nty;
-  const int n = t1 / g.nty;
-  const int y0 = by * 8, x0 = bx * 8, n0 = nt * 64;
-  const int zs = seg * g.tps * 4;
-  const int HW = g.H * g.W;
-  const int cb = wave & 1, kh = wave >> 1;
-  const int l32 = lane & 31, hh = lane >> 5;
-
-  // ---- weights: B[t][s] = W[n0 + 32 cb + l32][tap t][32 kh + 16 s + 8 hh .. + 7]
-  bf16x8 B[TAPS][2];
-  {
-    const u16* wl = wgt + (int64_t)(n0 + cb * 32 + l32) * g.Kpad + kh * 32 + hh * 8;
-#pragma unroll
-    for (int t = 0; t < TAPS; ++t)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-        B[t][s2] = *reinterpret_cast<const bf16x8*>(wl + t * 64 + s2 * 16);
-  }
-
-  // ---- plane DMA: plane q -> slot q % 8; pieces p = wave + 4 h (13 pieces of 8 rows)
-  const u16* __restrict__ srcn = src + (int64_t)n * g.D * HW * 64;
-  int poff[4];
-  uint32_t pdst[4];
-  {
-    const int lrow = lane >> 3;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int p = min(wave + H_NW * h, 12);
-      const int r = p * 8 + lrow;
-      const int px = r % PX, py = r / PX;
-      const int y = y0 - 1 + py, x = x0 - 1 + px;
-      const bool in = r < PROWS && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
-      const int chunk = (lane & 7) ^ h_swz(py, px);
-      poff[h] = in ? (y * g.W + x) * 64 + chunk * 8 : -1;
-      pdst[h] = p * 1024;
-    }
-  }
-  auto issue_plane = [&](int q) __attribute__((always_inline)) {
-    const int z = zs - 1 + q;
-    const bool zin = (unsigned)z < (unsigned)g.D;
-    const u16* base = srcn + (int64_t)(zin ? z : 0) * HW * 64;
-    char* slot = smem + (q & (NPS - 1)) * PSLOT;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const void* p = (zin && poff[h] >= 0) ? (const void*)(base + poff[h]) : (const void*)g_zero16z;
-      glds16_asm(p, lds_addr_of(slot + pdst[h]));
-    }
-  };
-
-  // ---- A fragment F (rows 32 F ..: plane F >> 1, y rows 4 (F & 1) + l32 >> 3, x = l32 & 7)
-  // of tap T, K16 step S2: lane address = slot + aoff[kx][S2][ky & 1] + row immediate
-  // (the swizzle depends on py only through py & 1 and 4 (F & 1) is even)
-  uint32_t aoff[3][2][2];
-  {
-    const int yl = l32 >> 3, xl = l32 & 7;
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int kyp = 0; kyp < 2; ++kyp)
-          aoff[kx][s2][kyp] =
-              (uint32_t)((yl * PX + xl + kx) * RB +
-                         (((4 * kh + 2 * s2 + hh) ^ h_swz(yl + kyp, xl + kx)) << 4));
-  }
-  typedef float f32x16 __attribute__((ext_vector_type(16)));
-  f32x16 acc[8];
-  bf16x8 a[H_NA];
-  auto rd = [&](auto sc, int q0) __attribute__((always_inline)) {
-    constexpr int S = decltype(sc)::value;
-    if constexpr (S < H_STEPS) {
-      constexpr int T = S / 16, S2 = (S / 8) % 2, F = S % 8;
-      constexpr int kz = T / 9, ky = (T / 3) % 3, kx = T % 3;
-      int pbase = __builtin_amdgcn_readfirstlane(((q0 + (F >> 1) + kz) & (NPS - 1)) * PSLOT);
-      asm volatile("" : "+s"(pbase));
-      a[S % H_NA] = *reinterpret_cast<const bf16x8*>(smem + pbase + aoff[kx][S2][ky & 1] +
-                                                     (4 * (F & 1) + ky) * PX * RB);
-    }
-  };
-  auto mm = [&](auto sc) __attribute__((always_inline)) {
-    constexpr int S = decltype(sc)::value;
-    constexpr int T = S / 16, S2 = (S / 8) % 2, F = S % 8;
-    acc[F] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[S % H_NA], B[T][S2], acc[F], 0, 0, 0);
-  };
-
-  const float bv = bias != nullptr ? bias[n0 + cb * 32 + l32] : 0.f;
-  const int64_t nbase = (int64_t)n * g.D;
-  f32x16* xb = reinterpret_cast<f32x16*>(smem + H_XOFF);
-  float* red = reinterpret_cast<float*>(smem + H_RED);
-
-  auto epilogue = [&](int i) __attribute__((always_inline)) {
-    const int z0 = zs + 4 * i;
-    // K-half exchange: kh = 0 finalises tiles 0..3, kh = 1 tiles 4..7; two rounds of 2 tiles
-#pragma unroll
-    for (int rnd = 0; rnd < 2; ++rnd) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const f32x16 v = kh == 0 ? acc[4 + 2 * rnd + j] : acc[2 * rnd + j];
-        f32x4* sl = reinterpret_cast<f32x4*>(xb + ((wave * 2 + j) * 64 + lane));
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sl[q] = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
-      }
-      lds_sync();
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int pw = wave ^ 2;                          // partner: same cb, other kh
-        const f32x4* sl = reinterpret_cast<const f32x4*>(xb + ((pw * 2 + j) * 64 + lane));
-        f32x16 v;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x4 u = sl[q];
-          v[4 * q] = u[0]; v[4 * q + 1] = u[1]; v[4 * q + 2] = u[2]; v[4 * q + 3] = u[3];
-        }
-        if (kh == 0) acc[2 * rnd + j] += v;
-        else acc[4 + 2 * rnd + j] += v;
-      }
-      lds_sync();
-    }
-    float cs = 0.f, cq = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f32x16 v = kh == 0 ? acc[j] : acc[4 + j];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float o = v[r] + bv;
-        cs += o;
-        cq += o * o;
-      }
-    }
-    if (stats != nullptr) {
-      cs += __shfl_xor(cs, 32, 64);
-      cq += __shfl_xor(cq, 32, 64);
-      if (kh == 1 && hh == 0) {
-        red[cb * 64 + l32] = cs;
-        red[cb * 64 + 32 + l32] = cq;
-      }
-    }
-    // stage the bf16 box [256][CROW]: tile F rows 32 F + (r & 3) + 8 (r >> 2) + 4 hh
-    u16* ctile = reinterpret_cast<u16*>(xb);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f32x16 v = kh == 0 ? acc[j] : acc[4 + j];
-      const int f = kh * 4 + j;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = f * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        ctile[row * (CROW / 2) + cb * 32 + l32] = f2bf(v[r] + bv);
-      }
-    }
-    lds_sync();
-    if (stats != nullptr && kh == 0) {
-      const int64_t mt = (((int64_t)n * (g.D / 4) + z0 / 4) * g.nty + by) * g.ntx + bx;
-      float* srow = stats + (mt * 2) * g.Nd + n0 + cb * 32 + l32;
-      st_f32(srow, cs + red[cb * 64 + l32]);             // fixed order: deterministic
-      st_f32(srow + g.Nd, cq + red[cb * 64 + 32 + l32]);
-    }
-#pragma unroll
-    for (int h = 0; h < H_EPI_ST; ++h) {                 // 256 rows x 8 chunks / 256 threads
-      const int qd = tid + H_NTHR * h;
-      const int v = qd >> 3, c8 = qd & 7;
-      const int64_t vox =
-          ((nbase + z0 + (v >> 6)) * g.H + y0 + ((v >> 3) & 7)) * g.W + x0 + (v & 7);
-      const int64_t o = vox * g.Nd + n0 + c8 * 8;
-      u32x4 val = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
-                                                  v * CROW + c8 * 16);
-      if (g.res != nullptr || g.relu) val = epi_res_relu(val, g.res ? g.res + o : nullptr, g.relu);
-      st_u32x4(dst + o, val);
-    }
-  };
-
-  for (int q = 0; q < 6; ++q) issue_plane(q);
-
-  auto box = [&](int i, auto nextc) __attribute__((always_inline)) {
-    constexpr bool NEXT = decltype(nextc)::value;
-    const int q0 = 4 * i;
-    if (i == 0) {
-      wait_vm_lgkm0<0>();
-    } else if (stats != nullptr && kh == 0) {
-      wait_vm_lgkm0<H_EPI_ST + H_STATS_ST>();
-    } else {
-      wait_vm_lgkm0<H_EPI_ST>();
-    }
-    raw_barrier();
-    if constexpr (NEXT) {
-      issue_plane(q0 + 6);
-      issue_plane(q0 + 7);
-    }
-#pragma unroll
-    for (int f = 0; f < 8; ++f) acc[f] = f32x16{};
-    [&]<int... S>(std::integer_sequence<int, S...>) {
-      (rd(std::integral_constant<int, S>{}, q0), ...);
-    }(std::make_integer_sequence<int, H_NA>{});
-    [&]<int... S>(std::integer_sequence<int, S...>) {
-      ((mm(std::integral_constant<int, S>{}), rd(std::integral_constant<int, S + H_NA>{}, q0),
-        __builtin_amdgcn_sched_barrier(0),
-        (S == 9 * 16 - 1 || S == 18 * 16 - 1)
-            ? [&] {
-                lds_sync();
-                if constexpr (NEXT) issue_plane(q0 + (S == 9 * 16 - 1 ? 8 : 9));
-              }()
-            : void()),
-       ...);
-    }(std::make_integer_sequence<int, H_STEPS>{});
-    epilogue(i);
-  };
-  for (int i = 0; i + 1 < g.tps; ++i) box(i, std::true_type{});
-  box(g.tps - 1, std::false_type{});
-}
-
 std::atomic<int> g_patchz_mode{-1};
 int patchz_mode() {
   int v = g_patchz_mode.load(std::memory_order_relaxed);
@@ -896,8 +646,8 @@ int patchz_mode() {
   return v;
 }
 
-// MMAD_PATCHZ_BS: 1 the weight-stationary 16x16 kernel, 2 the weight-stationary 32x32 one,
-// 0 (default) the weight-streaming one;
+// MMAD_PATCHZ_BS: 1 the weight-stationary kernel, 0 (default) the weight-streaming one
+// (a 32x32-tile stationary form was tried in round 4: it spilled and was dropped);
 // mmad_set_kernel_variant("patchz_bs", v) at run time
 std::atomic<int> g_bs_mode{-1};
 int bs_mode() {
@@ -964,9 +714,7 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
       hipFuncSetAttribute((const void*)patchz_conv_kernel,
                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS) == hipSuccess &&
       hipFuncSetAttribute((const void*)patchz_bs_kernel,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, BS_LDS) == hipSuccess &&
-      hipFuncSetAttribute((const void*)patchz_h_kernel,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, H_LDS) == hipSuccess;
+                          hipFuncAttributeMaxDynamicSharedMemorySize, BS_LDS) == hipSuccess;
   if (!attr) return MMAD_EUNSUPPORTED;
   PZ g{};
   g.nb = q.nb; g.Nd = q.Nd; g.Kpad = q.Kpad; g.D = q.Dd; g.H = q.Hd; g.W = q.Wd;
@@ -976,11 +724,7 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
   g.res = reinterpret_cast<const u16*>(q.res);
   g.relu = q.relu;
   const int64_t items = (int64_t)q.nb * g.nty * g.ntx * g.nbn * g.nseg;
-  if (bs_mode() == 2)
-    hipLaunchKernelGGL(patchz_h_kernel, dim3((unsigned)items), dim3(H_NTHR), H_LDS,
-                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                       stats);
-  else if (bs_on())
+  if (bs_on())
     hipLaunchKernelGGL(patchz_bs_kernel, dim3((unsigned)items), dim3(NTHR), BS_LDS,
                        as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
                        stats);
