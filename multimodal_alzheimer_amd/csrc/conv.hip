@@ -1294,11 +1294,15 @@ int igemm_bm(int64_t m, const Geom& g) {
 
 struct WSplit { int bmw, splits, m_per_split; };
 // 256 x 256 wgrad tiles (8 waves, one block per CU): measured 10-15 % SLOWER than the
-// 4-wave 128 x 128 tiles on layer3/4 (more split-K slabs, less latency hiding), so off
-// unless MMAD_WGRAD_BIG=1 (kept as the A/B switch for tuning).
+// 4-wave 128 x 128 tiles at config 2's 16^3 grids (M = 32768: more split-K slabs, less latency
+// hiding) but faster at config 5's 20^3 grids (M = 64000 at batch 8: the config-5 step
+// 158 -> 161 triples/s, r04q), so used from M = 49152 on.  MMAD_WGRAD_BIG: 0 never, 1
+// wherever the tile fits, unset the M rule.
 int wgrad_big(const Geom& g, int dtype) {
-  static const int v = [] { const char* e = getenv("MMAD_WGRAD_BIG"); return e ? atoi(e) : 0; }();
-  return (v && dtype == MMAD_BF16 && g.Nd % 256 == 0 && g.K >= 256 * 8) ? v : 0;
+  static const int v = [] { const char* e = getenv("MMAD_WGRAD_BIG"); return e ? atoi(e) : -1; }();
+  if (dtype != MMAD_BF16 || g.Nd % 256 || g.K < 256 * 8) return 0;
+  if (v >= 0) return v;
+  return g.M >= 49152 ? 1 : 0;
 }
 
 WSplit wgrad_split(const Geom& g, int dtype) {

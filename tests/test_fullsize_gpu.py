@@ -70,10 +70,18 @@ LAYERS = [
 ]
 
 
-@pytest.mark.parametrize("case", LAYERS, ids=[c[0] for c in LAYERS])
+# BASELINE config 5's 20^3 layers (160^3 input, batch 8): the implicit-GEMM route and, from
+# M = 49152 output voxels on, the 256 x 256 weight-gradient tiles
+LAYERS5 = [
+    ("c5.layer3.conv2", 8, 256, 20, 256, 3, 1, 2, 2),
+    ("c5.layer4.conv2", 8, 512, 20, 512, 3, 1, 4, 4),
+]
+
+
+@pytest.mark.parametrize("case", LAYERS + LAYERS5, ids=[c[0] for c in LAYERS + LAYERS5])
 def test_config2_conv_layer_full_size(case):
     name, n, ci, s_in, co, k, st, p, dl = case
-    g = _gen(100 + LAYERS.index(case))
+    g = _gen(100 + (LAYERS + LAYERS5).index(case))
     x = (torch.rand((n, ci, s_in, s_in, s_in), generator=g, device=DEV) * 2 - 1).to(BF)
     w = (torch.rand((co, ci, k, k, k), generator=g, device=DEV) * 2 - 1) * (3.0 / (ci * k ** 3)) ** 0.5
     xg = x.contiguous(memory_format=CL).requires_grad_(True)
