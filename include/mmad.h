@@ -111,6 +111,30 @@ int mmad_conv_pack_dual_batch(int dtype, int njobs, const mmad_pack_dual* jobs_d
                               int64_t total_tiles, void* stream);
 int mmad_conv_pack_batch(int dtype, int njobs, const mmad_pack_job* jobs_device,
                          int64_t total_tiles, void* stream);
+/* Adam step fused with the bf16 repack (the captured training step's optimizer,
+ * fused_optim.AdamRepack): replaces torch.optim.Adam(fused=True, capturable=True).step()
+ * over the reference's param groups (anat_cnn.py:111-126; amsgrad, maximize and grad
+ * scaling off) -- bit-identical update of param, exp_avg, exp_avg_sq and the device step --
+ * and, for a job with w_fwd != NULL, the updated conv weight's two bf16 layouts exactly as
+ * mmad_conv_pack_dual_batch writes them (co, ci multiples of 16, taps <= 27).  Blocks
+ * [tile0, tile0 + ntiles) of the launch belong to a job (jobs sorted by tile0; ntiles from
+ * mmad_adam_job_tiles); `arrivals` is one zeroed int per job, left zeroed. */
+typedef struct mmad_adam_job {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* step;                  /* the parameter's device step counter (float32) */
+  const float* lr;              /* the group's device learning rate (float32) */
+  double beta1, beta2, eps, weight_decay;
+  void* w_fwd;                  /* NULL: no repack */
+  void* w_dgrad;
+  int32_t co, ci, taps, flip;
+  int64_t numel, tile0, ntiles;
+} mmad_adam_job;
+int64_t mmad_adam_job_tiles(const mmad_adam_job* job);
+int mmad_adam_repack(int njobs, const mmad_adam_job* jobs_device, int64_t total_tiles,
+                     int* arrivals, void* stream);
 int64_t mmad_conv_unfolded_elems(const mmad_conv_desc* d);
 int mmad_conv_unfold_input(const mmad_conv_desc* d, int in_dtype, const void* x,
                            int dtype, void* x_unf, void* stream);
@@ -295,6 +319,26 @@ int mmad_gap_bwd(int dtype, int n, int64_t s, int c, const float* dy, void* dx, 
  * that take a pooled gradient as broadcast rows (g_rows in mmad_bn_bwd_reduce2 / _apply2). */
 int mmad_gap_bwd_compact(int dtype, int n, int64_t s, int c, const float* dy, void* dx,
                          void* stream);
+/* conv_seg's AdaptiveAvgPool3d(1) -> Flatten -> Linear (-> ReLU) (anat_cnn.py:66-76) as two
+ * launches forward and one backward, same values as mmad_gap_fwd_ws + mmad_linear_fwd and
+ * mmad_linear_bwd_ex + mmad_gap_bwd_compact:
+ *   mmad_gap_partial   the GAP's first level into ws (mmad_gap_fwd_ws_elems floats):
+ *                      mmad_gap_parts(n, s, c) = P partial rows per sample (the pooled means
+ *                      themselves when P == 1);
+ *   mmad_gap_linear_fwd  folds them (xs[b][i] = pooled input, kept for the backward) and
+ *                      y = act(xs W^T + bias);
+ *   mmad_linear_gap_bwd  dW, dbias and the input gradient as compact GAP rows
+ *                      rows[b][i] = (rows_dtype) ((dy' W)[b][i] / s), dy' = ReLU-masked dy
+ *                      (ymask = the forward output, or NULL). */
+int mmad_gap_parts(int n, int64_t s, int c);
+int mmad_gap_partial(int dtype, int n, int64_t s, int c, const void* x, float* ws,
+                     void* stream);
+int mmad_gap_linear_fwd(int b, int in, int out, int parts, int64_t s, const float* ws,
+                        const float* w, const float* bias, int relu, float* xs, float* y,
+                        void* stream);
+int mmad_linear_gap_bwd(int b, int in, int out, int64_t s, const float* x, const float* w,
+                        const float* dy, const float* ymask, int rows_dtype, void* rows,
+                        float* dw, float* dbias, void* stream);
 
 /* ---- fusion / classifier MLP head (fp32) ----------------------------------------
  * nn.Linear (+ReLU) of conv_seg (anat_cnn.py:68-76), reduce_dim_mri / stage2out /

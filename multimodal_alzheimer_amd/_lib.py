@@ -44,6 +44,16 @@ class PackDual(C.Structure):
                 [(n, C.c_int32) for n in ("co", "ci", "taps", "flip")] + [("tile0", C.c_int64)])
 
 
+class AdamJob(C.Structure):
+    """mirror of mmad_adam_job (include/mmad.h)"""
+    _fields_ = ([(n, C.c_void_p) for n in ("param", "grad", "exp_avg", "exp_avg_sq", "step",
+                                           "lr")] +
+                [(n, C.c_double) for n in ("beta1", "beta2", "eps", "weight_decay")] +
+                [("w_fwd", C.c_void_p), ("w_dgrad", C.c_void_p)] +
+                [(n, C.c_int32) for n in ("co", "ci", "taps", "flip")] +
+                [(n, C.c_int64) for n in ("numel", "tile0", "ntiles")])
+
+
 class BnFin(C.Structure):
     """mirror of mmad_bn_fin (include/mmad.h)"""
     _fields_ = ([("nparts", C.c_int32)] +
@@ -57,6 +67,7 @@ class BnFin(C.Structure):
 _P = C.POINTER(ConvDesc)
 _PJ = C.POINTER(PackJob)
 _PD = C.POINTER(PackDual)
+_PA = C.POINTER(AdamJob)
 _SIGS = {
     "mmad_abi_version": (_i32, []),
     "mmad_strerror": (C.c_char_p, [_i32]),
@@ -69,6 +80,8 @@ _SIGS = {
     "mmad_conv_pack_dual_job": (_i32, [_P, _i32, _vp, _vp, _vp, _i64, _PD]),
     "mmad_pack_dual_tiles": (_i64, [_PD]),
     "mmad_conv_pack_dual_batch": (_i32, [_i32, _i32, _vp, _i64, _vp]),
+    "mmad_adam_job_tiles": (_i64, [_PA]),
+    "mmad_adam_repack": (_i32, [_i32, _vp, _i64, _vp, _vp]),
     "mmad_conv_unfolded_elems": (_i64, [_P]),
     "mmad_conv_unfold_input": (_i32, [_P, _i32, _vp, _i32, _vp, _vp]),
     "mmad_conv3d_stats_rows": (_i64, [_P, _i32]),
@@ -117,6 +130,12 @@ _SIGS = {
     "mmad_gap_fwd_ws": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp, _vp]),
     "mmad_gap_bwd": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
     "mmad_gap_bwd_compact": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "mmad_gap_parts": (_i32, [_i32, _i64, _i32]),
+    "mmad_gap_partial": (_i32, [_i32, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "mmad_gap_linear_fwd": (_i32, [_i32, _i32, _i32, _i32, _i64, _vp, _vp, _vp, _i32, _vp,
+                                   _vp, _vp]),
+    "mmad_linear_gap_bwd": (_i32, [_i32, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp,
+                                   _vp, _vp]),
     "mmad_linear_fwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp]),
     "mmad_linear_bwd": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_linear_bwd_ex": (_i32, [_i32, _i32, _i32] + [_vp] * 8),

@@ -68,6 +68,77 @@ __global__ void linear_bwd_kernel(int B, int IN, int OUT, int nbx, const float* 
   }
 }
 
+// AdaptiveAvgPool3d(1) -> Flatten -> Linear (-> ReLU) forward in one launch after the GAP's
+// partial sums (mmad_gap_partial): x[b][i] = (sum over p, in order, of ws[b][p][i]) / S --
+// gap_fold_kernel's arithmetic -- or ws[b][i] itself when P == 1; the waves of o == 0 keep x
+// (xs, the linear backward's input); then linear_fwd_kernel's dot product
+__global__ __launch_bounds__(256) void gap_linear_fwd_kernel(int B, int IN, int OUT, int P,
+                                                             float Sf,
+                                                             const float* __restrict__ ws,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ bias,
+                                                             int relu, float* __restrict__ xs,
+                                                             float* __restrict__ y) {
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (wid >= B * OUT) return;
+  const int b = wid / OUT, o = wid % OUT;
+  float s = 0.f;
+  for (int i = lane; i < IN; i += 64) {
+    float xi;
+    if (P > 1) {
+      float acc = 0.f;
+#pragma unroll 16
+      for (int p = 0; p < P; ++p) acc += ws[((int64_t)b * P + p) * IN + i];
+      xi = acc / Sf;
+    } else {
+      xi = ws[(int64_t)b * IN + i];
+    }
+    if (o == 0) xs[(int64_t)b * IN + i] = xi;
+    s += xi * w[(int64_t)o * IN + i];
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    if (bias) s += bias[o];
+    y[(int64_t)b * OUT + o] = relu ? fmaxf(s, 0.f) : s;
+  }
+}
+
+// its backward in one launch: linear_bwd_kernel with the input gradient leaving as the GAP's
+// compact rows, rows[b][i] = T(dx[b][i] * inv) (gap_bwd_kernel's arithmetic, inv = 1 / S)
+template <typename T>
+__global__ void linear_gap_bwd_kernel(int B, int IN, int OUT, int nbx, float inv,
+                                      const float* __restrict__ x, const float* __restrict__ w,
+                                      const float* __restrict__ dy,
+                                      const float* __restrict__ ymask, T* __restrict__ rows,
+                                      float* __restrict__ dw, float* __restrict__ dbias) {
+  auto gval = [&](int64_t k) {
+    const float v = dy[k];
+    return ymask == nullptr || ymask[k] > 0.f ? v : 0.f;
+  };
+  if ((int)blockIdx.x < nbx) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= (int64_t)B * IN) return;
+    const int i = (int)(t % IN);
+    const int b = (int)(t / IN);
+    float s = 0.f;
+    for (int o = 0; o < OUT; ++o) s += gval((int64_t)b * OUT + o) * w[(int64_t)o * IN + i];
+    Elt<T>::st(rows, t, s * inv);
+    return;
+  }
+  const int64_t t = (blockIdx.x - nbx) * (int64_t)blockDim.x + threadIdx.x;
+  if (dw != nullptr && t < (int64_t)OUT * IN) {
+    const int o = (int)(t / IN), i = (int)(t % IN);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += gval((int64_t)b * OUT + o) * x[(int64_t)b * IN + i];
+    dw[t] = s;
+  }
+  if (dbias && t < OUT) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += gval((int64_t)b * OUT + t);
+    dbias[t] = s;
+  }
+}
+
 struct ColList {
   const float* p[8];
   float* q[8];
@@ -352,6 +423,39 @@ int mmad_linear_bwd_ex(int b, int in, int out, const float* x, const float* w, c
   if (nbx + nbw == 0) return MMAD_OK;
   hipLaunchKernelGGL(linear_bwd_kernel, dim3((unsigned)(nbx + nbw)), dim3(256), 0,
                      as_stream(stream), b, in, out, nbx, x, w, dy, ymask, dx, dw, dbias);
+  return launch_status();
+}
+
+int mmad_gap_linear_fwd(int b, int in, int out, int parts, int64_t s, const float* ws,
+                        const float* w, const float* bias, int relu, float* xs, float* y,
+                        void* stream) {
+  if (b <= 0 || in <= 0 || out <= 0 || parts <= 0 || s <= 0) return MMAD_EBADSHAPE;
+  if (!ws || !w || !xs || !y) return MMAD_ENULL;
+  hipLaunchKernelGGL(gap_linear_fwd_kernel, dim3((unsigned)cdiv((int64_t)b * out, 4)), dim3(256),
+                     0, as_stream(stream), b, in, out, parts, (float)s, ws, w, bias, relu, xs, y);
+  return launch_status();
+}
+
+int mmad_linear_gap_bwd(int b, int in, int out, int64_t s, const float* x, const float* w,
+                        const float* dy, const float* ymask, int rows_dtype, void* rows,
+                        float* dw, float* dbias, void* stream) {
+  if (b <= 0 || in <= 0 || out <= 0 || s <= 0) return MMAD_EBADSHAPE;
+  if (!dy) return MMAD_ENULL;
+  if (rows && !w) return MMAD_ENULL;
+  if ((dw || dbias) && (!x || !dw)) return MMAD_ENULL;
+  if (rows && rows_dtype != MMAD_BF16 && rows_dtype != MMAD_F32) return MMAD_EBADDTYPE;
+  const int nbx = rows ? (int)cdiv((int64_t)b * in, 256) : 0;
+  const int nbw = (dw || dbias) ? (int)cdiv(std::max<int64_t>((int64_t)out * in, out), 256) : 0;
+  if (nbx + nbw == 0) return MMAD_OK;
+  const float inv = 1.f / (float)s;
+  if (rows_dtype == MMAD_BF16)
+    hipLaunchKernelGGL(linear_gap_bwd_kernel<u16>, dim3((unsigned)(nbx + nbw)), dim3(256), 0,
+                       as_stream(stream), b, in, out, nbx, inv, x, w, dy, ymask, (u16*)rows, dw,
+                       dbias);
+  else
+    hipLaunchKernelGGL(linear_gap_bwd_kernel<float>, dim3((unsigned)(nbx + nbw)), dim3(256), 0,
+                       as_stream(stream), b, in, out, nbx, inv, x, w, dy, ymask, (float*)rows, dw,
+                       dbias);
   return launch_status();
 }
 

@@ -1124,6 +1124,32 @@ int mmad_gap_fwd_ws(int dtype, int n, int64_t s, int c, const void* x, float* y,
   return MMAD_EBADDTYPE;
 }
 
+int mmad_gap_parts(int n, int64_t s, int c) {
+  if (n <= 0 || s <= 0 || c <= 0) return -1;
+  return gap_parts(n, s, c);
+}
+
+// the first level of mmad_gap_fwd_ws only: ws[n][P][c] raw partial sums (P = mmad_gap_parts
+// > 1), or the pooled means ws[n][c] when P == 1; mmad_gap_linear_fwd folds them
+int mmad_gap_partial(int dtype, int n, int64_t s, int c, const void* x, float* ws,
+                     void* stream) {
+  if (n <= 0 || s <= 0 || c <= 0) return MMAD_EBADSHAPE;
+  if (!x || !ws) return MMAD_ENULL;
+  const int P = gap_parts(n, s, c);
+  const int cb = std::min(c, 256);
+  hipStream_t st = as_stream(stream);
+  if (dtype == MMAD_BF16 && c % Chunk<u16>::N == 0 && cb % Chunk<u16>::N == 0)
+    hipLaunchKernelGGL((gap_fwd_kernel<u16, Chunk<u16>::N>), dim3((unsigned)cdiv(c, cb),
+                       (unsigned)n, (unsigned)P), dim3(1024), 0, st, s, c, cb, (const u16*)x, ws);
+  else if (dtype == MMAD_F32 && c % Chunk<float>::N == 0 && cb % Chunk<float>::N == 0)
+    hipLaunchKernelGGL((gap_fwd_kernel<float, Chunk<float>::N>), dim3((unsigned)cdiv(c, cb),
+                       (unsigned)n, (unsigned)P), dim3(1024), 0, st, s, c, cb, (const float*)x,
+                       ws);
+  else
+    return MMAD_EUNSUPPORTED;
+  return launch_status();
+}
+
 int mmad_gap_bwd(int dtype, int n, int64_t s, int c, const float* dy, void* dx, void* stream) {
   if (n <= 0 || s <= 0 || c <= 0) return MMAD_EBADSHAPE;
   if (!dy || !dx) return MMAD_ENULL;

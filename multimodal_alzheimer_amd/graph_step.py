@@ -48,7 +48,7 @@ depends on it:
 """
 import torch
 
-from . import volume_ops
+from . import fused_optim, volume_ops
 
 COLLECTIVES = ("staged", "after", "inside")
 # Captures check only this thread's calls: ProcessGroupNCCL's watchdog thread polls the events
@@ -133,9 +133,9 @@ class StagedBackward:
                 self._rec[k].append(alias)
         return hook
 
-    def run(self, k, loss=None):
+    def run(self, k, loss=None, seed=None):
         if k == 0:
-            roots, grads = [loss], None
+            roots, grads = [loss], (None if seed is None else [seed])
         else:
             roots, grads = self._grads
         nxt = [t for t in self._rec[k] if t.requires_grad] if k < self.n - 1 else []
@@ -196,13 +196,51 @@ class GraphedTrainStep:
                                  "from backward_stages(model, cuts)")
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        loss = None
         with torch.cuda.stream(side):
             for _ in range(warmup):
-                self._eager()
+                loss = self._eager()
         torch.cuda.current_stream().wait_stream(side)
+        # the backward's seed gradient (d loss / d loss = 1) made before capture, so the
+        # captured step has no fill kernel for it
+        self._one = None if loss is None else torch.ones_like(loss)
         optimizer.zero_grad(set_to_none=True)
         self.graphs = []
         self.opt_graph = None
+        # Adam fused with the weight repack (fused_optim): the captured forwards skip the
+        # dual-layout repack, which the captured optimizer step writes for the next replay
+        self.fused = None
+        if fused_optim.supported(optimizer) and fused_optim.state_ready(optimizer):
+            self.fused = fused_optim.AdamRepack(optimizer, fused_optim.pack_plans(model))
+            self.fused.prepare(dev)
+            self.fused.set_external(True)
+        try:
+            self._capture(model, optimizer, reducer, staged)
+        finally:
+            if self.fused is not None:
+                self.fused.set_external(False)
+        if self.fused is not None:
+            self.fused.commit()              # the job table (gradient addresses from capture)
+            self.fused.refresh()             # packed weights of the current fp32 weights
+        self._versions = self._param_versions()
+        self.graph = self.graphs[0]
+        # keep the graph-owned output buffers, not their autograd graph: a live grad_fn chain
+        # would keep every parameter's AccumulateGrad node (created on the capture stream)
+        # alive, and later eager steps would reuse those nodes across streams
+        self.out = {k: v.detach() if torch.is_tensor(v) else v for k, v in self.out.items()}
+
+    def _opt_step(self):
+        if self.fused is not None:
+            self.fused.step()
+        else:
+            self.optimizer.step()
+
+    def _param_versions(self):
+        if self.fused is None:
+            return None
+        return tuple(p._version for p in self.fused.params())
+
+    def _capture(self, model, optimizer, reducer, staged):
         if self.mode in ("staged", "after"):
             reducer.defer = True             # the capture's hooks (if any) only count
             try:
@@ -210,7 +248,7 @@ class GraphedTrainStep:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                         self.out = model.general_step(self.static, 0, "train")
-                        self.out["loss"].backward()
+                        self.out["loss"].backward(self._one)
                     self.graphs.append(g)
                 else:
                     staged.arm()
@@ -218,7 +256,7 @@ class GraphedTrainStep:
                         g = torch.cuda.CUDAGraph()
                         with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                             self.out = model.general_step(self.static, 0, "train")
-                            staged.run(0, self.out["loss"])
+                            staged.run(0, self.out["loss"], self._one)
                     finally:
                         staged.disarm()
                     self.graphs.append(g)
@@ -235,28 +273,25 @@ class GraphedTrainStep:
             self.opt_graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.opt_graph, pool=self.graphs[0].pool(),
                                   capture_error_mode=_CAPTURE_MODE):
-                optimizer.step()
+                self._opt_step()
         else:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                 self.out = model.general_step(self.static, 0, "train")
-                self.out["loss"].backward()
+                self.out["loss"].backward(self._one)
                 if reducer is not None:
                     reducer.finish()
-                optimizer.step()
+                self._opt_step()
             self.graphs.append(g)
-        self.graph = self.graphs[0]
-        # keep the graph-owned output buffers, not their autograd graph: a live grad_fn chain
-        # would keep every parameter's AccumulateGrad node (created on the capture stream)
-        # alive, and later eager steps would reuse those nodes across streams
-        self.out = {k: v.detach() if torch.is_tensor(v) else v for k, v in self.out.items()}
 
     def _eager(self):
         self.optimizer.zero_grad(set_to_none=True)
-        self.model.general_step(self.static, 0, "train")["loss"].backward()
+        loss = self.model.general_step(self.static, 0, "train")["loss"]
+        loss.backward()
         if self.reducer is not None:
             self.reducer.finish()
         self.optimizer.step()
+        return loss.detach()
 
     def __call__(self, batch=None):
         """Replay one step; ``batch`` (same keys / shapes) is copied into the graph's input
@@ -266,6 +301,11 @@ class GraphedTrainStep:
             for k, v in batch.items():
                 if torch.is_tensor(v):
                     self.static[k].copy_(v, non_blocking=True)
+        if self.fused is not None:
+            v = self._param_versions()
+            if v != self._versions:          # weights changed outside the graph: repack
+                self.fused.refresh()
+                self._versions = v
         if self.mode is None or self.mode == "inside":
             self.graph.replay()
         else:

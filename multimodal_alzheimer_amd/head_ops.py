@@ -11,6 +11,7 @@ import ctypes as C
 import torch
 
 from . import _lib as L
+from . import volume_ops as V
 from .volume_ops import cast, grad_slot
 
 
@@ -58,6 +59,66 @@ class _LinearFn(torch.autograd.Function):
 
 def linear(x, weight, bias=None, relu=False):
     return _LinearFn.apply(x, weight, bias, bool(relu))
+
+
+class _GapLinearFn(torch.autograd.Function):
+    """conv_seg's AdaptiveAvgPool3d(1) -> Flatten -> Linear (-> ReLU) (anat_cnn.py:66-76):
+    forward = the GAP's partial sums + one launch folding them into the pooled rows and
+    applying the linear (mmad_gap_linear_fwd); backward = one launch for dW, dbias and the
+    input gradient as the GAP's compact broadcast rows (mmad_linear_gap_bwd).  Same values
+    as volume_ops.global_avg_pool + flatten + linear, two launches fewer."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu):
+        V._check_vol(x)
+        lib = L.load()
+        n, c = x.shape[:2]
+        s = x.numel() // (n * c)
+        parts = lib.mmad_gap_parts(n, s, c)
+        ws = torch.empty(lib.mmad_gap_fwd_ws_elems(n, s, c), dtype=torch.float32,
+                         device=x.device)
+        L.call("mmad_gap_partial", L.dtype_code(x.dtype), n, s, c, L.ptr(x), L.ptr(ws),
+               L.stream())
+        n_out = weight.shape[0]
+        w = weight.detach().contiguous()
+        bb = None if bias is None else bias.detach().contiguous()
+        xs = torch.empty((n, c), dtype=torch.float32, device=x.device)
+        y = torch.empty((n, n_out), dtype=torch.float32, device=x.device)
+        L.call("mmad_gap_linear_fwd", n, c, n_out, parts, s, L.ptr(ws), L.ptr(w), L.ptr(bb),
+               int(relu), L.ptr(xs), L.ptr(y), L.stream())
+        ctx.save_for_backward(xs, weight, y if relu else None)
+        ctx.has_bias = bias is not None
+        ctx.relu = relu
+        ctx.params = (weight, bias)
+        ctx.shape, ctx.dtype, ctx.s = tuple(x.shape), x.dtype, s
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        xs, weight, y = ctx.saved_tensors
+        g = g.contiguous()
+        if g.dtype != torch.float32:
+            g = cast(g, torch.float32)
+        n, c = xs.shape
+        n_out = weight.shape[0]
+        rows = dw = db = None
+        if ctx.needs_input_grad[0]:
+            rows = torch.empty((n, c), dtype=ctx.dtype, device=g.device)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dw = grad_slot(ctx.params[0], tuple(weight.shape), g.device)
+            if ctx.has_bias:
+                db = grad_slot(ctx.params[1], (n_out,), g.device)
+        L.call("mmad_linear_gap_bwd", n, c, n_out, ctx.s, L.ptr(xs), L.ptr(weight.detach()),
+               L.ptr(g), L.ptr(y if ctx.relu else None), L.dtype_code(ctx.dtype), L.ptr(rows),
+               L.ptr(dw), L.ptr(db), L.stream())
+        dx = None if rows is None else rows.view(n, c, 1, 1, 1).expand(ctx.shape)
+        return dx, (dw if ctx.needs_input_grad[1] else None), db, None
+
+
+def gap_linear(x, weight, bias=None, relu=False):
+    """linear(flatten(global_avg_pool(x)), weight, bias, relu) for an NDHWC volume x whose
+    GAP gradient may be handed on as broadcast rows (volume_ops.GAP_BCAST)."""
+    return _GapLinearFn.apply(x, weight, bias, bool(relu))
 
 
 class _ConcatFn(torch.autograd.Function):

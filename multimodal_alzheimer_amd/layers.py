@@ -7,6 +7,8 @@ Only ``forward`` changes.  Volumes flow as channels_last_3d tensors (NDHWC); the
 dtype of a conv is its ``compute_dtype`` attribute (float32 parity mode by default,
 bfloat16 throughput mode), and every downstream op follows the dtype of its input.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -117,6 +119,13 @@ class Sequential(nn.Sequential):
         while i < len(mods):
             m = mods[i]
             nxt = mods[i + 1] if i + 1 < len(mods) else None
+            # AdaptiveAvgPool3d(1) -> Flatten -> Linear (-> ReLU): head_ops.gap_linear
+            k = _gap_linear_run(mods, i, x)
+            if k:
+                lin = mods[i + 2]
+                x = head_ops.gap_linear(x, lin.weight, lin.bias, relu=k == 4)
+                i += k
+                continue
             if (type(m) is Linear and type(nxt) is ReLU and x.dim() == 2 and
                     not (m._forward_hooks or m._forward_pre_hooks or nxt._forward_hooks or
                          nxt._forward_pre_hooks)):
@@ -126,6 +135,30 @@ class Sequential(nn.Sequential):
             x = m(x)
             i += 1
         return x
+
+
+# MMAD_GAP_LINEAR=0: conv_seg's pool -> flatten -> linear run module by module (A/B)
+GAP_LINEAR = os.environ.get("MMAD_GAP_LINEAR", "1") != "0"
+
+
+def _gap_linear_run(mods, i, x):
+    """modules fused by head_ops.gap_linear at position i (4 with a trailing ReLU, 3
+    without), else 0"""
+    if not (GAP_LINEAR and volume_ops.GAP_BCAST) or i + 2 >= len(mods):
+        return 0
+    m, f, lin = mods[i], mods[i + 1], mods[i + 2]
+    if not (type(m) is AdaptiveAvgPool3d and type(f) is nn.Flatten and type(lin) is Linear):
+        return 0
+    if _triple(m.output_size) != (1, 1, 1) or f.start_dim != 1 or f.end_dim != -1:
+        return 0
+    if not (isinstance(x, torch.Tensor) and x.dim() == 5 and x.is_cuda and
+            x.dtype in (torch.float32, torch.bfloat16)):
+        return 0
+    relu = i + 3 < len(mods) and type(mods[i + 3]) is ReLU
+    used = mods[i:i + (4 if relu else 3)]
+    if any(u._forward_hooks or u._forward_pre_hooks for u in used):
+        return 0
+    return 4 if relu else 3
 
 
 class Dropout(nn.Dropout):

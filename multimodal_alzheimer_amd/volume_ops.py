@@ -207,6 +207,10 @@ class PackPlan:
             host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
             self.table = host.to(convs[0].weight.device)
         self.nduals, self.dtiles = len(duals), dtiles
+        self.duals = duals
+        # external: the dual repack is produced elsewhere (fused_optim.AdamRepack writes it
+        # at the end of the previous captured step), so run() skips that launch
+        self.external = False
         if duals:
             raw = (L.PackDual * len(duals))(*duals)
             host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
@@ -223,11 +227,16 @@ class PackPlan:
         if self.njobs:
             L.call("mmad_conv_pack_batch", self.dt, self.njobs, L.ptr(self.table), self.tiles,
                    L.stream())
+        if not self.external:
+            self.run_duals()
+        for conv, _, wp, wpt in self.entries:
+            conv._prepacked = (wp, wpt) if wp is not None or wpt is not None else None
+
+
+    def run_duals(self):
         if self.nduals:
             L.call("mmad_conv_pack_dual_batch", self.dt, self.nduals, L.ptr(self.dtable),
                    self.dtiles, L.stream())
-        for conv, _, wp, wpt in self.entries:
-            conv._prepacked = (wp, wpt) if wp is not None or wpt is not None else None
 
 
 def prepack(module, convs=None):
