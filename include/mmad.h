@@ -326,7 +326,7 @@ int mmad_gap_bwd_compact(int dtype, int n, int64_t s, int c, const float* dy, vo
  *                      mmad_gap_parts(n, s, c) = P partial rows per sample (the pooled means
  *                      themselves when P == 1);
  *   mmad_gap_linear_fwd  folds them (xs[b][i] = pooled input, kept for the backward) and
- *                      y = act(xs W^T + bias);
+ *                      y = act(xs W^T + bias) (in <= 4096, else MMAD_EUNSUPPORTED);
  *   mmad_linear_gap_bwd  dW, dbias and the input gradient as compact GAP rows
  *                      rows[b][i] = (rows_dtype) ((dy' W)[b][i] / s), dy' = ReLU-masked dy
  *                      (ymask = the forward output, or NULL). */

@@ -69,21 +69,17 @@ __global__ void linear_bwd_kernel(int B, int IN, int OUT, int nbx, const float* 
 }
 
 // AdaptiveAvgPool3d(1) -> Flatten -> Linear (-> ReLU) forward in one launch after the GAP's
-// partial sums (mmad_gap_partial): x[b][i] = (sum over p, in order, of ws[b][p][i]) / S --
-// gap_fold_kernel's arithmetic -- or ws[b][i] itself when P == 1; the waves of o == 0 keep x
-// (xs, the linear backward's input); then linear_fwd_kernel's dot product
-__global__ __launch_bounds__(256) void gap_linear_fwd_kernel(int B, int IN, int OUT, int P,
-                                                             float Sf,
-                                                             const float* __restrict__ ws,
-                                                             const float* __restrict__ w,
-                                                             const float* __restrict__ bias,
-                                                             int relu, float* __restrict__ xs,
-                                                             float* __restrict__ y) {
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (wid >= B * OUT) return;
-  const int b = wid / OUT, o = wid % OUT;
-  float s = 0.f;
-  for (int i = lane; i < IN; i += 64) {
+// partial sums (mmad_gap_partial).  Block b: x[b][i] = (sum over p, in order, of
+// ws[b][p][i]) / S -- gap_fold_kernel's arithmetic -- or ws[b][i] itself when P == 1, kept in
+// LDS and in xs (the linear backward's input); then each wave takes outputs o = wave, wave +
+// 8, ... with linear_fwd_kernel's dot product (lane-strided sum + wave_sum)
+constexpr int GL_THREADS = 512, GL_MAX_IN = 4096;
+__global__ __launch_bounds__(GL_THREADS) void gap_linear_fwd_kernel(
+    int IN, int OUT, int P, float Sf, const float* __restrict__ ws, const float* __restrict__ w,
+    const float* __restrict__ bias, int relu, float* __restrict__ xs, float* __restrict__ y) {
+  __shared__ float xsh[GL_MAX_IN];
+  const int b = blockIdx.x;
+  for (int i = threadIdx.x; i < IN; i += GL_THREADS) {
     float xi;
     if (P > 1) {
       float acc = 0.f;
@@ -93,13 +89,19 @@ __global__ __launch_bounds__(256) void gap_linear_fwd_kernel(int B, int IN, int 
     } else {
       xi = ws[(int64_t)b * IN + i];
     }
-    if (o == 0) xs[(int64_t)b * IN + i] = xi;
-    s += xi * w[(int64_t)o * IN + i];
+    xsh[i] = xi;
+    xs[(int64_t)b * IN + i] = xi;
   }
-  s = wave_sum(s);
-  if (lane == 0) {
-    if (bias) s += bias[o];
-    y[(int64_t)b * OUT + o] = relu ? fmaxf(s, 0.f) : s;
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int o = wave; o < OUT; o += GL_THREADS / 64) {
+    float s = 0.f;
+    for (int i = lane; i < IN; i += 64) s += xsh[i] * w[(int64_t)o * IN + i];
+    s = wave_sum(s);
+    if (lane == 0) {
+      if (bias) s += bias[o];
+      y[(int64_t)b * OUT + o] = relu ? fmaxf(s, 0.f) : s;
+    }
   }
 }
 
@@ -430,9 +432,10 @@ int mmad_gap_linear_fwd(int b, int in, int out, int parts, int64_t s, const floa
                         const float* w, const float* bias, int relu, float* xs, float* y,
                         void* stream) {
   if (b <= 0 || in <= 0 || out <= 0 || parts <= 0 || s <= 0) return MMAD_EBADSHAPE;
+  if (in > GL_MAX_IN) return MMAD_EUNSUPPORTED;
   if (!ws || !w || !xs || !y) return MMAD_ENULL;
-  hipLaunchKernelGGL(gap_linear_fwd_kernel, dim3((unsigned)cdiv((int64_t)b * out, 4)), dim3(256),
-                     0, as_stream(stream), b, in, out, parts, (float)s, ws, w, bias, relu, xs, y);
+  hipLaunchKernelGGL(gap_linear_fwd_kernel, dim3((unsigned)b), dim3(GL_THREADS), 0,
+                     as_stream(stream), in, out, parts, (float)s, ws, w, bias, relu, xs, y);
   return launch_status();
 }
 

@@ -149,6 +149,8 @@ def _gap_linear_run(mods, i, x):
     m, f, lin = mods[i], mods[i + 1], mods[i + 2]
     if not (type(m) is AdaptiveAvgPool3d and type(f) is nn.Flatten and type(lin) is Linear):
         return 0
+    if lin.in_features > 4096:                  # mmad_gap_linear_fwd's pooled-row buffer
+        return 0
     if _triple(m.output_size) != (1, 1, 1) or f.start_dim != 1 or f.end_dim != -1:
         return 0
     if not (isinstance(x, torch.Tensor) and x.dim() == 5 and x.is_cuda and

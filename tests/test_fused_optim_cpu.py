@@ -1,0 +1,77 @@
+"""Host side of the fused Adam + repack (fused_optim, mmad_adam_job_tiles): which optimizer
+configurations it takes over (torch.optim.Adam with fused=True only -- anything whose
+arithmetic the kernel does not restate keeps optimizer.step()), and the launch geometry of a
+job (no GPU needed)."""
+import ctypes
+
+import pytest
+import torch
+
+from multimodal_alzheimer_amd import _lib as L
+from multimodal_alzheimer_amd import fused_optim as F
+
+
+def _p(*shape):
+    return torch.nn.Parameter(torch.zeros(shape))
+
+
+def _adam(**kw):
+    # fused / capturable only gate the device kernels; on CPU the flags are just recorded
+    opt = torch.optim.Adam([_p(4)], lr=1e-3)
+    for g in opt.param_groups:
+        g.update({"fused": True, "amsgrad": False, "maximize": False, "differentiable": False})
+        g.update(kw)
+    return opt
+
+
+def test_supported_configurations():
+    assert F.supported(_adam())
+    assert not F.supported(_adam(fused=False))
+    assert not F.supported(_adam(fused=None))
+    assert not F.supported(_adam(amsgrad=True))
+    assert not F.supported(_adam(maximize=True))
+    assert not F.supported(_adam(betas=(torch.tensor(0.9), 0.999)))
+    assert not F.supported(torch.optim.AdamW([_p(4)]))
+    assert not F.supported(torch.optim.SGD([_p(4)], lr=0.1))
+
+    class Stepped(torch.optim.Adam):
+        def step(self, closure=None):
+            return super().step(closure)
+    opt = Stepped([_p(4)])
+    opt.param_groups[0]["fused"] = True
+    assert not F.supported(opt)            # an overridden step() is not restated
+
+
+def test_state_ready_needs_one_step():
+    p = _p(3)
+    p.grad = torch.ones(3)
+    opt = torch.optim.Adam([p], lr=1e-3)
+    assert not F.state_ready(opt)
+    opt.step()
+    assert F.state_ready(opt)
+
+
+def test_job_tiles():
+    lib = L.load()
+    j = L.AdamJob()
+    j.numel = 4096
+    assert lib.mmad_adam_job_tiles(ctypes.byref(j)) == 1
+    j.numel = 4097
+    assert lib.mmad_adam_job_tiles(ctypes.byref(j)) == 2
+    j.numel = 0
+    assert lib.mmad_adam_job_tiles(ctypes.byref(j)) == 0
+    j.numel = 64 * 128 * 27
+    j.w_fwd, j.w_dgrad = 16, 16          # any non-NULL: a dual-repack job
+    j.co, j.ci, j.taps = 64, 128, 27
+    assert lib.mmad_adam_job_tiles(ctypes.byref(j)) == 4 * 8      # 16 co x 16 ci tiles
+
+
+def test_struct_layout_matches_header():
+    # 6 pointers, 4 doubles, 2 pointers, 4 int32, 3 int64
+    assert ctypes.sizeof(L.AdamJob) == 6 * 8 + 4 * 8 + 2 * 8 + 4 * 4 + 3 * 8
+
+
+def test_launch_rejects_null_table():
+    lib = L.load()
+    assert lib.mmad_adam_repack(1, None, 1, None, None) != 0
+    assert lib.mmad_adam_repack(0, None, 0, None, None) == 0       # nothing to do
