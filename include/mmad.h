@@ -116,9 +116,11 @@ int mmad_conv_pack_batch(int dtype, int njobs, const mmad_pack_job* jobs_device,
  * over the reference's param groups (anat_cnn.py:111-126; amsgrad, maximize and grad
  * scaling off) -- bit-identical update of param, exp_avg, exp_avg_sq and the device step --
  * and, for a job with w_fwd != NULL, the updated conv weight's two bf16 layouts exactly as
- * mmad_conv_pack_dual_batch writes them (co, ci multiples of 16, taps <= 27).  Blocks
- * [tile0, tile0 + ntiles) of the launch belong to a job (jobs sorted by tile0; ntiles from
- * mmad_adam_job_tiles); `arrivals` is one zeroed int per job, left zeroed. */
+ * mmad_conv_pack_dual_batch writes them (co, ci multiples of 16, taps <= 27); for a job with
+ * unf_kw > 0 (the Cin = 1 stem: co rows, taps = kd*kh, kpad) the unfolded forward layout
+ * mmad_conv_pack_weight writes into w_fwd.  Blocks [tile0, tile0 + ntiles) of the launch
+ * belong to a job (jobs sorted by tile0; ntiles from mmad_adam_job_tiles); `arrivals` is one
+ * zeroed int per job, left zeroed. */
 typedef struct mmad_adam_job {
   float* param;
   const float* grad;
@@ -130,6 +132,7 @@ typedef struct mmad_adam_job {
   void* w_fwd;                  /* NULL: no repack */
   void* w_dgrad;
   int32_t co, ci, taps, flip;
+  int32_t unf_kw, kpad;         /* unfolded stem repack (unf_kw > 0) */
   int64_t numel, tile0, ntiles;
 } mmad_adam_job;
 int64_t mmad_adam_job_tiles(const mmad_adam_job* job);

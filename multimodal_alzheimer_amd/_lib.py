@@ -50,7 +50,7 @@ class AdamJob(C.Structure):
                                            "lr")] +
                 [(n, C.c_double) for n in ("beta1", "beta2", "eps", "weight_decay")] +
                 [("w_fwd", C.c_void_p), ("w_dgrad", C.c_void_p)] +
-                [(n, C.c_int32) for n in ("co", "ci", "taps", "flip")] +
+                [(n, C.c_int32) for n in ("co", "ci", "taps", "flip", "unf_kw", "kpad")] +
                 [(n, C.c_int64) for n in ("numel", "tile0", "ntiles")])
 
 

@@ -77,9 +77,10 @@ __global__ __launch_bounds__(NT) void adam_repack_kernel(const mmad_adam_job* __
   float* __restrict__ Q = jb.exp_avg_sq;
   const bool vec = al16(P) && al16(G) && al16(M) && al16(Q);
 
-  if (jb.w_fwd == nullptr) {
-    // plain job: elements [t * FLAT, (t + 1) * FLAT)
-    const int64_t e0 = t * FLAT, e1 = min(jb.numel, e0 + FLAT);
+  if (jb.w_fwd == nullptr || jb.unf_kw > 0) {
+    // plain job: elements [t * FLAT, (t + 1) * FLAT); the unfolded stem is one block over
+    // the whole weight
+    const int64_t e0 = t * FLAT, e1 = jb.unf_kw > 0 ? jb.numel : min(jb.numel, e0 + FLAT);
     if (vec && ((e1 - e0) & 3) == 0) {
       for (int64_t e = e0 + threadIdx.x * 4; e < e1; e += NT * 4) {
         const f32x4 p = *reinterpret_cast<const f32x4*>(P + e);
@@ -104,6 +105,23 @@ __global__ __launch_bounds__(NT) void adam_repack_kernel(const mmad_adam_job* __
         P[e] = adam_elem(k, P[e], G[e], m, v);
         M[e] = m;
         Q[e] = v;
+      }
+    }
+    if (jb.unf_kw > 0) {
+      // pack_weight_kernel's unfolded Cin = 1 forward layout (mode 2) from the updated
+      // weights this block just wrote: row co, k = (kd * KH + kh) * 8 + kw, zero for kw >=
+      // unf_kw and k >= taps * 8
+      __syncthreads();
+      u16* wf = reinterpret_cast<u16*>(jb.w_fwd);
+      const int kp = jb.kpad, K = jb.taps * 8, kw = jb.unf_kw;
+      for (int64_t idx = threadIdx.x; idx < (int64_t)jb.co * kp; idx += NT) {
+        const int r = (int)(idx / kp), kk = (int)(idx % kp);
+        float v = 0.f;
+        if (kk < K) {
+          const int tap = kk >> 3, c = kk & 7;
+          if (c < kw) v = P[((int64_t)r * jb.taps + tap) * kw + c];
+        }
+        Elt<u16>::st(wf, idx, v);
       }
     }
   } else {
@@ -190,6 +208,7 @@ extern "C" {
 
 int64_t mmad_adam_job_tiles(const mmad_adam_job* job) {
   if (job == nullptr || job->numel <= 0) return 0;
+  if (job->w_fwd != nullptr && job->unf_kw > 0) return 1;
   if (job->w_fwd != nullptr) return (int64_t)(job->co / 16) * (job->ci / 16);
   return (job->numel + FLAT - 1) / FLAT;
 }

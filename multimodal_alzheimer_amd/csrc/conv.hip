@@ -1374,6 +1374,12 @@ int big_min_k() {
   static const int v = [] { const char* e = getenv("MMAD_IGEMM_BIG_MINK"); return e ? atoi(e) : 1024; }();
   return v;
 }
+// fewest 256 x 256 tiles for the default big-tile rule (one per CU); MMAD_IGEMM_BIG_MINBLK
+// lowers it (A/B: config 5's 20^3 layer3, 250 tiles)
+int big_min_blocks() {
+  static const int v = [] { const char* e = getenv("MMAD_IGEMM_BIG_MINBLK"); return e ? atoi(e) : 256; }();
+  return v;
+}
 // ring depth of the default (4-wave) tiles: 3 (two stages of LDS-DMA in flight, still two
 // blocks per CU at 64 x 128 tiles) for strided forward convs with taps (those the stride-2
 // sub-patch kernel does not take: fp32, ragged grids), 2 elsewhere.  Measured in the
@@ -1393,7 +1399,7 @@ int big_cfg_for(const Geom& g, int dtype, int64_t m_max, int classes) {
                   // K is deep enough to amortise their epilogue (the 1x1x1 shortcut, K = 256,
                   // is epilogue-bound at one block per CU; MMAD_IGEMM_BIG_MINK=0 keeps them)
     return g.Nd % 256 == 0 && g.K >= big_min_k() &&
-                   cdiv(m_max, 256) * classes * (g.Nd / 256) >= 256 ? 2 : 0;
+                   cdiv(m_max, 256) * classes * (g.Nd / 256) >= big_min_blocks() ? 2 : 0;
   if (cfg == 4) return g.Nd % 128 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 128) >= 256 ? 4 : 0;
   if (cfg == 5 || cfg == 6)
     return g.Nd % 256 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 256) >= 256 ? cfg : 0;

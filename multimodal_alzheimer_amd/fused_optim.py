@@ -72,17 +72,19 @@ class AdamRepack:
         if not supported(optimizer):
             raise ValueError("AdamRepack: optimizer configuration not supported")
         self.optimizer = optimizer
-        self.plans = [p for p in plans if p.nduals]
+        self.plans = [p for p in plans if p.nduals or p.unfolds]
         self.table = None
         self.njobs = self.tiles = 0
         self._host = None
 
     def _jobs(self):
         lib = L.load()
-        dual = {}
+        dual, unf = {}, {}
         for plan in self.plans:
             for job in plan.duals:
                 dual[job.w] = job
+            for w, d, wp in plan.unfolds:
+                unf[w.data_ptr()] = (d, wp)
         jobs, tiles = [], 0
         for g in self.optimizer.param_groups:
             lr = g["lr"]
@@ -112,6 +114,12 @@ class AdamRepack:
                 if d is not None:
                     j.w_fwd, j.w_dgrad = d.w_fwd, d.w_dgrad
                     j.co, j.ci, j.taps, j.flip = d.co, d.ci, d.taps, d.flip
+                u = unf.get(p.data_ptr())
+                if u is not None:
+                    desc, wp = u
+                    j.w_fwd = wp.data_ptr()
+                    j.co, j.ci, j.taps = desc.co, 1, desc.kd * desc.kh
+                    j.unf_kw, j.kpad = desc.kw, wp.numel() // desc.co
                 j.numel = p.numel()
                 j.tile0 = tiles
                 j.ntiles = lib.mmad_adam_job_tiles(j)

@@ -169,9 +169,18 @@ class PackPlan:
         tiles = 0
         duals = []
         dtiles = 0
+        self.unfolds = []        # (weight, desc, forward buffer) of Cin = 1 stems
         for conv in convs:
             w = conv.weight
             d = _weight_desc(w, conv._stride3(), conv._pads(), conv._dilation3())
+            if d.ci == 1 and cdtype == torch.bfloat16:
+                # the stem's unfolded forward layout: packed here (one launch, as per call
+                # before) so a fused optimizer step can produce it instead (fused_optim)
+                wp = torch.empty(lib.mmad_conv_packed_elems(d, dt, 0), dtype=cdtype,
+                                 device=w.device)
+                self.unfolds.append((w, d, wp))
+                self.entries.append((conv, w.data_ptr(), wp, None))
+                continue
             if with_dgrad and cdtype == torch.bfloat16:
                 # both layouts from one read of the fp32 weight when the shapes allow it
                 nf = lib.mmad_conv_packed_elems(d, dt, 0)
@@ -234,9 +243,13 @@ class PackPlan:
 
 
     def run_duals(self):
+        """the repacks a fused optimizer step can take over (dual layouts, unfolded stems)"""
         if self.nduals:
             L.call("mmad_conv_pack_dual_batch", self.dt, self.nduals, L.ptr(self.dtable),
                    self.dtiles, L.stream())
+        for w, d, wp in self.unfolds:
+            L.call("mmad_conv_pack_weight", d, self.dt, L.ptr(w.detach()), L.ptr(wp), 0,
+                   L.stream())
 
 
 def prepack(module, convs=None):

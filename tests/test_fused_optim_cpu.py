@@ -64,11 +64,14 @@ def test_job_tiles():
     j.w_fwd, j.w_dgrad = 16, 16          # any non-NULL: a dual-repack job
     j.co, j.ci, j.taps = 64, 128, 27
     assert lib.mmad_adam_job_tiles(ctypes.byref(j)) == 4 * 8      # 16 co x 16 ci tiles
+    j.w_dgrad, j.unf_kw, j.co, j.ci, j.taps, j.kpad = None, 7, 64, 1, 49, 448
+    j.numel = 64 * 343
+    assert lib.mmad_adam_job_tiles(ctypes.byref(j)) == 1          # the stem: one block
 
 
 def test_struct_layout_matches_header():
-    # 6 pointers, 4 doubles, 2 pointers, 4 int32, 3 int64
-    assert ctypes.sizeof(L.AdamJob) == 6 * 8 + 4 * 8 + 2 * 8 + 4 * 4 + 3 * 8
+    # 6 pointers, 4 doubles, 2 pointers, 6 int32, 3 int64
+    assert ctypes.sizeof(L.AdamJob) == 6 * 8 + 4 * 8 + 2 * 8 + 6 * 4 + 3 * 8
 
 
 def test_launch_rejects_null_table():
