@@ -117,8 +117,8 @@ int mmad_conv_pack_batch(int dtype, int njobs, const mmad_pack_job* jobs_device,
  * scaling off) -- bit-identical update of param, exp_avg, exp_avg_sq and the device step --
  * and, for a job with w_fwd != NULL, the updated conv weight's two bf16 layouts exactly as
  * mmad_conv_pack_dual_batch writes them (co, ci multiples of 16, taps <= 27); for a job with
- * unf_kw > 0 (the Cin = 1 stem: co rows, taps = kd*kh, kpad) the unfolded forward layout
- * mmad_conv_pack_weight writes into w_fwd.  Blocks [tile0, tile0 + ntiles) of the launch
+ * unf_kw > 0 (the Cin = 1 stem: co rows, taps = kd*kh, kpad; one block per row) the
+ * unfolded forward layout mmad_conv_pack_weight writes into w_fwd.  Blocks [tile0, tile0 + ntiles) of the launch
  * belong to a job (jobs sorted by tile0; ntiles from mmad_adam_job_tiles); `arrivals` is one
  * zeroed int per job, left zeroed. */
 typedef struct mmad_adam_job {

@@ -78,10 +78,13 @@ __global__ __launch_bounds__(NT) void adam_repack_kernel(const mmad_adam_job* __
   const bool vec = al16(P) && al16(G) && al16(M) && al16(Q);
 
   if (jb.w_fwd == nullptr || jb.unf_kw > 0) {
-    // plain job: elements [t * FLAT, (t + 1) * FLAT); the unfolded stem is one block over
-    // the whole weight
-    const int64_t e0 = t * FLAT, e1 = jb.unf_kw > 0 ? jb.numel : min(jb.numel, e0 + FLAT);
-    if (vec && ((e1 - e0) & 3) == 0) {
+    // plain job: elements [t * FLAT, (t + 1) * FLAT); the unfolded stem: block t = output
+    // channel t (its taps * unf_kw weights, then its packed row)
+    const int64_t per = (int64_t)jb.taps * jb.unf_kw;
+    const int64_t e0 = jb.unf_kw > 0 ? t * per : t * FLAT;
+    const int64_t e1 = jb.unf_kw > 0 ? e0 + per : min(jb.numel, e0 + FLAT);
+    if (vec && ((e0 | e1) & 3) == 0) {
+#pragma unroll 2
       for (int64_t e = e0 + threadIdx.x * 4; e < e1; e += NT * 4) {
         const f32x4 p = *reinterpret_cast<const f32x4*>(P + e);
         const f32x4 g = *reinterpret_cast<const f32x4*>(G + e);
@@ -108,20 +111,19 @@ __global__ __launch_bounds__(NT) void adam_repack_kernel(const mmad_adam_job* __
       }
     }
     if (jb.unf_kw > 0) {
-      // pack_weight_kernel's unfolded Cin = 1 forward layout (mode 2) from the updated
-      // weights this block just wrote: row co, k = (kd * KH + kh) * 8 + kw, zero for kw >=
+      // pack_weight_kernel's unfolded Cin = 1 forward layout (mode 2) of row co = t from the
+      // updated weights this block just wrote: k = (kd * KH + kh) * 8 + kw, zero for kw >=
       // unf_kw and k >= taps * 8
       __syncthreads();
-      u16* wf = reinterpret_cast<u16*>(jb.w_fwd);
-      const int kp = jb.kpad, K = jb.taps * 8, kw = jb.unf_kw;
-      for (int64_t idx = threadIdx.x; idx < (int64_t)jb.co * kp; idx += NT) {
-        const int r = (int)(idx / kp), kk = (int)(idx % kp);
+      u16* wf = reinterpret_cast<u16*>(jb.w_fwd) + t * jb.kpad;
+      const int K = jb.taps * 8, kw = jb.unf_kw;
+      for (int kk = threadIdx.x; kk < jb.kpad; kk += NT) {
         float v = 0.f;
         if (kk < K) {
           const int tap = kk >> 3, c = kk & 7;
-          if (c < kw) v = P[((int64_t)r * jb.taps + tap) * kw + c];
+          if (c < kw) v = P[e0 + tap * kw + c];
         }
-        Elt<u16>::st(wf, idx, v);
+        Elt<u16>::st(wf, kk, v);
       }
     }
   } else {
@@ -132,6 +134,7 @@ __global__ __launch_bounds__(NT) void adam_repack_kernel(const mmad_adam_job* __
     const int co0 = (int)(t / nci) * 16, ci0 = (int)(t % nci) * 16;
     const int per_co = 16 * T, q4 = per_co / 4;
     if (vec) {
+#pragma unroll 2
       for (int e = threadIdx.x; e < 16 * q4; e += NT) {
         const int col = e / q4, rem0 = (e % q4) * 4;
         const int64_t o = ((int64_t)(co0 + col) * CI + ci0) * T + rem0;
@@ -208,7 +211,7 @@ extern "C" {
 
 int64_t mmad_adam_job_tiles(const mmad_adam_job* job) {
   if (job == nullptr || job->numel <= 0) return 0;
-  if (job->w_fwd != nullptr && job->unf_kw > 0) return 1;
+  if (job->w_fwd != nullptr && job->unf_kw > 0) return job->co;    // one block per row
   if (job->w_fwd != nullptr) return (int64_t)(job->co / 16) * (job->ci / 16);
   return (job->numel + FLAT - 1) / FLAT;
 }

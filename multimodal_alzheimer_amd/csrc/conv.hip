@@ -1374,10 +1374,11 @@ int big_min_k() {
   static const int v = [] { const char* e = getenv("MMAD_IGEMM_BIG_MINK"); return e ? atoi(e) : 1024; }();
   return v;
 }
-// fewest 256 x 256 tiles for the default big-tile rule (one per CU); MMAD_IGEMM_BIG_MINBLK
-// lowers it (A/B: config 5's 20^3 layer3, 250 tiles)
+// fewest 256 x 256 tiles for the default big-tile rule: 200, so config 5's 20^3 layer3
+// (64000 x 256, 250 tiles: 6 CUs idle) takes them too -- config-5 step 160.1 -> 165.8
+// triples/s (r04s); MMAD_IGEMM_BIG_MINBLK overrides (256: one tile per CU at least)
 int big_min_blocks() {
-  static const int v = [] { const char* e = getenv("MMAD_IGEMM_BIG_MINBLK"); return e ? atoi(e) : 256; }();
+  static const int v = [] { const char* e = getenv("MMAD_IGEMM_BIG_MINBLK"); return e ? atoi(e) : 200; }();
   return v;
 }
 // ring depth of the default (4-wave) tiles: 3 (two stages of LDS-DMA in flight, still two

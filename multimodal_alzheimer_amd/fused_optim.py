@@ -22,6 +22,7 @@ amsgrad / maximize / differentiable / decoupled weight decay off, float betas, f
 parameters and state, no gradient scaler.  ``supported(optimizer)`` says whether it
 applies; the caller keeps ``optimizer.step()`` otherwise."""
 import ctypes as C
+import inspect
 import os
 
 import torch
@@ -35,7 +36,10 @@ ENABLED = os.environ.get("MMAD_ADAM_REPACK", "1") != "0"
 def supported(optimizer):
     if not ENABLED or not isinstance(optimizer, torch.optim.Adam):
         return False
-    if isinstance(optimizer, torch.optim.AdamW) or type(optimizer).step is not torch.optim.Adam.step:
+    # (torch wraps a class's step with its profiling hook on first construction, on the
+    # subclass or on Adam itself: compare the functions underneath)
+    if isinstance(optimizer, torch.optim.AdamW) or \
+            inspect.unwrap(type(optimizer).step) is not inspect.unwrap(torch.optim.Adam.step):
         return False
     if getattr(optimizer, "grad_scale", None) is not None or \
             getattr(optimizer, "found_inf", None) is not None:

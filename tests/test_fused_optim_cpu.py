@@ -42,6 +42,21 @@ def test_supported_configurations():
     assert not F.supported(opt)            # an overridden step() is not restated
 
 
+def test_supported_whatever_was_constructed_first():
+    """torch hooks ``step`` on the first-constructed class (the subclass or Adam itself):
+    MergedAdam built before any plain Adam must still qualify (bench.py's order)."""
+    import subprocess
+    import sys
+    code = ("import torch\n"
+            "from multimodal_alzheimer_amd import fused_optim as F\n"
+            "from multimodal_alzheimer_amd.classifiers import MergedAdam\n"
+            "p = torch.nn.Parameter(torch.zeros(4))\n"
+            "o = MergedAdam([{'params': [p], 'lr': 1e-3}])\n"
+            "o.param_groups[0]['fused'] = True\n"
+            "assert F.supported(o)\n")
+    subprocess.run([sys.executable, "-c", code], check=True)
+
+
 def test_state_ready_needs_one_step():
     p = _p(3)
     p.grad = torch.ones(3)
@@ -66,7 +81,7 @@ def test_job_tiles():
     assert lib.mmad_adam_job_tiles(ctypes.byref(j)) == 4 * 8      # 16 co x 16 ci tiles
     j.w_dgrad, j.unf_kw, j.co, j.ci, j.taps, j.kpad = None, 7, 64, 1, 49, 448
     j.numel = 64 * 343
-    assert lib.mmad_adam_job_tiles(ctypes.byref(j)) == 1          # the stem: one block
+    assert lib.mmad_adam_job_tiles(ctypes.byref(j)) == 64         # the stem: a block per co
 
 
 def test_struct_layout_matches_header():

@@ -108,13 +108,19 @@ def traffic(fetch_dir, write_dir):
                           "scrubbed before each launch (cold)"}
 
 
+def _is_opt(name):
+    """a step's closing optimizer launch: torch's fused Adam (eager steps) or the captured
+    step's fused Adam + repack (csrc/adam.hip)"""
+    return ("FusedAdam" in name or "FusedOptimizerTensorListMetadata" in name or
+            "adam_repack_kernel" in name)
+
+
 def step(d):
     """Kernels of the last complete step, in launch order, with durations (us)."""
     rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # a step ends with the fused Adam launch(es); take the span between the last two
-    ends = [i for i, r in enumerate(rows) if "FusedAdam" in r["Kernel_Name"] or
-            "FusedOptimizerTensorListMetadata" in r["Kernel_Name"]]
+    ends = [i for i, r in enumerate(rows) if _is_opt(r["Kernel_Name"])]
     if len(ends) < 4:
         sel = rows
     else:
@@ -143,8 +149,7 @@ def stepavg(d, skip=2):
     (the first `skip` steps dropped), in launch order, plus the mean step sum."""
     rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ends = [i for i, r in enumerate(rows) if "FusedAdam" in r["Kernel_Name"] or
-            "FusedOptimizerTensorListMetadata" in r["Kernel_Name"]]
+    ends = [i for i, r in enumerate(rows) if _is_opt(r["Kernel_Name"])]
     groups, cur = [], [ends[0]]
     for e in ends[1:]:
         if e - cur[-1] <= 3:
