@@ -33,6 +33,7 @@
 //  * epilogue: bias, BN partial sums (sum, sum of squares per channel) from the fp32
 //    accumulators, bf16 tile transposed through LDS into 16-byte channel-vector stores.
 #include "common.h"
+#include "reduce.h"
 #include "patchconv.h"
 #include "pointwise.h"
 #include "stem.h"
@@ -813,102 +814,74 @@ __global__ void slab_group_sum_kernel(float* __restrict__ ws, int splits, int64_
   }
 }
 
-// Same sum, for the plain (not unfolded) layout: one block per (co, 64-channel slice);
-// slab reads run along ci, 16 bytes per lane (a wave covers 4 taps x 64 channels), and the
-// [ci][taps] result goes out through LDS as one contiguous run of the torch tensor.
+// The transposing slab reductions (bodies in reduce.h, shared with bn.hip, whose BN-backward
+// reduction launch can carry one as extra blocks: mmad_reduce_attach)
 __global__ __launch_bounds__(256) void wgrad_reduce_t_kernel(const float* __restrict__ ws,
                                                              float* __restrict__ dw, int splits,
                                                              int Nd, int K, int Cs, int taps) {
-  __shared__ float tile[64 * 33];
-  const int ct = min(64, Cs);                  // channels in this slice (Cs % 16 == 0)
-  const int q4 = ct / 4, tpi = 256 / q4;       // lanes per tap row, taps per block pass
-  const int co = blockIdx.y, c0 = blockIdx.x * ct;
-  const int e4 = threadIdx.x % q4, tg = threadIdx.x / q4;
-  const int64_t total = (int64_t)Nd * K;
-  const float* base = ws + (int64_t)co * K + c0 + e4 * 4;
-  for (int t = tg; t < taps; t += tpi) {
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-    for (int sp = 0; sp < splits; ++sp)
-      s += *reinterpret_cast<const f32x4*>(base + sp * total + (int64_t)t * Cs);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) tile[(e4 * 4 + q) * (taps + 1) + t] = s[q];
-  }
-  __syncthreads();
-  float* out = dw + ((int64_t)co * Cs + c0) * taps;
-  for (int l = threadIdx.x; l < ct * taps; l += 256)
-    out[l] = tile[(l / taps) * (taps + 1) + l % taps];
+  __shared__ float sm[mmad_reduce::SMEM_FLOATS];
+  mmad_reduce::t_body(ws, dw, splits, Nd, K, Cs, taps, blockIdx.x, blockIdx.y, sm);
 }
 
-// Same sum and layout for grids of few (co, channel-slice) blocks (the 64-channel layer1 and
-// layer2 shapes: 64-128 blocks for 128-69 slabs, ~3.5 TB/s): blockIdx.z takes a group of
-// taps, and each (tap, 4-channel) position's slabs are split over SP thread groups whose
-// partial sums are added in a fixed order (deterministic; the order differs from
-// wgrad_reduce_t_kernel's single chain only in fp32 rounding).
 __global__ __launch_bounds__(256) void wgrad_reduce_tz_kernel(const float* __restrict__ ws,
                                                               float* __restrict__ dw, int splits,
                                                               int Nd, int K, int Cs, int taps,
                                                               int tper) {
-  __shared__ f32x4 part[256];
-  __shared__ float tile[64 * 33];
-  const int ct = min(64, Cs);
-  const int q4 = ct / 4;
-  const int co = blockIdx.y, c0 = blockIdx.x * ct;
-  const int t0 = blockIdx.z * tper, nt = min(taps - t0, tper);
-  const int P = nt * q4;                         // (tap, 4-channel) positions of this block
-  const int SP = max(1, 256 / max(P, 1));        // slab groups per position
-  const int pos = threadIdx.x % P, sg = threadIdx.x / P;
-  const int64_t total = (int64_t)Nd * K;
-  if (nt <= 0) return;
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  const int e4 = pos % q4, tl = pos / q4;
-  if (sg < SP) {
-    const int per = (splits + SP - 1) / SP;
-    const int sp0 = sg * per, sp1 = min(splits, sp0 + per);
-    const float* base = ws + (int64_t)co * K + c0 + e4 * 4 + (int64_t)(t0 + tl) * Cs;
-#pragma unroll 8
-    for (int sp = sp0; sp < sp1; ++sp) s += *reinterpret_cast<const f32x4*>(base + sp * total);
-    part[threadIdx.x] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x < P) {
-    f32x4 a = part[threadIdx.x];
-    for (int g2 = 1; g2 < SP; ++g2) a += part[g2 * P + threadIdx.x];   // fixed order
-#pragma unroll
-    for (int q = 0; q < 4; ++q) tile[(e4 * 4 + q) * (tper + 1) + tl] = a[q];
-  }
-  __syncthreads();
-  // dW[co][c][t0 .. t0 + nt): runs of nt taps per channel
-  float* out = dw + ((int64_t)co * Cs + c0) * taps + t0;
-  for (int l = threadIdx.x; l < ct * nt; l += 256) {
-    const int c = l / nt, t = l % nt;
-    out[(int64_t)c * taps + t] = tile[c * (tper + 1) + t];
-  }
+  __shared__ float sm[mmad_reduce::SMEM_FLOATS];
+  mmad_reduce::tz_body(ws, dw, splits, Nd, K, Cs, taps, tper, blockIdx.x, blockIdx.y, blockIdx.z,
+                       sm);
 }
 
 // the transposing reduce: wgrad_reduce_t_kernel when its (channel slice, co) grid fills the
 // CUs, else wgrad_reduce_tz_kernel over tap groups (MMAD_REDUCE_TZ=0 keeps the former;
 // r03tz: layer1 16.4 / 16.2 -> 10.6 / 10.3 us, layer2.0.conv1 13.9 -> 11.5)
-int launch_reduce_t(const float* ws, float* dw, int splits, int Nd, int K, int Cs, int taps,
-                    hipStream_t st) {
+mmad_reduce_job plan_reduce_t(const float* ws, float* dw, int splits, int Nd, int K, int Cs,
+                              int taps) {
   static const bool tz_on = [] {
     const char* e = getenv("MMAD_REDUCE_TZ");
     return e == nullptr || atoi(e) != 0;
   }();
+  mmad_reduce_job j{};
+  j.ws = ws; j.dw = dw; j.splits = splits; j.nd = Nd; j.k = K; j.cs = Cs; j.taps = taps;
   const int64_t blocks = (int64_t)cdiv(Cs, 64) * Nd;
   const int ct = std::min(64, Cs);
+  j.gx = (int)cdiv(Cs, 64);
+  j.gy = Nd;
   if (tz_on && blocks < 256 && taps <= 32 && ct % 4 == 0) {
     int gz = (int)std::min<int64_t>(taps, cdiv(256, blocks));
     int tper = (int)cdiv(taps, gz);
     while (tper * (ct / 4) > 256) ++gz, tper = (int)cdiv(taps, gz);
-    gz = (int)cdiv(taps, tper);
-    hipLaunchKernelGGL(wgrad_reduce_tz_kernel, dim3((unsigned)cdiv(Cs, 64), (unsigned)Nd, gz),
-                       dim3(256), 0, st, ws, dw, splits, Nd, K, Cs, taps, tper);
+    j.gz = (int)cdiv(taps, tper);
+    j.tper = tper;
+    j.kind = mmad_reduce::KIND_TZ;
   } else {
-    hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)cdiv(Cs, 64), (unsigned)Nd),
-                       dim3(256), 0, st, ws, dw, splits, Nd, K, Cs, taps);
+    j.gz = 1;
+    j.kind = mmad_reduce::KIND_T;
   }
+  return j;
+}
+
+int run_reduce_job(const mmad_reduce_job& j, hipStream_t st) {
+  if (j.kind == mmad_reduce::KIND_TZ)
+    hipLaunchKernelGGL(wgrad_reduce_tz_kernel, dim3((unsigned)j.gx, (unsigned)j.gy, (unsigned)j.gz),
+                       dim3(256), 0, st, j.ws, j.dw, j.splits, j.nd, j.k, j.cs, j.taps, j.tper);
+  else if (j.kind == mmad_reduce::KIND_T)
+    hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)j.gx, (unsigned)j.gy), dim3(256), 0,
+                       st, j.ws, j.dw, j.splits, j.nd, j.k, j.cs, j.taps);
+  else
+    return MMAD_OK;
   return launch_status();
+}
+
+// the transposing reduce launched now, or (defer != NULL) described for a later launch
+int launch_reduce_t(const float* ws, float* dw, int splits, int Nd, int K, int Cs, int taps,
+                    hipStream_t st, mmad_reduce_job* defer = nullptr) {
+  const mmad_reduce_job j = plan_reduce_t(ws, dw, splits, Nd, K, Cs, taps);
+  if (defer != nullptr) {
+    *defer = j;
+    return MMAD_OK;
+  }
+  return run_reduce_job(j, st);
 }
 
 // ---- weight packing / input unfolding -------------------------------------------------
@@ -1857,7 +1830,8 @@ int fork_stream(hipStream_t st, hipStream_t rst) {
 // latency-bound BN backward kernels that follow on `st`
 int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* dy, float* dw,
                  float* dbias, void* workspace, hipStream_t st, hipStream_t rst,
-                 int raw_dtype = -1) {
+                 int raw_dtype = -1, mmad_reduce_job* defer = nullptr) {
+  if (defer != nullptr) *defer = mmad_reduce_job{};
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!x || !dy || !dw || !workspace) return MMAD_ENULL;
@@ -1896,7 +1870,8 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
              : mmad_lattice::wgrad(patch_geo(g), x, dy, (float*)workspace, &splits, stream);
     if (rc) return rc;
     if (rst != st && (rc = fork_stream(st, rst))) return rc;
-    rc = launch_reduce_t((const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.taps, rst);
+    rc = launch_reduce_t((const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.taps, rst,
+                         defer);
     if (rc) return rc;
     if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, rstream);
     return MMAD_OK;
@@ -1919,7 +1894,8 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
   // (the transposing reduce writes whole [ci][taps] runs of dW; scattered 4-byte dW stores
   // from an element-wise reduce cost ~2x in partial-line writes)
   if (!unfolded(d) && g.taps > 1 && g.taps <= 32) {
-    rc = launch_reduce_t((const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.taps, rst);
+    rc = launch_reduce_t((const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.taps, rst,
+                         defer);
     if (rc) return rc;
   } else if (sp.splits >= 8)
     hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
@@ -1951,6 +1927,19 @@ int mmad_conv3d_wgrad_split(const mmad_conv_desc* d, int dtype, const void* x, c
   if (!reduce_stream) return MMAD_ENULL;
   return conv3d_wgrad(d, dtype, x, dy, dw, dbias, workspace, as_stream(stream),
                       as_stream(reduce_stream));
+}
+
+int mmad_conv3d_wgrad_deferred(const mmad_conv_desc* d, int dtype, const void* x,
+                               const void* dy, float* dw, float* dbias, void* workspace,
+                               void* stream, mmad_reduce_job* job) {
+  if (!job) return MMAD_ENULL;
+  return conv3d_wgrad(d, dtype, x, dy, dw, dbias, workspace, as_stream(stream),
+                      as_stream(stream), -1, job);
+}
+
+int mmad_reduce_job_run(const mmad_reduce_job* job, void* stream) {
+  if (!job) return MMAD_ENULL;
+  return run_reduce_job(*job, as_stream(stream));
 }
 
 int mmad_stem_raw_ok(const mmad_conv_desc* d, int in_dtype, int dtype) {

@@ -1,0 +1,97 @@
+// Transposing split-K slab reductions of the weight gradients (the bodies of conv.hip's
+// wgrad_reduce_t_kernel / wgrad_reduce_tz_kernel), as device functions of explicit block
+// coordinates so that another launch can run them as extra blocks: bn.hip's BN-backward
+// reduction carries one attached job (mmad_reduce_attach) -- two HBM streams in one launch,
+// one dependent launch fewer.  Slabs ws[split][co][tap * Cs + ci] are summed in fixed order
+// into dW[co][ci][tap].
+#pragma once
+#include "common.h"
+
+namespace mmad_reduce {
+
+enum { KIND_NONE = 0, KIND_T = 1, KIND_TZ = 2 };
+// shared memory the bodies need (floats): tz's 256 f32x4 partials + the 64 x 33 tile
+constexpr int SMEM_FLOATS = 256 * 4 + 64 * 33;
+
+// one block per (co, 64-channel slice); slab reads run along ci, 16 bytes per lane (a wave
+// covers 4 taps x 64 channels), and the [ci][taps] result goes out through LDS as one
+// contiguous run of the torch tensor (taps <= 32)
+__device__ __forceinline__ void t_body(const float* __restrict__ ws, float* __restrict__ dw,
+                                       int splits, int Nd, int K, int Cs, int taps, int bx,
+                                       int by, float* sm) {
+  float* tile = sm;                            // [64][taps + 1]
+  const int ct = min(64, Cs);                  // channels in this slice (Cs % 16 == 0)
+  const int q4 = ct / 4, tpi = 256 / q4;       // lanes per tap row, taps per block pass
+  const int co = by, c0 = bx * ct;
+  const int e4 = threadIdx.x % q4, tg = threadIdx.x / q4;
+  const int64_t total = (int64_t)Nd * K;
+  const float* base = ws + (int64_t)co * K + c0 + e4 * 4;
+  for (int t = tg; t < taps; t += tpi) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int sp = 0; sp < splits; ++sp)
+      s += *reinterpret_cast<const f32x4*>(base + sp * total + (int64_t)t * Cs);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tile[(e4 * 4 + q) * (taps + 1) + t] = s[q];
+  }
+  __syncthreads();
+  float* out = dw + ((int64_t)co * Cs + c0) * taps;
+  for (int l = threadIdx.x; l < ct * taps; l += 256)
+    out[l] = tile[(l / taps) * (taps + 1) + l % taps];
+}
+
+// Same sum and layout for grids of few (co, channel-slice) blocks (the 64-channel layer1 and
+// layer2 shapes: 64-128 blocks for 128-69 slabs): bz takes a group of tper taps, and each
+// (tap, 4-channel) position's slabs are split over SP thread groups whose partial sums are
+// added in a fixed order (deterministic; the order differs from t_body's single chain only
+// in fp32 rounding)
+__device__ __forceinline__ void tz_body(const float* __restrict__ ws, float* __restrict__ dw,
+                                        int splits, int Nd, int K, int Cs, int taps, int tper,
+                                        int bx, int by, int bz, float* sm) {
+  f32x4* part = reinterpret_cast<f32x4*>(sm);  // [256]
+  float* tile = sm + 256 * 4;                  // [64][tper + 1]
+  const int ct = min(64, Cs);
+  const int q4 = ct / 4;
+  const int co = by, c0 = bx * ct;
+  const int t0 = bz * tper, nt = min(taps - t0, tper);
+  const int P = nt * q4;                         // (tap, 4-channel) positions of this block
+  const int SP = max(1, 256 / max(P, 1));        // slab groups per position
+  const int pos = threadIdx.x % P, sg = threadIdx.x / P;
+  const int64_t total = (int64_t)Nd * K;
+  if (nt <= 0) return;                           // (block-uniform)
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  const int e4 = pos % q4, tl = pos / q4;
+  if (sg < SP) {
+    const int per = (splits + SP - 1) / SP;
+    const int sp0 = sg * per, sp1 = min(splits, sp0 + per);
+    const float* base = ws + (int64_t)co * K + c0 + e4 * 4 + (int64_t)(t0 + tl) * Cs;
+#pragma unroll 8
+    for (int sp = sp0; sp < sp1; ++sp) s += *reinterpret_cast<const f32x4*>(base + sp * total);
+    part[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < P) {
+    f32x4 a = part[threadIdx.x];
+    for (int g2 = 1; g2 < SP; ++g2) a += part[g2 * P + threadIdx.x];   // fixed order
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tile[(e4 * 4 + q) * (tper + 1) + tl] = a[q];
+  }
+  __syncthreads();
+  // dW[co][c][t0 .. t0 + nt): runs of nt taps per channel
+  float* out = dw + ((int64_t)co * Cs + c0) * taps + t0;
+  for (int l = threadIdx.x; l < ct * nt; l += 256) {
+    const int c = l / nt, t = l % nt;
+    out[(int64_t)c * taps + t] = tile[c * (tper + 1) + t];
+  }
+}
+
+// block `lin` of job j's own grid (x fastest)
+__device__ __forceinline__ void run(const mmad_reduce_job& j, int lin, float* sm) {
+  const int bx = lin % j.gx, r = lin / j.gx, by = r % j.gy, bz = r / j.gy;
+  if (j.kind == KIND_TZ)
+    tz_body(j.ws, j.dw, j.splits, j.nd, j.k, j.cs, j.taps, j.tper, bx, by, bz, sm);
+  else
+    t_body(j.ws, j.dw, j.splits, j.nd, j.k, j.cs, j.taps, bx, by, sm);
+}
+
+}  // namespace mmad_reduce
