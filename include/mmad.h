@@ -119,7 +119,8 @@ int mmad_conv_pack_batch(int dtype, int njobs, const mmad_pack_job* jobs_device,
  * mmad_conv_pack_dual_batch writes them (co, ci multiples of 16, taps <= 27); for a job with
  * unf_kw > 0 (the Cin = 1 stem: co rows, taps = kd*kh, kpad; one block per row) the
  * unfolded forward layout mmad_conv_pack_weight writes into w_fwd.  Blocks [tile0, tile0 + ntiles) of the launch
- * belong to a job (jobs sorted by tile0; ntiles from mmad_adam_job_tiles); `arrivals` is one
+ * belong to a job (jobs sorted by tile0; ntiles from mmad_adam_job_tiles); block_job (device,
+ * may be NULL: a binary search over tile0 then) = each block's job index; `arrivals` is one
  * zeroed int per job, left zeroed. */
 typedef struct mmad_adam_job {
   float* param;
@@ -136,8 +137,8 @@ typedef struct mmad_adam_job {
   int64_t numel, tile0, ntiles;
 } mmad_adam_job;
 int64_t mmad_adam_job_tiles(const mmad_adam_job* job);
-int mmad_adam_repack(int njobs, const mmad_adam_job* jobs_device, int64_t total_tiles,
-                     int* arrivals, void* stream);
+int mmad_adam_repack(int njobs, const mmad_adam_job* jobs_device, const int* block_job,
+                     int64_t total_tiles, int* arrivals, void* stream);
 int64_t mmad_conv_unfolded_elems(const mmad_conv_desc* d);
 int mmad_conv_unfold_input(const mmad_conv_desc* d, int in_dtype, const void* x,
                            int dtype, void* x_unf, void* stream);

@@ -92,7 +92,7 @@ _SIGS = {
     "mmad_reduce_attach": (_i32, [_vp]),
     "mmad_reduce_attached": (_i32, []),
     "mmad_adam_job_tiles": (_i64, [_PA]),
-    "mmad_adam_repack": (_i32, [_i32, _vp, _i64, _vp, _vp]),
+    "mmad_adam_repack": (_i32, [_i32, _vp, _vp, _i64, _vp, _vp]),
     "mmad_conv_unfolded_elems": (_i64, [_P]),
     "mmad_conv_unfold_input": (_i32, [_P, _i32, _vp, _i32, _vp, _vp]),
     "mmad_conv3d_stats_rows": (_i64, [_P, _i32]),

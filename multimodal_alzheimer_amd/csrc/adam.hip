@@ -48,13 +48,19 @@ __device__ __forceinline__ bool al16(const void* p) {
 }
 
 __global__ __launch_bounds__(NT) void adam_repack_kernel(const mmad_adam_job* __restrict__ jobs,
-                                                         int njobs, int* __restrict__ arrivals) {
+                                                         int njobs,
+                                                         const int* __restrict__ block_job,
+                                                         int* __restrict__ arrivals) {
   __shared__ float tile[16 * 27 * 17];
   int lo = 0, hi = njobs - 1;
   const int64_t bid = blockIdx.x;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (jobs[mid].tile0 <= bid) lo = mid; else hi = mid - 1;
+  if (block_job != nullptr) {
+    lo = block_job[bid];              // one load instead of a chain of ~12 dependent ones
+  } else {
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].tile0 <= bid) lo = mid; else hi = mid - 1;
+    }
   }
   const mmad_adam_job& jb = jobs[lo];
   const int64_t t = bid - jb.tile0;
@@ -216,13 +222,13 @@ int64_t mmad_adam_job_tiles(const mmad_adam_job* job) {
   return (job->numel + FLAT - 1) / FLAT;
 }
 
-int mmad_adam_repack(int njobs, const mmad_adam_job* jobs_device, int64_t total_tiles,
-                     int* arrivals, void* stream) {
+int mmad_adam_repack(int njobs, const mmad_adam_job* jobs_device, const int* block_job,
+                     int64_t total_tiles, int* arrivals, void* stream) {
   if (njobs <= 0 || total_tiles <= 0) return MMAD_OK;
   if (jobs_device == nullptr || arrivals == nullptr || total_tiles > 0x7fffffff)
     return MMAD_ENULL;
   hipLaunchKernelGGL(adam_repack_kernel, dim3((unsigned)total_tiles), dim3(NT), 0,
-                     as_stream(stream), jobs_device, njobs, arrivals);
+                     as_stream(stream), jobs_device, njobs, block_job, arrivals);
   return launch_status();
 }
 

@@ -140,6 +140,18 @@ class AdamRepack:
         self.table = torch.empty(max(n, 1) * C.sizeof(L.AdamJob), dtype=torch.uint8,
                                  device=device)
         self.arrivals = torch.zeros(max(n, 1), dtype=torch.int32, device=device)
+        # each block's job index (sized for every parameter as repacked tiles or 4096-element
+        # chunks, the most blocks the jobs can need)
+        lib = L.load()
+        blocks = 0
+        for g in self.optimizer.param_groups:
+            for p in g["params"]:
+                j = L.AdamJob()
+                j.numel = p.numel()
+                blocks += max(lib.mmad_adam_job_tiles(C.byref(j)), 1)
+                if p.dim() == 5:
+                    blocks += p.shape[0] // 16 * max(p.shape[1] // 16, 1) + p.shape[0]
+        self.block_job = torch.zeros(max(blocks, 1), dtype=torch.int32, device=device)
 
     def step(self):
         """launch the fused update on the current stream (capturable: the job table is
@@ -149,18 +161,24 @@ class AdamRepack:
             self.prepare(next(iter(self.optimizer.param_groups))["params"][0].device)
         if len(jobs) * C.sizeof(L.AdamJob) > self.table.numel():
             raise ValueError("AdamRepack: more jobs than prepared")
+        if tiles > self.block_job.numel():
+            raise ValueError("AdamRepack: more blocks than prepared")
         self.njobs, self.tiles = len(jobs), tiles
         self._host = bytes((L.AdamJob * len(jobs))(*jobs)) if jobs else b""
+        self._host_map = torch.repeat_interleave(
+            torch.arange(len(jobs), dtype=torch.int32),
+            torch.tensor([j.ntiles for j in jobs], dtype=torch.int64)) if jobs else None
         if not torch.cuda.is_current_stream_capturing():
             self.commit()
-        L.call("mmad_adam_repack", self.njobs, L.ptr(self.table), self.tiles,
-               L.ptr(self.arrivals), L.stream())
+        L.call("mmad_adam_repack", self.njobs, L.ptr(self.table), L.ptr(self.block_job),
+               self.tiles, L.ptr(self.arrivals), L.stream())
 
     def commit(self):
         """copy the job table built by the last ``step()`` to the device (outside capture)"""
         if self._host:
             host = torch.frombuffer(bytearray(self._host), dtype=torch.uint8)
             self.table[:host.numel()].copy_(host)
+            self.block_job[:self._host_map.numel()].copy_(self._host_map)
 
     def set_external(self, on):
         for plan in self.plans:

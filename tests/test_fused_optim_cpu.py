@@ -91,5 +91,5 @@ def test_struct_layout_matches_header():
 
 def test_launch_rejects_null_table():
     lib = L.load()
-    assert lib.mmad_adam_repack(1, None, 1, None, None) != 0
-    assert lib.mmad_adam_repack(0, None, 0, None, None) == 0       # nothing to do
+    assert lib.mmad_adam_repack(1, None, None, 1, None, None) != 0
+    assert lib.mmad_adam_repack(0, None, None, 0, None, None) == 0     # nothing to do
