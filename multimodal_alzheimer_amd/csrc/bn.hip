@@ -11,6 +11,10 @@
 #include "common.h"
 #include "reduce.h"
 
+#ifndef MMAD_REDUCE_FIRST
+#define MMAD_REDUCE_FIRST 1
+#endif
+
 namespace {
 
 // Row ranges per partial-sum block: <= 1024 parts so the f64 finalize stays short, and
@@ -70,9 +74,23 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
   static_assert(sizeof(red) >= mmad_reduce::SMEM_FLOATS * sizeof(float), "reduce job LDS");
   // blocks past the column sums' grid run an attached weight-gradient slab reduction
   // (mmad_reduce_attach): a second HBM stream in the same launch
-  if (rj.kind != 0 && (int)blockIdx.x >= ncol) {
-    mmad_reduce::run(rj, (int)blockIdx.x - ncol, &red[0][0]);
-    return;
+  // (REDUCE_FIRST: the job's blocks come first, so they start with the column sums rather
+  // than after them)
+  const int nrj = rj.kind != 0 ? rj.gx * rj.gy * rj.gz : 0;
+  int bxc = (int)blockIdx.x;
+  if (nrj) {
+#if MMAD_REDUCE_FIRST
+    if (bxc < nrj) {
+      mmad_reduce::run(rj, bxc, &red[0][0]);
+      return;
+    }
+    bxc -= nrj;
+#else
+    if (bxc >= ncol) {
+      mmad_reduce::run(rj, bxc - ncol, &red[0][0]);
+      return;
+    }
+#endif
   }
   const int tid = threadIdx.x;
   const int CC = C / (int)gridDim.y;           // this block's channel slab
@@ -80,7 +98,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
   const int lpr = CC / V;
   const int rpar = 256 / lpr;
   const int cl = tid % lpr, rl = tid / lpr;
-  const int64_t r0 = (int64_t)blockIdx.x * rpp;
+  const int64_t r0 = (int64_t)bxc * rpp;
   const int64_t r1 = min(M, r0 + rpp);
   float s[V], q[V], q2[V];
 #pragma unroll
@@ -223,11 +241,11 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
       qq += red[1][k * CC + c];
       if constexpr (DUAL) q2q += red[DUAL ? 2 : 0][k * CC + c];
     }
-    parts[((int64_t)blockIdx.x * 2) * C + cb + c] = ss;
-    parts[((int64_t)blockIdx.x * 2 + 1) * C + cb + c] = qq;
+    parts[((int64_t)bxc * 2) * C + cb + c] = ss;
+    parts[((int64_t)bxc * 2 + 1) * C + cb + c] = qq;
     if constexpr (DUAL) {
-      parts2[((int64_t)blockIdx.x * 2) * C + cb + c] = ss;
-      parts2[((int64_t)blockIdx.x * 2 + 1) * C + cb + c] = q2q;
+      parts2[((int64_t)bxc * 2) * C + cb + c] = ss;
+      parts2[((int64_t)bxc * 2 + 1) * C + cb + c] = q2q;
     }
   }
 }
