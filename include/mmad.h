@@ -172,25 +172,6 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
 int mmad_conv3d_wgrad_split(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,
                             float* dw, float* dbias, void* workspace, void* stream,
                             void* reduce_stream);
-/* Deferred slab reduction of a weight gradient (the captured step, volume_ops): when the
- * split-K slabs are summed by the transposing reduction, mmad_conv3d_wgrad_deferred launches
- * the weight-gradient kernel and (bias gradient) but only DESCRIBES the reduction in *job
- * (kind != 0; kind 0: nothing deferred, dW is complete).  The job then runs as extra blocks
- * of the next BN-backward reduction launched on this host thread (mmad_reduce_attach(job),
- * then any of mmad_bn_bwd_reduce / mmad_bn_relu_bwd_reduce / mmad_bnpool_bwd_reduce /
- * mmad_bn_bwd_reduce2; mmad_reduce_attached() says whether one took it), or on its own
- * (mmad_reduce_job_run).  ws and dw must stay allocated until it has run. */
-typedef struct mmad_reduce_job {
-  const float* ws;
-  float* dw;
-  int32_t splits, nd, k, cs, taps, tper, kind, gx, gy, gz;
-} mmad_reduce_job;
-int mmad_conv3d_wgrad_deferred(const mmad_conv_desc* d, int dtype, const void* x,
-                               const void* dy, float* dw, float* dbias, void* workspace,
-                               void* stream, mmad_reduce_job* job);
-int mmad_reduce_job_run(const mmad_reduce_job* job, void* stream);
-int mmad_reduce_attach(const mmad_reduce_job* job);
-int mmad_reduce_attached(void);
 /* MedicalNet stem (Cin 1, 7^3, stride 2, pad 3; the descriptor mmad_conv_unfold_input
  * takes) straight from the raw volume (n, 1, D, H, W) in `in_dtype` MMAD_F64 (as the
  * reference DataLoader delivers it, dataloader.py:213-277 -> anat_cnn.py:29) or MMAD_F32,

@@ -54,13 +54,6 @@ class AdamJob(C.Structure):
                 [(n, C.c_int64) for n in ("numel", "tile0", "ntiles")])
 
 
-class ReduceJob(C.Structure):
-    """mirror of mmad_reduce_job (include/mmad.h)"""
-    _fields_ = ([("ws", C.c_void_p), ("dw", C.c_void_p)] +
-                [(n, C.c_int32) for n in ("splits", "nd", "k", "cs", "taps", "tper", "kind",
-                                          "gx", "gy", "gz")])
-
-
 class BnFin(C.Structure):
     """mirror of mmad_bn_fin (include/mmad.h)"""
     _fields_ = ([("nparts", C.c_int32)] +
@@ -87,10 +80,6 @@ _SIGS = {
     "mmad_conv_pack_dual_job": (_i32, [_P, _i32, _vp, _vp, _vp, _i64, _PD]),
     "mmad_pack_dual_tiles": (_i64, [_PD]),
     "mmad_conv_pack_dual_batch": (_i32, [_i32, _i32, _vp, _i64, _vp]),
-    "mmad_conv3d_wgrad_deferred": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "mmad_reduce_job_run": (_i32, [_vp, _vp]),
-    "mmad_reduce_attach": (_i32, [_vp]),
-    "mmad_reduce_attached": (_i32, []),
     "mmad_adam_job_tiles": (_i64, [_PA]),
     "mmad_adam_repack": (_i32, [_i32, _vp, _vp, _i64, _vp, _vp]),
     "mmad_conv_unfolded_elems": (_i64, [_P]),

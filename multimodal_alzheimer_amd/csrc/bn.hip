@@ -9,11 +9,6 @@
 // in fixed order in f64.  The conv forward kernel emits the same partial layout from its
 // epilogue, so a BN that follows one of our convs needs no separate statistics pass.
 #include "common.h"
-#include "reduce.h"
-
-#ifndef MMAD_REDUCE_FIRST
-#define MMAD_REDUCE_FIRST 1
-#endif
 
 namespace {
 
@@ -65,40 +60,17 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
                                                      float* __restrict__ parts2 = nullptr,
                                                      const T* __restrict__ g2 = nullptr,
                                                      T* __restrict__ gsum = nullptr,
-                                                     uint32_t gS = 0,
-                                                     mmad_reduce_job rj = mmad_reduce_job{},
-                                                     int ncol = 0) {
+                                                     uint32_t gS = 0) {
   static_assert(!DUAL || MODE == 1, "dual partial sums: BN backward with a relu_out mask");
   static_assert(!GB || (DUAL && V == Chunk<T>::N), "broadcast g: the pair kernel, 16-byte rows");
   __shared__ float red[DUAL ? 3 : 2][2048];
-  static_assert(sizeof(red) >= mmad_reduce::SMEM_FLOATS * sizeof(float), "reduce job LDS");
-  // blocks past the column sums' grid run an attached weight-gradient slab reduction
-  // (mmad_reduce_attach): a second HBM stream in the same launch
-  // (REDUCE_FIRST: the job's blocks come first, so they start with the column sums rather
-  // than after them)
-  const int nrj = rj.kind != 0 ? rj.gx * rj.gy * rj.gz : 0;
-  int bxc = (int)blockIdx.x;
-  if (nrj) {
-#if MMAD_REDUCE_FIRST
-    if (bxc < nrj) {
-      mmad_reduce::run(rj, bxc, &red[0][0]);
-      return;
-    }
-    bxc -= nrj;
-#else
-    if (bxc >= ncol) {
-      mmad_reduce::run(rj, bxc - ncol, &red[0][0]);
-      return;
-    }
-#endif
-  }
   const int tid = threadIdx.x;
   const int CC = C / (int)gridDim.y;           // this block's channel slab
   const int cb = (int)blockIdx.y * CC;
   const int lpr = CC / V;
   const int rpar = 256 / lpr;
   const int cl = tid % lpr, rl = tid / lpr;
-  const int64_t r0 = (int64_t)bxc * rpp;
+  const int64_t r0 = (int64_t)blockIdx.x * rpp;
   const int64_t r1 = min(M, r0 + rpp);
   float s[V], q[V], q2[V];
 #pragma unroll
@@ -241,11 +213,11 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
       qq += red[1][k * CC + c];
       if constexpr (DUAL) q2q += red[DUAL ? 2 : 0][k * CC + c];
     }
-    parts[((int64_t)bxc * 2) * C + cb + c] = ss;
-    parts[((int64_t)bxc * 2 + 1) * C + cb + c] = qq;
+    parts[((int64_t)blockIdx.x * 2) * C + cb + c] = ss;
+    parts[((int64_t)blockIdx.x * 2 + 1) * C + cb + c] = qq;
     if constexpr (DUAL) {
-      parts2[((int64_t)bxc * 2) * C + cb + c] = ss;
-      parts2[((int64_t)bxc * 2 + 1) * C + cb + c] = q2q;
+      parts2[((int64_t)blockIdx.x * 2) * C + cb + c] = ss;
+      parts2[((int64_t)blockIdx.x * 2 + 1) * C + cb + c] = q2q;
     }
   }
 }
@@ -264,20 +236,6 @@ __global__ void parts_fold_kernel(int C, int nparts, int group, const float* __r
   }
 }
 
-// the weight-gradient slab reduction the next BN-backward reduction launch on this thread
-// carries (mmad_reduce_attach); taken (and cleared) by a launch whose grid has one row
-thread_local mmad_reduce_job g_rj{};
-
-// extra blocks for the attached job (0 when none or the launch cannot take it), and the job
-// the kernel receives
-int take_attached(int grid_y, mmad_reduce_job& rj) {
-  rj = mmad_reduce_job{};
-  if (g_rj.kind == 0 || grid_y != 1) return 0;
-  rj = g_rj;
-  g_rj = mmad_reduce_job{};
-  return rj.gx * rj.gy * rj.gz;
-}
-
 template <typename T, int MODE>
 int launch_colsum(int64_t M, int C, const void* y, const void* g, const void* ro,
                   const float* mean, const float* invstd, float* parts, hipStream_t st,
@@ -290,21 +248,13 @@ int launch_colsum(int64_t M, int C, const void* y, const void* g, const void* ro
   // channel slabs for wide rows: the smallest power-of-two split whose slab fits one block
   int slabs = 1;
   while (C % (slabs * 2 * VEC) == 0 && C / (slabs * VEC) > 256) slabs *= 2;
-  // an attached weight-gradient reduction rides along in a BN-backward launch (MODE 1, 3)
-  mmad_reduce_job rj{};
-  const int extra = (MODE == 1 || MODE == 3) && C % (slabs * VEC) == 0 &&
-                            C / (slabs * VEC) <= 256
-                        ? take_attached(slabs, rj)
-                        : 0;
   // g2: its own instantiation, so the kernels without one keep their registers
 #define COLSUM(VV, G)                                                                       \
   hipLaunchKernelGGL((colsum_kernel<T, MODE, VV, false, G>), grid, dim3(256), 0, st, M, C, \
                      pp.rpp, (const T*)y, (const T*)g, (const T*)ro, mean, invstd, parts, act, \
-                     msc, msh, nullptr, nullptr, nullptr, nullptr, (const T*)g2, (T*)gsum, 0u, \
-                     rj, pp.nparts)
+                     msc, msh, nullptr, nullptr, nullptr, nullptr, (const T*)g2, (T*)gsum)
   if (C % (slabs * VEC) == 0 && C / (slabs * VEC) <= 256) {
     grid.y = (unsigned)slabs;
-    grid.x += (unsigned)extra;
     if constexpr (MODE == 1 || MODE == 3) {
       if (g2 != nullptr) COLSUM(VEC, true); else COLSUM(VEC, false);
     } else {
@@ -819,17 +769,6 @@ int64_t mmad_bn_stats_parts(int64_t m, int c) {
 }
 int64_t mmad_bn_bwd_parts(int64_t m, int c) { return mmad_bn_stats_parts(m, c); }
 
-int mmad_reduce_attach(const mmad_reduce_job* job) {
-  g_rj = job != nullptr ? *job : mmad_reduce_job{};
-  if (g_rj.kind != 0 && (g_rj.gx <= 0 || g_rj.gy <= 0 || g_rj.gz <= 0 || !g_rj.ws || !g_rj.dw)) {
-    g_rj = mmad_reduce_job{};
-    return MMAD_EBADSHAPE;
-  }
-  return MMAD_OK;
-}
-
-int mmad_reduce_attached(void) { return g_rj.kind != 0 ? 1 : 0; }
-
 int mmad_bn_stats(int dtype, int64_t m, int c, const void* y, float* parts, void* stream) {
   if (!dt_ok(dtype)) return MMAD_EBADDTYPE;
   if (m <= 0 || c <= 0) return MMAD_EBADSHAPE;
@@ -1091,12 +1030,10 @@ int mmad_bn_bwd_reduce2(int dtype, int64_t m, int c, const void* g, const void* 
                                           : colsum_kernel<T, 1, VEC, true, false, true>)
                         : (g2 != nullptr ? colsum_kernel<T, 1, VEC, true, true>
                                           : colsum_kernel<T, 1, VEC, true, false>);
-    mmad_reduce_job rj{};
-    const int extra = take_attached(slabs, rj);
-    hipLaunchKernelGGL(k, dim3((unsigned)(pp.nparts + extra), slabs), dim3(256), 0, st, m, c,
-                       pp.rpp, (const T*)y, (const T*)g, (const T*)relu_out, mean, invstd,
-                       parts, nullptr, nullptr, nullptr, (const T*)y2, mean2, invstd2, parts2,
-                       (const T*)g2, (T*)nullptr, (uint32_t)g_rows, rj, pp.nparts);
+    hipLaunchKernelGGL(k, dim3((unsigned)pp.nparts, slabs), dim3(256), 0, st, m, c, pp.rpp,
+                       (const T*)y, (const T*)g, (const T*)relu_out, mean, invstd, parts,
+                       nullptr, nullptr, nullptr, (const T*)y2, mean2, invstd2, parts2,
+                       (const T*)g2, (T*)nullptr, (uint32_t)g_rows);
     return launch_status();
   };
   return dtype == MMAD_BF16 ? go(u16{}) : go(float{});

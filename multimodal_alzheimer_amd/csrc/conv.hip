@@ -814,8 +814,7 @@ __global__ void slab_group_sum_kernel(float* __restrict__ ws, int splits, int64_
   }
 }
 
-// The transposing slab reductions (bodies in reduce.h, shared with bn.hip, whose BN-backward
-// reduction launch can carry one as extra blocks: mmad_reduce_attach)
+// The transposing slab reductions (bodies in reduce.h)
 __global__ __launch_bounds__(256) void wgrad_reduce_t_kernel(const float* __restrict__ ws,
                                                              float* __restrict__ dw, int splits,
                                                              int Nd, int K, int Cs, int taps) {
@@ -835,13 +834,13 @@ __global__ __launch_bounds__(256) void wgrad_reduce_tz_kernel(const float* __res
 // the transposing reduce: wgrad_reduce_t_kernel when its (channel slice, co) grid fills the
 // CUs, else wgrad_reduce_tz_kernel over tap groups (MMAD_REDUCE_TZ=0 keeps the former;
 // r03tz: layer1 16.4 / 16.2 -> 10.6 / 10.3 us, layer2.0.conv1 13.9 -> 11.5)
-mmad_reduce_job plan_reduce_t(const float* ws, float* dw, int splits, int Nd, int K, int Cs,
+mmad_reduce::Job plan_reduce_t(const float* ws, float* dw, int splits, int Nd, int K, int Cs,
                               int taps) {
   static const bool tz_on = [] {
     const char* e = getenv("MMAD_REDUCE_TZ");
     return e == nullptr || atoi(e) != 0;
   }();
-  mmad_reduce_job j{};
+  mmad_reduce::Job j{};
   j.ws = ws; j.dw = dw; j.splits = splits; j.nd = Nd; j.k = K; j.cs = Cs; j.taps = taps;
   const int64_t blocks = (int64_t)cdiv(Cs, 64) * Nd;
   const int ct = std::min(64, Cs);
@@ -861,7 +860,7 @@ mmad_reduce_job plan_reduce_t(const float* ws, float* dw, int splits, int Nd, in
   return j;
 }
 
-int run_reduce_job(const mmad_reduce_job& j, hipStream_t st) {
+int run_reduce_job(const mmad_reduce::Job& j, hipStream_t st) {
   if (j.kind == mmad_reduce::KIND_TZ)
     hipLaunchKernelGGL(wgrad_reduce_tz_kernel, dim3((unsigned)j.gx, (unsigned)j.gy, (unsigned)j.gz),
                        dim3(256), 0, st, j.ws, j.dw, j.splits, j.nd, j.k, j.cs, j.taps, j.tper);
@@ -873,15 +872,9 @@ int run_reduce_job(const mmad_reduce_job& j, hipStream_t st) {
   return launch_status();
 }
 
-// the transposing reduce launched now, or (defer != NULL) described for a later launch
 int launch_reduce_t(const float* ws, float* dw, int splits, int Nd, int K, int Cs, int taps,
-                    hipStream_t st, mmad_reduce_job* defer = nullptr) {
-  const mmad_reduce_job j = plan_reduce_t(ws, dw, splits, Nd, K, Cs, taps);
-  if (defer != nullptr) {
-    *defer = j;
-    return MMAD_OK;
-  }
-  return run_reduce_job(j, st);
+                    hipStream_t st) {
+  return run_reduce_job(plan_reduce_t(ws, dw, splits, Nd, K, Cs, taps), st);
 }
 
 // ---- weight packing / input unfolding -------------------------------------------------
@@ -1830,8 +1823,7 @@ int fork_stream(hipStream_t st, hipStream_t rst) {
 // latency-bound BN backward kernels that follow on `st`
 int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* dy, float* dw,
                  float* dbias, void* workspace, hipStream_t st, hipStream_t rst,
-                 int raw_dtype = -1, mmad_reduce_job* defer = nullptr) {
-  if (defer != nullptr) *defer = mmad_reduce_job{};
+                 int raw_dtype = -1) {
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!x || !dy || !dw || !workspace) return MMAD_ENULL;
@@ -1870,8 +1862,7 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
              : mmad_lattice::wgrad(patch_geo(g), x, dy, (float*)workspace, &splits, stream);
     if (rc) return rc;
     if (rst != st && (rc = fork_stream(st, rst))) return rc;
-    rc = launch_reduce_t((const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.taps, rst,
-                         defer);
+    rc = launch_reduce_t((const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.taps, rst);
     if (rc) return rc;
     if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, rstream);
     return MMAD_OK;
@@ -1894,8 +1885,7 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
   // (the transposing reduce writes whole [ci][taps] runs of dW; scattered 4-byte dW stores
   // from an element-wise reduce cost ~2x in partial-line writes)
   if (!unfolded(d) && g.taps > 1 && g.taps <= 32) {
-    rc = launch_reduce_t((const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.taps, rst,
-                         defer);
+    rc = launch_reduce_t((const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.taps, rst);
     if (rc) return rc;
   } else if (sp.splits >= 8)
     hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
@@ -1927,19 +1917,6 @@ int mmad_conv3d_wgrad_split(const mmad_conv_desc* d, int dtype, const void* x, c
   if (!reduce_stream) return MMAD_ENULL;
   return conv3d_wgrad(d, dtype, x, dy, dw, dbias, workspace, as_stream(stream),
                       as_stream(reduce_stream));
-}
-
-int mmad_conv3d_wgrad_deferred(const mmad_conv_desc* d, int dtype, const void* x,
-                               const void* dy, float* dw, float* dbias, void* workspace,
-                               void* stream, mmad_reduce_job* job) {
-  if (!job) return MMAD_ENULL;
-  return conv3d_wgrad(d, dtype, x, dy, dw, dbias, workspace, as_stream(stream),
-                      as_stream(stream), -1, job);
-}
-
-int mmad_reduce_job_run(const mmad_reduce_job* job, void* stream) {
-  if (!job) return MMAD_ENULL;
-  return run_reduce_job(*job, as_stream(stream));
 }
 
 int mmad_stem_raw_ok(const mmad_conv_desc* d, int in_dtype, int dtype) {

@@ -1,15 +1,20 @@
 // Transposing split-K slab reductions of the weight gradients (the bodies of conv.hip's
-// wgrad_reduce_t_kernel / wgrad_reduce_tz_kernel), as device functions of explicit block
-// coordinates so that another launch can run them as extra blocks: bn.hip's BN-backward
-// reduction carries one attached job (mmad_reduce_attach) -- two HBM streams in one launch,
-// one dependent launch fewer.  Slabs ws[split][co][tap * Cs + ci] are summed in fixed order
-// into dW[co][ci][tap].
+// wgrad_reduce_t_kernel / wgrad_reduce_tz_kernel) as device functions of explicit block
+// coordinates, and the job record that describes one launch of them.  Slabs
+// ws[split][co][tap * Cs + ci] are summed in fixed order into dW[co][ci][tap].  (Round 4 ran
+// them as extra blocks of the next BN-backward reduction launch: bit-identical, one launch
+// fewer, 2 % slower -- PERF_LOG.md.)
 #pragma once
 #include "common.h"
 
 namespace mmad_reduce {
 
 enum { KIND_NONE = 0, KIND_T = 1, KIND_TZ = 2 };
+struct Job {
+  const float* ws;
+  float* dw;
+  int32_t splits, nd, k, cs, taps, tper, kind, gx, gy, gz;
+};
 // shared memory the bodies need (floats): tz's 256 f32x4 partials + the 64 x 33 tile
 constexpr int SMEM_FLOATS = 256 * 4 + 64 * 33;
 
@@ -86,7 +91,7 @@ __device__ __forceinline__ void tz_body(const float* __restrict__ ws, float* __r
 }
 
 // block `lin` of job j's own grid (x fastest)
-__device__ __forceinline__ void run(const mmad_reduce_job& j, int lin, float* sm) {
+__device__ __forceinline__ void run(const Job& j, int lin, float* sm) {
   const int bx = lin % j.gx, r = lin / j.gx, by = r % j.gy, bz = r / j.gy;
   if (j.kind == KIND_TZ)
     tz_body(j.ws, j.dw, j.splits, j.nd, j.k, j.cs, j.taps, j.tper, bx, by, bz, sm);

@@ -188,8 +188,6 @@ class GradAllReduce:
         return [g for g, _ in pairs], [v for _, v in pairs]
 
     def _launch(self, bi, inline=False):
-        from .volume_ops import flush_pending
-        flush_pending()                          # every deferred dW slab reduction first
         flat = self.flats[bi]
         for p in self.buckets[bi]:
             if p.grad is None:                   # unused this step: contributes zeros

@@ -214,12 +214,9 @@ class GraphedTrainStep:
             self.fused = fused_optim.AdamRepack(optimizer, fused_optim.pack_plans(model))
             self.fused.prepare(dev)
             self.fused.set_external(True)
-        # deferred weight-gradient slab reductions (volume_ops.DEFER_REDUCE) in the captures
-        volume_ops.defer_reductions(True)
         try:
             self._capture(model, optimizer, reducer, staged)
         finally:
-            volume_ops.defer_reductions(False)
             if self.fused is not None:
                 self.fused.set_external(False)
         if self.fused is not None:

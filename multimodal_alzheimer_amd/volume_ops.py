@@ -94,62 +94,8 @@ REDUCE_STREAM = os.environ.get("MMAD_REDUCE_STREAM", "0") == "1"
 # MMAD_STEM_RAW=0: the Cin-1 stem reads the W-unfolded copy written by
 # mmad_conv_unfold_input instead of the raw volume (A/B switch; mmad_conv3d_fwd_raw)
 STEM_RAW = os.environ.get("MMAD_STEM_RAW", "1") != "0"
-# MMAD_DEFER_REDUCE=1: inside a captured training step (graph_step), a weight gradient's
-# transposing slab reduction is not launched on its own but rides as extra blocks in the next
-# BN-backward reduction launch (mmad_conv3d_wgrad_deferred + mmad_reduce_attach): two HBM
-# streams in one launch, one dependent launch (~4.6 us in a replay) fewer per conv.  Pending
-# reductions are flushed (launched alone) wherever a dW could be read: the end of the
-# backward, each staged-backward stage, any gradient all-reduce.
-DEFER_REDUCE = os.environ.get("MMAD_DEFER_REDUCE", "0") == "1"
-_DEFER = [False]
-_PENDING = []          # (mmad_reduce_job, the slab workspace it reads)
 _SIDE = {}
 _JOIN_PENDING = set()
-
-
-def defer_reductions(on):
-    """graph_step: defer weight-gradient slab reductions while ``on`` (DEFER_REDUCE only)"""
-    _DEFER[0] = bool(on) and DEFER_REDUCE
-    if not _DEFER[0]:
-        flush_pending()
-
-
-def flush_pending():
-    """launch every deferred slab reduction now, on the current stream"""
-    while _PENDING:
-        job, _keep = _PENDING.pop(0)
-        L.call("mmad_reduce_job_run", C.byref(job), L.stream())
-
-
-def _bwd_reduce_call(name, *args):
-    """a BN-backward reduction launch, carrying the oldest deferred slab reduction"""
-    if not _PENDING:
-        return L.call(name, *args)
-    lib = L.load()
-    lib.mmad_reduce_attach(C.byref(_PENDING[0][0]))
-    try:
-        L.call(name, *args)
-    finally:
-        if lib.mmad_reduce_attached():
-            lib.mmad_reduce_attach(None)       # not taken: it stays pending
-        else:
-            _PENDING.pop(0)
-
-
-_FLUSH_QUEUED = [False]
-
-
-def _queue_flush():
-    """flush the deferred reductions when the running backward pass ends"""
-    if _FLUSH_QUEUED[0]:
-        return
-    _FLUSH_QUEUED[0] = True
-
-    def flush():
-        _FLUSH_QUEUED[0] = False
-        flush_pending()
-
-    torch.autograd.Variable._execution_engine.queue_callback(flush)
 
 
 def grad_stream(device):
@@ -537,16 +483,6 @@ def _wgrad(ctx, d, dt, src, gy, weight, wparam=None, rside=None):
             if t is not None:
                 t.record_stream(rside)
         _queue_join(torch.cuda.current_stream(), rside)
-    elif (_DEFER[0] and not padded and wparam is not None and wparam.grad is None and
-          ctx.needs_input_grad[1] and not torch.is_grad_enabled()):
-        # dW itself is NOT held here: AccumulateGrad adopts a gradient tensor only while
-        # nothing else references it (else it clones it -- before the reduction has run)
-        job = L.ReduceJob()
-        L.call("mmad_conv3d_wgrad_deferred", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db),
-               L.ptr(ws), L.stream(), C.byref(job))
-        if job.kind:
-            _PENDING.append((job, (ws,)))
-            _queue_flush()
     else:
         L.call("mmad_conv3d_wgrad", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db),
                L.ptr(ws), L.stream())
@@ -787,10 +723,10 @@ def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask,
     parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
     if mask_affine is not None:
         sc, sh = mask_affine
-        _bwd_reduce_call("mmad_bn_relu_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(y), L.ptr(mean),
+        L.call("mmad_bn_relu_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(y), L.ptr(mean),
                L.ptr(invstd), L.ptr(sc), L.ptr(sh), L.ptr(parts), L.stream())
     else:
-        _bwd_reduce_call("mmad_bn_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(g2), L.ptr(relu_out), L.ptr(y),
+        L.call("mmad_bn_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(g2), L.ptr(relu_out), L.ptr(y),
                L.ptr(mean), L.ptr(invstd), L.ptr(parts), L.stream())
     dgamma = grad_slot(params[0], (c,), dev)
     dbeta = grad_slot(params[1], (c,), dev)
@@ -822,7 +758,7 @@ def _bn_backward_pair(g, relu_out, y, mean, invstd, gamma, batch_stats, y2, mean
     dt = L.dtype_code(y.dtype)
     nparts = L.load().mmad_bn_bwd_parts(m, c)
     parts = torch.empty((2, nparts, 2, c), dtype=torch.float32, device=dev)
-    _bwd_reduce_call("mmad_bn_bwd_reduce2", dt, m, c, L.ptr(g), L.ptr(g2), g_rows, L.ptr(relu_out),
+    L.call("mmad_bn_bwd_reduce2", dt, m, c, L.ptr(g), L.ptr(g2), g_rows, L.ptr(relu_out),
            L.ptr(y), L.ptr(mean), L.ptr(invstd), L.ptr(y2), L.ptr(mean2), L.ptr(invstd2),
            L.ptr(parts[0]), L.ptr(parts[1]), L.stream())
     dgamma = grad_slot(params[0], (c,), dev)
@@ -986,7 +922,7 @@ class _BNReluPoolFn(torch.autograd.Function):
         # a twin's gradient: the reduce also writes the summed gradient, which the apply
         # (reading each pooled gradient from up to 8 cells) then takes as its one input
         gsum = torch.empty_like(g) if g2 is not None else None
-        _bwd_reduce_call("mmad_bnpool_bwd_reduce", dt, mp, c, L.ptr(g), L.ptr(g2), L.ptr(gsum),
+        L.call("mmad_bnpool_bwd_reduce", dt, mp, c, L.ptr(g), L.ptr(g2), L.ptr(gsum),
                L.ptr(am), L.ptr(ymax), L.ptr(mean), L.ptr(invstd), L.ptr(parts), L.stream())
         if gsum is not None:
             g = gsum

@@ -60,53 +60,6 @@ def test_graph_replay_equals_eager_steps(precision):
         assert torch.equal(pa, pb), na
 
 
-def test_deferred_slab_reductions_replay_equals_eager(monkeypatch):
-    """volume_ops.DEFER_REDUCE: inside the capture every transposing weight-gradient
-    reduction rides in the next BN-backward reduction launch (mmad_reduce_attach) or is
-    flushed at the end of the backward -- same arithmetic, so replays stay bit-identical
-    to eager steps; and the captured step has fewer launches."""
-    from multimodal_alzheimer_amd import volume_ops
-    monkeypatch.setattr(volume_ops, "DEFER_REDUCE", True)
-    torch.manual_seed(3)
-    a = M.Anat_CNN(_hparams("bf16")).cuda()
-    b = copy.deepcopy(a)
-    batches = [_batch(60 + i) for i in range(3)]
-    opt_a = a.configure_optimizers()
-    for grp in opt_a.param_groups:
-        grp["capturable"] = True
-        grp["lr"] = torch.tensor(float(grp["lr"]), device="cuda")
-    warm = 2
-    for _ in range(warm):
-        opt_a.zero_grad(set_to_none=True)
-        a.general_step(batches[0], 0, "train")["loss"].backward()
-        opt_a.step()
-    losses_a = []
-    for i in range(3):
-        opt_a.zero_grad(set_to_none=True)
-        out = a.general_step(batches[i], 0, "train")
-        out["loss"].backward()
-        opt_a.step()
-        losses_a.append(out["loss"].detach().clone())
-    taken = []
-    real = volume_ops._bwd_reduce_call
-
-    def spy(name, *args):
-        pending = len(volume_ops._PENDING)
-        real(name, *args)
-        taken.append(pending - len(volume_ops._PENDING))
-    monkeypatch.setattr(volume_ops, "_bwd_reduce_call", spy)
-    opt_b = b.configure_optimizers()
-    gs = GraphedTrainStep(b, opt_b, batches[0], warmup=warm)
-    assert sum(taken) > 0, "no slab reduction rode along"
-    assert not volume_ops._PENDING and not volume_ops._DEFER[0]
-    losses_b = [gs(batches[i])["loss"].detach().clone() for i in range(3)]
-    torch.cuda.synchronize()
-    for la, lb in zip(losses_a, losses_b):
-        assert torch.equal(la, lb)
-    for (na, pa), (nb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
-        assert torch.equal(pa, pb), na
-
-
 def _batch(seed, n=2, s=32):
     g = torch.Generator(device="cuda").manual_seed(seed)
     return {"mri": torch.rand((n, s, s, s), device="cuda", dtype=torch.float64, generator=g),
