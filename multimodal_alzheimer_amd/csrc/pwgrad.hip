@@ -339,7 +339,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
         // (xr opaque per stage: the per-tap row-half offsets of the X reads are computed
         // where they are used, not hoisted and held across the plane loop -- spills)
         int xr = xrow;
-        asm volatile("" : "+v"(xr));
+        if constexpr (XSW) asm volatile("" : "+v"(xr));
         PFr f0, f1;
         kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, f0,
               xr);
