@@ -32,6 +32,7 @@ from . import head_ops
 from . import layers as Lyr
 from . import medicalnet
 from .lightning_compat import (LightningModule, MulticlassF1Score, MulticlassMatthewsCorrCoef)
+from .preprocess import apply_batch_spec
 from .volume_ops import cast
 
 PRETRAIN_TEMPLATE = ("/vol/chameleon/projects/adni/adni_1/MedicalNet/pretrain/"
@@ -109,6 +110,18 @@ class Base_Model(LightningModule, ABC):
     @abstractmethod
     def general_step(self, batch, batch_idx, mode) -> dict:
         pass
+
+    @staticmethod
+    def prepare_batch(batch):
+        """Opt-in device normalisation (dataset.MultiModalDataset(device_normalize=True)):
+        a batch carrying the loader's normalisation settings gets them applied here, on the
+        device, before any model math; every other batch passes through unchanged (the
+        default dataset already normalised it on fetch, as the reference loader does)."""
+        return apply_batch_spec(batch)
+
+    def on_after_batch_transfer(self, batch, dataloader_idx=0):
+        """Lightning hook (runs after the batch reaches the device)."""
+        return self.prepare_batch(batch)
 
     @property
     def is_cuda(self):
@@ -442,6 +455,7 @@ class Anat_CNN(Base_Model):
         return self.model(x)
 
     def general_step(self, batch, batch_idx, mode):
+        batch = self.prepare_batch(batch)
         x = batch[self.batch_key].unsqueeze(1)   # raw f64 volume; conv 1 unfolds + casts it
         y = batch["label"]
         y_hat, loss = _logits_and_loss(self.criterion, self.forward(x), y)
@@ -579,6 +593,7 @@ class Anat_PET_CNN(Base_Model):
         return self.model_fuse(head_ops.concat_features(out_pet, out_mri))
 
     def general_step(self, batch, batch_idx, mode):
+        batch = self.prepare_batch(batch)
         x_pet = batch["pet1451"].unsqueeze(1)
         x_mri = batch["mri"].unsqueeze(1)
         y = batch["label"]
@@ -647,6 +662,7 @@ class PET_MRI_EF(Base_Model):
         return self.model(x)
 
     def general_step(self, batch, batch_idx, mode):
+        batch = self.prepare_batch(batch)
         from .volume_ops import StackedVolumes
         x = StackedVolumes([batch["pet1451"], batch["mri"]])
         y = batch["label"]
@@ -723,6 +739,7 @@ class PET_MRI_FMF(Base_Model):
         return self.fuse_model(fused)
 
     def general_step(self, batch, batch_idx, mode):
+        batch = self.prepare_batch(batch)
         x_pet = batch["pet1451"].unsqueeze(1)      # raw f64; conv 1 unfolds + casts (:124-127)
         x_mri = batch["mri"].unsqueeze(1)
         y = batch["label"]
@@ -857,6 +874,7 @@ class All_Modalities_Fusion(Base_Model):
         return self.model_fuse(head_ops.concat_features(out_pet, out_mri, out_tab))
 
     def general_step(self, batch, batch_idx, mode):
+        batch = self.prepare_batch(batch)
         x_pet = batch["pet1451"].unsqueeze(1)
         x_mri = batch["mri"].unsqueeze(1)
         x_tab = cast(batch["tabular"].unsqueeze(1), torch.float32)

@@ -200,8 +200,11 @@ __global__ __launch_bounds__(NT) void adam_repack_kernel(const mmad_adam_job* __
       }
     }
   }
-  // step counter: every block has read *jb.step (its value fed the bias corrections above)
-  // before it arrives; the last to arrive stores step + 1 and re-arms the counter
+  // step counter: every wave of every block has read *jb.step (its value fed the bias
+  // corrections above) before its block arrives -- the barrier orders all of this block's
+  // waves before thread 0's arrival on every branch; the last to arrive stores step + 1 and
+  // re-arms the counter
+  __syncthreads();
   if (threadIdx.x == 0) {
     const int prev = atomicAdd(arrivals + lo, 1);
     if (prev == (int)jb.ntiles - 1) {

@@ -25,16 +25,21 @@ The result is identical to the reference's table (IDs, labels, paths, tabular va
 generated from the reference class itself, tests/golden/make_merge_golden.py).
 
 ``__getitem__`` reads the NIfTI volumes with :mod:`.nifti` (float64, nibabel's
-``get_fdata`` layout) and returns them raw; the reference's per-sample CPU normalisation
-(:200-284) runs batched on the device instead (``normalize_batch`` ->
-preprocess.VolumeNormalizer), for which the MRI brain mask is returned as ``mri_mask``.
+``get_fdata`` layout) and, like the reference (:197-321), returns them normalised per
+``normalize_pet`` / ``normalize_mri`` / ``quantile`` -- the loader's own float64 statements
+(preprocess.loader_normalize_*), so an unchanged ``train_*.py`` sees the reference's tensors.
+``device_normalize=True`` (opt-in) moves that work to the GPU: ``__getitem__`` then returns
+the raw volumes, the brain mask (``mri_mask``) and the settings (``preprocess.NORM_SPEC_KEY``),
+and the model applies them batched on the device before its first conv
+(classifiers.Base_Model.prepare_batch -> preprocess.VolumeNormalizer, norm.hip).
 """
 import numpy as np
 import pandas as pd
 import torch
 
 from . import nifti
-from .preprocess import VolumeNormalizer
+from .preprocess import (NORM_SPEC_KEY, VolumeNormalizer, loader_normalize_mri,
+                         loader_normalize_pet, spec_string)
 
 MODALITIES = ("pet1451", "t1w", "tabular")
 # the column whose presence selects each modality's rows (dataloader.py:108-121)
@@ -130,16 +135,19 @@ def modality_tables(table, modalities):
 class MultiModalDataset(torch.utils.data.Dataset):
     """Drop-in for pkg.utils.dataloader.MultiModalDataset (dataloader.py:21-344): same
     constructor arguments, merged table ``ds``, ``label_mapping``, ``__len__``,
-    ``get_label_distribution``.  ``__getitem__`` returns the raw float64 volumes (plus
-    ``mri_mask`` when a per-scan MRI normalisation is configured) and the 9 tabular
-    features; ``normalize_batch`` applies the configured normalisation to a collated
-    device batch (preprocess.VolumeNormalizer, bit-exact to the reference's per-sample
-    statements)."""
+    ``get_label_distribution`` and ``__getitem__`` (normalised float64 volumes, the 9
+    tabular features, the label).
+
+    ``device_normalize`` (build extension, default False = the reference's behaviour):
+    ``__getitem__`` returns raw volumes + ``mri_mask`` (per-scan MRI modes) + the settings
+    string, and the model normalises the collated batch on the GPU (``normalize_batch``
+    does the same for a caller that wants it explicitly)."""
 
     def __init__(self, path, binary_classification=False,
                  modalities=("pet1451", "t1w", "tabular"), days_threshold=180,
                  transform_pet=None, transform_mri=None, transform_tabular=None,
-                 normalize_pet=None, normalize_mri=None, quantile=0.99):
+                 normalize_pet=None, normalize_mri=None, quantile=0.99,
+                 device_normalize=False):
         self.entire_ds = pd.read_csv(path)
         if binary_classification == 2:
             binary_classification = True
@@ -171,8 +179,12 @@ class MultiModalDataset(torch.utils.data.Dataset):
         self.normalize_pet = normalize_pet
         self.normalize_mri = normalize_mri
         self.quantile = quantile
-        self.normalizer = VolumeNormalizer(normalize_mri or None, normalize_pet or None,
-                                           quantile)
+        self.device_normalize = bool(device_normalize)
+        # the reference checks normalize_mri when a sample is fetched (:236-281); the device
+        # path checks it here, where its settings are fixed
+        if self.device_normalize:
+            self.normalizer                                      # validates the settings
+        self._spec = spec_string(normalize_mri, normalize_pet, quantile)
 
     def __len__(self):
         return len(self.ds)
@@ -185,25 +197,43 @@ class MultiModalDataset(torch.utils.data.Dataset):
 
     def __getitem__(self, index):
         sample = self.ds.iloc[index]
+        host = not self.device_normalize
         data = {}
         p = sample.get("path_pet1451")
-        data["pet1451"] = None if p is None else self._volume(p, self.transform_pet)
+        if p is not None:
+            pet = self._volume(p, self.transform_pet)
+            if self.normalize_pet and host:
+                pet = loader_normalize_pet(pet, self.normalize_pet)      # :213-215
+            data["pet1451"] = pet
         p = sample.get("path_anat")
-        if p is None:
-            data["mri"] = None
-        else:
-            data["mri"] = self._volume(p, self.transform_mri)
-            if self.normalize_mri and "per_scan_norm" in self.normalize_mri:
-                data["mri_mask"] = torch.as_tensor(nifti.load(sample["path_anat_mask"]))
-        if sample.get("AGE") is None:
-            data["tabular"] = None
-        else:
+        if p is not None:
+            mri = self._volume(p, self.transform_mri)
+            nm = self.normalize_mri
+            if nm:
+                per_scan = isinstance(nm, dict) and "per_scan_norm" in nm
+                mask = (torch.as_tensor(nifti.load(sample["path_anat_mask"]))
+                        if per_scan else None)                           # :240-242
+                if host:
+                    mri = loader_normalize_mri(mri, mask, nm, self.quantile)   # :236-281
+                elif per_scan:
+                    data["mri_mask"] = mask
+            data["mri"] = mri
+        if sample.get("AGE") is not None:
             # dataloader.py:294-306, including its 'whole_brain' read from PTEDUCAT
             keys = ("AGE", "PTEDUCAT", "Ventricles", "Hippocampus", "PTEDUCAT", "Entorhinal",
                     "Fusiform", "MidTemp", "ICV")
             data["tabular"] = torch.tensor([sample[k] for k in keys])
         data["label"] = torch.tensor(self.label_mapping[sample["label"]])
-        return {k: v for k, v in data.items() if v is not None}
+        if not host and (self.normalize_mri or self.normalize_pet):
+            data[NORM_SPEC_KEY] = self._spec
+        # the reference's key order: pet1451, mri, tabular, label
+        order = ("pet1451", "mri", "mri_mask", "tabular", "label", NORM_SPEC_KEY)
+        return {k: data[k] for k in order if k in data}
+
+    @property
+    def normalizer(self):
+        return VolumeNormalizer(self.normalize_mri or None, self.normalize_pet or None,
+                                self.quantile)
 
     def normalize_batch(self, batch):
         """The reference's per-sample normalisation (dataloader.py:213-282), on a collated

@@ -18,10 +18,115 @@ first) and calls libmmad_hip.so; there is no CPU path (a CPU tensor raises).
 :class:`VolumeNormalizer` applies the reference's ``normalize_mri`` / ``normalize_pet``
 dicts to a batch dict on device, so a loader built with ``normalize_*=None`` (raw volumes +
 ``mri_mask``) feeds ``general_step`` exactly what the reference loader would.
+
+Two ways in (dataset.MultiModalDataset):
+
+* default -- the reference's contract: ``__getitem__`` normalises each sample on the host in
+  the loader worker (:func:`loader_normalize_pet` / :func:`loader_normalize_mri`, the
+  reference's own float64 torch statements), so an unchanged ``train_*.py`` gets the
+  reference's tensors;
+* ``device_normalize=True`` (opt-in) -- ``__getitem__`` returns the raw volumes, the brain
+  mask and a :data:`NORM_SPEC_KEY` string naming the settings; the model's
+  ``on_after_batch_transfer`` / ``general_step`` (classifiers.Base_Model.prepare_batch ->
+  :func:`apply_batch_spec`) runs the batched device kernels above on the collated batch.
+  Same values (min_max and the affine forms bit-exact, z-score to rounding).
 """
+import json
+
 import torch
 
 from . import _lib as L
+
+NORM_SPEC_KEY = "normalize"
+
+
+# ------------------------------------------------------------ loader-side (host) statements
+def loader_affine(x, mean, std):
+    """torchvision ``Normalize(mean, std)`` as the loader applies it to one (D, H, W) float64
+    volume (dataloader.py:213-215 PET, :256-257 per-scan z-score, :276-278 all-scan): the
+    statistics become 0-d tensors of the volume's dtype, then ``sub`` and ``div``."""
+    if x.ndim < 3:
+        raise ValueError("Normalize expects a tensor with at least 3 dimensions")
+    mean = torch.as_tensor(mean, dtype=x.dtype)
+    std = torch.as_tensor(std, dtype=x.dtype)
+    if bool((std == 0).any()):
+        raise ValueError("std evaluated to zero after conversion to float64, leading to "
+                         "division by zero.")
+    return x.sub(mean).div(std)
+
+
+def _brain_values(mri, mask):
+    """dataloader.py:244-249: the masked volume's nonzero entries, flattened."""
+    v = (mri * mask).reshape(-1)
+    return v[v.nonzero()]
+
+
+def loader_normalize_pet(pet, normalize_pet):
+    """dataloader.py:213-215."""
+    return loader_affine(pet, normalize_pet["mean"], normalize_pet["std"])
+
+
+def loader_normalize_mri(mri, mask, normalize_mri, quantile):
+    """dataloader.py:236-281 for one scan (float64 host tensors); ``mask`` is only read by the
+    per-scan modes."""
+    if not isinstance(normalize_mri, dict) or len(normalize_mri) != 1:
+        raise AssertionError("normalize_mri must be a dict with one key")
+    if "per_scan_norm" in normalize_mri:
+        mode = normalize_mri["per_scan_norm"]
+        v = _brain_values(mri, mask)
+        if mode == "normalize":
+            std, mean = torch.std_mean(v)
+            return loader_affine(mri, mean, std) * mask
+        if mode == "min_max":
+            if not 0 <= quantile <= 1:
+                raise AssertionError("quantile must lie in [0, 1]")
+            hi = torch.quantile(v, quantile, interpolation="linear")
+            lo = torch.quantile(v, 1 - quantile, interpolation="linear")
+            out = (mri - lo) / (hi - lo)
+            out[out > 1] = 1                  # masked stores, not clamp: -0.0 and NaN kept
+            out[out < 0] = 0                  # exactly as the loader leaves them
+            return out.mul_(mask)
+        raise ValueError('If you want to normalize per scan you have to pass either '
+                         '"normalize" or "min_max"')
+    if "all_scan_norm" in normalize_mri:
+        st = normalize_mri["all_scan_norm"]
+        return loader_affine(mri, st["mean"], st["std"])
+    raise ValueError('If you use the argument "normalize_mri" only "per_scan_norm" or '
+                     '"all_scan_norm" are allowed as keys!')
+
+
+# ------------------------------------------------------------------ opt-in device path spec
+def spec_string(normalize_mri, normalize_pet, quantile):
+    """The settings a device-normalising dataset attaches to every sample (a string, so the
+    DataLoader collates it into a list and the device transfer leaves it alone)."""
+    def _f(d):
+        return None if not d else {k: (_f(v) if isinstance(v, dict) else
+                                        (v if isinstance(v, str) else float(v)))
+                                    for k, v in d.items()}
+    return json.dumps({"normalize_mri": _f(normalize_mri), "normalize_pet": _f(normalize_pet),
+                       "quantile": float(quantile)}, sort_keys=True)
+
+
+_NORMALIZERS = {}
+
+
+def apply_batch_spec(batch):
+    """Run the device normalisation a collated batch asks for (its :data:`NORM_SPEC_KEY`
+    entry), returning the batch the reference loader would have produced: normalised
+    'mri' / 'pet1451', no 'mri_mask', no spec.  Batches without a spec pass through."""
+    if not isinstance(batch, dict) or NORM_SPEC_KEY not in batch:
+        return batch
+    spec = batch[NORM_SPEC_KEY]
+    if isinstance(spec, (list, tuple)):
+        if len(set(spec)) != 1:
+            raise ValueError("a batch mixes samples with different normalisation settings")
+        spec = spec[0]
+    norm = _NORMALIZERS.get(spec)
+    if norm is None:
+        norm = _NORMALIZERS[spec] = VolumeNormalizer(**json.loads(spec))
+    out = norm({k: v for k, v in batch.items() if k != NORM_SPEC_KEY})
+    out.pop("mri_mask", None)
+    return out
 
 
 def _scans(x):

@@ -102,10 +102,7 @@ def test_nifti_reader_round_trip(tmp_path):
         nifti.load(str(bad))
 
 
-def test_getitem_reads_volumes_and_tabular(tmp_path):
-    """__getitem__ of a merged PET + MRI + tabular triple: raw float64 volumes from the
-    NIfTI files, the MRI mask for per-scan normalisation, the reference's 9 tabular
-    features (dataloader.py:294-306, 'whole_brain' read from PTEDUCAT as there)."""
+def _triple(tmp_path, normalize_mri=None, normalize_pet=None, device_normalize=False):
     rng = np.random.RandomState(1)
     pet, mri, mask = rng.rand(4, 5, 6), rng.rand(4, 5, 6) * 9, (rng.rand(4, 5, 6) > 0.3)
     paths = {k: str(tmp_path / f"{k}.nii.gz") for k in ("pet", "mri", "mask")}
@@ -121,17 +118,109 @@ def test_getitem_reads_volumes_and_tabular(tmp_path):
     csv = tmp_path / "t.csv"
     pd.DataFrame(rows).to_csv(csv)
     d = MultiModalDataset(str(csv), modalities=["pet1451", "t1w", "tabular"],
-                          normalize_mri={"per_scan_norm": "min_max"})
+                          normalize_mri=normalize_mri, normalize_pet=normalize_pet,
+                          device_normalize=device_normalize)
+    return d, pet, mri.astype(np.float32).astype(np.float64), mask.astype(np.float64)
+
+
+def test_getitem_reads_volumes_and_tabular(tmp_path):
+    """__getitem__ of a merged PET + MRI + tabular triple without normalisation: raw float64
+    volumes from the NIfTI files, the reference's 9 tabular features (dataloader.py:294-306,
+    'whole_brain' read from PTEDUCAT as there), the reference's keys and key order."""
+    d, pet, mri, _ = _triple(tmp_path)
     assert len(d) == 1
     item = d[0]
-    assert set(item) == {"pet1451", "mri", "mri_mask", "tabular", "label"}
+    assert list(item) == ["pet1451", "mri", "tabular", "label"]
     np.testing.assert_array_equal(item["pet1451"].numpy(), pet)
-    np.testing.assert_array_equal(item["mri"].numpy(), mri.astype(np.float32).astype(np.float64))
-    np.testing.assert_array_equal(item["mri_mask"].numpy(), mask.astype(np.float64))
+    np.testing.assert_array_equal(item["mri"].numpy(), mri)
     assert item["tabular"].tolist() == [70.5, 16.0, 1.0, 2.0, 16.0, 4.0, 5.0, 6.0, 7.0]
     assert item["label"].item() == 1
     assert d.ds["min_time"][0] == pd.Timestamp("2018-01-01")
     assert d.ds["max_time"][0] == pd.Timestamp("2018-03-01")
+
+
+def test_getitem_normalises_on_fetch_like_the_reference(tmp_path):
+    """The reference normalises inside __getitem__ (dataloader.py:213-282); the drop-in does
+    too by default, with the reference's statements -- bit-identical to the oracle
+    restatement -- and returns no extra keys."""
+    from oracle import preprocess_ref as P
+    pet_st = {"mean": 0.4, "std": 0.3}
+    for nm in ({"per_scan_norm": "min_max"}, {"per_scan_norm": "normalize"},
+               {"all_scan_norm": {"mean": 2.5, "std": 1.5}}):
+        d, pet, mri, mask = _triple(tmp_path, normalize_mri=nm, normalize_pet=pet_st)
+        item = d[0]
+        assert list(item) == ["pet1451", "mri", "tabular", "label"]
+        assert torch.equal(item["pet1451"], P.affine_ref(torch.from_numpy(pet), 0.4, 0.3))
+        x, m = torch.from_numpy(mri), torch.from_numpy(mask)
+        if "all_scan_norm" in nm:
+            exp = P.affine_ref(x, 2.5, 1.5)
+        elif nm["per_scan_norm"] == "min_max":
+            exp = P.mri_minmax_ref(x.clone(), m, 0.99)[0]
+        else:
+            exp = P.mri_zscore_ref(x.clone(), m)
+        assert torch.equal(item["mri"], exp), nm
+    d, *_ = _triple(tmp_path, normalize_mri={"per_scan_norm": "bogus"})
+    with pytest.raises(ValueError):
+        d[0]
+
+
+def _scan_table(tmp_path, name, x, m):
+    rows = []
+    for b in range(x.shape[0]):
+        pv, pm = str(tmp_path / f"{name}{b}.nii.gz"), str(tmp_path / f"{name}{b}_mask.nii")
+        nifti.save(pv, x[b].numpy())
+        nifti.save(pm, m[b].numpy().astype(np.uint8))
+        rows.append({"ID": f"sub-{b}", "ses": "2019-05-01", "path_anat": pv,
+                     "path_anat_mask": pm, "label": ("CN", "MCI", "Dementia")[b % 3]})
+    csv = tmp_path / f"{name}.csv"
+    pd.DataFrame(rows).to_csv(csv)
+    return str(csv)
+
+
+@pytest.mark.parametrize("name", ["uniform", "ints_q97", "signed_q50", "q100"])
+def test_driver_built_dataset_matches_norm_golden(tmp_path, name):
+    """The alias built exactly as train_anat_cnn.py:180-185 builds it (t1w only, per-scan
+    min_max, quantile from hparams) over NIfTI files: every scan's __getitem__ value is
+    bit-identical to the reference statements' fixture (tests/golden/norm.npz); the
+    per-scan z-score likewise."""
+    from pkg.utils.dataloader import MultiModalDataset as Alias
+    from tests._norm_cases import CASES, make_case
+    spec = CASES[name]
+    x, m = make_case(spec)
+    gold = np.load(os.path.join(GOLDEN, "norm.npz"))
+    csv = _scan_table(tmp_path, name, x, m)
+    trainset = Alias(path=csv, modalities=["t1w"], normalize_mri={"per_scan_norm": "min_max"},
+                     binary_classification=False, quantile=spec["q"])
+    zs = Alias(path=csv, modalities=["t1w"], normalize_mri={"per_scan_norm": "normalize"})
+    assert len(trainset) == x.shape[0]
+    for b in range(x.shape[0]):
+        item = trainset[b]
+        assert list(item) == ["mri", "label"]
+        assert item["mri"].dtype == torch.float64
+        np.testing.assert_array_equal(item["mri"].numpy(), gold[f"{name}_minmax"][b])
+        np.testing.assert_array_equal(zs[b]["mri"].numpy(), gold[f"{name}_zscore"][b])
+
+
+def test_device_normalize_opt_in_returns_raw_mask_and_spec(tmp_path):
+    """device_normalize=True: raw volumes + mri_mask + the settings string, which the
+    DataLoader collates into a list and preprocess.apply_batch_spec reads back."""
+    import json
+    from multimodal_alzheimer_amd.preprocess import NORM_SPEC_KEY, VolumeNormalizer, _NORMALIZERS
+    nm, pet_st = {"per_scan_norm": "min_max"}, {"mean": 0.4, "std": 0.3}
+    d, pet, mri, mask = _triple(tmp_path, normalize_mri=nm, normalize_pet=pet_st,
+                                device_normalize=True)
+    item = d[0]
+    assert list(item) == ["pet1451", "mri", "mri_mask", "tabular", "label", NORM_SPEC_KEY]
+    np.testing.assert_array_equal(item["pet1451"].numpy(), pet)
+    np.testing.assert_array_equal(item["mri"].numpy(), mri)
+    np.testing.assert_array_equal(item["mri_mask"].numpy(), mask)
+    batch = next(iter(torch.utils.data.DataLoader(d, batch_size=1)))
+    assert batch[NORM_SPEC_KEY] == [item[NORM_SPEC_KEY]]
+    spec = json.loads(item[NORM_SPEC_KEY])
+    assert spec == {"normalize_mri": nm, "normalize_pet": pet_st, "quantile": 0.99}
+    v = VolumeNormalizer(**spec)
+    assert (v.normalize_mri, v.normalize_pet, v.quantile) == (nm, pet_st, 0.99)
+    assert not _NORMALIZERS or all(isinstance(k, str) for k in _NORMALIZERS)
 
 
 def test_shard_sampler_covers_the_merged_samples():
