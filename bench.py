@@ -25,9 +25,11 @@ every step).  Under torchrun (``--collectives``):
     the node (tools/spin_contention.py: 16 CUs held through a step cost ~0.5 ms);
   * ``inside`` (``--graph``): the all-reduces captured inside the step graph.
 Rank 0 prints one JSON line.
-``roofline`` times the dominant kernel (layer4.0.conv2 forward, the lattice conv) with HIP
-events recorded around each of its launches, on the stream it runs on -- inside the timed
-region when eager, over eager steps just before the capture when graph-replayed;
+``roofline`` times the dominant kernel (layer4.0.conv2 forward, the lattice conv; ``frac`` on
+the MACs it executes, ``dense_frac`` on the dense count) and, under ``kernels``, also that
+conv's weight gradient (the largest single launch) with HIP events recorded around each of
+their launches, on the stream they run on -- inside the timed region when eager, over eager
+steps just before the capture when graph-replayed;
 ``cpu_baseline`` times the CPU oracle (torch fp32, the reference path) on a bounded sample.
 """
 import argparse
@@ -69,41 +71,66 @@ def hparams(precision):
 
 
 def dominant_desc(batch, size):
-    """layer4.0.conv2 (512->512, 3^3, dilation 4, 16^3 at 128^3 input): the largest
-    implicit-GEMM launch of the step."""
+    """layer4.0.conv2 (512->512, 3^3, dilation 4, 16^3 at 128^3 input): the largest conv of
+    the step (its forward, dgrad and weight gradient are the three largest launches)."""
     s = size // 8
     d = volume_ops.conv_desc((batch, 512, s, s, s), (512, 512, 3, 3, 3), (1, 1, 1),
                              (4, 4, 4), (4, 4, 4))
     return volume_ops._desc_tuple(d), 2.0 * batch * s ** 3 * 512 * 512 * 27
 
 
-def dominant_kernel_roofline(events, batch, size, dtype, where="timed region"):
-    """Average duration of the dominant kernel's launches, from the HIP event pairs
-    volume_ops recorded around each launch on its own stream (inside the timed region for
-    eager runs; over eager steps just before the capture for graph-replayed runs)."""
+def _traffic(op):
+    tf = os.path.join(REPO, "profiles", f"traffic_layer4_conv2_{op}.json")
+    if not os.path.exists(tf):
+        return None
+    with open(tf) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
+def kernel_roofline(op, events, batch, size, dtype, where):
+    """One launch record of layer4.0.conv2 (``op`` "fwd": lattice_zp_kernel; "wgrad":
+    lattice_wgrad_kernel + its slab reduce, one mmad_conv3d_wgrad call): average duration
+    from the HIP event pairs volume_ops recorded around each call on its own stream.
+
+    The residue-class kernels skip the MACs that land in the zero padding: per dimension 10
+    of the 12 (position, tap) pairs of a 4-point sub-lattice are real.  The forward skips
+    them in all three dimensions ((10/12)^3 = 57.9 % of the dense MACs run), the weight
+    gradient in y and x only (its z-padding taps read a zero block: (10/12)^2 = 69.4 %).
+    ``frac`` = executed FLOP/s / peak (what the MFMA pipes did); ``dense_frac`` prices the
+    dense count, as cuDNN / MIOpen report conv FLOPs, and can exceed 1."""
     _, flops = dominant_desc(batch, size)
     if not events:
         return None
     sec = sum(a.elapsed_time(b) for a, b in events) / len(events) / 1e3
     peak = PEAK_BF16 if dtype == torch.bfloat16 else PEAK_F32
-    traffic = None
-    tf = os.path.join(REPO, "profiles", "traffic_layer4_conv2_fwd.json")
-    if os.path.exists(tf):
-        with open(tf) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
     s = size // 8
-    # the residue-class kernel skips the MACs that land in the zero padding: per dimension
-    # 10 of the 12 (position, tap) pairs of a 4-point sub-lattice are real, (10/12)^3 of the
-    # dense count runs on the MFMA pipes (achieved / frac use the dense count, as cuDNN /
-    # MIOpen report conv FLOPs)
-    executed = flops * (10 / 12) ** 3 if s == 16 else flops
-    return {"kernel": f"lattice_zp_kernel layer4.0.conv2 fwd (512->512, 3^3 dil 4, "
-                      f"{batch}x{s}^3)",
-            "bound": "mfma", "achieved": flops / sec / 1e12, "peak": peak / 1e12,
-            "unit": "TFLOP/s", "frac": flops / sec / peak, "traffic": traffic,
+    lattice = s == 16 and dtype == torch.bfloat16
+    executed = flops * ((10 / 12) ** (3 if op == "fwd" else 2) if lattice else 1.0)
+    vox = batch * s ** 3 * 512 * 2                         # one bf16 activation tensor
+    wbytes = 512 * 512 * 27 * (2 if op == "fwd" else 4)    # bf16 packed in / fp32 dW out
+    algo = 2 * vox + wbytes                                # X + Y (or dY) + weights
+    name = ("lattice_zp_kernel" if lattice else "igemm_kernel") if op == "fwd" else \
+        ("lattice_wgrad_kernel + wgrad_reduce_t_kernel" if lattice else "wgrad_kernel + reduce")
+    return {"kernel": f"{name} layer4.0.conv2 {op} (512->512, 3^3 dil 4, {batch}x{s}^3)",
+            "bound": "mfma", "achieved": executed / sec / 1e12, "peak": peak / 1e12,
+            "unit": "TFLOP/s", "frac": executed / sec / peak, "traffic": _traffic(op),
+            "algorithmic_bytes": algo,
             "flop_per_launch": flops, "executed_flop_per_launch": executed,
-            "executed_frac": executed / sec / peak,
+            "executed_frac": executed / sec / peak, "dense_frac": flops / sec / peak,
             "avg_launch_ms": sec * 1e3, "launches": len(events), "probe": where}
+
+
+def dominant_kernel_roofline(events, wevents, batch, size, dtype, where="timed region"):
+    """``roofline``: the dominant kernel (layer4.0.conv2's forward, the lattice_zp family
+    that also runs its dgrad) at top level, and both it and the same conv's weight gradient
+    (the step's largest single launch) under ``kernels``."""
+    fwd = kernel_roofline("fwd", events, batch, size, dtype, where)
+    if fwd is None:
+        return None
+    out = dict(fwd)
+    wg = kernel_roofline("wgrad", wevents, batch, size, dtype, where)
+    out["kernels"] = [fwd] + ([wg] if wg is not None else [])
+    return out
 
 
 def host_cores():
@@ -286,11 +313,12 @@ def main():
     # the same kernels, bit-identical to eager steps (tests/test_graph_step_gpu.py); eager,
     # the host needs ~2.9 of the GPU's ~3.5 ms per step to enqueue it, so a slower or busier
     # host makes the run launch-bound (measured: 1713 vol/s on one box).  N>1 replays the
-    # same kernels with the backward split into stage graphs, each stage's RCCL all-reduce
-    # overlapping the next stage (tests/test_dp_graph_world2_gpu.py); --after issues every
-    # all-reduce after the backward, --graph captures them inside the graph (one-rank
-    # checked only), --eager launches them from the backward's hooks (host-bound).
-    events = []
+    # same kernels in the launch mode the warm-up probe picks (--collectives auto): "staged"
+    # (the backward as stage graphs, each stage's RCCL all-reduce overlapping the next),
+    # "staged1" (one cut) or "after" (one all-reduce after the backward; the pick on one
+    # rank) -- tests/test_dp_graph_world2_gpu.py; --graph captures them inside the graph
+    # (one-rank checked only), --eager launches them from the backward's hooks (host-bound).
+    events, wevents = [], []
     if use_graph:
         if not args.no_roofline:
             # the dominant-kernel probe (HIP events around its launches) cannot sit inside a
@@ -301,10 +329,12 @@ def main():
                 step()
             if rank == 0:
                 volume_ops.FWD_PROBES[dominant_desc(B, S)[0]] = events
+                volume_ops.WGRAD_PROBES[dominant_desc(B, S)[0]] = wevents
             for _ in range(max(10, args.warmup)):
                 step()
             torch.cuda.synchronize()
             volume_ops.FWD_PROBES.clear()
+            volume_ops.WGRAD_PROBES.clear()
         probe = {}
         if dp and mode == "auto":
             # capture each candidate in turn, time a few replays (max over ranks), drop it;
@@ -345,6 +375,7 @@ def main():
         dist.barrier()
     if rank == 0 and not args.no_roofline and not use_graph:
         volume_ops.FWD_PROBES[dominant_desc(B, S)[0]] = events
+        volume_ops.WGRAD_PROBES[dominant_desc(B, S)[0]] = wevents
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -352,6 +383,7 @@ def main():
     t_issue = time.perf_counter() - t0     # host time to enqueue the K steps (diagnostic)
     torch.cuda.synchronize()
     volume_ops.FWD_PROBES.clear()
+    volume_ops.WGRAD_PROBES.clear()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -416,7 +448,7 @@ def main():
             result["dp"]["auto_probe_ms_per_step"] = {k: round(v, 4) for k, v in probe.items()}
     if rank == 0 and not args.no_roofline:
         result["roofline"] = dominant_kernel_roofline(
-            events, B, S, cdtype,
+            events, wevents, B, S, cdtype,
             "eager steps before the graph capture" if use_graph else "timed region")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(S)

@@ -10,13 +10,9 @@
 // epilogue, so a BN that follows one of our convs needs no separate statistics pass.
 #include "common.h"
 
-// rows in flight per thread of the column sums (16-byte rows), single and dual forms
-#ifndef COLSUM_U
-#define COLSUM_U 4
-#endif
-#ifndef COLSUM_UD
-#define COLSUM_UD 4
-#endif
+// rows in flight per thread of the column sums (16-byte rows; round 4 measured 2 and 8
+// for the single and dual forms, neither faster)
+constexpr int COLSUM_ROWS = 4;
 
 namespace {
 
@@ -138,7 +134,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
       // 4 rows' 16-byte loads issued before any is used (the loop is load-latency bound:
       // 512-1024 blocks of 4 waves keep too few bytes in flight with one row at a time);
       // rows are still added in the same order
-      constexpr int U = DUAL ? COLSUM_UD : COLSUM_U;
+      constexpr int U = COLSUM_ROWS;
       for (; r + (U - 1) * rpar < r1; r += U * rpar) {
         u32x4 yr[U], gr[U], orr[U], y2r[U], g2r[U];
 #pragma unroll

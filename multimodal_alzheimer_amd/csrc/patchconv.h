@@ -27,7 +27,6 @@ int fwd(const Geo& g, const void* src, const void* wp, const float* bias, void* 
 // boxes (patchz.hip, layer1): mmad_patch::fwd / tiles route to it when ok().
 namespace mmad_patchz {
 int set_mode(int v);              // MMAD_PATCHZ at run time; returns the previous mode
-int set_bs_mode(int v);           // MMAD_PATCHZ_BS (weight-stationary kernel) at run time
 bool ok(const mmad_patch::Geo& g);
 int64_t tiles(const mmad_patch::Geo& g);
 int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,

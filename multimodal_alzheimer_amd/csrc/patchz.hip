@@ -374,266 +374,6 @@ __global__ __launch_bounds__(NTHR) void patchz_conv_kernel(PZ g, const u16* __re
   box(g.tps - 1, std::false_type{}, std::true_type{});
 }
 
-// ---- weight-stationary form (round 4) ------------------------------------------------
-// The kernel above streams every tap's 64 x 64 weights (8 KiB) into LDS once per 4 x 8 x 8
-// box: 216 KiB of LDS-DMA per 256 output rows against 51 KiB of input planes, and its
-// skeleton without MFMAs took 44 of its 64 us (r04b: tools/probe_kernel.py --time on
-// variants built with PZ_NO_MMA / PZ_NO_EPI) -- the weight stream, not the MFMA, set the
-// time.  Here the weights never move after the prologue: wave (cb, kh) holds the 16 output
-// channels 16 cb .. of its co block times the 32 input channels 32 kh .. of all 27 taps as
-// MFMA B operands in registers (27 x 16 B per lane, loaded once per block), and the LDS
-// holds only the input-plane ring.  Per tap each wave reads the 16 A fragments of the box
-// (256 rows x its 32-channel K half) and runs 16 MFMAs; no per-tap barrier.  The two K
-// halves of every output are added through LDS in the epilogue (kh = 0 finalises the box's
-// first two planes, kh = 1 the last two, each adding the partner's partials in a fixed
-// order), so outputs are deterministic; per element the sum is (taps of ci 0-31) + (taps of
-// ci 32-63), a different order than the kernel above (results agree to fp32 rounding).
-// Planes: the box's six input planes are resident at its start; the next box's planes
-// 4i+6, 4i+7 go into slots freed by box i-1 right away, 4i+8 after the kz = 0 taps (which
-// alone read plane 4i) and 4i+9 after the kz = 1 taps (plane 4i+1), each behind a barrier.
-constexpr int BS_NA = 8;                        // A fragments in flight per wave
-constexpr int BS_STEPS = TAPS * 16;             // (tap, fragment) steps per box
-constexpr int BS_XB = 256 * CROW;               // exchange / staging region (36 KiB)
-constexpr int BS_RED = RING_OFF;                // BN sums of the kh = 1 waves after the ring
-constexpr int BS_XOFF = BS_RED + 4 * 32 * 4;
-constexpr int BS_LDS = BS_XOFF + BS_XB;
-static_assert(BS_LDS <= 160 * 1024, "LDS budget");
-constexpr int BS_EPI_ST = 4;                    // output stores per wave per box
-constexpr int BS_STATS_ST = 2;                  // BN partial-sum stores (kh = 0 waves)
-
-__device__ __forceinline__ void lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-__global__ __launch_bounds__(NTHR) void patchz_bs_kernel(PZ g, const u16* __restrict__ src,
-                                                         const u16* __restrict__ wgt,
-                                                         const float* __restrict__ bias,
-                                                         u16* __restrict__ dst,
-                                                         float* __restrict__ stats) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-  const int item = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  int t1 = item;
-  const int seg = t1 % g.nseg;
-  t1 /= g.nseg;
-  const int nt = t1 % g.nbn;
-  t1 /= g.nbn;
-  const int bx = t1 % g.ntx;
-  t1 /= g.ntx;
-  const int by = t1 % g.nty;
-  const int n = t1 / g.nty;
-  const int y0 = by * 8, x0 = bx * 8, n0 = nt * 64;
-  const int zs = seg * g.tps * 4;
-  const int HW = g.H * g.W;
-  const int cb = wave & 3, kh = wave >> 2;
-  const int lr = lane & 15, lk = lane >> 4;
-
-  // ---- the wave's weights: B[t] = W[n0 + 16 cb + lr][tap t][32 kh + 8 lk .. + 7]
-  bf16x8 B[TAPS];
-  {
-    const u16* wl = wgt + (int64_t)(n0 + cb * 16 + lr) * g.Kpad + kh * 32 + lk * 8;
-#pragma unroll
-    for (int t = 0; t < TAPS; ++t) B[t] = *reinterpret_cast<const bf16x8*>(wl + t * 64);
-  }
-
-  // ---- plane DMA (as the kernel above): plane q (input z = zs - 1 + q) -> slot q % 8
-  const u16* __restrict__ srcn = src + (int64_t)n * g.D * HW * 64;
-  int poff[2];
-  uint32_t pdst[2];
-  {
-    const int lrow = lane >> 3;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int p = min(wave + NW * h, 12);
-      const int r = p * 8 + lrow;
-      const int px = r % PX, py = r / PX;
-      const int y = y0 - 1 + py, x = x0 - 1 + px;
-      const bool in = r < PROWS && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
-      const int chunk = (lane & 7) ^ (px & 7);
-      poff[h] = in ? (y * g.W + x) * 64 + chunk * 8 : -1;
-      pdst[h] = p * 1024;
-    }
-  }
-  auto issue_plane = [&](int q) __attribute__((always_inline)) {
-    const int z = zs - 1 + q;
-    const bool zin = (unsigned)z < (unsigned)g.D;
-    const u16* base = srcn + (int64_t)(zin ? z : 0) * HW * 64;
-    char* slot = smem + (q & (NPS - 1)) * PSLOT;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const void* p = (zin && poff[h] >= 0) ? (const void*)(base + poff[h]) : (const void*)g_zero16z;
-      glds16_asm(p, lds_addr_of(slot + pdst[h]));
-    }
-  };
-
-  // ---- A fragment F (rows 16 F .. + 15 of the box: plane F >> 2, y rows 2 (F & 3) + lr >> 3,
-  // x = lr & 7) of tap T, the wave's K half: lane address = slot + aoff[kx] + row immediate
-  uint32_t aoff[3];
-#pragma unroll
-  for (int kx = 0; kx < 3; ++kx)
-    aoff[kx] = (uint32_t)(((lr >> 3) * PX + (lr & 7) + kx) * RB +
-                          (((4 * kh + lk) ^ (((lr & 7) + kx) & 7)) << 4));
-  f32x4 acc[16];
-  bf16x8 a[BS_NA];
-  auto rd = [&](auto sc, int q0) __attribute__((always_inline)) {
-    constexpr int S = decltype(sc)::value;
-    if constexpr (S < BS_STEPS) {
-      constexpr int T = S / 16, F = S % 16;
-      constexpr int kz = T / 9, ky = (T / 3) % 3, kx = T % 3;
-      int pbase = __builtin_amdgcn_readfirstlane(((q0 + (F >> 2) + kz) & (NPS - 1)) * PSLOT);
-      asm volatile("" : "+s"(pbase));
-#ifdef PZB_NO_READ   // timing skeleton (tools): no LDS fragment reads
-      bf16x8 av;
-      asm volatile("" : "=v"(av) : "s"(pbase));
-      a[S % BS_NA] = av;
-#else
-      a[S % BS_NA] = *reinterpret_cast<const bf16x8*>(smem + pbase + aoff[kx] +
-                                                      (2 * (F & 3) + ky) * PX * RB);
-#endif
-    }
-  };
-  auto mm = [&](auto sc) __attribute__((always_inline)) {
-    constexpr int S = decltype(sc)::value;
-    constexpr int T = S / 16, F = S % 16;
-#ifdef PZB_NO_MMA    // timing skeleton (tools): fragments consumed, no MFMA
-    const bf16x8 av = a[S % BS_NA], bw = B[T];
-    asm volatile("" ::"v"(av), "v"(bw));
-#else
-    acc[F] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[S % BS_NA], B[T], acc[F], 0, 0, 0);
-#endif
-  };
-
-  float bv = bias != nullptr ? bias[n0 + cb * 16 + lr] : 0.f;
-  asm volatile("" ::"v"(bv));
-  const int64_t nbase = (int64_t)n * g.D;
-  float* xb = reinterpret_cast<float*>(smem + BS_XOFF);
-  float* red = reinterpret_cast<float*>(smem + BS_RED);
-
-  // ---- epilogue of box i: K-half exchange, BN partial sums, staged 16-byte stores
-  auto epilogue = [&](int i) __attribute__((always_inline)) {
-    const int z0 = zs + 4 * i;
-    // frag f is finalised by kh = f >> 3; two rounds of 4 fragments each way
-#pragma unroll
-    for (int rnd = 0; rnd < 2; ++rnd) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int fs = (kh == 0 ? 8 : 0) + 4 * rnd + j;      // a fragment the partner owns
-        f32x4* slot = reinterpret_cast<f32x4*>(xb) + ((wave * 4 + j) * 64 + lane);
-        *slot = kh == 0 ? acc[8 + 4 * rnd + j] : acc[4 * rnd + j];
-        (void)fs;
-      }
-      lds_sync();
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int pw = wave ^ 4;                             // partner: same cb, other kh
-        const f32x4 v = reinterpret_cast<const f32x4*>(xb)[(pw * 4 + j) * 64 + lane];
-        if (kh == 0) acc[4 * rnd + j] += v;
-        else acc[8 + 4 * rnd + j] += v;
-      }
-      lds_sync();
-    }
-    // BN partial sums of the wave's 8 final fragments (kh = 0: rows 0..127, kh = 1: 128..255)
-    float cs = 0.f, cq = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f32x4 v = kh == 0 ? acc[j] : acc[8 + j];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float o = v[r] + bv;
-        cs += o;
-        cq += o * o;
-      }
-    }
-    if (stats != nullptr) {
-      cs += __shfl_xor(cs, 16, 64);
-      cs += __shfl_xor(cs, 32, 64);
-      cq += __shfl_xor(cq, 16, 64);
-      cq += __shfl_xor(cq, 32, 64);
-      if (kh == 1 && lk == 0) {
-        red[cb * 32 + lr] = cs;
-        red[cb * 32 + 16 + lr] = cq;
-      }
-    }
-    // stage the bf16 box: row-major [256][CROW], columns 16 cb + lr
-    u16* ctile = reinterpret_cast<u16*>(xb);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f32x4 v = kh == 0 ? acc[j] : acc[8 + j];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = (kh * 8 + j) * 16 + lk * 4 + r;
-        ctile[row * (CROW / 2) + cb * 16 + lr] = f2bf(v[r] + bv);
-      }
-    }
-    lds_sync();
-    if (stats != nullptr && kh == 0) {
-      const int64_t mt = (((int64_t)n * (g.D / 4) + z0 / 4) * g.nty + by) * g.ntx + bx;
-      float* srow = stats + (mt * 2) * g.Nd + n0 + cb * 16 + lr;
-      st_f32(srow, cs + red[cb * 32 + lr]);             // fixed order: deterministic
-      st_f32(srow + g.Nd, cq + red[cb * 32 + 16 + lr]);
-    }
-#pragma unroll
-    for (int h = 0; h < BS_EPI_ST; ++h) {               // 256 rows x 8 chunks / 512 threads
-      const int qd = tid + NTHR * h;
-      const int v = qd >> 3, c8 = qd & 7;
-      const int64_t vox =
-          ((nbase + z0 + (v >> 6)) * g.H + y0 + ((v >> 3) & 7)) * g.W + x0 + (v & 7);
-      const int64_t o = vox * g.Nd + n0 + c8 * 8;
-      u32x4 val = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
-                                                  v * CROW + c8 * 16);
-      if (g.res != nullptr || g.relu) val = epi_res_relu(val, g.res ? g.res + o : nullptr, g.relu);
-      st_u32x4(dst + o, val);
-    }
-  };
-
-  // ---- prologue: the first box's six planes (the weight loads above are older)
-  for (int q = 0; q < 6; ++q) issue_plane(q);
-
-  auto box = [&](int i, auto nextc) __attribute__((always_inline)) {
-    constexpr bool NEXT = decltype(nextc)::value;
-    const int q0 = 4 * i;
-    // this box's planes have landed: every VMEM op except the previous box's epilogue stores
-    if (i == 0) {
-      wait_vm_lgkm0<0>();
-    } else if (stats != nullptr && kh == 0) {
-      wait_vm_lgkm0<BS_EPI_ST + BS_STATS_ST>();
-    } else {
-      wait_vm_lgkm0<BS_EPI_ST>();
-    }
-    raw_barrier();
-    if constexpr (NEXT) {                       // slots of planes 4i-2, 4i-1: free
-      issue_plane(q0 + 6);
-      issue_plane(q0 + 7);
-    }
-#pragma unroll
-    for (int f = 0; f < 16; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-    [&]<int... S>(std::integer_sequence<int, S...>) {
-      (rd(std::integral_constant<int, S>{}, q0), ...);
-    }(std::make_integer_sequence<int, BS_NA>{});
-    [&]<int... S>(std::integer_sequence<int, S...>) {
-      ((mm(std::integral_constant<int, S>{}), rd(std::integral_constant<int, S + BS_NA>{}, q0),
-        // keep each read BS_NA steps ahead of its MFMA (the scheduler would pull it close)
-        __builtin_amdgcn_sched_barrier(0),
-        (S == 9 * 16 - 1 || S == 18 * 16 - 1)
-            ? [&] {
-                // kz = 0 taps done (plane 4i dead) / kz = 1 taps done (plane 4i+1 dead)
-                lds_sync();
-                if constexpr (NEXT) issue_plane(q0 + (S == 9 * 16 - 1 ? 8 : 9));
-              }()
-            : void()),
-       ...);
-    }(std::make_integer_sequence<int, BS_STEPS>{});
-    epilogue(i);
-  };
-  for (int i = 0; i + 1 < g.tps; ++i) box(i, std::true_type{});
-  box(g.tps - 1, std::false_type{});
-}
-
 std::atomic<int> g_patchz_mode{-1};
 int patchz_mode() {
   int v = g_patchz_mode.load(std::memory_order_relaxed);
@@ -645,22 +385,6 @@ int patchz_mode() {
   }
   return v;
 }
-
-// MMAD_PATCHZ_BS: 1 the weight-stationary kernel, 0 (default) the weight-streaming one
-// (a 32x32-tile stationary form was tried in round 4: it spilled and was dropped);
-// mmad_set_kernel_variant("patchz_bs", v) at run time
-std::atomic<int> g_bs_mode{-1};
-int bs_mode() {
-  int v = g_bs_mode.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("MMAD_PATCHZ_BS");
-    int expect = -1;
-    g_bs_mode.compare_exchange_strong(expect, e ? atoi(e) : 0);
-    v = g_bs_mode.load(std::memory_order_relaxed);
-  }
-  return v;
-}
-bool bs_on() { return bs_mode() != 0; }
 
 // z segments per column: the fewest that give every CU a work item, each >= 2 boxes
 int segments(const mmad_patch::Geo& q) {
@@ -678,12 +402,6 @@ namespace mmad_patchz {
 int set_mode(int v) {
   const int prev = patchz_mode();
   if (v >= 0) g_patchz_mode.store(v, std::memory_order_relaxed);
-  return prev;
-}
-
-int set_bs_mode(int v) {
-  const int prev = bs_mode();
-  if (v >= 0) g_bs_mode.store(v, std::memory_order_relaxed);
   return prev;
 }
 
@@ -712,9 +430,7 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
   if (!mmad_patchz::ok(q)) return MMAD_EUNSUPPORTED;
   static const bool attr =
       hipFuncSetAttribute((const void*)patchz_conv_kernel,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS) == hipSuccess &&
-      hipFuncSetAttribute((const void*)patchz_bs_kernel,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, BS_LDS) == hipSuccess;
+                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS) == hipSuccess;
   if (!attr) return MMAD_EUNSUPPORTED;
   PZ g{};
   g.nb = q.nb; g.Nd = q.Nd; g.Kpad = q.Kpad; g.D = q.Dd; g.H = q.Hd; g.W = q.Wd;
@@ -724,14 +440,9 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
   g.res = reinterpret_cast<const u16*>(q.res);
   g.relu = q.relu;
   const int64_t items = (int64_t)q.nb * g.nty * g.ntx * g.nbn * g.nseg;
-  if (bs_on())
-    hipLaunchKernelGGL(patchz_bs_kernel, dim3((unsigned)items), dim3(NTHR), BS_LDS,
-                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                       stats);
-  else
-    hipLaunchKernelGGL(patchz_conv_kernel, dim3((unsigned)items), dim3(NTHR), LDS,
-                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                       stats);
+  hipLaunchKernelGGL(patchz_conv_kernel, dim3((unsigned)items), dim3(NTHR), LDS,
+                     as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
+                     stats);
   return launch_status();
 }
 

@@ -75,19 +75,6 @@ struct PWG {
 
 __device__ __forceinline__ int pw_wsz128(int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); }
 
-// PW_XSWZ (32-wide and 16-wide forms): the X image's two 32-byte row halves swap on rows with
-// bit 3 set.  A transposing fragment read of 32 lanes covers image rows {r .. r + 3} and
-// {r + 8 .. r + 11}; 64-byte rows put rows r and r + 8 on the same 16 banks (2-way conflict,
-// 37 % of the kernel's LDS cycles in round 3); with the swap they take the other half's banks.
-// The DMA fetches the swapped chunk from the source, and each read adds its row's half offset
-// (the tap shift moves the row, so that offset is per read: a few VALU ops).  Measured r04ae:
-// bit-identical, but layer1's pwgrad 47.5 -> 54.9 us and layer2's 29.3 -> 32.5 us (the per-read
-// offsets and +14-22 VGPRs cost more than the conflicts did), so off by default.
-#ifndef PW_XSWZ
-#define PW_XSWZ 0
-#endif
-__device__ __forceinline__ int pw_xsw(int row) { return PW_XSWZ ? (row >> 2) & 2 : 0; }
-
 template <int MODE>
 __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __restrict__ x,
                                                          const u16* __restrict__ dy,
@@ -139,15 +126,12 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
     } else if constexpr (W16) {
       const int yv = row / XR - 1, xv = row % XR - 1;
       const bool ok = row < C::XROWS && (unsigned)yv < (unsigned)g.H && (unsigned)xv < 16u;
-      return ok ? (uint32_t)(((yv * 16 + xv) * g.Cs + ci0 + ((lane & 3) ^ pw_xsw(row)) * 8) * 2)
-                : PW_OOB;
+      return ok ? (uint32_t)(((yv * 16 + xv) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
     } else {
       const int yv = y0 - 1 + row / XR, xv = row % XR - 1;
       const bool ok = row < C::XROWS && (unsigned)yv < (unsigned)g.H &&
                       (unsigned)xv < (unsigned)PW_XW;
-      return ok ? (uint32_t)(((yv * PW_XW + xv) * g.Cs + ci0 + ((lane & 3) ^ pw_xsw(row)) * 8) *
-                             2)
-                : PW_OOB;
+      return ok ? (uint32_t)(((yv * PW_XW + xv) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
     }
   };
   const uint32_t xplane = LAT ? (uint32_t)(16 * 16 * g.Cs * 2) : (uint32_t)(g.H * VW * g.Cs * 2);
@@ -200,10 +184,8 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   // (LAT: the 16-lane group lk reads segment lk, whose image positions start at 10 lk)
   // (W16: groups lk = 0, 1 read x 0-7, 8-15 of segment 0 -- image row y -- and lk = 2, 3 those
   // of segment 1, one image row group (18 positions) further)
-  // this lane's image row within a fragment read (plus the tap's row offset r0)
-  const int xrow = LAT ? 10 * lk + q4 : W16 ? 18 * (lk >> 1) + 8 * (lk & 1) + q4 : rsel;
-  constexpr bool XSW = PW_XSWZ && MODE != 1;       // (the residue-class image is not swapped)
-  const uint32_t xb = (uint32_t)(xrow * 64 + (XSW ? 0 : cf * 32) + 8 * p4);
+  const uint32_t xb = (uint32_t)((LAT ? 10 * lk + q4 : W16 ? 18 * (lk >> 1) + 8 * (lk & 1) + q4 : rsel) *
+                                     64 + cf * 32 + 8 * p4);
   f32x4 acc[4][7];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -238,7 +220,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
       return !LAT || ((unsigned)(yl + (t / 3) % 3 - 1) < 8u);
     };
     // one K step = output row YL of the current plane (compile time)
-    auto kread = [&](const char* yimg, auto qc, auto ylc, PFr& f, int xr) {
+    auto kread = [&](const char* yimg, auto qc, auto ylc, PFr& f) {
       constexpr int Q = decltype(qc)::value, YL = decltype(ylc)::value;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -252,16 +234,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
           constexpr int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;   // 0..2 (shift + 1)
           constexpr int r0 = ((W16 ? 2 : 1) * YL + ky) * XR + kx;
           const char* img = xbase[kz] + r0 * 64;
-          if constexpr (XSW) {
-            // the half this lane reads in rows xrow + r0 and xrow + r0 + 4 (see pw_xsw)
-            const int hlo = (cf ^ (((xr + r0) >> 3) & 1)) << 5;
-            const int hhi = (cf ^ (((xr + r0 + 4) >> 3) & 1)) << 5;
-            f.b[K] = __builtin_shufflevector(tr8(img + hlo), tr8(img + 4 * 64 + hhi), 0, 1, 2, 3,
-                                             4, 5, 6, 7);
-          } else {
-            f.b[K] = __builtin_shufflevector(tr8(img), tr8(img + 4 * 64), 0, 1, 2, 3, 4, 5, 6,
-                                             7);
-          }
+          f.b[K] = __builtin_shufflevector(tr8(img), tr8(img + 4 * 64), 0, 1, 2, 3, 4, 5, 6, 7);
         }
       };
       one(std::integral_constant<int, 0>{});
@@ -336,15 +309,10 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
         int yoff = C::Y_OFF + (s % PW_YSLOTS) * PW_YST;
         asm volatile("" : "+s"(yoff));
         const char* yimg = smem + yoff;
-        // (xr opaque per stage: the per-tap row-half offsets of the X reads are computed
-        // where they are used, not hoisted and held across the plane loop -- spills)
-        int xr = xrow;
-        if constexpr (XSW) asm volatile("" : "+v"(xr));
         PFr f0, f1;
-        kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, f0,
-              xr);
+        kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, f0);
         kread(yimg, std::integral_constant<int, 1>{}, std::integral_constant<int, 2 * M + 1>{},
-              f1, xr);
+              f1);
         kmma(f0, std::integral_constant<int, 2 * M>{});
         kmma(f1, std::integral_constant<int, 2 * M + 1>{});
       };

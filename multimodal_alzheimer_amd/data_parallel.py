@@ -28,6 +28,7 @@ import os
 
 import torch
 import torch.distributed as dist
+from torch.autograd.graph import increment_version
 
 
 def shard_indices(n_samples, rank, world, epoch=0, shuffle=True, seed=15):
@@ -75,6 +76,9 @@ def broadcast_module_state(module, src=0, group=None, buffers_only=False):
     with torch.no_grad():
         for t in ts:
             dist.broadcast(t.data, src=src, group=group)
+            # a write through .data leaves the version counter alone; bump it so consumers
+            # that cache derived layouts (graph_step's packed bf16 weights) see the change
+            increment_version(t)
 
 
 # MMAD_DP_GRAD_SLOTS=0: conv weight gradients go to fresh tensors and are copied into the

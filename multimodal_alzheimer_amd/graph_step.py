@@ -17,7 +17,8 @@ first replay.
 With a data-parallel gradient all-reduce (``reducer``, data_parallel.GradAllReduce) there
 are three ways to place the RCCL collectives (``collectives=``):
 
-* ``"staged"`` (bench.py's default at N > 1): the backward is split at backbone stage
+* ``"staged"`` (one of the three modes bench.py's ``auto`` default probes at N > 1; it
+  picks the fastest, ``after`` on one rank): the backward is split at backbone stage
   boundaries (``backward_stages``: head + layer4 | layer3 | layer2 | layer1 + stem of every
   MedicalNet ResNet in the model) and each part is captured as its own graph
   (``StagedBackward``: ``torch.autograd.grad`` from the previous boundary's gradients to
@@ -234,6 +235,15 @@ class GraphedTrainStep:
             self.fused.step()
         else:
             self.optimizer.step()
+
+    def refresh(self):
+        """Repack the bf16 weight layouts from the current fp32 weights.  Replays do this by
+        themselves when a parameter's ``_version`` moved (an in-place op, or a helper that
+        bumps it, as data_parallel.broadcast_module_state does); call it after editing
+        weights through ``.data``, which the version counter does not see."""
+        if self.fused is not None:
+            self.fused.refresh()
+            self._versions = self._param_versions()
 
     def _param_versions(self):
         if self.fused is None:

@@ -156,7 +156,9 @@ def _gap_linear_run(mods, i, x):
     if not (isinstance(x, torch.Tensor) and x.dim() == 5 and x.is_cuda and
             x.dtype in (torch.float32, torch.bfloat16)):
         return 0
-    relu = i + 3 < len(mods) and type(mods[i + 3]) is ReLU
+    if x.shape[1] != lin.in_features:           # unfused: the Linear raises its shape error
+        return 0
+    relu =i + 3 < len(mods) and type(mods[i + 3]) is ReLU
     used = mods[i:i + (4 if relu else 3)]
     if any(u._forward_hooks or u._forward_pre_hooks for u in used):
         return 0

@@ -68,6 +68,9 @@ def _desc_tuple(d):
 # Live kernel timing: map a conv descriptor tuple to a list; every forward launch with that
 # geometry appends a (start, end) HIP event pair recorded on the launch stream around it.
 FWD_PROBES = {}
+# the same for the weight gradient (the event pair brackets the whole mmad_conv3d_wgrad call:
+# the MFMA kernel and its slab reduce)
+WGRAD_PROBES = {}
 
 # training-mode BN statistic updates so far (the running buffers are written by our kernels,
 # which torch's tensor version counters do not see); keys the eval-mode folded-weight caches
@@ -484,8 +487,15 @@ def _wgrad(ctx, d, dt, src, gy, weight, wparam=None, rside=None):
                 t.record_stream(rside)
         _queue_join(torch.cuda.current_stream(), rside)
     else:
+        probe = WGRAD_PROBES.get(_desc_tuple(d)) if WGRAD_PROBES else None
+        if probe is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         L.call("mmad_conv3d_wgrad", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(db),
                L.ptr(ws), L.stream())
+        if probe is not None:
+            e1.record()
+            probe.append((e0, e1))
     if padded:                             # cut the zero-lane channels back off
         taps = d.kd * d.kh * d.kw
         dw = _pad_rows(dw, d.co, d.ci * taps, ctx.ci_real * taps, weight.shape)

@@ -4,7 +4,7 @@
 Two processes share the test box's one GPU (RCCL refuses two ranks on one device, so the
 collective is gloo over the same CUDA tensors); everything else is the benched path:
 ``GraphedTrainStep(reducer=GradAllReduce(...), collectives=mode)`` for
-  * "staged" (bench.py's default at N > 1): the backward replayed as four captured graphs
+  * "staged" (one of the modes bench.py's "auto" default probes at N > 1): the backward replayed as four captured graphs
     (head + layer4 | layer3 | layer2 | layer1 + stem of both backbones), each stage's bucket
     all-reduced on the side stream while the next graph replays;
   * "after": forward + backward in one graph, every bucket all-reduced after it.

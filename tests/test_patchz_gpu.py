@@ -1,17 +1,12 @@
 """Persistent z-walking layer1 conv (csrc/patchz.hip) at BASELINE config 2's layer1 shape
-(8 x 64 x 32^3), both of its forms:
-
-* weight-streaming (``patchz_bs`` 0): accumulates every output element in the same K order
-  as the per-box patch conv (csrc/patchconv.hip) it replaces (tap-major, 32-channel halves),
-  so forward outputs and input gradients must be bit-identical to it;
-* weight-stationary (``patchz_bs`` 1, the default): each wave keeps its weights in
-  registers and the two 32-channel K halves are added in the epilogue, a different
-  summation order -- checked against a plain fp32 PyTorch conv of the same bf16 operands
-  (one bf16 rounding + fp32 sums: |err| <= 2^-7 |ref| + 1e-3 max|ref|) and against the
-  patch conv to one bf16 rounding step.
+(8 x 64 x 32^3): it accumulates every output element in the same K order as the per-box
+patch conv (csrc/patchconv.hip) it replaces (tap-major, 32-channel halves), so forward
+outputs and input gradients must be bit-identical to it, and within one bf16 rounding of a
+plain fp32 PyTorch conv of the same bf16 operands (|err| <= 2^-7 |ref| + 1e-3 max|ref|).
 The BN partial sums are grouped into different rows (4x8x8 boxes instead of 2x8x8), so their
 per-channel totals agree to fp32 rounding.  Also: the eval-mode epilogue (residual + ReLU),
-and grids whose columns need several z segments (mode 2 at batch 1, a 16^3 grid)."""
+and grids whose columns need several z segments (mode 2 at batch 1, a 16^3 grid).  (The
+round-4 weight-stationary form measured no faster and was removed in round 5.)"""
 import pytest
 import torch
 
@@ -61,39 +56,31 @@ IDS = ["config2_layer1", "batch1_segments", "grid16"]
 
 
 @pytest.mark.parametrize("n,size,mode", CASES, ids=IDS)
-@pytest.mark.parametrize("bs", [0, 1], ids=["streaming", "stationary"])
-def test_patchz_matches_patch_and_fp32(n, size, mode, bs):
+def test_patchz_matches_patch_and_fp32(n, size, mode):
     g = torch.Generator(device=DEV).manual_seed(size + n)
     x = (torch.rand((n, 64, size, size, size), generator=g, device=DEV) * 2 - 1).to(BF) \
         .contiguous(memory_format=CL)
     w = (torch.rand((64, 64, 3, 3, 3), generator=g, device=DEV) * 2 - 1) * (3.0 / (64 * 27)) ** 0.5
-    prev, prev_bs = _variant("patchz", 0), _variant("patchz_bs", bs)
+    prev = _variant("patchz", 0)
     try:
         ref = _conv(x, w)
         _variant("patchz", mode)
         got = _conv(x, w)
     finally:
         _variant("patchz", prev)
-        _variant("patchz_bs", prev_bs)
     assert got[4] == n * (size // 4) * (size // 8) ** 2, "not routed to the z-walking kernel"
     assert torch.equal(got[3], ref[3]), "weight gradient differs (same wgrad kernel)"
-    if bs == 0:
-        assert torch.equal(got[0], ref[0]), "forward differs"
-        assert torch.equal(got[2], ref[2]), "input gradient differs"
-    else:
-        # a different fp32 summation order: the bf16 outputs differ by at most one rounding
-        _close(got[0], ref[0], "forward vs patch conv", rel=2 ** -7, absf=1e-4)
-        _close(got[2], ref[2], "input gradient vs patch conv", rel=2 ** -7, absf=1e-4)
-        yr, dxr = _ref_conv(x, w, got[5])
-        _close(got[0], yr, "forward vs fp32")
-        _close(got[2], dxr, "input gradient vs fp32")
+    assert torch.equal(got[0], ref[0]), "forward differs"
+    assert torch.equal(got[2], ref[2]), "input gradient differs"
+    yr, dxr = _ref_conv(x, w, got[5])
+    _close(got[0], yr, "forward vs fp32")
+    _close(got[2], dxr, "input gradient vs fp32")
     y = ref[0].float()
     mag = torch.stack((y.abs().sum(dim=(0, 2, 3, 4)), (y * y).sum(dim=(0, 2, 3, 4))))
     assert ((got[1] - ref[1]).abs() <= 1e-5 * mag + 1e-6).all(), "BN partial-sum totals differ"
 
 
-@pytest.mark.parametrize("bs", [0, 1], ids=["streaming", "stationary"])
-def test_patchz_eval_epilogue_residual_relu(bs):
+def test_patchz_eval_epilogue_residual_relu():
     from multimodal_alzheimer_amd import layers as Lyr
     torch.manual_seed(7)
     conv = Lyr.Conv3d(64, 64, 3, padding=1, bias=False).to(DEV)
@@ -107,7 +94,7 @@ def test_patchz_eval_epilogue_residual_relu(bs):
         .contiguous(memory_format=CL)
     res = (torch.rand((8, 64, 32, 32, 32), generator=g, device=DEV) * 2 - 1).to(BF) \
         .contiguous(memory_format=CL)
-    prev, prev_bs = _variant("patchz", 0), _variant("patchz_bs", bs)
+    prev = _variant("patchz", 0)
     try:
         with torch.no_grad():
             ref = V.conv_bn_act_eval(x, conv, bn, relu=True, res=res)
@@ -116,12 +103,4 @@ def test_patchz_eval_epilogue_residual_relu(bs):
         torch.cuda.synchronize()
     finally:
         _variant("patchz", prev)
-        _variant("patchz_bs", prev_bs)
-    if bs == 0:
-        assert torch.equal(got, ref)
-    else:
-        # conv + shift is rounded to bf16 before the residual is added (and the sum rounded
-        # again): one rounding of the intermediate, whose magnitude is bounded by |out| + |res|
-        err = (got.float() - ref.float()).abs()
-        bound = 2 ** -7 * (ref.float().abs() + res.float().abs()) + 1e-3 * ref.float().abs().max()
-        assert (err <= bound).all(), f"eval epilogue: max|err| {err.max().item():.3e}"
+    assert torch.equal(got, ref)

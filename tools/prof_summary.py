@@ -83,29 +83,42 @@ def dispatches(d, name):
     return "\n".join(out)
 
 
-def counter(d, name):
+FWD_KERNELS = ("igemm_kernel", "lattice_conv_kernel", "lattice_zp_kernel")
+WGRAD_KERNELS = ("lattice_wgrad_kernel", "wgrad_reduce_t_kernel")
+LABELS = {"fwd": "layer4.0.conv2 fwd residue-class kernel (bf16, 8x512x16^3, 3^3 dil 4)",
+          "wgrad": "layer4.0.conv2 wgrad: lattice_wgrad_kernel + its slab reduce "
+                   "(bf16, 8x512x16^3, 3^3 dil 4)"}
+
+
+def counter(d, name, kernels=FWD_KERNELS):
+    """per-launch values of one counter, {kernel: [values in launch order]}"""
     rows = list(csv.DictReader(open(f"{d}/run_counter_collection.csv")))
-    vals = [float(r["Counter_Value"]) for r in rows
-            if any(k in r["Kernel_Name"] for k in ("igemm_kernel", "lattice_conv_kernel",
-                                                   "lattice_zp_kernel"))
-            and r["Counter_Name"] == name]
-    return vals
+    out = collections.defaultdict(list)
+    for r in rows:
+        k = next((k for k in kernels if k in r["Kernel_Name"]), None)
+        if k is not None and r["Counter_Name"] == name:
+            out[k].append(float(r["Counter_Value"]))
+    return out
 
 
-def traffic(fetch_dir, write_dir):
-    f = counter(fetch_dir, "FETCH_SIZE")
-    w = counter(write_dir, "WRITE_SIZE")
+def traffic(fetch_dir, write_dir, op="fwd"):
+    """HBM bytes per call of the probed op: per kernel the median over launches (FETCH_SIZE
+    x2, WRITE_SIZE as reported), summed over the op's kernels (wgrad: the MFMA kernel and
+    its slab reduce)"""
+    kernels = WGRAD_KERNELS if op == "wgrad" else FWD_KERNELS
+    f = counter(fetch_dir, "FETCH_SIZE", kernels)
+    w = counter(write_dir, "WRITE_SIZE", kernels)
     # rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB
-    fb = statistics.median(f) * 1024 * 2
-    wb = statistics.median(w) * 1024
-    return {"kernel": "layer4.0.conv2 fwd residue-class kernel (bf16, 8x512x16^3, 3^3 dil 4)",
-            "launches": [len(f), len(w)],
+    fb = sum(statistics.median(v) for v in f.values()) * 1024 * 2
+    wb = sum(statistics.median(v) for v in w.values()) * 1024
+    return {"kernel": LABELS[op],
+            "launches": [sum(map(len, f.values())), sum(map(len, w.values()))],
             "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
             "hbm_bytes_per_launch": fb + wb,
-            "raw_fetch_size_kib": f, "raw_write_size_kib": w,
+            "raw_fetch_size_kib": dict(f), "raw_write_size_kib": dict(w),
             "correction": "FETCH_SIZE x2 (gfx950 half-count of 16B/lane reads); "
-                          "WRITE_SIZE as reported; median over launches; on-die cache "
-                          "scrubbed before each launch (cold)"}
+                          "WRITE_SIZE as reported; median over launches per kernel; on-die "
+                          "cache scrubbed before each call (cold)"}
 
 
 def _is_opt(name):
@@ -186,4 +199,4 @@ if __name__ == "__main__":
     elif mode == "stepavg":
         print(stepavg(sys.argv[2]))
     elif mode == "traffic":
-        print(json.dumps(traffic(sys.argv[2], sys.argv[3]), indent=1))
+        print(json.dumps(traffic(sys.argv[2], sys.argv[3], *sys.argv[4:5]), indent=1))
