@@ -182,6 +182,26 @@ int mmad_stem_raw_ok(const mmad_conv_desc* d, int in_dtype, int dtype);
 int mmad_conv3d_fwd_raw(const mmad_conv_desc* d, int in_dtype, const void* x, int dtype,
                         const void* w_packed, const float* bias, void* y, float* stats,
                         void* stream);
+/* Deferred slab reduction (round 5): the weight gradient's split-K kernel runs now, its
+ * slab reduction is described in *job (kind != 0) instead of launched, and
+ * mmad_wgrad_reduce_batch later runs the pending reductions of many convs (the whole
+ * backward's, or one data-parallel stage's) as ONE launch -- the same per-element sums in the
+ * same fixed order, so dW is bit-identical to mmad_conv3d_wgrad.  Where a path has no
+ * separate reduction to defer (the stem's two-level sum, bias gradients, no split) it runs
+ * inline and job->kind = 0.  The caller keeps workspace and dw alive, and reads dw only
+ * after the batch.  Replaces the per-conv reduction launches behind loss.backward()
+ * (anat_cnn.py:99-109 via Lightning's training_step). */
+typedef struct mmad_wgrad_job {
+  const float* ws;
+  float* dw;
+  int32_t splits, nd, k, cs, taps, tper, kind, gx, gy, gz;
+} mmad_wgrad_job;
+int mmad_conv3d_wgrad_deferred(const mmad_conv_desc* d, int dtype, const void* x,
+                               const void* dy, float* dw, void* workspace, mmad_wgrad_job* job,
+                               void* stream);
+/* jobs: host array (copied into the launch's arguments, so a captured launch replays the
+ * same jobs); any njobs (16 per launch) */
+int mmad_wgrad_reduce_batch(int njobs, const mmad_wgrad_job* jobs, void* stream);
 /* reduce_stream may be NULL (everything on stream); see mmad_conv3d_wgrad_split */
 int mmad_conv3d_wgrad_raw(const mmad_conv_desc* d, int in_dtype, const void* x, int dtype,
                           const void* dy, float* dw, float* dbias, void* workspace,

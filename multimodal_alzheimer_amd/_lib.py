@@ -64,6 +64,13 @@ class BnFin(C.Structure):
                                            "num_batches_tracked")])
 
 
+class WgradJob(C.Structure):
+    """mirror of mmad_wgrad_job (include/mmad.h): one deferred slab reduction"""
+    _fields_ = ([("ws", C.c_void_p), ("dw", C.c_void_p)] +
+                [(n, C.c_int32) for n in ("splits", "nd", "k", "cs", "taps", "tper", "kind",
+                                          "gx", "gy", "gz")])
+
+
 _P = C.POINTER(ConvDesc)
 _PJ = C.POINTER(PackJob)
 _PD = C.POINTER(PackDual)
@@ -90,6 +97,9 @@ _SIGS = {
     "mmad_conv3d_wgrad_workspace": (_i64, [_P, _i32]),
     "mmad_conv3d_wgrad": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_conv3d_wgrad_split": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmad_conv3d_wgrad_deferred": (_i32, [_P, _i32, _vp, _vp, _vp, _vp,
+                                          C.POINTER(WgradJob), _vp]),
+    "mmad_wgrad_reduce_batch": (_i32, [_i32, C.POINTER(WgradJob), _vp]),
     "mmad_stem_raw_ok": (_i32, [_P, _i32, _i32]),
     "mmad_conv3d_fwd_raw": (_i32, [_P, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mmad_conv3d_wgrad_raw": (_i32, [_P, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -831,6 +831,24 @@ __global__ __launch_bounds__(256) void wgrad_reduce_tz_kernel(const float* __res
                        sm);
 }
 
+// Many pending reductions (mmad_wgrad_reduce_batch) in one launch: the jobs travel in the
+// kernel arguments (a captured launch replays them as recorded); block b runs block
+// b - start[j] of job j, the same body and per-element order as the job's own launch.
+constexpr int kReduceBatch = 16;
+struct ReduceBatch {
+  int n, n_total;
+  int start[kReduceBatch + 1];
+  mmad_reduce::Job jobs[kReduceBatch];
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_kernel(ReduceBatch b) {
+  __shared__ float sm[mmad_reduce::SMEM_FLOATS];
+  const int bid = blockIdx.x;
+  int j = 0;
+  while (j + 1 < b.n && bid >= b.start[j + 1]) ++j;
+  mmad_reduce::run(b.jobs[j], bid - b.start[j], sm);
+}
+
 // the transposing reduce: wgrad_reduce_t_kernel when its (channel slice, co) grid fills the
 // CUs, else wgrad_reduce_tz_kernel over tap groups (MMAD_REDUCE_TZ=0 keeps the former;
 // r03tz: layer1 16.4 / 16.2 -> 10.6 / 10.3 us, layer2.0.conv1 13.9 -> 11.5)
@@ -1821,9 +1839,15 @@ int fork_stream(hipStream_t st, hipStream_t rst) {
 // weight gradient: the split-K kernel on `st`, then the slab reduction (and the bias
 // gradient) on `rst` -- a second stream lets the memory-bound reduction overlap the
 // latency-bound BN backward kernels that follow on `st`
+// defer (non-null, no bias): the slab reduction is recorded there instead of launched when
+// the path has one (defer->kind = KIND_NONE: everything ran inline)
 int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* dy, float* dw,
                  float* dbias, void* workspace, hipStream_t st, hipStream_t rst,
-                 int raw_dtype = -1) {
+                 int raw_dtype = -1, mmad_reduce::Job* defer = nullptr) {
+  if (defer != nullptr) {
+    *defer = mmad_reduce::Job{};
+    if (dbias != nullptr) return MMAD_EUNSUPPORTED;
+  }
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!x || !dy || !dw || !workspace) return MMAD_ENULL;
@@ -1861,6 +1885,10 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
              ? mmad_pwgrad::wgrad(patch_geo(g), x, dy, (float*)workspace, &splits, stream)
              : mmad_lattice::wgrad(patch_geo(g), x, dy, (float*)workspace, &splits, stream);
     if (rc) return rc;
+    if (defer != nullptr) {
+      *defer = plan_reduce_t((const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.taps);
+      return MMAD_OK;
+    }
     if (rst != st && (rc = fork_stream(st, rst))) return rc;
     rc = launch_reduce_t((const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.taps, rst);
     if (rc) return rc;
@@ -1880,8 +1908,21 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
     rc = sp.bmw == 64 ? launch_wgrad<float, 64>(g, sp, x, dy, (float*)workspace, st)
                       : launch_wgrad<float, 128>(g, sp, x, dy, (float*)workspace, st);
   if (rc) return rc;
-  if (rst != st && (rc = fork_stream(st, rst))) return rc;
   const int64_t total = (int64_t)g.Nd * g.K;
+  if (defer != nullptr && !unfolded(d)) {
+    if (g.taps > 1 && g.taps <= 32) {
+      *defer = plan_reduce_t((const float*)workspace, dw, sp.splits, g.Nd, g.K, g.Cs, g.taps);
+      return MMAD_OK;
+    }
+    if (g.taps == 1 && sp.splits >= 8 && total % 4 == 0 && ((uintptr_t)dw & 15) == 0) {
+      mmad_reduce::Job& j = *defer;
+      j.ws = (const float*)workspace; j.dw = dw; j.splits = sp.splits; j.nd = g.Nd;
+      j.k = g.K; j.cs = g.Cs; j.taps = 1; j.kind = mmad_reduce::KIND_WIDE;
+      j.gx = (int)cdiv(total, 256); j.gy = 1; j.gz = 1;
+      return MMAD_OK;
+    }
+  }
+  if (rst != st && (rc = fork_stream(st, rst))) return rc;
   // (the transposing reduce writes whole [ci][taps] runs of dW; scattered 4-byte dW stores
   // from an element-wise reduce cost ~2x in partial-line writes)
   if (!unfolded(d) && g.taps > 1 && g.taps <= 32) {
@@ -1909,6 +1950,42 @@ int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const v
                       float* dw, float* dbias, void* workspace, void* stream) {
   return conv3d_wgrad(d, dtype, x, dy, dw, dbias, workspace, as_stream(stream),
                       as_stream(stream));
+}
+
+int mmad_conv3d_wgrad_deferred(const mmad_conv_desc* d, int dtype, const void* x,
+                               const void* dy, float* dw, void* workspace, mmad_wgrad_job* job,
+                               void* stream) {
+  if (job == nullptr) return MMAD_ENULL;
+  hipStream_t st = as_stream(stream);
+  return conv3d_wgrad(d, dtype, x, dy, dw, nullptr, workspace, st, st, -1, job);
+}
+
+int mmad_wgrad_reduce_batch(int njobs, const mmad_wgrad_job* jobs, void* stream) {
+  if (njobs < 0 || (njobs > 0 && jobs == nullptr)) return MMAD_ENULL;
+  hipStream_t st = as_stream(stream);
+  ReduceBatch b{};
+  auto flush = [&]() -> int {
+    if (b.n == 0) return MMAD_OK;
+    const int64_t blocks = b.start[b.n];
+    b.n_total = (int)blocks;
+    hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b);
+    b = ReduceBatch{};
+    return launch_status();
+  };
+  for (int i = 0; i < njobs; ++i) {
+    const mmad_reduce::Job& j = jobs[i];
+    const int64_t nb = mmad_reduce::job_blocks(j);
+    if (nb <= 0) continue;
+    if (!j.ws || !j.dw) return MMAD_ENULL;
+    if (b.n == kReduceBatch || (int64_t)b.start[b.n] + nb > 0x7fffffff) {
+      const int rc = flush();
+      if (rc) return rc;
+    }
+    b.jobs[b.n] = j;
+    b.start[b.n + 1] = b.start[b.n] + (int)nb;
+    ++b.n;
+  }
+  return flush();
 }
 
 int mmad_conv3d_wgrad_split(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,

@@ -9,12 +9,10 @@
 
 namespace mmad_reduce {
 
-enum { KIND_NONE = 0, KIND_T = 1, KIND_TZ = 2 };
-struct Job {
-  const float* ws;
-  float* dw;
-  int32_t splits, nd, k, cs, taps, tper, kind, gx, gy, gz;
-};
+enum { KIND_NONE = 0, KIND_T = 1, KIND_TZ = 2, KIND_WIDE = 3 };
+// the C ABI's record of one pending reduction (include/mmad.h); KIND_WIDE: 1x1x1 slabs
+// [split][co][ci] (dW in the same order), gx blocks of 256 elements
+using Job = mmad_wgrad_job;
 // shared memory the bodies need (floats): tz's 256 f32x4 partials + the 64 x 33 tile
 constexpr int SMEM_FLOATS = 256 * 4 + 64 * 33;
 
@@ -90,13 +88,40 @@ __device__ __forceinline__ void tz_body(const float* __restrict__ ws, float* __r
   }
 }
 
+// 1x1x1 slabs (conv.hip's wgrad_reduce_wide_kernel, stride 1, taps 1): block bx sums 256
+// consecutive elements, 4 groups of 64 lanes taking every 4th slab (16 bytes per lane per
+// load), the groups combined in fixed order; dW[co][ci] is the slab order itself
+__device__ __forceinline__ void wide_body(const float* __restrict__ ws, float* __restrict__ dw,
+                                          int splits, int64_t total, int bx, float* sm) {
+  f32x4* red = reinterpret_cast<f32x4*>(sm);   // [4][64]
+  const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t idx = ((int64_t)bx * 64 + e) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (idx < total) {
+#pragma unroll 4
+    for (int sp = grp; sp < splits; sp += 4)
+      s += *reinterpret_cast<const f32x4*>(ws + sp * total + idx);
+  }
+  red[grp * 64 + e] = s;
+  __syncthreads();
+  if (grp != 0 || idx >= total) return;
+  s = ((red[e] + red[64 + e]) + red[128 + e]) + red[192 + e];
+  *reinterpret_cast<f32x4*>(dw + idx) = s;
+}
+
 // block `lin` of job j's own grid (x fastest)
 __device__ __forceinline__ void run(const Job& j, int lin, float* sm) {
   const int bx = lin % j.gx, r = lin / j.gx, by = r % j.gy, bz = r / j.gy;
-  if (j.kind == KIND_TZ)
+  if (j.kind == KIND_WIDE)
+    wide_body(j.ws, j.dw, j.splits, (int64_t)j.nd * j.k, bx, sm);
+  else if (j.kind == KIND_TZ)
     tz_body(j.ws, j.dw, j.splits, j.nd, j.k, j.cs, j.taps, j.tper, bx, by, bz, sm);
   else
     t_body(j.ws, j.dw, j.splits, j.nd, j.k, j.cs, j.taps, bx, by, sm);
+}
+
+__host__ __device__ inline int64_t job_blocks(const Job& j) {
+  return j.kind == KIND_NONE ? 0 : (int64_t)j.gx * j.gy * j.gz;
 }
 
 }  // namespace mmad_reduce

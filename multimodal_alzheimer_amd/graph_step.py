@@ -47,6 +47,8 @@ depends on it:
 * dropout draws its seed on the device (``head_ops.dropout``), so every replay gets a
   fresh mask.
 """
+import os
+
 import torch
 
 from . import fused_optim, volume_ops
@@ -56,6 +58,10 @@ COLLECTIVES = ("staged", "after", "inside")
 # of collectives issued before a capture (hipEventQuery), which "global" mode turns into a
 # capture error that aborts the process (seen when a blocking all-reduce ran just before one)
 _CAPTURE_MODE = "thread_local"
+# MMAD_DEFER_WGRAD=0: every conv's weight-gradient slab reduction launches right after its
+# split-K kernel inside the captured backward (A/B switch for volume_ops'
+# deferred_wgrad_reduce)
+DEFER_WGRAD = os.environ.get("MMAD_DEFER_WGRAD", "1") != "0"
 DEFAULT_CUTS = ("layer4", "layer3", "layer2")
 
 
@@ -147,6 +153,7 @@ class StagedBackward:
         if not roots:
             raise RuntimeError(f"backward stage {k}: no gradient reached its boundary")
         out = torch.autograd.grad(roots, nxt + ps, grads, allow_unused=True)
+        volume_ops.flush_wgrad_reduce()      # this stage's queued dW reductions (if any)
         for p, g in zip(ps, out[len(nxt):]):
             if g is None:
                 continue
@@ -251,6 +258,13 @@ class GraphedTrainStep:
         return tuple(p._version for p in self.fused.params())
 
     def _capture(self, model, optimizer, reducer, staged):
+        # the weight-gradient slab reductions queue up and run as one launch at the end of
+        # the backward (each stage's, when staged) -- not with collectives captured inside,
+        # whose bucket hooks would read the queued gradients
+        with volume_ops.deferred_wgrad_reduce(DEFER_WGRAD and self.mode != "inside"):
+            self._capture_body(model, optimizer, reducer, staged)
+
+    def _capture_body(self, model, optimizer, reducer, staged):
         if self.mode in ("staged", "after"):
             reducer.defer = True             # the capture's hooks (if any) only count
             try:
@@ -259,6 +273,7 @@ class GraphedTrainStep:
                     with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                         self.out = model.general_step(self.static, 0, "train")
                         self.out["loss"].backward(self._one)
+                        volume_ops.flush_wgrad_reduce()
                     self.graphs.append(g)
                 else:
                     staged.arm()
@@ -289,6 +304,7 @@ class GraphedTrainStep:
             with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                 self.out = model.general_step(self.static, 0, "train")
                 self.out["loss"].backward(self._one)
+                volume_ops.flush_wgrad_reduce()
                 if reducer is not None:
                     reducer.finish()
                 self._opt_step()

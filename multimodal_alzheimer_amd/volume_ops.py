@@ -72,6 +72,48 @@ FWD_PROBES = {}
 # the MFMA kernel and its slab reduce)
 WGRAD_PROBES = {}
 
+# Deferred weight-gradient slab reductions (round 5).  Inside ``deferred_wgrad_reduce()`` a
+# conv weight gradient whose dW autograd adopts as-is (no existing .grad, no bias, no channel
+# padding) runs only its split-K kernel (mmad_conv3d_wgrad_deferred) and queues its slab
+# reduction; ``flush_wgrad_reduce()`` then runs every queued reduction as ONE launch
+# (mmad_wgrad_reduce_batch, bit-identical sums).  graph_step captures the backward this way
+# and flushes at its end (per stage when staged), so the replay has one reduction launch
+# instead of one per conv.  Nothing may read a queued dW before the flush: eager backward
+# hooks that all-reduce buckets keep it off.
+_WGRAD_DEFER = {"on": False, "jobs": [], "keep": []}
+
+
+class deferred_wgrad_reduce:
+    """context manager: queue the weight-gradient slab reductions (see above)"""
+
+    def __init__(self, on=True):
+        self.on = on
+
+    def __enter__(self):
+        self.prev = _WGRAD_DEFER["on"]
+        _WGRAD_DEFER["on"] = self.on
+        return self
+
+    def __exit__(self, *exc):
+        flush_wgrad_reduce()
+        _WGRAD_DEFER["on"] = self.prev
+        return False
+
+
+def flush_wgrad_reduce():
+    """run every queued weight-gradient slab reduction (one launch per 16) on the current
+    stream"""
+    jobs = _WGRAD_DEFER["jobs"]
+    if not jobs:
+        return
+    arr = (L.WgradJob * len(jobs))(*jobs)
+    L.call("mmad_wgrad_reduce_batch", len(jobs), arr, L.stream())
+    # (stream-ordered: the workspaces return to the caching allocator only for work queued
+    # after this launch)
+    jobs.clear()
+    _WGRAD_DEFER["keep"].clear()
+
+
 # training-mode BN statistic updates so far (the running buffers are written by our kernels,
 # which torch's tensor version counters do not see); keys the eval-mode folded-weight caches
 _BN_UPDATES = [0]
@@ -486,6 +528,14 @@ def _wgrad(ctx, d, dt, src, gy, weight, wparam=None, rside=None):
             if t is not None:
                 t.record_stream(rside)
         _queue_join(torch.cuda.current_stream(), rside)
+    elif _WGRAD_DEFER["on"] and not ctx.has_bias and not padded and \
+            (wparam is None or wparam.grad is None):
+        job = L.WgradJob()
+        L.call("mmad_conv3d_wgrad_deferred", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(ws),
+               C.byref(job), L.stream())
+        if job.kind:
+            _WGRAD_DEFER["jobs"].append(job)
+            _WGRAD_DEFER["keep"].append(ws)
     else:
         probe = WGRAD_PROBES.get(_desc_tuple(d)) if WGRAD_PROBES else None
         if probe is not None:

@@ -1,0 +1,87 @@
+"""Deferred weight-gradient slab reductions (volume_ops.deferred_wgrad_reduce ->
+mmad_conv3d_wgrad_deferred + mmad_wgrad_reduce_batch): every conv route of the benched
+config-2 step, at its real geometry (batch 2), gives a dW bit-identical to the immediate
+reduction -- the batched launch runs the same per-element sums in the same order -- and
+several convs' reductions share one launch."""
+import pytest
+import torch
+
+from multimodal_alzheimer_amd import _lib
+from multimodal_alzheimer_amd import volume_ops as V
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CL = torch.channels_last_3d
+BF = torch.bfloat16
+
+# (name, x shape, w shape, stride, padding, dilation): the routes of the ResNet-10 step
+ROUTES = [
+    ("layer4_conv2_lattice", (2, 512, 16, 16, 16), (512, 512, 3, 3, 3), 1, 4, 4),
+    ("layer3_conv_pwgrad_lat", (2, 256, 16, 16, 16), (256, 256, 3, 3, 3), 1, 2, 2),
+    ("layer2_conv2_pwgrad_w16", (2, 128, 16, 16, 16), (128, 128, 3, 3, 3), 1, 1, 1),
+    ("layer1_pwgrad", (2, 64, 32, 32, 32), (64, 64, 3, 3, 3), 1, 1, 1),
+    ("layer2_conv1_s2_generic", (2, 64, 32, 32, 32), (128, 64, 3, 3, 3), 2, 1, 1),
+    ("layer4_downsample_wide", (2, 256, 16, 16, 16), (512, 256, 1, 1, 1), 1, 0, 1),
+    ("layer3_downsample_wide", (2, 128, 16, 16, 16), (256, 128, 1, 1, 1), 1, 0, 1),
+    ("layer2_downsample_s2", (2, 64, 32, 32, 32), (128, 64, 1, 1, 1), 2, 0, 1),
+]
+
+
+def _operands(xs, ws, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = (torch.rand(xs, generator=g, device=DEV) * 2 - 1).to(BF).contiguous(memory_format=CL)
+    w = (torch.rand(ws, generator=g, device=DEV) * 2 - 1) * (3.0 / (ws[1] * ws[2] ** 3)) ** 0.5
+    return x, w
+
+
+def _wgrad(x, w, s, p, d, gy=None, defer=False):
+    wg = w.clone().requires_grad_(True)
+    y = V.conv3d(x, wg, None, (s,) * 3, (p,) * 3, (d,) * 3, BF)
+    if gy is None:
+        g = torch.Generator(device=DEV).manual_seed(5)
+        gy = (torch.rand(y.shape, generator=g, device=DEV) * 2 - 1).to(BF) \
+            .contiguous(memory_format=CL)
+    with V.deferred_wgrad_reduce(defer):
+        y.backward(gy)
+        queued = len(V._WGRAD_DEFER["jobs"])
+    torch.cuda.synchronize()
+    return wg.grad, gy, queued
+
+
+@pytest.mark.parametrize("name,xs,ws,s,p,d", ROUTES, ids=[r[0] for r in ROUTES])
+def test_deferred_reduce_bit_identical(name, xs, ws, s, p, d):
+    x, w = _operands(xs, ws, hash(name) % 1000)
+    ref, gy, _ = _wgrad(x, w, s, p, d)
+    got, _, queued = _wgrad(x, w, s, p, d, gy, defer=True)
+    assert queued <= 1
+    assert torch.equal(got, ref), f"{name}: max |diff| {(got - ref).abs().max().item():.3e}"
+
+
+def test_many_convs_one_batch():
+    """all routes queued, then one flush: each dW equals its immediate reduction"""
+    refs, gys, xs_ws = [], [], []
+    for i, (name, xs, ws, s, p, d) in enumerate(ROUTES):
+        x, w = _operands(xs, ws, 100 + i)
+        r, gy, _ = _wgrad(x, w, s, p, d)
+        refs.append(r)
+        gys.append(gy)
+        xs_ws.append((x, w))
+    wgs = []
+    with V.deferred_wgrad_reduce(True):
+        for (x, w), gy, (name, _, _, s, p, d) in zip(xs_ws, gys, ROUTES):
+            wg = w.clone().requires_grad_(True)
+            V.conv3d(x, wg, None, (s,) * 3, (p,) * 3, (d,) * 3, BF).backward(gy)
+            wgs.append(wg)
+        n = len(V._WGRAD_DEFER["jobs"])
+    torch.cuda.synchronize()
+    assert n >= 6, "expected most routes to queue a reduction"
+    for (name, *_), wg, r in zip(ROUTES, wgs, refs):
+        assert torch.equal(wg.grad, r), name
+
+
+def test_reduce_batch_rejects_bad_jobs():
+    lib = _lib.load()
+    job = _lib.WgradJob()
+    job.kind, job.gx, job.gy, job.gz = 1, 1, 1, 1       # ws / dw left NULL
+    assert lib.mmad_wgrad_reduce_batch(1, job, None) == 1003
+    assert lib.mmad_wgrad_reduce_batch(0, None, None) == 0
