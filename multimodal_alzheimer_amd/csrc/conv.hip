@@ -1808,6 +1808,8 @@ int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype) {
     slabs = std::max<int64_t>(slabs, mmad_lattice::wgrad_workspace(patch_geo(g)));
   if (!unfolded(d) && use_pwgrad(g, dtype))
     slabs = std::max<int64_t>(slabs, mmad_pwgrad::workspace(patch_geo(g)));
+  if (!unfolded(d) && mmad_pw::wgrad_ok(d, dtype))
+    slabs = std::max<int64_t>(slabs, mmad_pw::wgrad_splits(d) * g.Nd * g.K * 4);
   if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on())
     slabs = std::max<int64_t>(slabs, mmad_stem::wgrad_blocks(d) * g.Nd * g.K * 4);
   const int64_t parts = (int64_t)1024 * 2 * g.Nd * 4;   // bias-gradient column sums
@@ -1891,6 +1893,28 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
     }
     if (rst != st && (rc = fork_stream(st, rst))) return rc;
     rc = launch_reduce_t((const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.taps, rst);
+    if (rc) return rc;
+    if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, rstream);
+    return MMAD_OK;
+  }
+  if (!unfolded(d) && mmad_pw::wgrad_ok(d, dtype)) {
+    // 1x1x1 (the shortcuts): the pointwise split-K GEMM, then the wide slab reduction
+    rc = mmad_pw::wgrad(d, x, dy, (float*)workspace, st);
+    if (rc) return rc;
+    const int splits = (int)mmad_pw::wgrad_splits(d);
+    const int64_t total = (int64_t)g.Nd * g.K;
+    if (defer != nullptr && ((uintptr_t)dw & 15) == 0) {
+      mmad_reduce::Job& j = *defer;
+      j.ws = (const float*)workspace; j.dw = dw; j.splits = splits; j.nd = g.Nd;
+      j.k = g.K; j.cs = g.Cs; j.taps = 1; j.kind = mmad_reduce::KIND_WIDE;
+      j.gx = (int)cdiv(total, 256); j.gy = 1; j.gz = 1;
+      return MMAD_OK;
+    }
+    if (rst != st && (rc = fork_stream(st, rst))) return rc;
+    hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                       rst, (const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.cs_shift,
+                       g.taps, 0, 1);
+    rc = launch_status();
     if (rc) return rc;
     if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, rstream);
     return MMAD_OK;

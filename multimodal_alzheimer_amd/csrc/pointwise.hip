@@ -239,6 +239,173 @@ bool pw_on() {
   return v;
 }
 
+// ---- weight gradient (round 5) ------------------------------------------------------
+//   dW[co][ci] = sum_m dY[m][co] * X[src(m)][ci]      (src(m) = m, or s2_src for stride 2)
+// K = the voxels, split over blocks: block = 128 co x CIT ci over one K range of a split;
+// fp32 partial slabs [split][co][ci] (the torch layout of a 1x1x1 dW), summed by the wide
+// slab reduction (deferred or not: conv.hip).  Both operands are K-strided in memory (NDHWC
+// rows), so each stage DMAs 32 voxel rows of dY (128 co = 256 B) and of X (CIT ci) into LDS
+// lane-linearly, and the MFMA fragments are read with transposing ds_read_b64_tr_b16: lane
+// 4q + p of a 16-lane group supplies row q (a voxel), 4 channels; lane i receives channel i
+// of 4 voxels.  The 16-byte chunks are XOR-swizzled per row on the DMA's source address so
+// that the 8 rows x 2 chunks a 32-lane half reads hit 64 distinct banks (pw_tsw256 /
+// pw_tsw128: rows {0-3, 8-11} + 16 t map to distinct chunk pairs).  4 waves = 2 (64 co) x 2
+// (CIT / 2 ci); 4-slot ring, three 32-voxel stages in flight, one barrier per stage; two
+// blocks per CU.  The row-gather wgrad_kernel (conv.hip) ran these GEMMs at 20-30 GB/s per
+// CU of operand traffic (its 8-split run took 97 us per 4096-voxel block).
+constexpr int WG_KS = 32;                 // voxels per stage (one MFMA k step)
+constexpr int WG_NS = 4;                  // ring slots
+constexpr int WG_NTHR = 256;
+
+__device__ __forceinline__ int pw_tsw256(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+__device__ __forceinline__ int pw_tsw128(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
+
+template <int CIT>
+struct WGC {
+  static constexpr int YROW = 256;                    // 128 co x 2 B
+  static constexpr int XROW = CIT * 2;
+  static constexpr int YIMG = WG_KS * YROW;           // 8 KiB
+  static constexpr int XIMG = WG_KS * XROW;           // 8 / 4 KiB
+  static constexpr int SLOT = YIMG + XIMG;
+  static constexpr int LDS = WG_NS * SLOT;            // 64 / 48 KiB
+  static constexpr int NQ = SLOT / 1024;              // DMA instructions per stage: 16 / 12
+  static constexpr int WI = NQ / 4;                   // per wave: 4 / 3
+  static constexpr int TJ = CIT / 32;                 // 16-column ci tiles per wave: 4 / 2
+};
+
+template <int CIT, int MODE>   // MODE 0: stride 1; 1: X row of voxel m is s2_src(m)
+__global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ dy, float* __restrict__ out, int Ci,
+    int Co, int kper, int ntiles, PwS2 s2) {
+  using C = WGC<CIT>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware order: the tiles of one split (the same voxel rows) on one XCD
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int tile = lin % ntiles, split = lin / ntiles;
+  const int nci = Ci / CIT;
+  const int co0 = (tile / nci) * 128, ci0 = (tile % nci) * CIT;
+  const int64_t m0 = (int64_t)split * kper;
+  const int nstage = kper / WG_KS;
+
+  // DMA instruction q (= wave + 4 h) of a stage: q < 8 the dY image (rows 4q .. 4q + 3),
+  // else the X image (256-B rows: 4 per instruction; 128-B rows: 8)
+  const u16* sp[C::WI];
+  int64_t srow[C::WI];                  // the voxel (stage 0) this lane's row reads
+  uint32_t lofs[C::WI];
+  bool isx[C::WI];
+#pragma unroll
+  for (int h = 0; h < C::WI; ++h) {
+    const int q = wave + 4 * h;
+    lofs[h] = (uint32_t)(q * 1024);
+    if (q < 8) {
+      const int row = 4 * q + (lane >> 4);
+      const int ch = (lane & 15) ^ pw_tsw256(row);
+      isx[h] = false;
+      srow[h] = m0 + row;
+      sp[h] = dy + (int64_t)co0 + ch * 8;
+    } else {
+      const int qx = q - 8;
+      const int row = CIT == 128 ? 4 * qx + (lane >> 4) : 8 * qx + (lane >> 3);
+      const int ch = CIT == 128 ? (lane & 15) ^ pw_tsw256(row) : (lane & 7) ^ pw_tsw128(row);
+      isx[h] = true;
+      srow[h] = m0 + row;
+      sp[h] = x + (int64_t)ci0 + ch * 8;
+    }
+  }
+  const uint32_t smem_l = lds_addr_of(smem);
+  auto issue = [&](int s) {
+    const uint32_t slot = smem_l + (uint32_t)((s % WG_NS) * C::SLOT);
+#pragma unroll
+    for (int h = 0; h < C::WI; ++h) {
+      const int64_t m = srow[h] + (int64_t)s * WG_KS;
+      const int64_t v = (MODE == 1 && isx[h]) ? s2_src(s2, m) : m;
+      glds16_asm(sp[h] + v * (isx[h] ? Ci : Co), slot + lofs[h]);
+    }
+  };
+
+  const int wm = wave & 1, wn = wave >> 1;
+  const int lk = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  // fragment byte offsets inside a slot: lo = voxel rows 8 lk + q4, hi = + 4
+  uint32_t ya_lo[4], ya_hi[4], xb_lo[C::TJ], xb_hi[C::TJ];
+  const int rlo = 8 * lk + q4, rhi = rlo + 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = wm * 64 + i * 16 + 4 * p4;
+    ya_lo[i] = (uint32_t)(rlo * C::YROW + (((col >> 3) ^ pw_tsw256(rlo)) << 4) + (col & 7) * 2);
+    ya_hi[i] = (uint32_t)(rhi * C::YROW + (((col >> 3) ^ pw_tsw256(rhi)) << 4) + (col & 7) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < C::TJ; ++j) {
+    const int col = wn * (CIT / 2) + j * 16 + 4 * p4;
+    const int slo = CIT == 128 ? pw_tsw256(rlo) : pw_tsw128(rlo);
+    const int shi = CIT == 128 ? pw_tsw256(rhi) : pw_tsw128(rhi);
+    xb_lo[j] = (uint32_t)(C::YIMG + rlo * C::XROW + (((col >> 3) ^ slo) << 4) + (col & 7) * 2);
+    xb_hi[j] = (uint32_t)(C::YIMG + rhi * C::XROW + (((col >> 3) ^ shi) << 4) + (col & 7) * 2);
+  }
+  auto tr8 = [](const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p);
+  };
+  f32x4 acc[4][C::TJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (nstage > 1) issue(1);
+  if (nstage > 2) issue(2);
+  for (int s = 0; s < nstage; ++s) {
+    if (s + 2 < nstage) wait_vm_lgkm0<2 * C::WI>();   // stage s landed, s+1 and s+2 in flight
+    else if (s + 1 < nstage) wait_vm_lgkm0<C::WI>();
+    else wait_vm_lgkm0<0>();
+    raw_barrier();                                     // every wave's part of stage s; and
+    if (s + 3 < nstage) issue(s + 3);                  // all are past stage s - 1's slot
+    int so = (s % WG_NS) * C::SLOT;
+    asm volatile("" : "+s"(so));
+    const char* slot = smem + so;
+    bf16x8 a[4], b[C::TJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a[i] = __builtin_shufflevector(tr8(slot + ya_lo[i]), tr8(slot + ya_hi[i]), 0, 1, 2, 3, 4,
+                                     5, 6, 7);
+#pragma unroll
+    for (int j = 0; j < C::TJ; ++j)
+      b[j] = __builtin_shufflevector(tr8(slot + xb_lo[j]), tr8(slot + xb_hi[j]), 0, 1, 2, 3, 4,
+                                     5, 6, 7);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < C::TJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+
+  // acc[i][j][r]: co = wm*64 + i*16 + 4 lk + r, ci = wn*CIT/2 + j*16 + (lane & 15)
+  float* o = out + (int64_t)split * Co * Ci;
+  const int lr = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * 64 + i * 16 + 4 * lk + r;
+        const int ci = ci0 + wn * (CIT / 2) + j * 16 + lr;
+        o[(int64_t)co * Ci + ci] = acc[i][j][r];
+      }
+}
+
+bool pw_wgrad_on() {
+  static const bool v = [] {
+    const char* e = getenv("MMAD_PW_WGRAD");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return v;
+}
+
 }  // namespace
 
 namespace mmad_pw {
@@ -325,6 +492,57 @@ int fwd(const mmad_conv_desc* d, const void* x, const void* wp, const float* bia
   const dim3 grid((unsigned)(m / TM), (unsigned)(d->co / 256));
   return s2 ? launch<256, 1>(grid, d->ci, x, wp, y, d->co, stats, bias, q, stream)
             : launch<256, 0>(grid, d->ci, x, wp, y, d->co, stats, bias, q, stream);
+}
+
+namespace {
+int wg_cit(const mmad_conv_desc* d) { return d->ci % 128 == 0 && d->ci >= 256 ? 128 : 64; }
+}  // namespace
+
+bool wgrad_ok(const mmad_conv_desc* d, int dtype) {
+  if (!pw_on() || !pw_wgrad_on() || dtype != MMAD_BF16) return false;
+  if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw) return false;
+  if (!stride1_geom(d) && !s2_geom(d)) return false;
+  if (d->co % 128 || d->ci % 64) return false;
+  const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
+  const int64_t mi = (int64_t)d->n * d->di * d->hi * d->wi;
+  return m % WG_KS == 0 && m * d->co < (int64_t(1) << 40) && mi * d->ci < (int64_t(1) << 40);
+}
+
+// voxels per split: the split count that gives ~512 blocks (two per CU), K ranges of at least
+// 4 stages, a divisor of the voxel count
+int64_t wgrad_kper(const mmad_conv_desc* d) {
+  const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
+  const int64_t tiles = (int64_t)(d->co / 128) * (d->ci / wg_cit(d));
+  int64_t kper = m;
+  while (kper % 2 == 0 && (kper / 2) % WG_KS == 0 && kper / 2 >= 4 * WG_KS &&
+         tiles * (m / kper) < 512)
+    kper /= 2;
+  return kper;
+}
+
+int64_t wgrad_splits(const mmad_conv_desc* d) {
+  return (int64_t)d->n * d->do_ * d->ho * d->wo / wgrad_kper(d);
+}
+
+int wgrad(const mmad_conv_desc* d, const void* x, const void* dy, float* ws, void* stream) {
+  if (!wgrad_ok(d, MMAD_BF16)) return MMAD_EUNSUPPORTED;
+  const int cit = wg_cit(d);
+  const int64_t kper = wgrad_kper(d), sp = wgrad_splits(d);
+  const int ntiles = (d->co / 128) * (d->ci / cit);
+  const int64_t nblk = sp * ntiles;
+  if (nblk > 0x7fffffff || kper > 0x7fffffff) return MMAD_EUNSUPPORTED;
+  const PwS2 q = s2_of(d);
+  const bool s2 = s2_geom(d);
+  auto go = [&](auto kern, int lds) {
+    static_cast<void>(hipFuncSetAttribute((const void*)kern,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(WG_NTHR), lds, as_stream(stream),
+                       (const u16*)x, (const u16*)dy, ws, d->ci, d->co, (int)kper, ntiles, q);
+    return launch_status();
+  };
+  if (cit == 128)
+    return s2 ? go(pw_wgrad_kernel<128, 1>, WGC<128>::LDS) : go(pw_wgrad_kernel<128, 0>, WGC<128>::LDS);
+  return s2 ? go(pw_wgrad_kernel<64, 1>, WGC<64>::LDS) : go(pw_wgrad_kernel<64, 0>, WGC<64>::LDS);
 }
 
 }  // namespace mmad_pw

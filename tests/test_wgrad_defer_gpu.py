@@ -85,3 +85,20 @@ def test_reduce_batch_rejects_bad_jobs():
     job.kind, job.gx, job.gy, job.gz = 1, 1, 1, 1       # ws / dw left NULL
     assert lib.mmad_wgrad_reduce_batch(1, job, None) == 1003
     assert lib.mmad_wgrad_reduce_batch(0, None, None) == 0
+
+
+@pytest.mark.parametrize("xs,co,s", [((2, 256, 16, 16, 16), 512, 1), ((2, 128, 16, 16, 16), 256, 1),
+                                     ((2, 64, 32, 32, 32), 128, 2), ((1, 256, 8, 12, 10), 128, 1),
+                                     ((3, 64, 9, 8, 7), 128, 2)],
+                         ids=["layer4_ds", "layer3_ds", "layer2_ds_s2", "ragged", "ragged_s2"])
+def test_pointwise_wgrad_vs_float64(xs, co, s):
+    """the 1x1x1 weight gradient (pointwise.hip pw_wgrad_kernel + wide slab reduction)
+    against a float64 sum over the same bf16 operands: within 1e-3 |ref| + 1e-4 sum|gY||X|"""
+    x, w = _operands(xs, (co, xs[1], 1, 1, 1), 7)
+    got, gy, _ = _wgrad(x, w, s, 0, 1)
+    xd = x.double()[:, :, ::s, ::s, ::s]
+    gd = gy.double()
+    ref = torch.einsum("nczyx,nkzyx->ck", gd, xd)
+    mag = torch.einsum("nczyx,nkzyx->ck", gd.abs(), xd.abs())
+    err = (got.double().reshape(ref.shape) - ref).abs()
+    assert (err <= 1e-3 * ref.abs() + 1e-4 * mag).all(), f"max err {err.max().item():.3e}"
