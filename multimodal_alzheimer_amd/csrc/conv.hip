@@ -32,6 +32,8 @@
 //  * XCD-aware tile order: each XCD walks a contiguous range of (m, n) tiles, n fastest;
 //  * epilogue: bias, BN partial sums (sum, sum of squares per channel) from the fp32
 //    accumulators, bf16 tile transposed through LDS into 16-byte channel-vector stores.
+#include <atomic>
+
 #include "common.h"
 #include "reduce.h"
 #include "patchconv.h"
@@ -53,6 +55,13 @@ struct Geom {
   // shaped like the output (added after bias), ReLU flag
   const void* res;
   int relu;
+  // residue-class row order (round 5; FWD, stride 1, 'same' 3^3 dilation lat >= 2 on grids
+  // that are lat x (lz, ly, lx)): row m = position q of the sub-lattice (qz, qy, qx) major,
+  // then sample and residue class (rz, ry, rx) -- every tile's rows share q, so the taps whose
+  // shift leaves the sub-lattice are padding for the whole tile and are skipped (no DMA, no
+  // MFMA); with fewer subs than tile rows a tile holds consecutive positions and skips the
+  // taps none of them reaches; 0 = the plain voxel order
+  int lat, lz, ly, lx;
 };
 
 enum { FWD = 0, DGRAD = 1 };
@@ -71,6 +80,19 @@ __device__ __forceinline__ bool src_voxel(const Geom& g, int bz, int by, int bx,
   x = bx + ((to >> 16) & 255) - 128;
   return (unsigned)z < (unsigned)g.Ds && (unsigned)y < (unsigned)g.Hs &&
          (unsigned)x < (unsigned)g.Ws;
+}
+
+// voxel of row m in the residue-class order (Geom::lat)
+__device__ __forceinline__ void lat_voxel(const Geom& g, int m, int& n, int& z, int& y, int& x) {
+  const int d = g.lat, d3 = d * d * d;
+  const int S = g.nb * d3;
+  const int q = m / S, s = m - q * S;
+  n = s / d3;
+  const int r = s - n * d3;
+  const int qx = q % g.lx, qy = (q / g.lx) % g.ly, qz = q / (g.lx * g.ly);
+  z = r / (d * d) + d * qz;
+  y = (r / d) % d + d * qy;
+  x = r % d + d * qx;
 }
 
 // forward tap table: offsets kd*d (base = out*s - p)
@@ -136,7 +158,35 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
   const int m0 = mt * BM, n0 = nt * BN;
 
   int ntap = g.taps, Kc = g.K;
-  if (MODE == FWD) {
+  if (MODE == FWD && g.lat) {
+    // the taps that land inside the volume for this tile's sub-lattice position(s) -- the
+    // same for all rows of one position; a tile of several positions (fewer subs than
+    // rows) takes their union and its rows mask the rest as padding -- compacted; the
+    // weights are addressed through tapidx as in DGRAD
+    if (tid == 0) {
+      const int S = g.nb * g.lat * g.lat * g.lat;
+      const int m1 = min(Mc, m0 + BM);
+      int n = 0;
+      for (int t = 0; t < g.taps; ++t) {
+        const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
+        const int to = pack_off(kd * g.dd, kh * g.dh, kw * g.dw);
+        bool any = false;
+        for (int mq = m0; mq < m1 && !any; mq += S) {
+          int nb0, z0, y0, x0, z, y, x;
+          lat_voxel(g, mq, nb0, z0, y0, x0);
+          any = src_voxel(g, z0 - g.pd, y0 - g.ph, x0 - g.pw, to, z, y, x);
+        }
+        if (!any) continue;
+        tapoff[n] = to;
+        tapidx[n] = t;
+        ++n;
+      }
+      tapidx[MAXTAPS - 1] = n;
+    }
+    __syncthreads();
+    ntap = tapidx[MAXTAPS - 1];
+    Kc = ntap * g.Cs;
+  } else if (MODE == FWD) {
     fill_taps_fwd(g, tapoff);
   } else {
     // (count kept in the unused last tap-index slot: a second __shared__ object beside
@@ -171,11 +221,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
     const int m = m0 + (wave * AI + i) * RPI + lrow;
     rok[i] = m < Mc;
     const int mm = rok[i] ? m : 0;
-    const int xw = mm % Wc;
+    int xw = mm % Wc;
     int t1 = mm / Wc;
-    const int yh = t1 % Hc;
+    int yh = t1 % Hc;
     t1 /= Hc;
-    const int zd = t1 % Dc, nbi = t1 / Dc;
+    int zd = t1 % Dc, nbi = t1 / Dc;
+    if (MODE == FWD && g.lat) lat_voxel(g, mm, nbi, zd, yh, xw);
     if (MODE == FWD) {
       rz[i] = zd * g.sd - g.pd; ry[i] = yh * g.sh - g.ph; rx[i] = xw * g.sw - g.pw;
     } else {
@@ -239,7 +290,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
         glds16_asm(p, lds_addr_of(sbase + (wave * AI + i) * 1024));
       }
     }
-    const int woff = MODE == FWD ? k : (kok ? (tapidx[ti] << g.cs_shift) + ci : 0);
+    const int woff = MODE == FWD && !g.lat ? k : (kok ? (tapidx[ti] << g.cs_shift) + ci : 0);
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int co = n0 + (wave * BI + i) * RPI + lrow;
@@ -338,6 +389,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
 
   // dst voxel of a tile row
   auto dst_row = [&](int m) -> int64_t {
+    if (MODE == FWD && g.lat) {
+      int n, z, y, x;
+      lat_voxel(g, m, n, z, y, x);
+      return (((int64_t)n * g.Dd + z) * g.Hd + y) * g.Wd + x;
+    }
     if (MODE == FWD) return m;
     const int xw = m % Wc;
     int t1 = m / Wc;
@@ -1326,6 +1382,29 @@ WSplit wgrad_split(const Geom& g, int dtype) {
   return s;
 }
 
+// the residue-class row order of igemm_kernel (Geom::lat) applies: a stride-1 'same' 3^3
+// conv of dilation d >= 2 whose grid is d x a whole sub-lattice per dimension (config 5's
+// 20^3 layer3 / layer4: 10^3 / 5^3 sub-lattices; the 4d^3 / 8-wide grids of config 2 go to
+// the residue-class kernels first).  MMAD_IGEMM_LAT=0 keeps the voxel order (A/B switch).
+std::atomic<int> g_igemm_lat{-1};
+int igemm_lat_mode() {
+  int v = g_igemm_lat.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("MMAD_IGEMM_LAT");
+    int expect = -1;
+    g_igemm_lat.compare_exchange_strong(expect, e ? atoi(e) : 1);
+    v = g_igemm_lat.load(std::memory_order_relaxed);
+  }
+  return v;
+}
+bool lat_geom(const Geom& g) {
+  const int d = g.dd;
+  return igemm_lat_mode() != 0 && d >= 2 && g.dh == d && g.dw == d && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
+         g.KD == 3 && g.KH == 3 && g.KW == 3 && g.pd == d && g.ph == d && g.pw == d &&
+         g.Ds == g.Dd && g.Hs == g.Hd && g.Ws == g.Wd && g.Dd % d == 0 && g.Hd % d == 0 &&
+         g.Wd % d == 0;
+}
+
 template <typename F>
 bool set_lds(F* kern, size_t lds) {
   return lds <= 65536 || hipFuncSetAttribute((const void*)kern,
@@ -1343,9 +1422,16 @@ int launch_igemm_bm(const Geom& g, int64_t m_max, int classes, const void* src, 
   static const bool ok = set_lds(igemm_kernel<T, BN, MODE, BMT, WGM, WGN, NST, RBT>, lds);
   if (!ok) return MMAD_EUNSUPPORTED;
   const int nbm = (int)cdiv(m_max, BMT), nbn = (int)cdiv(g.Nd, BN);
+  Geom gl = g;
+  if (MODE == FWD && classes == 1 && m_max == g.M && sizeof(T) == 2 && lat_geom(g) &&
+      (((int64_t)g.nb * g.dd * g.dd * g.dd) % BMT == 0 ||
+       BMT % ((int64_t)g.nb * g.dd * g.dd * g.dd) == 0)) {
+    gl.lat = g.dd;
+    gl.lz = g.Dd / g.dd; gl.ly = g.Hd / g.dd; gl.lx = g.Wd / g.dd;
+  }
   hipLaunchKernelGGL((igemm_kernel<T, BN, MODE, BMT, WGM, WGN, NST, RBT>),
                      dim3((unsigned)(nbm * nbn), (unsigned)classes), dim3(64 * WGM * WGN), lds,
-                     st, g, (const T*)src, (const T*)w, bias, (T*)dst, stats, nbm, nbn);
+                     st, gl, (const T*)src, (const T*)w, bias, (T*)dst, stats, nbm, nbn);
   return launch_status();
 }
 
@@ -2065,3 +2151,11 @@ int zero_fill(void* p, int64_t bytes, hipStream_t st) {
                      (uint32_t*)p, words);
   return launch_status();
 }
+
+namespace mmad_igemm {
+int set_lat_mode(int v) {
+  const int prev = igemm_lat_mode();
+  if (v >= 0) g_igemm_lat.store(v, std::memory_order_relaxed);
+  return prev;
+}
+}  // namespace mmad_igemm

@@ -1,0 +1,64 @@
+"""The implicit GEMM's residue-class row order (csrc/conv.hip, Geom::lat; round 5) on config
+5's 20^3 layer3 / layer4 geometry (pet_resnet_cnn.py:12-138 at 160^3, anat_cnn.py:29-31):
+rows ordered sub-lattice position major, so each tile skips the taps that leave the
+sub-lattice.  Only exact zero products are skipped and each output element keeps its K
+order, so the forward output and the input gradient (a forward over reversed taps) must be
+bit-identical to the plain voxel order; the BN partial sums group other rows per tile, so
+their per-channel totals agree to fp32 rounding; the weight gradient is the same kernel."""
+import pytest
+import torch
+
+from multimodal_alzheimer_amd import _lib
+from multimodal_alzheimer_amd import volume_ops as V
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CL = torch.channels_last_3d
+BF = torch.bfloat16
+
+CASES = [
+    ("layer4_20cube_b2", (2, 512, 20, 20, 20), 512, 4),
+    ("layer3_20cube_b8", (8, 256, 20, 20, 20), 256, 2),
+    ("layer4_ragged", (2, 256, 12, 20, 8), 256, 4),
+    ("layer4_4cube", (2, 512, 4, 4, 4), 512, 4),
+]
+
+
+def _variant(v):
+    return _lib.load().mmad_set_kernel_variant(b"igemm_lat", v)
+
+
+def _run(x, w, d):
+    xg = x.clone().requires_grad_(True)
+    wg = w.clone().requires_grad_(True)
+    y, stats = V.conv3d(xg, wg, None, (1,) * 3, (d,) * 3, (d,) * 3, BF, want_stats=True)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    gy = (torch.rand(y.shape, generator=g, device=DEV) * 2 - 1).to(BF).contiguous(memory_format=CL)
+    y.backward(gy)
+    torch.cuda.synchronize()
+    return y.detach(), stats.sum(0), xg.grad, wg.grad
+
+
+@pytest.mark.parametrize("name,xs,co,d", CASES, ids=[c[0] for c in CASES])
+def test_lattice_order_matches_voxel_order(name, xs, co, d):
+    g = torch.Generator(device=DEV).manual_seed(len(name))
+    x = (torch.rand(xs, generator=g, device=DEV) * 2 - 1).to(BF).contiguous(memory_format=CL)
+    w = (torch.rand((co, xs[1], 3, 3, 3), generator=g, device=DEV) * 2 - 1) * \
+        (3.0 / (xs[1] * 27)) ** 0.5
+    prev = _variant(0)
+    try:
+        ref = _run(x, w, d)
+        _variant(1)
+        got = _run(x, w, d)
+    finally:
+        _variant(prev)
+    assert torch.equal(got[0], ref[0]), "forward differs"
+    assert torch.equal(got[2], ref[2]), "input gradient differs"
+    assert torch.equal(got[3], ref[3]), "weight gradient differs"
+    yv = ref[0].float()
+    mag = torch.stack((yv.abs().sum(dim=(0, 2, 3, 4)), (yv * yv).sum(dim=(0, 2, 3, 4))))
+    assert ((got[1] - ref[1]).abs() <= 1e-5 * mag + 1e-6).all(), "BN partial-sum totals differ"
+    # and the conv itself against a plain fp32 conv of the same bf16 operands
+    yr = torch.nn.functional.conv3d(x.float(), w.to(BF).float(), None, 1, d, d)
+    err = (got[0].float() - yr).abs()
+    assert (err <= 2 ** -7 * yr.abs() + 1e-3 * yr.abs().max()).all()
