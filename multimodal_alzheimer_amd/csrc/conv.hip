@@ -519,8 +519,14 @@ __device__ __forceinline__ int wswz(int r) {
 // is a whole number of output rows, WBK % Wd == 0) x never changes, so the x test is made
 // once and only y/z carry.  (Index math was ~1/4 of the kernel's time: a build with the B
 // addressing stubbed out ran 12-30 % faster.)
+// LATW (round 5; g.lat set, bf16): the rows m are in igemm_kernel's residue-class order
+// (Geom::lat), the block's k tile lies inside one tap, and a stage's 32 rows share one
+// sub-lattice position -- so the stages where this tap leaves the sub-lattice (pure padding)
+// are dropped from the block's stage list (built once, wave 0, in LDS after the ring): no
+// DMA, no MFMA.  Row voxels are recomputed per stage from (position, sub) with shifts
+// (d and the sub count are powers of two).
 template <typename T, int BMW, int WBK, int NST, int WBNT = WBN, int WGM = 2, int WGN = 2,
-          bool XFIX = false>
+          bool XFIX = false, bool LATW = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* __restrict__ src,
                                                        const T* __restrict__ dy,
                                                        float* __restrict__ ws, int m_per_split,
@@ -595,12 +601,15 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
   const int dcz = -g.Dd * g.sd * HW + DHW;
   const int bshift = g.cs_shift + (sizeof(T) == 2 ? 1 : 2);
   int bci2[BIPW], bx[BIPW], by[BIPW], bz[BIPW], box[BIPW], boy[BIPW], boz[BIPW];
-  int srow[BIPW], tdel[BIPW];
+  int srow[BIPW], tdel[BIPW], browl[BIPW];
+  bool bkok[BIPW];
 #pragma unroll
   for (int i = 0; i < BIPW; ++i) {
     const int brow = (wave * BIPW + i) * BRPI + lane / BLPR;
     const int k = k0 + ((lane % BLPR) ^ wswz<T, BROWB>(brow)) * EPC;
     const bool kok = k < g.K;
+    browl[i] = brow;
+    bkok[i] = kok;
     bci2[i] = (k & (g.Cs - 1)) * (int)sizeof(T);
     const int to = tapoff[kok ? (k >> g.cs_shift) : 0];
     box[i] = ((to >> 16) & 255) - 128 - g.pw;
@@ -648,6 +657,38 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
       d += cy ? dcy : 0;
       d += cz ? dcz : 0;
       srow[i] += d;
+    }
+  };
+
+  // LATW: (position, sub) -> voxel.  S = nb * d^3 subs per position, d = 2^ld
+  const int latd = g.lat, ld = 31 - __builtin_clz(latd > 0 ? latd : 1);
+  const int lsub = g.nb * latd * latd * latd;
+  auto sub_vox = [&](int sv) -> int {
+    const int n = sv >> (3 * ld), r = sv & ((1 << (3 * ld)) - 1);
+    return ((n * g.Dd + (r >> (2 * ld))) * g.Hd + ((r >> ld) & (latd - 1))) * g.Wd +
+           (r & (latd - 1));
+  };
+  int acol[AIPW];
+#pragma unroll
+  for (int i = 0; i < AIPW; ++i) acol[i] = co0 + ((lane % ALPR) ^ wswz<T, AROWB>(arow[i])) * EPC;
+  auto issue_lat = [&](int stage, int ms) {
+    char* sbase = ring + stage * STAGE;
+    const int q = ms / lsub, sb = ms - q * lsub;
+    const int qx = q % g.lx, qy = (q / g.lx) % g.ly, qz = q / (g.lx * g.ly);
+    const int pos = ((latd * qz) * g.Hd + latd * qy) * g.Wd + latd * qx;
+#pragma unroll
+    for (int i = 0; i < AIPW; ++i) {
+      const bool ok = acok[i] && ms + arow[i] < mend;
+      const int v = pos + sub_vox(sb + arow[i]);
+      const uint32_t off = (uint32_t)(v * g.Nd + acol[i]) * (uint32_t)sizeof(T);
+      buf_lds16_asm(ok ? off : OOB, rsy, lds_addr_of(sbase + (wave * AIPW + i) * 1024));
+    }
+#pragma unroll
+    for (int i = 0; i < BIPW; ++i) {
+      const bool ok = bkok[i] && ms + browl[i] < mend;
+      const int v = pos + sub_vox(sb + browl[i]) + tdel[i];
+      const uint32_t off = ((uint32_t)v << bshift) + bci2[i];
+      buf_lds16_asm(ok ? off : OOB, rsx, lds_addr_of(sbase + A_BYTES + (wave * BIPW + i) * 1024));
     }
   };
 
@@ -751,13 +792,42 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
   // NST-deep ring, NST-1 stages of DMA in flight (asm DMA: hipcc adds no drains).  At the
   // top of step ks: wait until only the younger stages' DMA is outstanding, barrier (all
   // waves' DMA for ks landed; all waves done reading ks-1), refill buffer (ks-1) % NST.
-  const int nk = (mend - mbeg + WBK - 1) / WBK;
+  int nk = (mend - mbeg + WBK - 1) / WBK;
   constexpr int LPS = AIPW + BIPW;          // DMA instructions per stage per wave
   constexpr int PD = NST - 1;
+  uint16_t* vlist = reinterpret_cast<uint16_t*>(ring + NST * STAGE);
+  if constexpr (LATW) {
+    // this block's tap (its k tile lies in one) and the stages whose position it reaches
+    const int t = k0 >> g.cs_shift;
+    const int kz = t / (g.KW * g.KH) - 1, ky = (t / g.KW) % g.KH - 1, kx = t % g.KW - 1;
+    if (wave == 0) {
+      int cnt = 0;
+      for (int base = 0; base < nk; base += 64) {
+        const int j = base + lane;
+        bool v = false;
+        if (j < nk) {
+          const int q = (mbeg + j * WBK) / lsub;
+          const int qx = q % g.lx + kx, qy = (q / g.lx) % g.ly + ky, qz = q / (g.lx * g.ly) + kz;
+          v = (unsigned)qx < (unsigned)g.lx && (unsigned)qy < (unsigned)g.ly &&
+              (unsigned)qz < (unsigned)g.lz;
+        }
+        const uint64_t msk = __ballot(v);
+        if (v) vlist[cnt + __popcll(msk & ((uint64_t(1) << lane) - 1))] = (uint16_t)j;
+        cnt += __popcll(msk);
+      }
+      if (lane == 0) tapoff[MAXTAPS] = cnt;
+    }
+    __syncthreads();
+    nk = tapoff[MAXTAPS];
+  }
+  auto issue_at = [&](int stage, int s) {
+    if constexpr (LATW) issue_lat(stage, mbeg + (int)vlist[s] * WBK);
+    else issue(stage, mbeg + s * WBK);
+  };
   if (nk > 0) {
 #pragma unroll
     for (int s = 0; s < PD; ++s)
-      if (s < nk) issue(s, mbeg + s * WBK);
+      if (s < nk) issue_at(s, s);
     for (int ks = 0; ks < nk; ++ks) {
       const int younger = min(PD - 1, nk - 1 - ks);
       if constexpr (PD >= 3) {
@@ -771,7 +841,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
         wait_vm_lgkm0<0>();
       }
       raw_barrier();
-      if (ks + PD < nk) issue((ks + PD) % NST, mbeg + (ks + PD) * WBK);
+      if (ks + PD < nk) issue_at((ks + PD) % NST, ks + PD);
       if constexpr (sizeof(T) == 2) {
         read_frags(ks % NST);
         mma_frags();
@@ -1546,19 +1616,39 @@ int wgrad_xcd() {
   return v;
 }
 
-template <typename T, int BMW, int WBK, int NST, int WBNT, int WGM, int WGN, bool XFIX>
+template <typename T, int BMW, int WBK, int NST, int WBNT, int WGM, int WGN, bool XFIX,
+          bool LATW = false>
 int launch_wgrad_x(const Geom& g, const WSplit& sp, const void* x, const void* dy, float* ws,
                    hipStream_t st) {
-  const size_t lds = TAPB + NST * WBK * (BMW + WBNT) * sizeof(T);
-  static const bool ok = set_lds(wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX>, lds);
-  if (!ok) return MMAD_EUNSUPPORTED;
+  const size_t list = LATW ? (size_t)cdiv(cdiv(sp.m_per_split, WBK) * 2, 16) * 16 : 0;
+  const size_t lds = TAPB + NST * WBK * (BMW + WBNT) * sizeof(T) + list;
+  static const bool ok =
+      set_lds(wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX, LATW>,
+              TAPB + NST * WBK * (BMW + WBNT) * sizeof(T) + (LATW ? 32768 : 0));
+  if (!ok || lds > TAPB + NST * WBK * (BMW + WBNT) * sizeof(T) + (LATW ? 32768 : 0))
+    return MMAD_EUNSUPPORTED;
   const uint32_t xb = (uint32_t)((int64_t)g.nb * g.Ds * g.Hs * g.Ws * g.Cs * sizeof(T));
   const uint32_t yb = (uint32_t)((int64_t)g.M * g.Nd * sizeof(T));
   dim3 grid((unsigned)cdiv(g.K, WBNT), (unsigned)cdiv(g.Nd, BMW), (unsigned)sp.splits);
-  hipLaunchKernelGGL((wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX>), grid,
-                     dim3(64 * WGM * WGN), lds, st, g, (const T*)x, (const T*)dy, ws,
+  Geom gl = g;
+  if (LATW) {
+    gl.lat = g.dd;
+    gl.lz = g.Dd / g.dd; gl.ly = g.Hd / g.dd; gl.lx = g.Wd / g.dd;
+  }
+  hipLaunchKernelGGL((wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX, LATW>), grid,
+                     dim3(64 * WGM * WGN), lds, st, gl, (const T*)x, (const T*)dy, ws,
                      sp.m_per_split, xb, yb, wgrad_xcd());
   return launch_status();
+}
+
+// the residue-class stage skipping of wgrad_kernel (LATW) applies: igemm's lattice geometry,
+// bf16, power-of-two dilation and sub count, whole-tap k tiles, 32-row stages inside one
+// position, stage indices in 16 bits, list within 32 KiB
+bool lat_wgrad_ok(const Geom& g, int wbnt, int64_t m_per_split) {
+  if (!lat_geom(g) || !is_pow2(g.dd)) return false;
+  const int64_t S = (int64_t)g.nb * g.dd * g.dd * g.dd;
+  return is_pow2((int)S) && S % 32 == 0 && g.Cs % wbnt == 0 &&
+         cdiv(m_per_split, 32) <= 16384;
 }
 
 template <typename T, int BMW, int WBK, int NST, int WBNT = WBN, int WGM = 2, int WGN = 2>
@@ -1568,6 +1658,9 @@ int launch_wgrad_k(const Geom& g, const WSplit& sp, const void* x, const void* d
   if ((int64_t)g.nb * g.Ds * g.Hs * g.Ws * g.Cs * (int64_t)sizeof(T) >= (int64_t(1) << 31) ||
       (int64_t)g.M * g.Nd * (int64_t)sizeof(T) >= (int64_t(1) << 31))
     return MMAD_EUNSUPPORTED;
+  if constexpr (sizeof(T) == 2 && WBK == 32)
+    if (lat_wgrad_ok(g, WBNT, sp.m_per_split))
+      return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, false, true>(g, sp, x, dy, ws, st);
   if (WBK % g.Wd == 0)
     return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, true>(g, sp, x, dy, ws, st);
   return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, false>(g, sp, x, dy, ws, st);
