@@ -2077,11 +2077,23 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
     return MMAD_OK;
   }
   if (!unfolded(d) && mmad_pw::wgrad_ok(d, dtype)) {
-    // 1x1x1 (the shortcuts): the pointwise split-K GEMM, then the wide slab reduction
+    // 1x1x1 (the shortcuts) and the stride-2 3^3 conv: the pointwise split-K GEMM, then the
+    // wide (1^3) or transposing (3^3) slab reduction
     rc = mmad_pw::wgrad(d, x, dy, (float*)workspace, st);
     if (rc) return rc;
     const int splits = (int)mmad_pw::wgrad_splits(d);
     const int64_t total = (int64_t)g.Nd * g.K;
+    if (g.taps > 1) {
+      if (defer != nullptr) {
+        *defer = plan_reduce_t((const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.taps);
+        return MMAD_OK;
+      }
+      if (rst != st && (rc = fork_stream(st, rst))) return rc;
+      rc = launch_reduce_t((const float*)workspace, dw, splits, g.Nd, g.K, g.Cs, g.taps, rst);
+      if (rc) return rc;
+      if (dbias) return mmad_colsum_ws(dtype, g.M, g.Nd, dy, (float*)workspace, dbias, rstream);
+      return MMAD_OK;
+    }
     if (defer != nullptr && ((uintptr_t)dw & 15) == 0) {
       mmad_reduce::Job& j = *defer;
       j.ws = (const float*)workspace; j.dw = dw; j.splits = splits; j.nd = g.Nd;

@@ -20,9 +20,10 @@ bool fwd_ok(const mmad_conv_desc* d, int dtype);
 int64_t fwd_tiles(const mmad_conv_desc* d);
 int fwd(const mmad_conv_desc* d, const void* x, const void* wp, const float* bias, void* y,
         float* stats, void* stream);
-// the weight gradient of a bf16 1x1x1 conv of stride 1 or 2 with co % 128 == 0, ci % 64 == 0
-// (the shortcuts): split-K MFMA GEMM over the voxels into fp32 slabs [split][co][ci]
-// (wgrad_splits slabs), summed by the caller's wide slab reduction
+// the weight gradient of a bf16 1x1x1 conv of stride 1 or 2 (the shortcuts), or of a 3^3
+// stride-2 pad-1 conv (layer2.0.conv1), with co % 128 == 0, ci % 64 == 0: split-K MFMA GEMM
+// over the voxels into fp32 slabs [split][co][tap * ci + ci'] (wgrad_splits slabs), summed by
+// the caller's slab reduction (wide for 1^3, transposing for 3^3)
 bool wgrad_ok(const mmad_conv_desc* d, int dtype);
 int64_t wgrad_splits(const mmad_conv_desc* d);
 int wgrad(const mmad_conv_desc* d, const void* x, const void* dy, float* ws, void* stream);

@@ -260,24 +260,36 @@ constexpr int WG_NTHR = 256;
 __device__ __forceinline__ int pw_tsw256(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
 __device__ __forceinline__ int pw_tsw128(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
 
-template <int CIT>
+// NTAP = 3 (MODE 2, round 5): the stride-2 3^3 conv of layer2.0.conv1 (64 -> 128, pad 1):
+// dW[co][tap][ci] = sum_m dY[m][co] * X[2 o(m) + tap - 1][ci].  A block takes one (kz, ky)
+// and the three kx taps, so each stage's dY rows feed three X images (one gathered row set
+// per kx: input voxel 2o + k - 1 per dimension, a zero block outside the volume) and three
+// accumulator sets; slabs [split][co][tap * Ci + ci] for the transposing reduction.  The
+// row-gather wgrad_kernel ran it with 69 splits (61 MB of slabs) at 0.13 of peak.
+template <int CIT, int NTAP = 1>
 struct WGC {
   static constexpr int YROW = 256;                    // 128 co x 2 B
   static constexpr int XROW = CIT * 2;
   static constexpr int YIMG = WG_KS * YROW;           // 8 KiB
-  static constexpr int XIMG = WG_KS * XROW;           // 8 / 4 KiB
-  static constexpr int SLOT = YIMG + XIMG;
-  static constexpr int LDS = WG_NS * SLOT;            // 64 / 48 KiB
-  static constexpr int NQ = SLOT / 1024;              // DMA instructions per stage: 16 / 12
-  static constexpr int WI = NQ / 4;                   // per wave: 4 / 3
+  static constexpr int XIMG = WG_KS * XROW;           // 8 / 4 KiB per tap
+  static constexpr int SLOT = YIMG + NTAP * XIMG;
+  static constexpr int LDS = WG_NS * SLOT;            // 64 / 48 / 80 KiB
+  static constexpr int NQ = SLOT / 1024;              // DMA instructions per stage
+  static constexpr int WI = NQ / 4;                   // per wave
+  static_assert(WI * 4 == NQ, "stage DMA split over 4 waves");
   static constexpr int TJ = CIT / 32;                 // 16-column ci tiles per wave: 4 / 2
+  static constexpr int XQ = XIMG / 1024;              // DMA instructions per X image
 };
 
-template <int CIT, int MODE>   // MODE 0: stride 1; 1: X row of voxel m is s2_src(m)
+__device__ const u32x4 pw_zero_chunk[8] = {};
+
+// MODE 0: stride 1, X row = m; 1: stride 2 1^3, X row = s2_src(m); 2: stride 2 3^3 (NTAP 3)
+template <int CIT, int MODE, int NTAP = 1>
 __global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, float* __restrict__ out, int Ci,
     int Co, int kper, int ntiles, PwS2 s2) {
-  using C = WGC<CIT>;
+  using C = WGC<CIT, NTAP>;
+  static_assert(MODE != 2 || NTAP == 3, "the 3^3 form takes the three kx taps");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -286,15 +298,17 @@ __global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
   const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
   const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
   const int tile = lin % ntiles, split = lin / ntiles;
-  const int nci = Ci / CIT;
-  const int co0 = (tile / nci) * 128, ci0 = (tile % nci) * CIT;
+  const int nci = Ci / CIT, nco = Co / 128;
+  const int ci0 = (tile % nci) * CIT, co0 = ((tile / nci) % nco) * 128;
+  const int kzy = MODE == 2 ? tile / (nci * nco) : 0;          // (kz, ky) of the 3^3 form
+  const int kz = kzy / 3, ky = kzy % 3;
   const int64_t m0 = (int64_t)split * kper;
   const int nstage = kper / WG_KS;
 
   // DMA instruction q (= wave + 4 h) of a stage: q < 8 the dY image (rows 4q .. 4q + 3),
-  // else the X image (256-B rows: 4 per instruction; 128-B rows: 8)
+  // else X image (q - 8) / XQ (256-B rows: 4 per instruction; 128-B rows: 8)
   const u16* sp[C::WI];
-  int64_t srow[C::WI];                  // the voxel (stage 0) this lane's row reads
+  int srow[C::WI], tapx[C::WI];
   uint32_t lofs[C::WI];
   bool isx[C::WI];
 #pragma unroll
@@ -305,14 +319,16 @@ __global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
       const int row = 4 * q + (lane >> 4);
       const int ch = (lane & 15) ^ pw_tsw256(row);
       isx[h] = false;
-      srow[h] = m0 + row;
+      tapx[h] = 0;
+      srow[h] = row;
       sp[h] = dy + (int64_t)co0 + ch * 8;
     } else {
-      const int qx = q - 8;
+      const int qx = (q - 8) % C::XQ;
       const int row = CIT == 128 ? 4 * qx + (lane >> 4) : 8 * qx + (lane >> 3);
       const int ch = CIT == 128 ? (lane & 15) ^ pw_tsw256(row) : (lane & 7) ^ pw_tsw128(row);
       isx[h] = true;
-      srow[h] = m0 + row;
+      tapx[h] = (q - 8) / C::XQ;                                 // kx of this image
+      srow[h] = row;
       sp[h] = x + (int64_t)ci0 + ch * 8;
     }
   }
@@ -321,9 +337,28 @@ __global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
     const uint32_t slot = smem_l + (uint32_t)((s % WG_NS) * C::SLOT);
 #pragma unroll
     for (int h = 0; h < C::WI; ++h) {
-      const int64_t m = srow[h] + (int64_t)s * WG_KS;
-      const int64_t v = (MODE == 1 && isx[h]) ? s2_src(s2, m) : m;
-      glds16_asm(sp[h] + v * (isx[h] ? Ci : Co), slot + lofs[h]);
+      const int64_t m = m0 + (int64_t)s * WG_KS + srow[h];
+      const void* p;
+      if (!isx[h]) {
+        p = sp[h] + m * Co;
+      } else if (MODE == 0) {
+        p = sp[h] + m * Ci;
+      } else if (MODE == 1) {
+        p = sp[h] + s2_src(s2, m) * Ci;
+      } else {
+        const int ox = (int)(m % s2.Wo);
+        int64_t t = m / s2.Wo;
+        const int oy = (int)(t % s2.Ho);
+        t /= s2.Ho;
+        const int oz = (int)(t % s2.Do);
+        const int64_t n = t / s2.Do;
+        const int iz = 2 * oz + kz - 1, iy = 2 * oy + ky - 1, ix = 2 * ox + tapx[h] - 1;
+        const bool ok = (unsigned)iz < (unsigned)s2.Di && (unsigned)iy < (unsigned)s2.Hi &&
+                        (unsigned)ix < (unsigned)s2.Wi;
+        p = ok ? (const void*)(sp[h] + (((n * s2.Di + iz) * s2.Hi + iy) * s2.Wi + ix) * Ci)
+               : (const void*)pw_zero_chunk;
+      }
+      glds16_asm(p, slot + lofs[h]);
     }
   };
 
@@ -349,11 +384,13 @@ __global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
   auto tr8 = [](const char* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p);
   };
-  f32x4 acc[4][C::TJ];
+  f32x4 acc[NTAP][4][C::TJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int t = 0; t < NTAP; ++t)
 #pragma unroll
-    for (int j = 0; j < C::TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < C::TJ; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   issue(0);
   if (nstage > 1) issue(1);
@@ -367,35 +404,44 @@ __global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
     int so = (s % WG_NS) * C::SLOT;
     asm volatile("" : "+s"(so));
     const char* slot = smem + so;
-    bf16x8 a[4], b[C::TJ];
+    bf16x8 a[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       a[i] = __builtin_shufflevector(tr8(slot + ya_lo[i]), tr8(slot + ya_hi[i]), 0, 1, 2, 3, 4,
                                      5, 6, 7);
 #pragma unroll
-    for (int j = 0; j < C::TJ; ++j)
-      b[j] = __builtin_shufflevector(tr8(slot + xb_lo[j]), tr8(slot + xb_hi[j]), 0, 1, 2, 3, 4,
-                                     5, 6, 7);
+    for (int t = 0; t < NTAP; ++t) {
+      bf16x8 b[C::TJ];
+#pragma unroll
+      for (int j = 0; j < C::TJ; ++j)
+        b[j] = __builtin_shufflevector(tr8(slot + t * C::XIMG + xb_lo[j]),
+                                       tr8(slot + t * C::XIMG + xb_hi[j]), 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TJ; ++j)
+          acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[t][i][j], 0, 0, 0);
+    }
+  }
+
+  // acc[t][i][j][r]: co = wm*64 + i*16 + 4 lk + r, ci = wn*CIT/2 + j*16 + (lane & 15);
+  // slab column tap * Ci + ci (taps = 27 for the 3^3 form, tap = (kz*3 + ky)*3 + kx)
+  const int K = MODE == 2 ? 27 * Ci : Ci;
+  float* o = out + (int64_t)split * Co * K;
+  const int lr = lane & 15;
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < C::TJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-  }
-
-  // acc[i][j][r]: co = wm*64 + i*16 + 4 lk + r, ci = wn*CIT/2 + j*16 + (lane & 15)
-  float* o = out + (int64_t)split * Co * Ci;
-  const int lr = lane & 15;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < C::TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * 64 + i * 16 + 4 * lk + r;
-        const int ci = ci0 + wn * (CIT / 2) + j * 16 + lr;
-        o[(int64_t)co * Ci + ci] = acc[i][j][r];
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + wm * 64 + i * 16 + 4 * lk + r;
+          const int ci = ci0 + wn * (CIT / 2) + j * 16 + lr;
+          const int col = MODE == 2 ? (kzy * 3 + t) * Ci + ci : ci;
+          o[(int64_t)co * K + col] = acc[t][i][j][r];
+        }
 }
 
 bool pw_wgrad_on() {
@@ -496,26 +542,38 @@ int fwd(const mmad_conv_desc* d, const void* x, const void* wp, const float* bia
 
 namespace {
 int wg_cit(const mmad_conv_desc* d) { return d->ci % 128 == 0 && d->ci >= 256 ? 128 : 64; }
+// the 3^3 stride-2 form (layer2.0.conv1): pad 1, dilation 1, the s2 grid relation
+bool wg3_geom(const mmad_conv_desc* d) {
+  return d->kd == 3 && d->kh == 3 && d->kw == 3 && d->pd == 1 && d->ph == 1 && d->pw == 1 &&
+         d->dd == 1 && d->dh == 1 && d->dw == 1 && s2_geom(d);
+}
+int64_t wg_tiles(const mmad_conv_desc* d) {
+  const int64_t t = (int64_t)(d->co / 128) * (d->ci / (wg3_geom(d) ? 64 : wg_cit(d)));
+  return wg3_geom(d) ? 9 * t : t;
+}
 }  // namespace
 
 bool wgrad_ok(const mmad_conv_desc* d, int dtype) {
   if (!pw_on() || !pw_wgrad_on() || dtype != MMAD_BF16) return false;
-  if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw) return false;
-  if (!stride1_geom(d) && !s2_geom(d)) return false;
+  const bool one = d->kd == 1 && d->kh == 1 && d->kw == 1 && !d->pd && !d->ph && !d->pw &&
+                   (stride1_geom(d) || s2_geom(d));
+  if (!one && !wg3_geom(d)) return false;
   if (d->co % 128 || d->ci % 64) return false;
   const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
   const int64_t mi = (int64_t)d->n * d->di * d->hi * d->wi;
   return m % WG_KS == 0 && m * d->co < (int64_t(1) << 40) && mi * d->ci < (int64_t(1) << 40);
 }
 
-// voxels per split: the split count that gives ~512 blocks (two per CU), K ranges of at least
-// 4 stages, a divisor of the voxel count
+// voxels per split: the split count that gives ~512 blocks (two per CU) -- ~256 for the 3^3
+// form, whose slabs hold 27 taps -- K ranges of at least 4 stages, a divisor of the voxel
+// count
 int64_t wgrad_kper(const mmad_conv_desc* d) {
   const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
-  const int64_t tiles = (int64_t)(d->co / 128) * (d->ci / wg_cit(d));
+  const int64_t tiles = wg_tiles(d);
+  const int64_t want = wg3_geom(d) ? 256 : 512;
   int64_t kper = m;
   while (kper % 2 == 0 && (kper / 2) % WG_KS == 0 && kper / 2 >= 4 * WG_KS &&
-         tiles * (m / kper) < 512)
+         tiles * (m / kper) < want)
     kper /= 2;
   return kper;
 }
@@ -526,21 +584,22 @@ int64_t wgrad_splits(const mmad_conv_desc* d) {
 
 int wgrad(const mmad_conv_desc* d, const void* x, const void* dy, float* ws, void* stream) {
   if (!wgrad_ok(d, MMAD_BF16)) return MMAD_EUNSUPPORTED;
-  const int cit = wg_cit(d);
   const int64_t kper = wgrad_kper(d), sp = wgrad_splits(d);
-  const int ntiles = (d->co / 128) * (d->ci / cit);
+  const int64_t ntiles = wg_tiles(d);
   const int64_t nblk = sp * ntiles;
   if (nblk > 0x7fffffff || kper > 0x7fffffff) return MMAD_EUNSUPPORTED;
   const PwS2 q = s2_of(d);
-  const bool s2 = s2_geom(d);
   auto go = [&](auto kern, int lds) {
     static_cast<void>(hipFuncSetAttribute((const void*)kern,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(WG_NTHR), lds, as_stream(stream),
-                       (const u16*)x, (const u16*)dy, ws, d->ci, d->co, (int)kper, ntiles, q);
+                       (const u16*)x, (const u16*)dy, ws, d->ci, d->co, (int)kper, (int)ntiles,
+                       q);
     return launch_status();
   };
-  if (cit == 128)
+  if (wg3_geom(d)) return go(pw_wgrad_kernel<64, 2, 3>, WGC<64, 3>::LDS);
+  const bool s2 = s2_geom(d);
+  if (wg_cit(d) == 128)
     return s2 ? go(pw_wgrad_kernel<128, 1>, WGC<128>::LDS) : go(pw_wgrad_kernel<128, 0>, WGC<128>::LDS);
   return s2 ? go(pw_wgrad_kernel<64, 1>, WGC<64>::LDS) : go(pw_wgrad_kernel<64, 0>, WGC<64>::LDS);
 }

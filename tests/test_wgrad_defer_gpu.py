@@ -102,3 +102,20 @@ def test_pointwise_wgrad_vs_float64(xs, co, s):
     mag = torch.einsum("nczyx,nkzyx->ck", gd.abs(), xd.abs())
     err = (got.double().reshape(ref.shape) - ref).abs()
     assert (err <= 1e-3 * ref.abs() + 1e-4 * mag).all(), f"max err {err.max().item():.3e}"
+
+
+@pytest.mark.parametrize("xs,co", [((2, 64, 32, 32, 32), 128), ((2, 64, 15, 16, 16), 128),
+                                   ((1, 128, 16, 16, 16), 256)],
+                         ids=["layer2_conv1", "odd_depth", "wide_ci"])
+def test_stride2_3cube_wgrad_vs_float64(xs, co):
+    """the stride-2 3^3 weight gradient (pw_wgrad_kernel's 3-tap form + transposing slab
+    reduction; layer2.0.conv1) against torch's float64 weight gradient of the same bf16
+    operands: within 1e-3 |ref| + 1e-4 sum |gY| |X|"""
+    x, w = _operands(xs, (co, xs[1], 3, 3, 3), 11)
+    got, gy, _ = _wgrad(x, w, 2, 1, 1)
+    xd, gd = x.double(), gy.double()
+    ref = torch.nn.grad.conv3d_weight(xd, w.shape, gd, 2, 1, 1)
+    mag = torch.nn.grad.conv3d_weight(xd.abs(), w.shape, gd.abs(), 2, 1, 1)
+    err = (got.double() - ref).abs()
+    assert (err <= 1e-3 * ref.abs() + 1e-4 * mag).all(), f"max err {err.max().item():.3e}"
+
