@@ -1645,7 +1645,8 @@ int launch_wgrad_x(const Geom& g, const WSplit& sp, const void* x, const void* d
 // bf16, power-of-two dilation and sub count, whole-tap k tiles, 32-row stages inside one
 // position, stage indices in 16 bits, list within 32 KiB
 bool lat_wgrad_ok(const Geom& g, int wbnt, int64_t m_per_split) {
-  if (!lat_geom(g) || !is_pow2(g.dd)) return false;
+  // (MMAD_IGEMM_LAT=2: the forward / input-gradient order only, A/B)
+  if (!lat_geom(g) || !is_pow2(g.dd) || igemm_lat_mode() == 2) return false;
   const int64_t S = (int64_t)g.nb * g.dd * g.dd * g.dd;
   return is_pow2((int)S) && S % 32 == 0 && g.Cs % wbnt == 0 &&
          cdiv(m_per_split, 32) <= 16384;

@@ -281,13 +281,11 @@ struct WGC {
   static constexpr int XQ = XIMG / 1024;              // DMA instructions per X image
 };
 
-__device__ const u32x4 pw_zero_chunk[8] = {};
-
 // MODE 0: stride 1, X row = m; 1: stride 2 1^3, X row = s2_src(m); 2: stride 2 3^3 (NTAP 3)
 template <int CIT, int MODE, int NTAP = 1>
 __global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, float* __restrict__ out, int Ci,
-    int Co, int kper, int ntiles, PwS2 s2) {
+    int Co, int kper, int ntiles, PwS2 s2, uint32_t xbytes, uint32_t ybytes) {
   using C = WGC<CIT, NTAP>;
   static_assert(MODE != 2 || NTAP == 3, "the 3^3 form takes the three kx taps");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -306,59 +304,81 @@ __global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
   const int nstage = kper / WG_KS;
 
   // DMA instruction q (= wave + 4 h) of a stage: q < 8 the dY image (rows 4q .. 4q + 3),
-  // else X image (q - 8) / XQ (256-B rows: 4 per instruction; 128-B rows: 8)
-  const u16* sp[C::WI];
-  int srow[C::WI], tapx[C::WI];
-  uint32_t lofs[C::WI];
+  // else X image (q - 8) / XQ (256-B rows: 4 per instruction; 128-B rows: 8).  Operands
+  // move by buffer_load ... lds with 32-bit byte offsets (an offset past the buffer reads
+  // zeros: the 3^3 form's padding); each row's offset advances incrementally per stage --
+  // dY / stride-1 X by a constant, the strided X rows as a mixed-radix (x, y, z, n) add of
+  // the 32-voxel step with at most one carry per digit (no divisions in the loop)
+  constexpr uint32_t OOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dy, 0, (int)__builtin_amdgcn_readfirstlane((int)ybytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, 0, (int)__builtin_amdgcn_readfirstlane((int)xbytes), 0x00020000);
+  // the 32-voxel step in the output grid's (x, y, z, n) digits (MODE 1 / 2)
+  const int stx = WG_KS % s2.Wo, st1 = WG_KS / s2.Wo;
+  const int sty = MODE ? st1 % s2.Ho : 0, st2 = MODE ? st1 / s2.Ho : 0;
+  const int stz = MODE ? st2 % s2.Do : 0, stn = MODE ? st2 / s2.Do : 0;
+  uint32_t off[C::WI], lofs[C::WI], cix[C::WI];
+  int ox[C::WI], oy[C::WI], oz[C::WI], on[C::WI], tapx[C::WI];
   bool isx[C::WI];
 #pragma unroll
   for (int h = 0; h < C::WI; ++h) {
     const int q = wave + 4 * h;
     lofs[h] = (uint32_t)(q * 1024);
+    int row, ch;
     if (q < 8) {
-      const int row = 4 * q + (lane >> 4);
-      const int ch = (lane & 15) ^ pw_tsw256(row);
+      row = 4 * q + (lane >> 4);
+      ch = (lane & 15) ^ pw_tsw256(row);
       isx[h] = false;
       tapx[h] = 0;
-      srow[h] = row;
-      sp[h] = dy + (int64_t)co0 + ch * 8;
+      off[h] = (uint32_t)((m0 + row) * Co + co0 + ch * 8) * 2u;
     } else {
       const int qx = (q - 8) % C::XQ;
-      const int row = CIT == 128 ? 4 * qx + (lane >> 4) : 8 * qx + (lane >> 3);
-      const int ch = CIT == 128 ? (lane & 15) ^ pw_tsw256(row) : (lane & 7) ^ pw_tsw128(row);
+      row = CIT == 128 ? 4 * qx + (lane >> 4) : 8 * qx + (lane >> 3);
+      ch = CIT == 128 ? (lane & 15) ^ pw_tsw256(row) : (lane & 7) ^ pw_tsw128(row);
       isx[h] = true;
       tapx[h] = (q - 8) / C::XQ;                                 // kx of this image
-      srow[h] = row;
-      sp[h] = x + (int64_t)ci0 + ch * 8;
+      off[h] = (uint32_t)((m0 + row) * Ci + ci0 + ch * 8) * 2u;   // (MODE 0)
     }
+    cix[h] = (uint32_t)(ci0 + ch * 8) * 2u;
+    const int64_t m = m0 + row;
+    ox[h] = (int)(m % s2.Wo);
+    const int64_t t1 = m / s2.Wo;
+    oy[h] = (int)(t1 % s2.Ho);
+    oz[h] = (int)((t1 / s2.Ho) % s2.Do);
+    on[h] = (int)(t1 / s2.Ho / s2.Do);
   }
+  const uint32_t ystep = (uint32_t)(WG_KS * Co) * 2u, xstep = (uint32_t)(WG_KS * Ci) * 2u;
   const uint32_t smem_l = lds_addr_of(smem);
   auto issue = [&](int s) {
     const uint32_t slot = smem_l + (uint32_t)((s % WG_NS) * C::SLOT);
 #pragma unroll
     for (int h = 0; h < C::WI; ++h) {
-      const int64_t m = m0 + (int64_t)s * WG_KS + srow[h];
-      const void* p;
       if (!isx[h]) {
-        p = sp[h] + m * Co;
+        buf_lds16_asm(off[h], rsy, slot + lofs[h]);
+        off[h] += ystep;
       } else if (MODE == 0) {
-        p = sp[h] + m * Ci;
-      } else if (MODE == 1) {
-        p = sp[h] + s2_src(s2, m) * Ci;
+        buf_lds16_asm(off[h], rsx, slot + lofs[h]);
+        off[h] += xstep;
       } else {
-        const int ox = (int)(m % s2.Wo);
-        int64_t t = m / s2.Wo;
-        const int oy = (int)(t % s2.Ho);
-        t /= s2.Ho;
-        const int oz = (int)(t % s2.Do);
-        const int64_t n = t / s2.Do;
-        const int iz = 2 * oz + kz - 1, iy = 2 * oy + ky - 1, ix = 2 * ox + tapx[h] - 1;
+        const int dz = MODE == 2 ? kz - 1 : 0, dyy = MODE == 2 ? ky - 1 : 0;
+        const int dx = MODE == 2 ? tapx[h] - 1 : 0;
+        const int iz = 2 * oz[h] + dz, iy = 2 * oy[h] + dyy, ix = 2 * ox[h] + dx;
         const bool ok = (unsigned)iz < (unsigned)s2.Di && (unsigned)iy < (unsigned)s2.Hi &&
                         (unsigned)ix < (unsigned)s2.Wi;
-        p = ok ? (const void*)(sp[h] + (((n * s2.Di + iz) * s2.Hi + iy) * s2.Wi + ix) * Ci)
-               : (const void*)pw_zero_chunk;
+        const uint32_t v = (uint32_t)(((on[h] * s2.Di + iz) * s2.Hi + iy) * s2.Wi + ix);
+        buf_lds16_asm(ok ? v * (uint32_t)Ci * 2u + cix[h] : OOB, rsx, slot + lofs[h]);
+        ox[h] += stx;
+        const int cx = ox[h] >= s2.Wo;
+        ox[h] -= cx ? s2.Wo : 0;
+        oy[h] += sty + cx;
+        const int cy = oy[h] >= s2.Ho;
+        oy[h] -= cy ? s2.Ho : 0;
+        oz[h] += stz + cy;
+        const int cz = oz[h] >= s2.Do;
+        oz[h] -= cz ? s2.Do : 0;
+        on[h] += stn + cz;
       }
-      glds16_asm(p, slot + lofs[h]);
     }
   };
 
@@ -561,7 +581,9 @@ bool wgrad_ok(const mmad_conv_desc* d, int dtype) {
   if (d->co % 128 || d->ci % 64) return false;
   const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
   const int64_t mi = (int64_t)d->n * d->di * d->hi * d->wi;
-  return m % WG_KS == 0 && m * d->co < (int64_t(1) << 40) && mi * d->ci < (int64_t(1) << 40);
+  // (32-bit byte offsets, bit 31 marking padding)
+  return m % WG_KS == 0 && m * d->co * 2 < (int64_t(1) << 31) &&
+         mi * d->ci * 2 < (int64_t(1) << 31);
 }
 
 // voxels per split: the split count that gives ~512 blocks (two per CU) -- ~256 for the 3^3
@@ -587,14 +609,19 @@ int wgrad(const mmad_conv_desc* d, const void* x, const void* dy, float* ws, voi
   const int64_t kper = wgrad_kper(d), sp = wgrad_splits(d);
   const int64_t ntiles = wg_tiles(d);
   const int64_t nblk = sp * ntiles;
-  if (nblk > 0x7fffffff || kper > 0x7fffffff) return MMAD_EUNSUPPORTED;
+  const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
+  const int64_t mi = (int64_t)d->n * d->di * d->hi * d->wi;
+  // 32-bit byte offsets (bit 31 marks padding)
+  if (nblk > 0x7fffffff || m * d->co * 2 >= (int64_t(1) << 31) ||
+      mi * d->ci * 2 >= (int64_t(1) << 31))
+    return MMAD_EUNSUPPORTED;
   const PwS2 q = s2_of(d);
   auto go = [&](auto kern, int lds) {
     static_cast<void>(hipFuncSetAttribute((const void*)kern,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(WG_NTHR), lds, as_stream(stream),
                        (const u16*)x, (const u16*)dy, ws, d->ci, d->co, (int)kper, (int)ntiles,
-                       q);
+                       q, (uint32_t)(mi * d->ci * 2), (uint32_t)(m * d->co * 2));
     return launch_status();
   };
   if (wg3_geom(d)) return go(pw_wgrad_kernel<64, 2, 3>, WGC<64, 3>::LDS);
