@@ -82,6 +82,43 @@ __device__ __forceinline__ bool src_voxel(const Geom& g, int bz, int by, int bx,
          (unsigned)x < (unsigned)g.Ws;
 }
 
+// Sub-lattice position of rank k, heavy first: positions grouped by how many of the
+// sub-lattice's faces they touch (none, then one, two, three -- 27, 18, 12, 8 taps for a
+// 3^3 kernel), each group enumerated face pattern by face pattern (z, y, x bits), interior
+// coordinates raster order.  Tiles are dispatched in rank order, so the first wave of blocks
+// holds the 27-tap positions and the light ones fill the tail (in raster order two heavy
+// tiles could share a CU while others idle: the tap skipping then bought nothing).
+__device__ __forceinline__ void lat_pos(const Geom& g, int k, int& qz, int& qy, int& qx) {
+  const int L[3] = {g.lx, g.ly, g.lz};                      // x, y, z
+  int v[3] = {0, 0, 0};
+  constexpr int masks[8] = {0, 1, 2, 4, 3, 5, 6, 7};        // faces touched: 0, 1, 1, 1, 2, ...
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int mk = masks[mi];
+    int cnt = 1;
+#pragma unroll
+    for (int dd = 0; dd < 3; ++dd)
+      cnt *= (mk >> dd) & 1 ? min(L[dd], 2) : max(L[dd] - 2, 0);
+    if (k < cnt) {
+#pragma unroll
+      for (int dd = 0; dd < 3; ++dd) {
+        if ((mk >> dd) & 1) {
+          const int nb = min(L[dd], 2);
+          v[dd] = (k % nb) ? L[dd] - 1 : 0;
+          k /= nb;
+        } else {
+          const int ni = L[dd] - 2;
+          v[dd] = 1 + k % ni;
+          k /= ni;
+        }
+      }
+      break;
+    }
+    k -= cnt;
+  }
+  qx = v[0]; qy = v[1]; qz = v[2];
+}
+
 // voxel of row m in the residue-class order (Geom::lat)
 __device__ __forceinline__ void lat_voxel(const Geom& g, int m, int& n, int& z, int& y, int& x) {
   const int d = g.lat, d3 = d * d * d;
@@ -89,7 +126,8 @@ __device__ __forceinline__ void lat_voxel(const Geom& g, int m, int& n, int& z, 
   const int q = m / S, s = m - q * S;
   n = s / d3;
   const int r = s - n * d3;
-  const int qx = q % g.lx, qy = (q / g.lx) % g.ly, qz = q / (g.lx * g.ly);
+  int qx, qy, qz;
+  lat_pos(g, q, qz, qy, qx);
   z = r / (d * d) + d * qz;
   y = (r / d) % d + d * qy;
   x = r % d + d * qx;
