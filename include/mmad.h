@@ -199,6 +199,10 @@ typedef struct mmad_wgrad_job {
 int mmad_conv3d_wgrad_deferred(const mmad_conv_desc* d, int dtype, const void* x,
                                const void* dy, float* dw, void* workspace, mmad_wgrad_job* job,
                                void* stream);
+/* the same for the stem straight from the raw volume (mmad_conv3d_wgrad_raw) */
+int mmad_conv3d_wgrad_raw_deferred(const mmad_conv_desc* d, int in_dtype, const void* x,
+                                   int dtype, const void* dy, float* dw, void* workspace,
+                                   mmad_wgrad_job* job, void* stream);
 /* jobs: host array (copied into the launch's arguments, so a captured launch replays the
  * same jobs); any njobs (16 per launch) */
 int mmad_wgrad_reduce_batch(int njobs, const mmad_wgrad_job* jobs, void* stream);

@@ -99,6 +99,8 @@ _SIGS = {
     "mmad_conv3d_wgrad_split": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_conv3d_wgrad_deferred": (_i32, [_P, _i32, _vp, _vp, _vp, _vp,
                                           C.POINTER(WgradJob), _vp]),
+    "mmad_conv3d_wgrad_raw_deferred": (_i32, [_P, _i32, _vp, _i32, _vp, _vp, _vp,
+                                              C.POINTER(WgradJob), _vp]),
     "mmad_wgrad_reduce_batch": (_i32, [_i32, C.POINTER(WgradJob), _vp]),
     "mmad_stem_raw_ok": (_i32, [_P, _i32, _i32]),
     "mmad_conv3d_fwd_raw": (_i32, [_P, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),

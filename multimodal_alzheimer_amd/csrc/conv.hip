@@ -2084,11 +2084,19 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
       g.K == 392) {
     rc = mmad_stem::wgrad(d, x, dy, (float*)workspace, stream, raw_dtype);
     if (rc) return rc;
-    if (rst != st && (rc = fork_stream(st, rst))) return rc;
     // (one slab per block: sum 16-slab groups in place first, so no thread walks them all)
     const int nb = (int)mmad_stem::wgrad_blocks(d);
     const int64_t total = (int64_t)g.Nd * g.K;
     constexpr int G = 16;
+    static_assert(G == mmad_reduce::STEM_G, "the deferred stem reduction sums the same groups");
+    if (defer != nullptr && cdiv(nb, G) <= 32) {
+      mmad_reduce::Job& j = *defer;
+      j.ws = (const float*)workspace; j.dw = dw; j.splits = nb; j.nd = g.Nd; j.k = g.K;
+      j.cs = g.Cs; j.taps = g.taps; j.tper = d->kw; j.kind = mmad_reduce::KIND_STEM;
+      j.gx = (int)cdiv(total, 64); j.gy = 1; j.gz = 1;
+      return MMAD_OK;
+    }
+    if (rst != st && (rc = fork_stream(st, rst))) return rc;
     hipLaunchKernelGGL(slab_group_sum_kernel, dim3(grid_for(total * cdiv(nb, G))), dim3(256), 0,
                        rst, (float*)workspace, nb, total, G);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, rst,
@@ -2240,6 +2248,16 @@ int mmad_wgrad_reduce_batch(int njobs, const mmad_wgrad_job* jobs, void* stream)
     ++b.n;
   }
   return flush();
+}
+
+int mmad_conv3d_wgrad_raw_deferred(const mmad_conv_desc* d, int in_dtype, const void* x,
+                                   int dtype, const void* dy, float* dw, void* workspace,
+                                   mmad_wgrad_job* job, void* stream) {
+  if (!desc_ok(d)) return MMAD_EBADSHAPE;
+  if (job == nullptr) return MMAD_ENULL;
+  if (!mmad_stem_raw_ok(d, in_dtype, dtype)) return MMAD_EUNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  return conv3d_wgrad(d, dtype, x, dy, dw, nullptr, workspace, st, st, in_dtype, job);
 }
 
 int mmad_conv3d_wgrad_split(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,

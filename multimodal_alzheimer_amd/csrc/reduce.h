@@ -9,7 +9,7 @@
 
 namespace mmad_reduce {
 
-enum { KIND_NONE = 0, KIND_T = 1, KIND_TZ = 2, KIND_WIDE = 3 };
+enum { KIND_NONE = 0, KIND_T = 1, KIND_TZ = 2, KIND_WIDE = 3, KIND_STEM = 4 };
 // the C ABI's record of one pending reduction (include/mmad.h); KIND_WIDE: 1x1x1 slabs
 // [split][co][ci] (dW in the same order), gx blocks of 256 elements
 using Job = mmad_wgrad_job;
@@ -109,11 +109,44 @@ __device__ __forceinline__ void wide_body(const float* __restrict__ ws, float* _
   *reinterpret_cast<f32x4*>(dw + idx) = s;
 }
 
+// The stem's slabs (one per stem wgrad block, [co][K = (kd*KH + kh)*8 + j] on the W-unfolded
+// input, dW[co][kd*KH + kh][j < unf_kw]): conv.hip's two-level sum (slab_group_sum_kernel's
+// groups of 16 slabs, then the group sums in order; wgrad_reduce_kernel's scatter) in one
+// pass -- 4 thread groups of 64 consecutive elements each take every 4th slab group, keep
+// each group's sum, and lane group 0 adds the group sums in order: bit-identical
+constexpr int STEM_G = 16;
+__device__ __forceinline__ void stem_body(const float* __restrict__ ws, float* __restrict__ dw,
+                                          int splits, int Nd, int K, int taps, int unf_kw, int bx,
+                                          float* sm) {
+  const int64_t total = (int64_t)Nd * K;
+  const int e = threadIdx.x & 63, g4 = threadIdx.x >> 6;
+  const int64_t idx = (int64_t)bx * 64 + e;
+  const int ng = (splits + STEM_G - 1) / STEM_G;      // <= 32 (host-checked)
+  if (idx < total) {
+    for (int gi = g4; gi < ng; gi += 4) {
+      float s = 0.f;
+      const int s1 = min(splits, (gi + 1) * STEM_G);
+#pragma unroll 16
+      for (int sp = gi * STEM_G; sp < s1; ++sp) s += ws[sp * total + idx];
+      sm[gi * 64 + e] = s;
+    }
+  }
+  __syncthreads();
+  if (g4 != 0 || idx >= total) return;
+  float s = 0.f;
+  for (int gi = 0; gi < ng; ++gi) s += sm[gi * 64 + e];
+  const int co = (int)(idx / K), k = (int)(idx % K);
+  const int j = k & 7, tkh = k >> 3;
+  if (j < unf_kw) dw[((int64_t)co * taps + tkh) * unf_kw + j] = s;
+}
+
 // block `lin` of job j's own grid (x fastest)
 __device__ __forceinline__ void run(const Job& j, int lin, float* sm) {
   const int bx = lin % j.gx, r = lin / j.gx, by = r % j.gy, bz = r / j.gy;
   if (j.kind == KIND_WIDE)
     wide_body(j.ws, j.dw, j.splits, (int64_t)j.nd * j.k, bx, sm);
+  else if (j.kind == KIND_STEM)
+    stem_body(j.ws, j.dw, j.splits, j.nd, j.k, j.taps, j.tper, bx, sm);
   else if (j.kind == KIND_TZ)
     tz_body(j.ws, j.dw, j.splits, j.nd, j.k, j.cs, j.taps, j.tper, bx, by, bz, sm);
   else

@@ -509,7 +509,15 @@ def _wgrad(ctx, d, dt, src, gy, weight, wparam=None, rside=None):
     # a dW that autograd will not adopt as-is (an existing .grad it is added into, or the
     # channel-padded copy cut below) is read on the main stream: no split then
     raw = getattr(ctx, "raw", None)
-    if raw is not None:
+    if raw is not None and _WGRAD_DEFER["on"] and not ctx.has_bias and not padded and \
+            (wparam is None or wparam.grad is None):
+        job = L.WgradJob()
+        L.call("mmad_conv3d_wgrad_raw_deferred", d, raw, L.ptr(src), dt, L.ptr(gy), L.ptr(dw),
+               L.ptr(ws), C.byref(job), L.stream())
+        if job.kind:
+            _WGRAD_DEFER["jobs"].append(job)
+            _WGRAD_DEFER["keep"].append(ws)
+    elif raw is not None:
         # the raw stem input (see _Conv3dFn.forward); slab reduction on rside when given
         split = rside is not None and (wparam is None or wparam.grad is None)
         L.call("mmad_conv3d_wgrad_raw", d, raw, L.ptr(src), dt, L.ptr(gy), L.ptr(dw),

@@ -119,3 +119,28 @@ def test_stride2_3cube_wgrad_vs_float64(xs, co):
     err = (got.double() - ref).abs()
     assert (err <= 1e-3 * ref.abs() + 1e-4 * mag).all(), f"max err {err.max().item():.3e}"
 
+
+def test_deferred_stem_reduce_bit_identical():
+    """the MedicalNet stem's weight gradient straight from the raw f64 volume (7^3 / 2, the
+    bench's 128^3 at batch 2): its two-level slab sum deferred into the batched launch is
+    bit-identical to the immediate one"""
+    from multimodal_alzheimer_amd import layers as Lyr
+    torch.manual_seed(5)
+    conv = Lyr.Conv3d(1, 64, 7, stride=2, padding=3, bias=False).to(DEV)
+    conv.compute_dtype = BF
+    g = torch.Generator(device=DEV).manual_seed(6)
+    vol = torch.rand((2, 1, 128, 128, 128), generator=g, device=DEV, dtype=torch.float64)
+    grads = []
+    for defer in (False, True):
+        conv.weight.grad = None
+        y = conv(vol)
+        gy = (torch.rand(y.shape, generator=torch.Generator(device=DEV).manual_seed(7),
+                         device=DEV) * 2 - 1).to(BF).contiguous(memory_format=CL)
+        with V.deferred_wgrad_reduce(defer):
+            y.backward(gy)
+            queued = len(V._WGRAD_DEFER["jobs"])
+        torch.cuda.synchronize()
+        assert queued == (1 if defer else 0)
+        grads.append(conv.weight.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+
