@@ -32,8 +32,6 @@
 //  * XCD-aware tile order: each XCD walks a contiguous range of (m, n) tiles, n fastest;
 //  * epilogue: bias, BN partial sums (sum, sum of squares per channel) from the fp32
 //    accumulators, bf16 tile transposed through LDS into 16-byte channel-vector stores.
-#include <atomic>
-
 #include "common.h"
 #include "reduce.h"
 #include "patchconv.h"
@@ -55,13 +53,6 @@ struct Geom {
   // shaped like the output (added after bias), ReLU flag
   const void* res;
   int relu;
-  // residue-class row order (round 5; FWD, stride 1, 'same' 3^3 dilation lat >= 2 on grids
-  // that are lat x (lz, ly, lx)): row m = position q of the sub-lattice (qz, qy, qx) major,
-  // then sample and residue class (rz, ry, rx) -- every tile's rows share q, so the taps whose
-  // shift leaves the sub-lattice are padding for the whole tile and are skipped (no DMA, no
-  // MFMA); with fewer subs than tile rows a tile holds consecutive positions and skips the
-  // taps none of them reaches; 0 = the plain voxel order
-  int lat, lz, ly, lx;
 };
 
 enum { FWD = 0, DGRAD = 1 };
@@ -80,57 +71,6 @@ __device__ __forceinline__ bool src_voxel(const Geom& g, int bz, int by, int bx,
   x = bx + ((to >> 16) & 255) - 128;
   return (unsigned)z < (unsigned)g.Ds && (unsigned)y < (unsigned)g.Hs &&
          (unsigned)x < (unsigned)g.Ws;
-}
-
-// Sub-lattice position of rank k, heavy first: positions grouped by how many of the
-// sub-lattice's faces they touch (none, then one, two, three -- 27, 18, 12, 8 taps for a
-// 3^3 kernel), each group enumerated face pattern by face pattern (z, y, x bits), interior
-// coordinates raster order.  Tiles are dispatched in rank order, so the first wave of blocks
-// holds the 27-tap positions and the light ones fill the tail (in raster order two heavy
-// tiles could share a CU while others idle: the tap skipping then bought nothing).
-__device__ __forceinline__ void lat_pos(const Geom& g, int k, int& qz, int& qy, int& qx) {
-  const int L[3] = {g.lx, g.ly, g.lz};                      // x, y, z
-  int v[3] = {0, 0, 0};
-  constexpr int masks[8] = {0, 1, 2, 4, 3, 5, 6, 7};        // faces touched: 0, 1, 1, 1, 2, ...
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-    const int mk = masks[mi];
-    int cnt = 1;
-#pragma unroll
-    for (int dd = 0; dd < 3; ++dd)
-      cnt *= (mk >> dd) & 1 ? min(L[dd], 2) : max(L[dd] - 2, 0);
-    if (k < cnt) {
-#pragma unroll
-      for (int dd = 0; dd < 3; ++dd) {
-        if ((mk >> dd) & 1) {
-          const int nb = min(L[dd], 2);
-          v[dd] = (k % nb) ? L[dd] - 1 : 0;
-          k /= nb;
-        } else {
-          const int ni = L[dd] - 2;
-          v[dd] = 1 + k % ni;
-          k /= ni;
-        }
-      }
-      break;
-    }
-    k -= cnt;
-  }
-  qx = v[0]; qy = v[1]; qz = v[2];
-}
-
-// voxel of row m in the residue-class order (Geom::lat)
-__device__ __forceinline__ void lat_voxel(const Geom& g, int m, int& n, int& z, int& y, int& x) {
-  const int d = g.lat, d3 = d * d * d;
-  const int S = g.nb * d3;
-  const int q = m / S, s = m - q * S;
-  n = s / d3;
-  const int r = s - n * d3;
-  int qx, qy, qz;
-  lat_pos(g, q, qz, qy, qx);
-  z = r / (d * d) + d * qz;
-  y = (r / d) % d + d * qy;
-  x = r % d + d * qx;
 }
 
 // forward tap table: offsets kd*d (base = out*s - p)
@@ -196,35 +136,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
   const int m0 = mt * BM, n0 = nt * BN;
 
   int ntap = g.taps, Kc = g.K;
-  if (MODE == FWD && g.lat) {
-    // the taps that land inside the volume for this tile's sub-lattice position(s) -- the
-    // same for all rows of one position; a tile of several positions (fewer subs than
-    // rows) takes their union and its rows mask the rest as padding -- compacted; the
-    // weights are addressed through tapidx as in DGRAD
-    if (tid == 0) {
-      const int S = g.nb * g.lat * g.lat * g.lat;
-      const int m1 = min(Mc, m0 + BM);
-      int n = 0;
-      for (int t = 0; t < g.taps; ++t) {
-        const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
-        const int to = pack_off(kd * g.dd, kh * g.dh, kw * g.dw);
-        bool any = false;
-        for (int mq = m0; mq < m1 && !any; mq += S) {
-          int nb0, z0, y0, x0, z, y, x;
-          lat_voxel(g, mq, nb0, z0, y0, x0);
-          any = src_voxel(g, z0 - g.pd, y0 - g.ph, x0 - g.pw, to, z, y, x);
-        }
-        if (!any) continue;
-        tapoff[n] = to;
-        tapidx[n] = t;
-        ++n;
-      }
-      tapidx[MAXTAPS - 1] = n;
-    }
-    __syncthreads();
-    ntap = tapidx[MAXTAPS - 1];
-    Kc = ntap * g.Cs;
-  } else if (MODE == FWD) {
+  if (MODE == FWD) {
     fill_taps_fwd(g, tapoff);
   } else {
     // (count kept in the unused last tap-index slot: a second __shared__ object beside
@@ -259,12 +171,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
     const int m = m0 + (wave * AI + i) * RPI + lrow;
     rok[i] = m < Mc;
     const int mm = rok[i] ? m : 0;
-    int xw = mm % Wc;
+    const int xw = mm % Wc;
     int t1 = mm / Wc;
-    int yh = t1 % Hc;
+    const int yh = t1 % Hc;
     t1 /= Hc;
-    int zd = t1 % Dc, nbi = t1 / Dc;
-    if (MODE == FWD && g.lat) lat_voxel(g, mm, nbi, zd, yh, xw);
+    const int zd = t1 % Dc, nbi = t1 / Dc;
     if (MODE == FWD) {
       rz[i] = zd * g.sd - g.pd; ry[i] = yh * g.sh - g.ph; rx[i] = xw * g.sw - g.pw;
     } else {
@@ -328,7 +239,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
         glds16_asm(p, lds_addr_of(sbase + (wave * AI + i) * 1024));
       }
     }
-    const int woff = MODE == FWD && !g.lat ? k : (kok ? (tapidx[ti] << g.cs_shift) + ci : 0);
+    const int woff = MODE == FWD ? k : (kok ? (tapidx[ti] << g.cs_shift) + ci : 0);
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int co = n0 + (wave * BI + i) * RPI + lrow;
@@ -427,11 +338,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
 
   // dst voxel of a tile row
   auto dst_row = [&](int m) -> int64_t {
-    if (MODE == FWD && g.lat) {
-      int n, z, y, x;
-      lat_voxel(g, m, n, z, y, x);
-      return (((int64_t)n * g.Dd + z) * g.Hd + y) * g.Wd + x;
-    }
     if (MODE == FWD) return m;
     const int xw = m % Wc;
     int t1 = m / Wc;
@@ -557,14 +463,8 @@ __device__ __forceinline__ int wswz(int r) {
 // is a whole number of output rows, WBK % Wd == 0) x never changes, so the x test is made
 // once and only y/z carry.  (Index math was ~1/4 of the kernel's time: a build with the B
 // addressing stubbed out ran 12-30 % faster.)
-// LATW (round 5; g.lat set, bf16): the rows m are in igemm_kernel's residue-class order
-// (Geom::lat), the block's k tile lies inside one tap, and a stage's 32 rows share one
-// sub-lattice position -- so the stages where this tap leaves the sub-lattice (pure padding)
-// are dropped from the block's stage list (built once, wave 0, in LDS after the ring): no
-// DMA, no MFMA.  Row voxels are recomputed per stage from (position, sub) with shifts
-// (d and the sub count are powers of two).
 template <typename T, int BMW, int WBK, int NST, int WBNT = WBN, int WGM = 2, int WGN = 2,
-          bool XFIX = false, bool LATW = false>
+          bool XFIX = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* __restrict__ src,
                                                        const T* __restrict__ dy,
                                                        float* __restrict__ ws, int m_per_split,
@@ -639,15 +539,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
   const int dcz = -g.Dd * g.sd * HW + DHW;
   const int bshift = g.cs_shift + (sizeof(T) == 2 ? 1 : 2);
   int bci2[BIPW], bx[BIPW], by[BIPW], bz[BIPW], box[BIPW], boy[BIPW], boz[BIPW];
-  int srow[BIPW], tdel[BIPW], browl[BIPW];
-  bool bkok[BIPW];
+  int srow[BIPW], tdel[BIPW];
 #pragma unroll
   for (int i = 0; i < BIPW; ++i) {
     const int brow = (wave * BIPW + i) * BRPI + lane / BLPR;
     const int k = k0 + ((lane % BLPR) ^ wswz<T, BROWB>(brow)) * EPC;
     const bool kok = k < g.K;
-    browl[i] = brow;
-    bkok[i] = kok;
     bci2[i] = (k & (g.Cs - 1)) * (int)sizeof(T);
     const int to = tapoff[kok ? (k >> g.cs_shift) : 0];
     box[i] = ((to >> 16) & 255) - 128 - g.pw;
@@ -695,38 +592,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
       d += cy ? dcy : 0;
       d += cz ? dcz : 0;
       srow[i] += d;
-    }
-  };
-
-  // LATW: (position, sub) -> voxel.  S = nb * d^3 subs per position, d = 2^ld
-  const int latd = g.lat, ld = 31 - __builtin_clz(latd > 0 ? latd : 1);
-  const int lsub = g.nb * latd * latd * latd;
-  auto sub_vox = [&](int sv) -> int {
-    const int n = sv >> (3 * ld), r = sv & ((1 << (3 * ld)) - 1);
-    return ((n * g.Dd + (r >> (2 * ld))) * g.Hd + ((r >> ld) & (latd - 1))) * g.Wd +
-           (r & (latd - 1));
-  };
-  int acol[AIPW];
-#pragma unroll
-  for (int i = 0; i < AIPW; ++i) acol[i] = co0 + ((lane % ALPR) ^ wswz<T, AROWB>(arow[i])) * EPC;
-  auto issue_lat = [&](int stage, int ms) {
-    char* sbase = ring + stage * STAGE;
-    const int q = ms / lsub, sb = ms - q * lsub;
-    const int qx = q % g.lx, qy = (q / g.lx) % g.ly, qz = q / (g.lx * g.ly);
-    const int pos = ((latd * qz) * g.Hd + latd * qy) * g.Wd + latd * qx;
-#pragma unroll
-    for (int i = 0; i < AIPW; ++i) {
-      const bool ok = acok[i] && ms + arow[i] < mend;
-      const int v = pos + sub_vox(sb + arow[i]);
-      const uint32_t off = (uint32_t)(v * g.Nd + acol[i]) * (uint32_t)sizeof(T);
-      buf_lds16_asm(ok ? off : OOB, rsy, lds_addr_of(sbase + (wave * AIPW + i) * 1024));
-    }
-#pragma unroll
-    for (int i = 0; i < BIPW; ++i) {
-      const bool ok = bkok[i] && ms + browl[i] < mend;
-      const int v = pos + sub_vox(sb + browl[i]) + tdel[i];
-      const uint32_t off = ((uint32_t)v << bshift) + bci2[i];
-      buf_lds16_asm(ok ? off : OOB, rsx, lds_addr_of(sbase + A_BYTES + (wave * BIPW + i) * 1024));
     }
   };
 
@@ -830,42 +695,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
   // NST-deep ring, NST-1 stages of DMA in flight (asm DMA: hipcc adds no drains).  At the
   // top of step ks: wait until only the younger stages' DMA is outstanding, barrier (all
   // waves' DMA for ks landed; all waves done reading ks-1), refill buffer (ks-1) % NST.
-  int nk = (mend - mbeg + WBK - 1) / WBK;
+  const int nk = (mend - mbeg + WBK - 1) / WBK;
   constexpr int LPS = AIPW + BIPW;          // DMA instructions per stage per wave
   constexpr int PD = NST - 1;
-  uint16_t* vlist = reinterpret_cast<uint16_t*>(ring + NST * STAGE);
-  if constexpr (LATW) {
-    // this block's tap (its k tile lies in one) and the stages whose position it reaches
-    const int t = k0 >> g.cs_shift;
-    const int kz = t / (g.KW * g.KH) - 1, ky = (t / g.KW) % g.KH - 1, kx = t % g.KW - 1;
-    if (wave == 0) {
-      int cnt = 0;
-      for (int base = 0; base < nk; base += 64) {
-        const int j = base + lane;
-        bool v = false;
-        if (j < nk) {
-          const int q = (mbeg + j * WBK) / lsub;
-          const int qx = q % g.lx + kx, qy = (q / g.lx) % g.ly + ky, qz = q / (g.lx * g.ly) + kz;
-          v = (unsigned)qx < (unsigned)g.lx && (unsigned)qy < (unsigned)g.ly &&
-              (unsigned)qz < (unsigned)g.lz;
-        }
-        const uint64_t msk = __ballot(v);
-        if (v) vlist[cnt + __popcll(msk & ((uint64_t(1) << lane) - 1))] = (uint16_t)j;
-        cnt += __popcll(msk);
-      }
-      if (lane == 0) tapoff[MAXTAPS] = cnt;
-    }
-    __syncthreads();
-    nk = tapoff[MAXTAPS];
-  }
-  auto issue_at = [&](int stage, int s) {
-    if constexpr (LATW) issue_lat(stage, mbeg + (int)vlist[s] * WBK);
-    else issue(stage, mbeg + s * WBK);
-  };
   if (nk > 0) {
 #pragma unroll
     for (int s = 0; s < PD; ++s)
-      if (s < nk) issue_at(s, s);
+      if (s < nk) issue(s, mbeg + s * WBK);
     for (int ks = 0; ks < nk; ++ks) {
       const int younger = min(PD - 1, nk - 1 - ks);
       if constexpr (PD >= 3) {
@@ -879,7 +715,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
         wait_vm_lgkm0<0>();
       }
       raw_barrier();
-      if (ks + PD < nk) issue_at((ks + PD) % NST, ks + PD);
+      if (ks + PD < nk) issue((ks + PD) % NST, mbeg + (ks + PD) * WBK);
       if constexpr (sizeof(T) == 2) {
         read_frags(ks % NST);
         mma_frags();
@@ -1490,29 +1326,6 @@ WSplit wgrad_split(const Geom& g, int dtype) {
   return s;
 }
 
-// the residue-class row order of igemm_kernel (Geom::lat) applies: a stride-1 'same' 3^3
-// conv of dilation d >= 2 whose grid is d x a whole sub-lattice per dimension (config 5's
-// 20^3 layer3 / layer4: 10^3 / 5^3 sub-lattices; the 4d^3 / 8-wide grids of config 2 go to
-// the residue-class kernels first).  MMAD_IGEMM_LAT=0 keeps the voxel order (A/B switch).
-std::atomic<int> g_igemm_lat{-1};
-int igemm_lat_mode() {
-  int v = g_igemm_lat.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("MMAD_IGEMM_LAT");
-    int expect = -1;
-    g_igemm_lat.compare_exchange_strong(expect, e ? atoi(e) : 1);
-    v = g_igemm_lat.load(std::memory_order_relaxed);
-  }
-  return v;
-}
-bool lat_geom(const Geom& g) {
-  const int d = g.dd;
-  return igemm_lat_mode() != 0 && d >= 2 && g.dh == d && g.dw == d && g.sd == 1 && g.sh == 1 && g.sw == 1 &&
-         g.KD == 3 && g.KH == 3 && g.KW == 3 && g.pd == d && g.ph == d && g.pw == d &&
-         g.Ds == g.Dd && g.Hs == g.Hd && g.Ws == g.Wd && g.Dd % d == 0 && g.Hd % d == 0 &&
-         g.Wd % d == 0;
-}
-
 template <typename F>
 bool set_lds(F* kern, size_t lds) {
   return lds <= 65536 || hipFuncSetAttribute((const void*)kern,
@@ -1530,16 +1343,9 @@ int launch_igemm_bm(const Geom& g, int64_t m_max, int classes, const void* src, 
   static const bool ok = set_lds(igemm_kernel<T, BN, MODE, BMT, WGM, WGN, NST, RBT>, lds);
   if (!ok) return MMAD_EUNSUPPORTED;
   const int nbm = (int)cdiv(m_max, BMT), nbn = (int)cdiv(g.Nd, BN);
-  Geom gl = g;
-  if (MODE == FWD && classes == 1 && m_max == g.M && sizeof(T) == 2 && lat_geom(g) &&
-      (((int64_t)g.nb * g.dd * g.dd * g.dd) % BMT == 0 ||
-       BMT % ((int64_t)g.nb * g.dd * g.dd * g.dd) == 0)) {
-    gl.lat = g.dd;
-    gl.lz = g.Dd / g.dd; gl.ly = g.Hd / g.dd; gl.lx = g.Wd / g.dd;
-  }
   hipLaunchKernelGGL((igemm_kernel<T, BN, MODE, BMT, WGM, WGN, NST, RBT>),
                      dim3((unsigned)(nbm * nbn), (unsigned)classes), dim3(64 * WGM * WGN), lds,
-                     st, gl, (const T*)src, (const T*)w, bias, (T*)dst, stats, nbm, nbn);
+                     st, g, (const T*)src, (const T*)w, bias, (T*)dst, stats, nbm, nbn);
   return launch_status();
 }
 
@@ -1654,40 +1460,19 @@ int wgrad_xcd() {
   return v;
 }
 
-template <typename T, int BMW, int WBK, int NST, int WBNT, int WGM, int WGN, bool XFIX,
-          bool LATW = false>
+template <typename T, int BMW, int WBK, int NST, int WBNT, int WGM, int WGN, bool XFIX>
 int launch_wgrad_x(const Geom& g, const WSplit& sp, const void* x, const void* dy, float* ws,
                    hipStream_t st) {
-  const size_t list = LATW ? (size_t)cdiv(cdiv(sp.m_per_split, WBK) * 2, 16) * 16 : 0;
-  const size_t lds = TAPB + NST * WBK * (BMW + WBNT) * sizeof(T) + list;
-  static const bool ok =
-      set_lds(wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX, LATW>,
-              TAPB + NST * WBK * (BMW + WBNT) * sizeof(T) + (LATW ? 32768 : 0));
-  if (!ok || lds > TAPB + NST * WBK * (BMW + WBNT) * sizeof(T) + (LATW ? 32768 : 0))
-    return MMAD_EUNSUPPORTED;
+  const size_t lds = TAPB + NST * WBK * (BMW + WBNT) * sizeof(T);
+  static const bool ok = set_lds(wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX>, lds);
+  if (!ok) return MMAD_EUNSUPPORTED;
   const uint32_t xb = (uint32_t)((int64_t)g.nb * g.Ds * g.Hs * g.Ws * g.Cs * sizeof(T));
   const uint32_t yb = (uint32_t)((int64_t)g.M * g.Nd * sizeof(T));
   dim3 grid((unsigned)cdiv(g.K, WBNT), (unsigned)cdiv(g.Nd, BMW), (unsigned)sp.splits);
-  Geom gl = g;
-  if (LATW) {
-    gl.lat = g.dd;
-    gl.lz = g.Dd / g.dd; gl.ly = g.Hd / g.dd; gl.lx = g.Wd / g.dd;
-  }
-  hipLaunchKernelGGL((wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX, LATW>), grid,
-                     dim3(64 * WGM * WGN), lds, st, gl, (const T*)x, (const T*)dy, ws,
+  hipLaunchKernelGGL((wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX>), grid,
+                     dim3(64 * WGM * WGN), lds, st, g, (const T*)x, (const T*)dy, ws,
                      sp.m_per_split, xb, yb, wgrad_xcd());
   return launch_status();
-}
-
-// the residue-class stage skipping of wgrad_kernel (LATW) applies: igemm's lattice geometry,
-// bf16, power-of-two dilation and sub count, whole-tap k tiles, 32-row stages inside one
-// position, stage indices in 16 bits, list within 32 KiB
-bool lat_wgrad_ok(const Geom& g, int wbnt, int64_t m_per_split) {
-  // (MMAD_IGEMM_LAT=2: the forward / input-gradient order only, A/B)
-  if (!lat_geom(g) || !is_pow2(g.dd) || igemm_lat_mode() == 2) return false;
-  const int64_t S = (int64_t)g.nb * g.dd * g.dd * g.dd;
-  return is_pow2((int)S) && S % 32 == 0 && g.Cs % wbnt == 0 &&
-         cdiv(m_per_split, 32) <= 16384;
 }
 
 template <typename T, int BMW, int WBK, int NST, int WBNT = WBN, int WGM = 2, int WGN = 2>
@@ -1697,9 +1482,6 @@ int launch_wgrad_k(const Geom& g, const WSplit& sp, const void* x, const void* d
   if ((int64_t)g.nb * g.Ds * g.Hs * g.Ws * g.Cs * (int64_t)sizeof(T) >= (int64_t(1) << 31) ||
       (int64_t)g.M * g.Nd * (int64_t)sizeof(T) >= (int64_t(1) << 31))
     return MMAD_EUNSUPPORTED;
-  if constexpr (sizeof(T) == 2 && WBK == 32)
-    if (lat_wgrad_ok(g, WBNT, sp.m_per_split))
-      return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, false, true>(g, sp, x, dy, ws, st);
   if (WBK % g.Wd == 0)
     return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, true>(g, sp, x, dy, ws, st);
   return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, false>(g, sp, x, dy, ws, st);
@@ -2313,11 +2095,3 @@ int zero_fill(void* p, int64_t bytes, hipStream_t st) {
                      (uint32_t*)p, words);
   return launch_status();
 }
-
-namespace mmad_igemm {
-int set_lat_mode(int v) {
-  const int prev = igemm_lat_mode();
-  if (v >= 0) g_igemm_lat.store(v, std::memory_order_relaxed);
-  return prev;
-}
-}  // namespace mmad_igemm

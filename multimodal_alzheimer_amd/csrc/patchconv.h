@@ -94,7 +94,3 @@ namespace mmad_pool {
 // MMAD_POOL_RUN run-time override (mmad_set_kernel_variant("pool_run", v)); returns the old mode
 int set_run_mode(int v);
 }  // namespace mmad_pool
-
-namespace mmad_igemm {
-int set_lat_mode(int v);          // MMAD_IGEMM_LAT (residue-class row order) at run time
-}  // namespace mmad_igemm
