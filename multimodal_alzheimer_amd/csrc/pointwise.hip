@@ -254,7 +254,9 @@ bool pw_on() {
 // blocks per CU.  The row-gather wgrad_kernel (conv.hip) ran these GEMMs at 20-30 GB/s per
 // CU of operand traffic (its 8-split run took 97 us per 4096-voxel block).
 constexpr int WG_KS = 32;                 // voxels per stage (one MFMA k step)
-constexpr int WG_NS = 4;                  // ring slots
+// ring slots: every stage but one in flight (WGC<...>::NS: 8, or 7 for the 3^3 form's
+// 20 KiB stages), one block per CU (round 5: 4 slots at two blocks per CU left the 16-stage
+// blocks latency-bound at ~1.2 us per stage, with twice the slabs)
 constexpr int WG_NTHR = 256;
 
 __device__ __forceinline__ int pw_tsw256(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
@@ -268,12 +270,13 @@ __device__ __forceinline__ int pw_tsw128(int r) { return 2 * (((r >> 1) & 1) | (
 // row-gather wgrad_kernel ran it with 69 splits (61 MB of slabs) at 0.13 of peak.
 template <int CIT, int NTAP = 1>
 struct WGC {
+  static constexpr int NS = NTAP == 3 ? 7 : 8;
   static constexpr int YROW = 256;                    // 128 co x 2 B
   static constexpr int XROW = CIT * 2;
   static constexpr int YIMG = WG_KS * YROW;           // 8 KiB
   static constexpr int XIMG = WG_KS * XROW;           // 8 / 4 KiB per tap
   static constexpr int SLOT = YIMG + NTAP * XIMG;
-  static constexpr int LDS = WG_NS * SLOT;            // 64 / 48 / 80 KiB
+  static constexpr int LDS = NS * SLOT;               // 128 / 96 / 140 KiB
   static constexpr int NQ = SLOT / 1024;              // DMA instructions per stage
   static constexpr int WI = NQ / 4;                   // per wave
   static_assert(WI * 4 == NQ, "stage DMA split over 4 waves");
@@ -283,7 +286,7 @@ struct WGC {
 
 // MODE 0: stride 1, X row = m; 1: stride 2 1^3, X row = s2_src(m); 2: stride 2 3^3 (NTAP 3)
 template <int CIT, int MODE, int NTAP = 1>
-__global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
+__global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, float* __restrict__ out, int Ci,
     int Co, int kper, int ntiles, PwS2 s2, uint32_t xbytes, uint32_t ybytes) {
   using C = WGC<CIT, NTAP>;
@@ -351,7 +354,7 @@ __global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
   const uint32_t ystep = (uint32_t)(WG_KS * Co) * 2u, xstep = (uint32_t)(WG_KS * Ci) * 2u;
   const uint32_t smem_l = lds_addr_of(smem);
   auto issue = [&](int s) {
-    const uint32_t slot = smem_l + (uint32_t)((s % WG_NS) * C::SLOT);
+    const uint32_t slot = smem_l + (uint32_t)((s % C::NS) * C::SLOT);
 #pragma unroll
     for (int h = 0; h < C::WI; ++h) {
       if (!isx[h]) {
@@ -412,16 +415,19 @@ __global__ __launch_bounds__(WG_NTHR, 2) void pw_wgrad_kernel(
 #pragma unroll
       for (int j = 0; j < C::TJ; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0);
-  if (nstage > 1) issue(1);
-  if (nstage > 2) issue(2);
+  constexpr int PD = C::NS - 1;                        // stages in flight
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+    if (p < nstage) issue(p);
   for (int s = 0; s < nstage; ++s) {
-    if (s + 2 < nstage) wait_vm_lgkm0<2 * C::WI>();   // stage s landed, s+1 and s+2 in flight
-    else if (s + 1 < nstage) wait_vm_lgkm0<C::WI>();
-    else wait_vm_lgkm0<0>();
+    // stage s landed; the younger stages already issued stay in flight
+    const int younger = min(PD - 1, nstage - 1 - s);
+    [&]<int... Y>(std::integer_sequence<int, Y...>) {
+      ((younger == Y ? wait_vm_lgkm0<Y * C::WI>() : void()), ...);
+    }(std::make_integer_sequence<int, PD>{});
     raw_barrier();                                     // every wave's part of stage s; and
-    if (s + 3 < nstage) issue(s + 3);                  // all are past stage s - 1's slot
-    int so = (s % WG_NS) * C::SLOT;
+    if (s + PD < nstage) issue(s + PD);                // all are past stage s - 1's slot
+    int so = (s % C::NS) * C::SLOT;
     asm volatile("" : "+s"(so));
     const char* slot = smem + so;
     bf16x8 a[4];
@@ -586,13 +592,12 @@ bool wgrad_ok(const mmad_conv_desc* d, int dtype) {
          mi * d->ci * 2 < (int64_t(1) << 31);
 }
 
-// voxels per split: the split count that gives ~512 blocks (two per CU) -- ~256 for the 3^3
-// form, whose slabs hold 27 taps -- K ranges of at least 4 stages, a divisor of the voxel
-// count
+// voxels per split: the split count that gives ~256 blocks (one per CU), K ranges of at
+// least 4 stages, a divisor of the voxel count
 int64_t wgrad_kper(const mmad_conv_desc* d) {
   const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
   const int64_t tiles = wg_tiles(d);
-  const int64_t want = wg3_geom(d) ? 256 : 512;
+  const int64_t want = 256;
   int64_t kper = m;
   while (kper % 2 == 0 && (kper / 2) % WG_KS == 0 && kper / 2 >= 4 * WG_KS &&
          tiles * (m / kper) < want)
