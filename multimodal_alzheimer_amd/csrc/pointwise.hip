@@ -288,7 +288,7 @@ struct WGC {
 template <int CIT, int MODE, int NTAP = 1>
 __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, float* __restrict__ out, int Ci,
-    int Co, int kper, int ntiles, PwS2 s2, uint32_t xbytes, uint32_t ybytes) {
+    int Co, int kper, int ntiles, PwS2 s2, uint32_t xbytes, uint32_t ybytes, int mrows) {
   using C = WGC<CIT, NTAP>;
   static_assert(MODE != 2 || NTAP == 3, "the 3^3 form takes the three kx taps");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
   const int kzy = MODE == 2 ? tile / (nci * nco) : 0;          // (kz, ky) of the 3^3 form
   const int kz = kzy / 3, ky = kzy % 3;
   const int64_t m0 = (int64_t)split * kper;
-  const int nstage = kper / WG_KS;
+  const int nstage = (int)(min((int64_t)kper, (int64_t)mrows - m0) / WG_KS);   // last: ragged
 
   // DMA instruction q (= wave + 4 h) of a stage: q < 8 the dY image (rows 4q .. 4q + 3),
   // else X image (q - 8) / XQ (256-B rows: 4 per instruction; 128-B rows: 8).  Operands
@@ -592,21 +592,16 @@ bool wgrad_ok(const mmad_conv_desc* d, int dtype) {
          mi * d->ci * 2 < (int64_t(1) << 31);
 }
 
-// voxels per split: the split count that gives ~256 blocks (one per CU), K ranges of at
-// least 4 stages, a divisor of the voxel count
+// voxels per split: as many splits as give every CU one block (256 / tiles), each a whole
+// number of 32-voxel stages (the last split takes the remainder)
 int64_t wgrad_kper(const mmad_conv_desc* d) {
   const int64_t m = (int64_t)d->n * d->do_ * d->ho * d->wo;
-  const int64_t tiles = wg_tiles(d);
-  const int64_t want = 256;
-  int64_t kper = m;
-  while (kper % 2 == 0 && (kper / 2) % WG_KS == 0 && kper / 2 >= 4 * WG_KS &&
-         tiles * (m / kper) < want)
-    kper /= 2;
-  return kper;
+  const int64_t want = std::max<int64_t>(1, 256 / wg_tiles(d));
+  return std::max<int64_t>(WG_KS, cdiv(cdiv(m, want), WG_KS) * WG_KS);
 }
 
 int64_t wgrad_splits(const mmad_conv_desc* d) {
-  return (int64_t)d->n * d->do_ * d->ho * d->wo / wgrad_kper(d);
+  return cdiv((int64_t)d->n * d->do_ * d->ho * d->wo, wgrad_kper(d));
 }
 
 int wgrad(const mmad_conv_desc* d, const void* x, const void* dy, float* ws, void* stream) {
@@ -626,7 +621,7 @@ int wgrad(const mmad_conv_desc* d, const void* x, const void* dy, float* ws, voi
                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(WG_NTHR), lds, as_stream(stream),
                        (const u16*)x, (const u16*)dy, ws, d->ci, d->co, (int)kper, (int)ntiles,
-                       q, (uint32_t)(mi * d->ci * 2), (uint32_t)(m * d->co * 2));
+                       q, (uint32_t)(mi * d->ci * 2), (uint32_t)(m * d->co * 2), (int)m);
     return launch_status();
   };
   if (wg3_geom(d)) return go(pw_wgrad_kernel<64, 2, 3>, WGC<64, 3>::LDS);
