@@ -213,6 +213,65 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
     __syncthreads();
   }
 
+  // Tap culling (round 5, bf16 forward): a tap that lands in the padding for EVERY row of
+  // the tile (e.g. the z-shifted taps of a tile inside the first / last d planes of a dilated
+  // 'same' conv: config 5's 20^3 layer3 / layer4) is dropped from the tile's K loop -- no
+  // DMA, no MFMA.  Its MACs were exact zeros, so the outputs are bit-identical.  The union of
+  // the rows' masks decides; the tap tables are compacted in place and the weights addressed
+  // through tapidx (as DGRAD does), each row's mask compressed to the kept taps.
+  bool culled = false;
+  if constexpr (MODE == FWD && sizeof(T) == 2) {
+    if (use_mask && ntap > 1) {
+      uint64_t u = 0;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) u |= rmask[i];
+      uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        lo |= __shfl_xor(lo, o, 64);
+        hi |= __shfl_xor(hi, o, 64);
+      }
+      uint32_t* un = reinterpret_cast<uint32_t*>(tapidx + MAXTAPS - 2 * NW - 2);
+      if (lane == 0) {
+        un[2 * wave] = lo;
+        un[2 * wave + 1] = hi;
+      }
+      __syncthreads();
+      uint64_t full = 0;
+      for (int w = 0; w < NW; ++w) full |= (uint64_t)un[2 * w] | ((uint64_t)un[2 * w + 1] << 32);
+      const uint64_t all = ntap == 64 ? ~uint64_t(0) : (uint64_t(1) << ntap) - 1;
+      if (full != all) {
+        culled = true;
+        __syncthreads();                       // every wave has read the union words
+        if (tid == 0) {
+          int n = 0;
+          for (int t = 0; t < ntap; ++t) {
+            if (!((full >> t) & 1)) continue;
+            tapoff[n] = tapoff[t];
+            tapdelta[n] = tapdelta[t];
+            tapidx[n] = t;
+            ++n;
+          }
+          tapidx[MAXTAPS - 1] = n;
+        }
+#pragma unroll
+        for (int i = 0; i < AI; ++i) {
+          uint64_t c = 0;
+          int j = 0;
+          for (int t = 0; t < ntap; ++t) {
+            if (!((full >> t) & 1)) continue;
+            c |= ((rmask[i] >> t) & 1) << j;
+            ++j;
+          }
+          rmask[i] = c;
+        }
+        __syncthreads();
+        ntap = tapidx[MAXTAPS - 1];
+        Kc = ntap * g.Cs;
+      }
+    }
+  }
+
   auto issue = [&](int stage, int k0) {
     char* sbase = ring + stage * STAGE;
     const int k = k0 + lchunk * EPC;
@@ -239,7 +298,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
         glds16_asm(p, lds_addr_of(sbase + (wave * AI + i) * 1024));
       }
     }
-    const int woff = MODE == FWD ? k : (kok ? (tapidx[ti] << g.cs_shift) + ci : 0);
+    const int woff = MODE == FWD && !culled ? k : (kok ? (tapidx[ti] << g.cs_shift) + ci : 0);
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int co = n0 + (wave * BI + i) * RPI + lrow;

@@ -1,0 +1,47 @@
+"""Tap culling in the implicit GEMM's forward (csrc/conv.hip, round 5): a tile whose rows all
+see a tap in the zero padding (the first / last d planes of a dilated 'same' conv, config 5's
+20^3 layer3 / layer4 at 160^3 input: pet_resnet_cnn.py:12-138, anat_cnn.py:29-31) drops that
+tap from its K loop.  Only exact zero products go, so the forward output and the input
+gradient (run as a forward over reversed taps) stay within one bf16 rounding of a plain fp32
+PyTorch conv of the same bf16 operands -- the same bar as every other conv kernel."""
+import pytest
+import torch
+
+from multimodal_alzheimer_amd import volume_ops as V
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CL = torch.channels_last_3d
+BF = torch.bfloat16
+
+CASES = [
+    ("layer4_20cube", (2, 512, 20, 20, 20), 512, 4),
+    ("layer3_20cube", (2, 256, 20, 20, 20), 256, 2),
+    ("ragged_12x20x8", (2, 256, 12, 20, 8), 256, 4),
+    ("undilated_9cube", (1, 256, 9, 9, 9), 256, 1),
+]
+
+
+def _close(got, ref, name):
+    err = (got.float() - ref).abs()
+    bound = 2 ** -7 * ref.abs() + 1e-3 * ref.abs().max()
+    bad = int((err > bound).sum())
+    assert bad == 0, f"{name}: {bad} beyond bound, max|err| {err.max().item():.3e}"
+
+
+@pytest.mark.parametrize("name,xs,co,d", CASES, ids=[c[0] for c in CASES])
+def test_culled_conv_matches_fp32(name, xs, co, d):
+    g = torch.Generator(device=DEV).manual_seed(len(name) + 3)
+    x = (torch.rand(xs, generator=g, device=DEV) * 2 - 1).to(BF).contiguous(memory_format=CL)
+    w = (torch.rand((co, xs[1], 3, 3, 3), generator=g, device=DEV) * 2 - 1) * \
+        (3.0 / (xs[1] * 27)) ** 0.5
+    xg = x.clone().requires_grad_(True)
+    y = V.conv3d(xg, w, None, (1,) * 3, (d,) * 3, (d,) * 3, BF)
+    gy = (torch.rand(y.shape, generator=g, device=DEV) * 2 - 1).to(BF).contiguous(memory_format=CL)
+    y.backward(gy)
+    torch.cuda.synchronize()
+    xr = x.float().requires_grad_(True)
+    yr = torch.nn.functional.conv3d(xr, w.to(BF).float(), None, 1, d, d)
+    yr.backward(gy.float())
+    _close(y.detach(), yr.detach(), "forward")
+    _close(xg.grad, xr.grad, "input gradient")
