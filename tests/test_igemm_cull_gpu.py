@@ -3,7 +3,10 @@ see a tap in the zero padding (the first / last d planes of a dilated 'same' con
 20^3 layer3 / layer4 at 160^3 input: pet_resnet_cnn.py:12-138, anat_cnn.py:29-31) drops that
 tap from its K loop.  Only exact zero products go, so the forward output and the input
 gradient (run as a forward over reversed taps) stay within one bf16 rounding of a plain fp32
-PyTorch conv of the same bf16 operands -- the same bar as every other conv kernel."""
+PyTorch conv of the same bf16 operands -- the same bar as every other conv kernel.  The
+weight gradient culls the same way (wgrad_kernel's CULL: 32-voxel stages whose rows all see
+the block's tap in the z padding); it is checked against a float64 weight gradient of the
+same bf16 operands, within 1e-3 |ref| + 1e-4 sum |gY| |X|."""
 import pytest
 import torch
 
@@ -36,7 +39,8 @@ def test_culled_conv_matches_fp32(name, xs, co, d):
     w = (torch.rand((co, xs[1], 3, 3, 3), generator=g, device=DEV) * 2 - 1) * \
         (3.0 / (xs[1] * 27)) ** 0.5
     xg = x.clone().requires_grad_(True)
-    y = V.conv3d(xg, w, None, (1,) * 3, (d,) * 3, (d,) * 3, BF)
+    wg = w.clone().requires_grad_(True)
+    y = V.conv3d(xg, wg, None, (1,) * 3, (d,) * 3, (d,) * 3, BF)
     gy = (torch.rand(y.shape, generator=g, device=DEV) * 2 - 1).to(BF).contiguous(memory_format=CL)
     y.backward(gy)
     torch.cuda.synchronize()
@@ -45,3 +49,8 @@ def test_culled_conv_matches_fp32(name, xs, co, d):
     yr.backward(gy.float())
     _close(y.detach(), yr.detach(), "forward")
     _close(xg.grad, xr.grad, "input gradient")
+    xd, gd = x.double(), gy.double()
+    wr = torch.nn.grad.conv3d_weight(xd, w.shape, gd, 1, d, d)
+    mag = torch.nn.grad.conv3d_weight(xd.abs(), w.shape, gd.abs(), 1, d, d)
+    err = (wg.grad.double() - wr).abs()
+    assert (err <= 1e-3 * wr.abs() + 1e-4 * mag).all(), f"weight gradient: max err {err.max().item():.3e}"
