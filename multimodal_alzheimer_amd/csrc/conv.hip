@@ -213,6 +213,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
     __syncthreads();
   }
 
+#ifndef MMAD_IGEMM_CULL
+#define MMAD_IGEMM_CULL 1                  // (-DMMAD_IGEMM_CULL=0: variant build for A/B)
+#endif
   // Tap culling (round 5, bf16 forward): a tap that lands in the padding for EVERY row of
   // the tile (e.g. the z-shifted taps of a tile inside the first / last d planes of a dilated
   // 'same' conv: config 5's 20^3 layer3 / layer4) is dropped from the tile's K loop -- no
@@ -220,7 +223,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void igemm_kernel(Geom g, const T* 
   // the rows' masks decides; the tap tables are compacted in place and the weights addressed
   // through tapidx (as DGRAD does), each row's mask compressed to the kept taps.
   bool culled = false;
-  if constexpr (MODE == FWD && sizeof(T) == 2) {
+  if constexpr (MODE == FWD && sizeof(T) == 2 && MMAD_IGEMM_CULL) {
     if (use_mask && ntap > 1) {
       uint64_t u = 0;
 #pragma unroll
@@ -522,13 +525,8 @@ __device__ __forceinline__ int wswz(int r) {
 // is a whole number of output rows, WBK % Wd == 0) x never changes, so the x test is made
 // once and only y/z carry.  (Index math was ~1/4 of the kernel's time: a build with the B
 // addressing stubbed out ran 12-30 % faster.)
-// CULL (round 5; bf16, the k tile inside one tap): stages whose 32 rows all see this tap in
-// the z padding (their output planes lie outside the tap's valid z range, same sample) are
-// dropped from the block's stage list (wave 0 builds it with ballots, in LDS after the ring);
-// a jump over dropped stages re-derives the rows' offsets (seek).  Those stages were exact
-// zero products: dW is bit-identical.  Config 5's 20^3 dilated layer3 / layer4.
 template <typename T, int BMW, int WBK, int NST, int WBNT = WBN, int WGM = 2, int WGN = 2,
-          bool XFIX = false, bool CULL = false>
+          bool XFIX = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* __restrict__ src,
                                                        const T* __restrict__ dy,
                                                        float* __restrict__ ws, int m_per_split,
@@ -577,13 +575,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
 
   // A chunks (dY rows, fixed channel slice per lane): byte offset advances WBK rows a stage
   uint32_t aoff[AIPW];
-  int arow[AIPW], acol[AIPW];
+  int arow[AIPW];
   bool acok[AIPW];
 #pragma unroll
   for (int i = 0; i < AIPW; ++i) {
     arow[i] = (wave * AIPW + i) * ARPI + lane / ALPR;
     const int aco = co0 + ((lane % ALPR) ^ wswz<T, AROWB>(arow[i])) * EPC;
-    acol[i] = aco;
     acok[i] = aco < g.Nd;
     aoff[i] = (uint32_t)(((int64_t)(mbeg + arow[i]) * g.Nd + aco) * (int)sizeof(T));
   }
@@ -604,11 +601,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
   const int dcz = -g.Dd * g.sd * HW + DHW;
   const int bshift = g.cs_shift + (sizeof(T) == 2 ? 1 : 2);
   int bci2[BIPW], bx[BIPW], by[BIPW], bz[BIPW], box[BIPW], boy[BIPW], boz[BIPW];
-  int srow[BIPW], tdel[BIPW], browl[BIPW];
+  int srow[BIPW], tdel[BIPW];
 #pragma unroll
   for (int i = 0; i < BIPW; ++i) {
     const int brow = (wave * BIPW + i) * BRPI + lane / BLPR;
-    browl[i] = brow;
     const int k = k0 + ((lane % BLPR) ^ wswz<T, BROWB>(brow)) * EPC;
     const bool kok = k < g.K;
     bci2[i] = (k & (g.Cs - 1)) * (int)sizeof(T);
@@ -761,66 +757,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
   // NST-deep ring, NST-1 stages of DMA in flight (asm DMA: hipcc adds no drains).  At the
   // top of step ks: wait until only the younger stages' DMA is outstanding, barrier (all
   // waves' DMA for ks landed; all waves done reading ks-1), refill buffer (ks-1) % NST.
-  int nk = (mend - mbeg + WBK - 1) / WBK;
+  const int nk = (mend - mbeg + WBK - 1) / WBK;
   constexpr int LPS = AIPW + BIPW;          // DMA instructions per stage per wave
   constexpr int PD = NST - 1;
-  uint16_t* vlist = reinterpret_cast<uint16_t*>(ring + NST * STAGE);
-  if constexpr (CULL) {
-    // output planes z whose source plane z * sd + oz lies inside the volume, for this tap
-    const int t = k0 >> g.cs_shift;
-    const int oz = (t / (g.KW * g.KH)) * g.dd - g.pd;
-    const int zlo = oz >= 0 ? 0 : (-oz + g.sd - 1) / g.sd;
-    const int zhi = g.Ds - 1 - oz < 0 ? -1 : (g.Ds - 1 - oz) / g.sd;
-    if (wave == 0) {
-      int cnt = 0;
-      for (int base = 0; base < nk; base += 64) {
-        const int j = base + lane;
-        bool v = false;
-        if (j < nk) {
-          const int ma = mbeg + j * WBK, mb = min(mend, ma + WBK) - 1;
-          const int pa = ma / (g.Wd * g.Hd), pb = mb / (g.Wd * g.Hd);   // (n, z) planes
-          const int na = pa / g.Dd, nb2 = pb / g.Dd, za = pa % g.Dd, zb = pb % g.Dd;
-          v = na != nb2 || !(zb < zlo || za > zhi);
-        }
-        const uint64_t msk = __ballot(v);
-        if (v) vlist[cnt + __popcll(msk & ((uint64_t(1) << lane) - 1))] = (uint16_t)j;
-        cnt += __popcll(msk);
-      }
-      if (lane == 0) tapoff[MAXTAPS] = cnt;
-    }
-    __syncthreads();
-    nk = tapoff[MAXTAPS];
-  }
-  // (CULL) re-derive every row's offsets for a stage that does not follow the last issued
-  auto seek = [&](int mk) {
-#pragma unroll
-    for (int i = 0; i < AIPW; ++i)
-      aoff[i] = (uint32_t)(((int64_t)(mk + arow[i]) * g.Nd + acol[i]) * (int)sizeof(T));
-#pragma unroll
-    for (int i = 0; i < BIPW; ++i) {
-      int m = mk + browl[i];
-      bx[i] = m % g.Wd; m /= g.Wd;
-      by[i] = m % g.Hd; m /= g.Hd;
-      bz[i] = m % g.Dd;
-      const int bn = m / g.Dd;
-      srow[i] = bn * DHW + bz[i] * g.sd * HW + by[i] * g.sh * g.Ws + bx[i] * g.sw;
-    }
-  };
-  int jnext = 0;                                  // the stage the row state points at
-  auto issue_at = [&](int stage, int s) {
-    if constexpr (CULL) {
-      const int j = vlist[s];
-      if (j != jnext) seek(mbeg + j * WBK);
-      issue(stage, mbeg + j * WBK);
-      jnext = j + 1;
-    } else {
-      issue(stage, mbeg + s * WBK);
-    }
-  };
   if (nk > 0) {
 #pragma unroll
     for (int s = 0; s < PD; ++s)
-      if (s < nk) issue_at(s, s);
+      if (s < nk) issue(s, mbeg + s * WBK);
     for (int ks = 0; ks < nk; ++ks) {
       const int younger = min(PD - 1, nk - 1 - ks);
       if constexpr (PD >= 3) {
@@ -834,7 +777,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_kernel(Geom g, const T* 
         wait_vm_lgkm0<0>();
       }
       raw_barrier();
-      if (ks + PD < nk) issue_at((ks + PD) % NST, ks + PD);
+      if (ks + PD < nk) issue((ks + PD) % NST, mbeg + (ks + PD) * WBK);
       if constexpr (sizeof(T) == 2) {
         read_frags(ks % NST);
         mma_frags();
@@ -1579,19 +1522,16 @@ int wgrad_xcd() {
   return v;
 }
 
-template <typename T, int BMW, int WBK, int NST, int WBNT, int WGM, int WGN, bool XFIX,
-          bool CULL = false>
+template <typename T, int BMW, int WBK, int NST, int WBNT, int WGM, int WGN, bool XFIX>
 int launch_wgrad_x(const Geom& g, const WSplit& sp, const void* x, const void* dy, float* ws,
                    hipStream_t st) {
-  constexpr size_t base = TAPB + NST * WBK * (BMW + WBNT) * sizeof(T);
-  const size_t lds = base + (CULL ? (size_t)cdiv(cdiv(sp.m_per_split, WBK) * 2, 16) * 16 : 0);
-  static const bool ok =
-      set_lds(wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX, CULL>, base + (CULL ? 32768 : 0));
-  if (!ok || lds > base + (CULL ? 32768 : 0)) return MMAD_EUNSUPPORTED;
+  const size_t lds = TAPB + NST * WBK * (BMW + WBNT) * sizeof(T);
+  static const bool ok = set_lds(wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX>, lds);
+  if (!ok) return MMAD_EUNSUPPORTED;
   const uint32_t xb = (uint32_t)((int64_t)g.nb * g.Ds * g.Hs * g.Ws * g.Cs * sizeof(T));
   const uint32_t yb = (uint32_t)((int64_t)g.M * g.Nd * sizeof(T));
   dim3 grid((unsigned)cdiv(g.K, WBNT), (unsigned)cdiv(g.Nd, BMW), (unsigned)sp.splits);
-  hipLaunchKernelGGL((wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX, CULL>), grid,
+  hipLaunchKernelGGL((wgrad_kernel<T, BMW, WBK, NST, WBNT, WGM, WGN, XFIX>), grid,
                      dim3(64 * WGM * WGN), lds, st, g, (const T*)x, (const T*)dy, ws,
                      sp.m_per_split, xb, yb, wgrad_xcd());
   return launch_status();
@@ -1604,17 +1544,6 @@ int launch_wgrad_k(const Geom& g, const WSplit& sp, const void* x, const void* d
   if ((int64_t)g.nb * g.Ds * g.Hs * g.Ws * g.Cs * (int64_t)sizeof(T) >= (int64_t(1) << 31) ||
       (int64_t)g.M * g.Nd * (int64_t)sizeof(T) >= (int64_t(1) << 31))
     return MMAD_EUNSUPPORTED;
-  // stage culling: bf16, the k tile inside one tap, a z-padded tap set (pd > 0), 16-bit stage
-  // indices; MMAD_WGRAD_CULL=0 keeps every stage (A/B)
-  static const bool cull_on = [] { const char* e = getenv("MMAD_WGRAD_CULL"); return !e || atoi(e) != 0; }();
-  if constexpr (sizeof(T) == 2) {
-    if (cull_on && g.Cs % WBNT == 0 && g.pd > 0 && g.KD > 1 &&
-        cdiv(sp.m_per_split, WBK) <= 16384) {
-      if (WBK % g.Wd == 0)
-        return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, true, true>(g, sp, x, dy, ws, st);
-      return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, false, true>(g, sp, x, dy, ws, st);
-    }
-  }
   if (WBK % g.Wd == 0)
     return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, true>(g, sp, x, dy, ws, st);
   return launch_wgrad_x<T, BMW, WBK, NST, WBNT, WGM, WGN, false>(g, sp, x, dy, ws, st);

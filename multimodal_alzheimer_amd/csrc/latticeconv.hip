@@ -938,6 +938,7 @@ static int planes(const mmad_patch::Geo& q) {
 }
 
 bool ok(const mmad_patch::Geo& q) {
+  if (mmad_lattice5::ok(q)) return true;          // 5d^3 grids (lattice5.hip)
   if (lattice_mode() <= 0) return false;
   const int d = q.dd;
   if (q.KD != 3 || q.KH != 3 || q.KW != 3 || q.dh != d || q.dw != d || d < 2) return false;
@@ -957,6 +958,7 @@ bool ok(const mmad_patch::Geo& q) {
 }
 
 int64_t tiles(const mmad_patch::Geo& q) {
+  if (mmad_lattice5::ok(q)) return mmad_lattice5::tiles(q);
   if (exact(q) && mmad_lattice_zp::ok(q)) return mmad_lattice_zp::tiles(q);
   return (int64_t)q.nb * q.dd * q.dd * q.dd / NS * planes(q);
 }
@@ -1019,6 +1021,7 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
 
 int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias,
         void* dst, float* stats, void* stream) {
+  if (mmad_lattice5::ok(q)) return mmad_lattice5::fwd(q, src, wp, bias, dst, stats, stream);
   if (!mmad_lattice::ok(q)) return MMAD_EUNSUPPORTED;
   const bool rag = !exact(q);
   if (!rag && mmad_lattice_zp::ok(q))

@@ -653,6 +653,7 @@ extern "C" int mmad_set_kernel_variant(const char* name, int value) {
   }
   if (std::strcmp(name, "lattice") == 0) return mmad_lattice::set_mode(value);
   if (std::strcmp(name, "lattice8") == 0) return mmad_lattice8::set_mode(value);
+  if (std::strcmp(name, "lattice5") == 0) return mmad_lattice5::set_mode(value);
   if (std::strcmp(name, "pool_run") == 0) return mmad_pool::set_run_mode(value);
   if (std::strcmp(name, "patchz") == 0) return mmad_patchz::set_mode(value);
   return -1;

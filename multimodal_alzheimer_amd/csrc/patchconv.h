@@ -72,6 +72,16 @@ int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* 
         float* stats, void* stream);
 }  // namespace mmad_lattice_zp
 
+// Residue-class conv on 5d^3 grids (lattice5.hip: config 5's 20^3 layer4, 5^3 sub-lattices):
+// mmad_lattice::ok / tiles / fwd route to it first.
+namespace mmad_lattice5 {
+int set_mode(int v);              // MMAD_LATTICE5 at run time; returns the previous mode
+bool ok(const mmad_patch::Geo& g);
+int64_t tiles(const mmad_patch::Geo& g);
+int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,
+        float* stats, void* stream);
+}  // namespace mmad_lattice5
+
 // Residue-class conv for dilation-2 3^3 convs on a 16^3 grid (lattice8.hip, layer3).
 namespace mmad_lattice8 {
 int set_mode(int v);              // MMAD_LATTICE8 at run time; returns the previous mode

@@ -3,13 +3,16 @@ see a tap in the zero padding (the first / last d planes of a dilated 'same' con
 20^3 layer3 / layer4 at 160^3 input: pet_resnet_cnn.py:12-138, anat_cnn.py:29-31) drops that
 tap from its K loop.  Only exact zero products go, so the forward output and the input
 gradient (run as a forward over reversed taps) stay within one bf16 rounding of a plain fp32
-PyTorch conv of the same bf16 operands -- the same bar as every other conv kernel.  The
-weight gradient culls the same way (wgrad_kernel's CULL: 32-voxel stages whose rows all see
-the block's tap in the z padding); it is checked against a float64 weight gradient of the
-same bf16 operands, within 1e-3 |ref| + 1e-4 sum |gY| |X|."""
+PyTorch conv of the same bf16 operands -- the same bar as every other conv kernel.  (The
+residue-class kernel for 20^3 grids, lattice5.hip, is switched off here so that the implicit
+GEMM runs.)  The weight gradient of the same geometry (wgrad_kernel, no culling: a z-band
+stage culling was built in round 5 and measured 1.7 % slower on the config-5 step, so it was
+removed) is checked against a float64 weight gradient of the same bf16 operands, within
+1e-3 |ref| + 1e-4 sum |gY| |X|."""
 import pytest
 import torch
 
+from multimodal_alzheimer_amd import _lib
 from multimodal_alzheimer_amd import volume_ops as V
 
 pytestmark = pytest.mark.gpu
@@ -40,10 +43,16 @@ def test_culled_conv_matches_fp32(name, xs, co, d):
         (3.0 / (xs[1] * 27)) ** 0.5
     xg = x.clone().requires_grad_(True)
     wg = w.clone().requires_grad_(True)
-    y = V.conv3d(xg, wg, None, (1,) * 3, (d,) * 3, (d,) * 3, BF)
-    gy = (torch.rand(y.shape, generator=g, device=DEV) * 2 - 1).to(BF).contiguous(memory_format=CL)
-    y.backward(gy)
-    torch.cuda.synchronize()
+    lib = _lib.load()
+    prev = lib.mmad_set_kernel_variant(b"lattice5", 0)
+    try:
+        y = V.conv3d(xg, wg, None, (1,) * 3, (d,) * 3, (d,) * 3, BF)
+        gy = (torch.rand(y.shape, generator=g, device=DEV) * 2 - 1).to(BF) \
+            .contiguous(memory_format=CL)
+        y.backward(gy)
+        torch.cuda.synchronize()
+    finally:
+        lib.mmad_set_kernel_variant(b"lattice5", prev)
     xr = x.float().requires_grad_(True)
     yr = torch.nn.functional.conv3d(xr, w.to(BF).float(), None, 1, d, d)
     yr.backward(gy.float())

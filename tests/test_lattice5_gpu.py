@@ -1,0 +1,99 @@
+"""Residue-class conv on 5d^3 grids (csrc/lattice5.hip): config 5's layer4 -- dilation-4
+3^3 convs on the 20^3 grids a 160^3 input reaches (pet_resnet_cnn.py:12-138, anat_cnn.py:29-31
+via MedicalNet) -- forward, input gradient (the same kernel over reversed taps) and the
+eval-mode epilogue, against a plain fp32 PyTorch conv of the same bf16 operands: outputs and
+input gradients within one bf16 rounding of it (2^-7 |ref| + 1e-3 max |ref|, the bar of every
+conv kernel), BN partial-sum totals within fp32 rounding of the fp32 output's sums.  The route
+is checked through the partial-sum row count (one row per sample x sub group x plane)."""
+import pytest
+import torch
+
+from multimodal_alzheimer_amd import _lib
+from multimodal_alzheimer_amd import volume_ops as V
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CL = torch.channels_last_3d
+BF = torch.bfloat16
+
+
+def _variant(v):
+    return _lib.load().mmad_set_kernel_variant(b"lattice5", v)
+
+
+def _close(got, ref, name):
+    err = (got.float() - ref).abs()
+    bound = 2 ** -7 * ref.abs() + 1e-3 * ref.abs().max()
+    bad = int((err > bound).sum())
+    assert bad == 0, f"{name}: {bad} beyond bound, max|err| {err.max().item():.3e}"
+
+
+# (name, x shape, output channels, dilation): the bench's batch-8 layer4 convs, a batch-2
+# case below the block-count threshold (forced on), and d = 8 on a 40^3 grid (512 classes)
+CASES = [
+    ("l4c2_b8", (8, 512, 20, 20, 20), 512, 4),
+    ("l4c1_b8", (8, 256, 20, 20, 20), 512, 4),
+    ("l4c2_b2", (2, 512, 20, 20, 20), 512, 4),
+    ("d8_40cube", (1, 64, 40, 40, 40), 128, 8),
+]
+
+
+@pytest.mark.parametrize("name,xs,co,d", CASES, ids=[c[0] for c in CASES])
+def test_lattice5_matches_fp32(name, xs, co, d):
+    g = torch.Generator(device=DEV).manual_seed(len(name) * 7 + d)
+    x = (torch.rand(xs, generator=g, device=DEV) * 2 - 1).to(BF).contiguous(memory_format=CL)
+    w = (torch.rand((co, xs[1], 3, 3, 3), generator=g, device=DEV) * 2 - 1) * \
+        (3.0 / (xs[1] * 27)) ** 0.5
+    prev = _variant(2)
+    try:
+        xg = x.clone().requires_grad_(True)
+        y, stats = V.conv3d(xg, w.clone(), None, (1,) * 3, (d,) * 3, (d,) * 3, BF,
+                            want_stats=True)
+        gy = (torch.rand(y.shape, generator=g, device=DEV) * 2 - 1).to(BF) \
+            .contiguous(memory_format=CL)
+        y.backward(gy)
+        torch.cuda.synchronize()
+    finally:
+        _variant(prev)
+    assert stats.shape[0] == xs[0] * (d ** 3 // 16) * 5, "not routed to the lattice5 kernel"
+    xr = x.float().requires_grad_(True)
+    yr = torch.nn.functional.conv3d(xr, w.to(BF).float(), None, 1, d, d)
+    yr.backward(gy.float())
+    _close(y.detach(), yr.detach(), "forward")
+    _close(xg.grad, xr.grad, "input gradient")
+    tot = stats.sum(0)
+    yd = yr.detach().double()
+    mag = torch.stack((yd.abs().sum(dim=(0, 2, 3, 4)), (yd * yd).sum(dim=(0, 2, 3, 4))))
+    ref = torch.stack((yd.sum(dim=(0, 2, 3, 4)), (yd * yd).sum(dim=(0, 2, 3, 4))))
+    assert ((tot.double() - ref).abs() <= 1e-3 * mag + 1e-6).all(), "BN partial sums"
+
+
+def test_lattice5_eval_epilogue_residual_relu():
+    """conv_bn_act_eval's fused epilogue (folded BN, residual, ReLU) on the lattice5 kernel
+    against the row-gather implicit GEMM it replaces: within one bf16 rounding of the
+    output (the two sum the taps in different orders)."""
+    from multimodal_alzheimer_amd import layers as Lyr
+    torch.manual_seed(5)
+    conv = Lyr.Conv3d(512, 512, 3, padding=4, dilation=4, bias=False).to(DEV)
+    conv.compute_dtype = BF
+    bn = torch.nn.BatchNorm3d(512).to(DEV).eval()
+    with torch.no_grad():
+        bn.running_var.uniform_(0.5, 2.0)
+        bn.bias.uniform_(-0.3, 0.3)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    x = (torch.rand((8, 512, 20, 20, 20), generator=g, device=DEV) * 2 - 1).to(BF) \
+        .contiguous(memory_format=CL)
+    res = (torch.rand((8, 512, 20, 20, 20), generator=g, device=DEV) * 2 - 1).to(BF) \
+        .contiguous(memory_format=CL)
+    prev = _variant(0)
+    try:
+        with torch.no_grad():
+            ref = V.conv_bn_act_eval(x, conv, bn, relu=True, res=res)
+            _variant(2)
+            got = V.conv_bn_act_eval(x, conv, bn, relu=True, res=res)
+        torch.cuda.synchronize()
+    finally:
+        _variant(prev)
+    err = (got.float() - ref.float()).abs()
+    assert (err <= 2 ** -6 * ref.float().abs() + 2e-2).all(), err.max().item()
+    assert (got == 0).any() and (got > 0).any()
