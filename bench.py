@@ -256,7 +256,9 @@ def main():
         model = M.All_Modalities_Fusion(dict(hparams(args.precision), fl_gamma=2,
                                              resnet_depth_mri=34, resnet_depth_pet=18)).cuda()
     opt = model.configure_optimizers()
-    use_graph = not args.eager and (args.graph or args.workload in ("mri", "fusion"))
+    # config 5 is graphed at one rank (its multi-rank launch modes are not rehearsed)
+    use_graph = not args.eager and (args.graph or args.workload in ("mri", "fusion") or
+                                    (args.workload == "three" and not dp))
     mode = "inside" if args.graph else "after" if args.after else args.collectives
     if not use_graph:
         mode = "eager"

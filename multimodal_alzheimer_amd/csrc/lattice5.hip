@@ -26,6 +26,7 @@
 //  * edge planes (tz = 0, 4) carry 2/3 of the work of interior ones: one block runs tz = 0
 //    and then tz = 4, the others one interior plane each, the pair blocks dispatched first
 //    on every XCD (each XCD holds whole sub groups, so their input planes share one L2).
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <utility>
@@ -377,6 +378,341 @@ __global__ __launch_bounds__(NTHR) void lattice5_conv_kernel(
   }
 }
 
+// ---- weight gradient on the 5^3 sub-lattices ----------------------------------------------
+// dW[co][tap][ci] = sum over output voxels v of dY[v][co] X[v + tap][ci], v walked as (sub
+// group, plane tz, K step): a K step of 32 voxels is the 16 subs at TWO output positions
+// (pa, pb), so a tap's X rows for it are the 16 subs at each shifted position of one input
+// plane.  The pairs are chosen so that both positions see the same taps in the padding
+// wherever possible (interior with interior, edge with edge of the same side; the four
+// corners go with an edge neighbour and differ in one tap column or row): a tap whose shift
+// leaves the sub-lattice for both has neither reads nor MFMAs (compile time: wave, plane,
+// K step and tap are template constants), and one that leaves it for a single position reads
+// that half's rows from a 1 KiB zero block (a per-lane select between two constants).  25
+// positions make 12 pairs + (18, none) + an empty step: 7 stages of 2 K steps per plane.
+//  * block = 64 output channels x 32 input channels x all 27 taps over a split of the sub
+//    groups; 8 waves = 2 (16-channel ci halves) x 4 tap groups of 7 (6), 4 x 7 accumulator
+//    tiles per wave (as latticeconv.hip's lattice_wgrad_kernel);
+//  * X input planes (16 subs x 25 positions x 32 channels = 25 KiB) stream through a 4-slot
+//    ring, each loaded once per sub group: output plane o reads planes o - 1 .. o + 1 of its
+//    group, and plane o + 2 of the stream is issued when output plane o starts;
+//  * dY (2 K steps x 32 rows x 64 channels = 8 KiB per stage) through a 3-slot ring;
+//  * both operands are m-major images read with transposing ds_read_b64_tr_b16 fragment
+//    reads; fp32 partial slabs [split][co][tap * Cs + ci] as latticeconv.hip's (summed and
+//    transposed by conv.hip's slab reduction).
+constexpr int WXROW = 64;                 // X rows: 32 ci x 2 B
+constexpr int WYROW = 128;                // dY rows: 64 co x 2 B
+constexpr int WXSLOTS = 4;
+constexpr int WPLANE = PLB;               // one X plane: 25 KiB
+constexpr int KSP = 14;                   // K steps per plane (13 + an empty one)
+constexpr int WST = KSP / 2;              // stages per plane
+constexpr int WYST = 2 * 32 * WYROW;      // 8 KiB per stage
+constexpr int WYSLOTS = 3;
+constexpr int WZERO_OFF = WXSLOTS * WPLANE;
+constexpr int WY_OFF = WZERO_OFF + NS * WXROW;
+constexpr int WLDS = WY_OFF + WYSLOTS * WYST;
+static_assert(WLDS <= 160 * 1024, "LDS");
+
+// position of half h of K step j (NP: none)
+__host__ __device__ constexpr int kpos(int j, int h) {
+  constexpr int t[KSP][2] = {{6, 7},   {8, 11},  {12, 13}, {16, 17}, {1, 2},
+                             {21, 22}, {5, 10},  {9, 14},  {0, 3},   {24, 23},
+                             {4, 19},  {20, 15}, {18, NP}, {NP, NP}};
+  return t[j][h];
+}
+// the position whose dY rows half h of K step j loads: a real one everywhere (finite rows;
+// a half without a position meets zero X rows)
+__host__ __device__ constexpr int kpos_dma(int j, int h) {
+  return kpos(j, h) < NP ? kpos(j, h) : kpos(j, 0) < NP ? kpos(j, 0) : 18;
+}
+// position p shifted by tap t's (ky, kx): inside the 5 x 5 plane?
+__host__ __device__ constexpr bool yx_in(int p, int t) {
+  if (p >= NP) return false;
+  const int y = p / S + (t / 3) % 3 - 1, x = p % S + t % 3 - 1;
+  return y >= 0 && y < S && x >= 0 && x < S;
+}
+__host__ __device__ constexpr bool z_in(int tz, int t) {
+  const int z = tz + t / 9 - 1;
+  return z >= 0 && z < S;
+}
+
+// tap K (of tap group TG: taps 7 TG ..) at half h of K step j, output plane tz: inside?
+template <int TG>
+__host__ __device__ constexpr bool w_on(int k, int j, int tz, int h) {
+  const int t = TG * 7 + k;
+  return k < (TG == 3 ? 6 : 7) && z_in(tz, t) && yx_in(kpos(j, h), t);
+}
+template <int TG>
+__host__ __device__ constexpr bool w_any(int j, int tz) {
+  for (int k = 0; k < 7; ++k)
+    if (w_on<TG>(k, j, tz, 0) || w_on<TG>(k, j, tz, 1)) return true;
+  return false;
+}
+
+__device__ __forceinline__ int wsz64(int r) { return 2 * ((r >> 3) & 1); }
+__device__ __forceinline__ int wsz128(int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); }
+
+#ifndef L5W_SEQ
+#define L5W_SEQ 1
+#endif
+
+struct LW5 {
+  int Cs, Nd, d, E, G, K;
+  int groups_per_split;
+  uint32_t xbytes, ybytes;                // operand sizes (buffer-resource ranges)
+};
+
+__global__ __launch_bounds__(NTHR) void lattice5_wgrad_kernel(LW5 g, const u16* __restrict__ src,
+                                                              const u16* __restrict__ dy,
+                                                              float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware order: the co tiles of one (ci chunk, split) read the same X planes
+  const int nci = g.Cs / KC, nco = g.Nd / 64;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int cot = tile % nco;
+  const int t2 = tile / nco;
+  const int cit = t2 % nci, split = t2 / nci;
+  const int co0 = cot * 64, ci0 = cit * KC;
+  const int d = g.d, E = g.E;
+  const int g0 = split * g.groups_per_split;
+  const int nplane_out = g.groups_per_split * S;
+
+  for (int i = tid; i < NS * WXROW / 16; i += NTHR)
+    *reinterpret_cast<u32x4*>(smem + WZERO_OFF + i * 16) = u32x4{0u, 0u, 0u, 0u};
+
+  // voxel of (sub group gi, plane z, position ty, tx) for the group's first class; a sub's
+  // class digits never carry into the group's (16-aligned classes, d^2 >= 16), so sub s adds
+  // a constant
+  auto grp_vox = [&](int gi, int z, int ty, int tx) -> int64_t {
+    const int n = gi / g.G, q = (gi % g.G) * NS;
+    const int rz = q / (d * d), ry = (q / d) % d, rx = q % d;
+    return (((int64_t)n * E + rz + d * z) * E + ry + d * ty) * E + rx + d * tx;
+  };
+  auto sub_part = [&](int s) -> int {
+    return ((s / (d * d)) * E + (s / d) % d) * E + s % d;
+  };
+  // X plane: instruction k of wave w = position w + 8k (clamped, as the forward)
+  uint32_t xl[PI];
+#pragma unroll
+  for (int k = 0; k < PI; ++k) {
+    const int pos = min(wave + NW * k, NP - 1), s = lane >> 2;
+    const int row = pos * NS + s;
+    xl[k] = (uint32_t)((sub_part(s) + d * (pos / S) * E + d * (pos % S)) * g.Cs + ci0 +
+                       (((lane & 3) ^ wsz64(row)) * 8)) * 2u;
+  }
+  // both operands through buffer resources: 32-bit byte offsets (wgrad_ok bounds the
+  // tensors), a scalar plane part + a constant lane part, no 64-bit lane addresses
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)src, 0, (int)__builtin_amdgcn_readfirstlane(g.xbytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dy, 0, (int)__builtin_amdgcn_readfirstlane(g.ybytes), 0x00020000);
+  auto issue_x = [&](int e) {
+    const int gi = g0 + e / S, pz = e % S;
+    char* slot = smem + (e % WXSLOTS) * WPLANE;
+    const uint32_t zb = (uint32_t)(grp_vox(gi, pz, 0, 0) * g.Cs) * 2u;
+#pragma unroll
+    for (int k = 0; k < PI; ++k) {
+      const int pos = min(wave + NW * k, NP - 1);
+      buf_lds16_asm(zb + xl[k], rsx, lds_addr_of(slot + pos * 1024));
+    }
+  };
+  // dY of a stage: one instruction per wave, rows 8w .. 8w + 7 = K step q = w >> 2, half
+  // h = (w >> 1) & 1, subs (w & 1) * 8 ..
+  const int yrow = wave * 8 + (lane >> 3);
+  const int yq = wave >> 2, yh = (wave >> 1) & 1;
+  const uint32_t ylane = (uint32_t)(sub_part(yrow & 15) * g.Nd + co0 +
+                                    (((lane & 7) ^ wsz128(yrow)) * 8)) * 2u;
+  auto issue_y = [&](int o, auto mc, int sl) {
+    constexpr int M = decltype(mc)::value;
+    const int p = yq == 0 ? (yh == 0 ? kpos_dma(2 * M, 0) : kpos_dma(2 * M, 1))
+                          : (yh == 0 ? kpos_dma(2 * M + 1, 0) : kpos_dma(2 * M + 1, 1));
+    const uint32_t pb = (uint32_t)(grp_vox(g0 + o / S, o % S, p / S, p % S) * g.Nd) * 2u;
+    buf_lds16_asm(pb + ylane, rsy, lds_addr_of(smem + WY_OFF + sl * WYST + wave * 1024));
+  };
+
+  const int cf = wave & 1, tg = wave >> 1;          // ci half, tap group
+  const int t0 = tg * 7, nt = tg == 3 ? 6 : 7;
+  const int lk = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int rsel = 8 * lk + q4;                     // this lane's K rows r, r + 4 of a step
+  const bool hb = (rsel >> 4) & 1;                  // ... in the step's second half
+  auto tr_off = [&](int rowb, int r, int col, int sw) -> uint32_t {
+    return (uint32_t)(r * rowb + (((col >> 3) ^ sw) << 4) + (col & 7) * 2);
+  };
+  uint32_t ya_lo[4], ya_hi[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = i * 16 + 4 * p4;
+    ya_lo[i] = tr_off(WYROW, rsel, col, wsz128(rsel));
+    ya_hi[i] = tr_off(WYROW, rsel + 4, col, wsz128(rsel + 4));
+  }
+  const uint32_t xb_lo = tr_off(WXROW, rsel & 15, cf * 16 + 4 * p4, wsz64(rsel));
+  const uint32_t xb_hi = tr_off(WXROW, (rsel + 4) & 15, cf * 16 + 4 * p4, wsz64(rsel + 4));
+  auto tr8 = [](const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p);
+  };
+  f32x4 acc[4][7];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_x(0);
+  if (nplane_out > 1) issue_x(1);
+  issue_y(0, std::integral_constant<int, 0>{}, 0);
+  issue_y(0, std::integral_constant<int, 1>{}, 1);
+
+  struct WFr { bf16x8 a[4], b[7]; };
+  auto run = [&](auto tgc) {
+    constexpr int TG = decltype(tgc)::value;
+    uint32_t xp[3];                                 // X ring offsets of planes o - 1, o, o + 1
+    uint32_t hsel = 0;                              // this lane reads the step's second half
+    auto kread = [&](const char* yimg, auto qc, auto jc, auto tzc, WFr& f) {
+      constexpr int Q = decltype(qc)::value, J = decltype(jc)::value;
+      constexpr int TZ = decltype(tzc)::value;
+      if constexpr (w_any<TG>(J, TZ)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          f.a[i] = __builtin_shufflevector(tr8(yimg + Q * 32 * WYROW + ya_lo[i]),
+                                           tr8(yimg + Q * 32 * WYROW + ya_hi[i]), 0, 1, 2, 3, 4,
+                                           5, 6, 7);
+        auto one = [&](auto kc) {
+          constexpr int K = decltype(kc)::value;
+          constexpr bool va = w_on<TG>(K, J, TZ, 0), vb = w_on<TG>(K, J, TZ, 1);
+          if constexpr (va || vb) {
+            constexpr int t = TG * 7 + K;
+            constexpr int dys = ((t / 3) % 3 - 1) * S + t % 3 - 1;
+            constexpr int oa = (kpos(J, 0) + dys) * NS * WXROW;
+            constexpr int ob = (kpos(J, 1) + dys) * NS * WXROW;
+            const uint32_t pl = xp[t / 9];
+            uint32_t off;
+            if constexpr (va && vb) off = pl + oa + (hsel ? (uint32_t)(ob - oa) : 0u);
+            else if constexpr (va) off = hsel ? (uint32_t)WZERO_OFF : pl + oa;
+            else off = hsel ? pl + ob : (uint32_t)WZERO_OFF;
+            f.b[K] = __builtin_shufflevector(tr8(smem + off + xb_lo), tr8(smem + off + xb_hi), 0,
+                                             1, 2, 3, 4, 5, 6, 7);
+          }
+        };
+        one(std::integral_constant<int, 0>{});
+        one(std::integral_constant<int, 1>{});
+        one(std::integral_constant<int, 2>{});
+        one(std::integral_constant<int, 3>{});
+        one(std::integral_constant<int, 4>{});
+        one(std::integral_constant<int, 5>{});
+        one(std::integral_constant<int, 6>{});
+      }
+    };
+    auto kmma = [&](const WFr& f, auto jc, auto tzc) {
+      constexpr int J = decltype(jc)::value, TZ = decltype(tzc)::value;
+      auto one = [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        if constexpr (w_on<TG>(K, J, TZ, 0) || w_on<TG>(K, J, TZ, 1)) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i][K] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[K], acc[i][K], 0, 0,
+                                                                0);
+        }
+      };
+      one(std::integral_constant<int, 0>{});
+      one(std::integral_constant<int, 1>{});
+      one(std::integral_constant<int, 2>{});
+      one(std::integral_constant<int, 3>{});
+      one(std::integral_constant<int, 4>{});
+      one(std::integral_constant<int, 5>{});
+      one(std::integral_constant<int, 6>{});
+    };
+
+    // output plane o of the block's stream, TZ = its z position in the sub group
+    auto plane = [&](int o, auto tzc) {
+      constexpr int TZ = decltype(tzc)::value;
+      const bool xnow = o + 2 < nplane_out;         // X plane o + 2 issued at stage 0
+      const bool lastp = o + 1 == nplane_out;
+      uint32_t xq[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) xq[k] = (uint32_t)(((o + k + 3) & 3) * WPLANE);
+      auto stage = [&](auto mc) {
+        constexpr int M = decltype(mc)::value;
+        const int s = o * WST + M;
+        const int sl = s % WYSLOTS;
+        // dY of this stage landed (issued two stages ago); younger: the next stage's dY and,
+        // at stages 1 and 2, the X plane issued at stage 0 after stage 2's dY
+        if ((M == 1 || M == 2) && xnow) wait_vm_lgkm0<PI + 1>();
+        else if (lastp && M == WST - 1) wait_vm_lgkm0<0>();
+        else wait_vm_lgkm0<1>();
+        raw_barrier();
+        if constexpr (M + 2 < WST) issue_y(o, std::integral_constant<int, M + 2>{}, (s + 2) % WYSLOTS);
+        else if (!lastp) issue_y(o + 1, std::integral_constant<int, M + 2 - WST>{}, (s + 2) % WYSLOTS);
+        if (M == 0 && xnow) issue_x(o + 2);
+        // (opaque after the barrier, so that no stage's fragment addresses are computed
+        // early and held in VGPRs)
+        int yoff = WY_OFF + sl * WYST;
+        asm volatile("" : "+s"(yoff));
+        const char* yimg = smem + yoff;
+        xp[0] = xq[0]; xp[1] = xq[1]; xp[2] = xq[2];
+        asm volatile("" : "+s"(xp[0]), "+s"(xp[1]), "+s"(xp[2]));
+        hsel = hb ? 1u : 0u;
+        asm volatile("" : "+v"(hsel));
+#if L5W_SEQ
+        // one fragment set: step 0's reads, MFMAs, then step 1's (the reads of step 1 overlap
+        // step 0's MFMAs only as far as the compiler hoists them)
+        WFr f0;
+        kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, tzc,
+              f0);
+        kmma(f0, std::integral_constant<int, 2 * M>{}, tzc);
+        kread(yimg, std::integral_constant<int, 1>{}, std::integral_constant<int, 2 * M + 1>{},
+              tzc, f0);
+        kmma(f0, std::integral_constant<int, 2 * M + 1>{}, tzc);
+#else
+        WFr f0, f1;
+        kread(yimg, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * M>{}, tzc,
+              f0);
+        kread(yimg, std::integral_constant<int, 1>{}, std::integral_constant<int, 2 * M + 1>{},
+              tzc, f1);
+        kmma(f0, std::integral_constant<int, 2 * M>{}, tzc);
+        kmma(f1, std::integral_constant<int, 2 * M + 1>{}, tzc);
+#endif
+      };
+      stage(std::integral_constant<int, 0>{});
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
+      stage(std::integral_constant<int, 4>{});
+      stage(std::integral_constant<int, 5>{});
+      stage(std::integral_constant<int, 6>{});
+    };
+    for (int og = 0; og < nplane_out; og += S) {    // a sub group's 5 planes
+      plane(og + 0, std::integral_constant<int, 0>{});
+      plane(og + 1, std::integral_constant<int, 1>{});
+      plane(og + 2, std::integral_constant<int, 2>{});
+      plane(og + 3, std::integral_constant<int, 3>{});
+      plane(og + 4, std::integral_constant<int, 4>{});
+    }
+  };
+  switch (tg) {                                     // wave-uniform
+    case 0: run(std::integral_constant<int, 0>{}); break;
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    default: run(std::integral_constant<int, 3>{}); break;
+  }
+
+  // partial slab [split][co][tap * Cs + ci]
+  float* out = ws + (int64_t)split * g.Nd * g.K;
+  const int lr = lane & 15;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    if (k < nt) {
+      const int kcol = (t0 + k) * g.Cs + ci0 + cf * 16 + lr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          out[(int64_t)(co0 + i * 16 + lk * 4 + r) * g.K + kcol] = acc[i][k][r];
+    }
+  }
+}
+
 // MMAD_LATTICE5: 1 (default) where the blocks fill the CUs, 2 at any size, 0 off;
 // mmad_set_kernel_variant("lattice5", v) overrides it at run time
 std::atomic<int> g_mode{-1};
@@ -443,6 +779,55 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
   hipLaunchKernelGGL(lattice5_conv_kernel, dim3((unsigned)blocks(q)), dim3(NTHR), LDS,
                      as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
                      stats);
+  return launch_status();
+}
+
+// weight gradient: splits of the sub groups until the (ci chunk, co tile) blocks fill the CUs
+static bool wgrad_geom(const mmad_patch::Geo& q) {
+  const int d = q.dd;
+  if (q.KD != 3 || q.KH != 3 || q.KW != 3 || q.dh != d || q.dw != d || d < 2) return false;
+  if (q.pd != d || q.ph != d || q.pw != d || (d * d * d) % NS) return false;
+  const int E = S * d;
+  if (q.Ds != E || q.Hs != E || q.Ws != E || q.Dd != E || q.Hd != E || q.Wd != E) return false;
+  if (q.Cs % KC || q.Nd % 64) return false;
+  // 32-bit byte offsets into X and dY (buffer resources)
+  return (int64_t)q.nb * E * E * E * std::max(q.Cs, q.Nd) * 2 < (int64_t(1) << 31);
+}
+int wgrad_splits(const mmad_patch::Geo& q) {
+  const int64_t tiles = (int64_t)(q.Cs / KC) * (q.Nd / 64);
+  const int64_t ngroups = (int64_t)q.nb * (q.dd * q.dd * q.dd / NS);
+  int sp = 1;
+  while (tiles * sp < 256 && ngroups % (sp * 2) == 0) sp *= 2;
+  return sp;
+}
+bool wgrad_ok(const mmad_patch::Geo& q) {
+  if (mode() <= 0 || !wgrad_geom(q)) return false;
+  const int64_t nblk = (int64_t)(q.Cs / KC) * (q.Nd / 64) * wgrad_splits(q);
+  if (nblk >= (int64_t(1) << 31)) return false;
+  return mode() == 2 || nblk >= 256;
+}
+int64_t wgrad_workspace(const mmad_patch::Geo& q) {
+  return (int64_t)wgrad_splits(q) * q.Nd * 27 * q.Cs * 4;
+}
+int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, int* splits,
+          void* stream) {
+  if (!wgrad_ok(q)) return MMAD_EUNSUPPORTED;
+  static const bool attr = hipFuncSetAttribute((const void*)lattice5_wgrad_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               WLDS) == hipSuccess;
+  if (!attr) return MMAD_EUNSUPPORTED;
+  const int sp = wgrad_splits(q);
+  LW5 g{};
+  g.Cs = q.Cs; g.Nd = q.Nd; g.d = q.dd; g.E = S * q.dd; g.G = q.dd * q.dd * q.dd / NS;
+  g.K = 27 * q.Cs;
+  g.groups_per_split = q.nb * g.G / sp;
+  const int64_t vox = (int64_t)q.nb * g.E * g.E * g.E;
+  g.xbytes = (uint32_t)(vox * q.Cs * 2);
+  g.ybytes = (uint32_t)(vox * q.Nd * 2);
+  const int64_t nblk = (int64_t)(q.Cs / KC) * (q.Nd / 64) * sp;
+  hipLaunchKernelGGL(lattice5_wgrad_kernel, dim3((unsigned)nblk), dim3(NTHR), WLDS,
+                     as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  *splits = sp;
   return launch_status();
 }
 

@@ -985,6 +985,7 @@ int lattice_wgrad_mode() {
 }
 
 bool wgrad_ok(const mmad_patch::Geo& q) {
+  if (mmad_lattice5::wgrad_ok(q)) return true;    // 5d^3 grids (lattice5.hip)
   if (lattice_mode() <= 0 || lattice_wgrad_mode() <= 0) return false;
   const int d = q.dd;
   if (q.KD != 3 || q.KH != 3 || q.KW != 3 || q.dh != d || q.dw != d || d < 2) return false;
@@ -998,11 +999,13 @@ bool wgrad_ok(const mmad_patch::Geo& q) {
 }
 
 int64_t wgrad_workspace(const mmad_patch::Geo& q) {
+  if (mmad_lattice5::wgrad_ok(q)) return mmad_lattice5::wgrad_workspace(q);
   return (int64_t)wgrad_splits(q) * q.Nd * 27 * q.Cs * 4;
 }
 
 int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, int* splits,
           void* stream) {
+  if (mmad_lattice5::wgrad_ok(q)) return mmad_lattice5::wgrad(q, x, dy, ws, splits, stream);
   if (!wgrad_ok(q)) return MMAD_EUNSUPPORTED;
   static const bool attr = hipFuncSetAttribute((const void*)lattice_wgrad_kernel,
                                                hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -80,6 +80,12 @@ bool ok(const mmad_patch::Geo& g);
 int64_t tiles(const mmad_patch::Geo& g);
 int fwd(const mmad_patch::Geo& g, const void* src, const void* wp, const float* bias, void* dst,
         float* stats, void* stream);
+// weight gradient (mmad_lattice::wgrad_ok / wgrad_workspace / wgrad route to it first):
+// fp32 partial slabs [splits][Nd][27 * Cs]
+bool wgrad_ok(const mmad_patch::Geo& g);
+int64_t wgrad_workspace(const mmad_patch::Geo& g);
+int wgrad(const mmad_patch::Geo& g, const void* x, const void* dy, float* ws, int* splits,
+          void* stream);
 }  // namespace mmad_lattice5
 
 // Residue-class conv for dilation-2 3^3 convs on a 16^3 grid (lattice8.hip, layer3).

@@ -44,6 +44,7 @@ struct StemG {
   int nyb, nzc, zsteps;           // y-pairs, z-chunks, z-steps per block
   int ring_off, c_off, red_off;   // LDS offsets (bytes)
   int wi;                         // raw input width (raw-input forms)
+  int nxt, tw;                    // output column tiles (wo > 64: config 5's 80) and width
 };
 
 // ---- raw-input rows (round 4) -----------------------------------------------------------
@@ -325,7 +326,9 @@ __global__ __launch_bounds__(512) void stem_fwdq_kernel(StemG g, const TI* __res
   const int bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid0 >> 3);
   const int zc = bid % g.nzc;
   const int yb = (bid / g.nzc) % g.nyb;
-  const int nb = bid / (g.nzc * g.nyb);
+  const int xt = (bid / (g.nzc * g.nyb)) % g.nxt;  // column tile (U form only; raw: nxt 1)
+  const int nb = bid / (g.nzc * g.nyb * g.nxt);
+  const int x0 = xt * g.tw;
   const int oz0 = zc * g.zsteps;
   const int oz1 = min(g.do_, oz0 + g.zsteps);
   const int ybase = yb * YQ * 2 - g.ph;
@@ -366,11 +369,12 @@ __global__ __launch_bounds__(512) void stem_fwdq_kernel(StemG g, const TI* __res
   };
   auto load_row = [&](int zi, int slot, int t) __attribute__((always_inline)) {
     const int yi = ybase + t;
-    bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi && lane < g.wo;
+    bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi && lane < g.tw &&
+              x0 + lane < g.wo;
 #ifdef STEMQ_NO_DMA
     ok = false;                                   // (experiment: no input traffic)
 #endif
-    const uint32_t voff = ok ? (uint32_t)(((zi * g.hi + yi) * g.wo + lane) * 16) : OOBQ;
+    const uint32_t voff = ok ? (uint32_t)(((zi * g.hi + yi) * g.wo + x0 + lane) * 16) : OOBQ;
     buf_lds16_asm(voff, rsu, lds_addr_of(smem) + (uint32_t)(slot * PLQ + t * ROWB));
   };
   // the 2 new planes of z-step ozn: 26 rows over the 8 waves (waves 0-1: 4, others 3)
@@ -470,8 +474,9 @@ __global__ __launch_bounds__(512) void stem_fwdq_kernel(StemG g, const TI* __res
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int x = i * 16 + lr;
-    xok[i] = x < g.wo;
-    so[i] = yok && xok[i] ? (uint32_t)(((oy * g.wo + x) * CO + ch * 32 + lk * 8) * 2) : OOBQ;
+    xok[i] = x < g.tw && x0 + x < g.wo;
+    so[i] = yok && xok[i] ? (uint32_t)(((oy * g.wo + x0 + x) * CO + ch * 32 + lk * 8) * 2)
+                          : OOBQ;
   }
   float cs[2][4], cq[2][4];
 #pragma unroll
@@ -798,7 +803,9 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const TI* __r
   const int bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid0 >> 3);
   const int zc = bid % g.nzc;
   const int yb = (bid / g.nzc) % g.nyb;
-  const int nb = bid / (g.nzc * g.nyb);
+  const int xt = (bid / (g.nzc * g.nyb)) % g.nxt;  // column tile (U form only; raw: nxt 1)
+  const int nb = bid / (g.nzc * g.nyb * g.nxt);
+  const int x0 = xt * g.tw;
   const int oz0 = zc * g.zsteps;
   const int oz1 = min(g.do_, oz0 + g.zsteps);
   const int ybase = yb * YT * SH - g.ph;
@@ -827,13 +834,14 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const TI* __r
       const int kd = KD - SD + f / YIN, yi = ybase + f % YIN;
       if (RAW && (unsigned)yi < (unsigned)g.hi && 2 * lane < g.wi)
         voff[h] = (uint32_t)((((kd - g.pd) * g.hi + yi) * g.wi + 2 * lane) * (int)sizeof(TI));
-      else if (!RAW && (unsigned)yi < (unsigned)g.hi && lane < g.wo)
-        voff[h] = (uint32_t)((((kd - g.pd) * g.hi + yi) * g.wo + lane) * 16);
+      else if (!RAW && (unsigned)yi < (unsigned)g.hi && lane < g.tw && x0 + lane < g.wo)
+        voff[h] = (uint32_t)((((kd - g.pd) * g.hi + yi) * g.wo + x0 + lane) * 16);
     } else if (f < RSTEP + 16) {
       const int row = (f - RSTEP) * 8 + (lane >> 3);
       const int x = row & 63, yy = yb * YT + (row >> 6);
       const int ch = (lane & 7) ^ dswz(row);
-      if (x < g.wo && yy < g.ho) voff[h] = (uint32_t)(((yy * g.wo + x) * CO + ch * 8) * 2);
+      if (x < g.tw && x0 + x < g.wo && yy < g.ho)
+        voff[h] = (uint32_t)(((yy * g.wo + x0 + x) * CO + ch * 8) * 2);
     }
   }
   // raw form: this wave's U rows of the next step in registers (issued with its dY DMAs),
@@ -902,8 +910,8 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const TI* __r
       for (int f = wave; f < (KD - SD) * YIN; f += 8) {
         const int kd = f / YIN, zi = oz0 * SD - g.pd + kd, yi = ybase + f % YIN;
         const bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi &&
-                        lane < g.wo;
-        buf_lds16_asm(ok ? (uint32_t)(((zi * g.hi + yi) * g.wo + lane) * 16) : OOB, rsu,
+                        lane < g.tw && x0 + lane < g.wo;
+        buf_lds16_asm(ok ? (uint32_t)(((zi * g.hi + yi) * g.wo + x0 + lane) * 16) : OOB, rsu,
                       ring_l + (uint32_t)((((oz0 * SD + kd) % g.rz) * YIN + f % YIN) * ROWB_W));
       }
       load_step(oz0);
@@ -1031,8 +1039,12 @@ bool quad_on() {
 bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds, bool quad = false) {
   if (d->ci != 1 || d->co != CO || d->kd != 7 || d->kh != 7 || d->kw > 8) return false;
   if (d->sd != 2 || d->sh != 2) return false;     // the instantiated form (MedicalNet)
-  if (d->dd != 1 || d->dh != 1 || d->dw != 1 || d->wo > XW || d->wo < 1) return false;
+  if (d->dd != 1 || d->dh != 1 || d->dw != 1 || d->wo < 1) return false;
   g = StemG{};
+  // rows wider than the 64 lanes (config 5's 160^3: wo 80) split into equal column tiles,
+  // one per block; the tiled forms read the W-unfolded U (the raw forms need wi <= 128)
+  g.nxt = (int)cdiv(d->wo, XW);
+  g.tw = (int)cdiv(d->wo, g.nxt);
   g.n = d->n; g.di = d->di; g.hi = d->hi; g.wo = d->wo; g.do_ = d->do_; g.ho = d->ho;
   g.wi = d->wi;
   g.sd = d->sd; g.sh = d->sh; g.pd = d->pd; g.ph = d->ph;
@@ -1053,7 +1065,7 @@ bool geom_for(const mmad_conv_desc* d, StemG& g, int& blocks, size_t& lds, bool 
                g.yin != YINQ || g.nks != NKSQ))
     return false;
   g.nyb = (int)cdiv(g.ho, yt);
-  const int64_t base = (int64_t)g.n * g.nyb;
+  const int64_t base = (int64_t)g.n * g.nyb * g.nxt;
   g.nzc = (int)std::max<int64_t>(1, std::min<int64_t>(g.do_, cdiv(256, base)));
   g.zsteps = (int)cdiv(g.do_, g.nzc);
   g.nzc = (int)cdiv(g.do_, g.zsteps);
@@ -1086,7 +1098,9 @@ bool fwd_ok(const mmad_conv_desc* d, int dtype) {
   StemG g;
   int blocks;
   size_t lds;
-  return dtype == MMAD_BF16 && geom_for(d, g, blocks, lds);
+  if (dtype != MMAD_BF16 || !geom_for(d, g, blocks, lds)) return false;
+  // column tiles: the y-quad forward and the hoisted weight gradient only
+  return g.nxt == 1 || (quad_on() && wg2_on() && geom_for(d, g, blocks, lds, true));
 }
 
 int64_t fwd_stats_rows(const mmad_conv_desc* d) {
@@ -1113,6 +1127,7 @@ int wgrad(const mmad_conv_desc* d, const void* x_unf, const void* dy, float* ws,
   size_t lds;
   if (!geom_for(d, g, blocks, lds)) return MMAD_EUNSUPPORTED;
   if (in_dtype >= 0 && !raw_ok(d, in_dtype)) return MMAD_EUNSUPPORTED;
+  if (g.nxt > 1 && in_dtype >= 0) return MMAD_EUNSUPPORTED;
   // LDS: U plane ring, then two dY tiles
   g.ring_off = g.rz * g.yin * ROWB_W;
   const size_t wl = (size_t)g.ring_off + 2 * YT * XW * CO * 2;
@@ -1134,6 +1149,8 @@ int wgrad(const mmad_conv_desc* d, const void* x_unf, const void* dy, float* ws,
   else if (wg2_on() && small)
     hipLaunchKernelGGL((stem_wgrad2_kernel<7, 7, 2, 2, u16>), dim3((unsigned)blocks), dim3(512), wl,
                        as_stream(stream), g, (const u16*)x_unf, (const u16*)dy, ws);
+  else if (g.nxt > 1)
+    return MMAD_EUNSUPPORTED;                     // (the first kernel has no column tiles)
   else
     hipLaunchKernelGGL((stem_wgrad_kernel<7, 7, 2, 2>), dim3((unsigned)blocks), dim3(512), wl,
                        as_stream(stream), g, (const u16*)x_unf, (const u16*)dy, ws);
@@ -1172,7 +1189,7 @@ int fwd(const mmad_conv_desc* d, const void* x_unf, const void* w_packed, const 
   }
   if (quad_on() && geom_for(d, g, blocks, lds, true))
     return launch_fwdq<u16>(g, blocks, x_unf, w_packed, bias, y, stats, stream);
-  if (!geom_for(d, g, blocks, lds)) return MMAD_EUNSUPPORTED;
+  if (!geom_for(d, g, blocks, lds) || g.nxt > 1) return MMAD_EUNSUPPORTED;
   static const bool ok = hipFuncSetAttribute((const void*)stem_fwd_kernel<7, 7, 2, 2>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
                                              160 * 1024) == hipSuccess;

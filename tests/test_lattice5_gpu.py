@@ -1,10 +1,12 @@
 """Residue-class conv on 5d^3 grids (csrc/lattice5.hip): config 5's layer4 -- dilation-4
 3^3 convs on the 20^3 grids a 160^3 input reaches (pet_resnet_cnn.py:12-138, anat_cnn.py:29-31
-via MedicalNet) -- forward, input gradient (the same kernel over reversed taps) and the
-eval-mode epilogue, against a plain fp32 PyTorch conv of the same bf16 operands: outputs and
-input gradients within one bf16 rounding of it (2^-7 |ref| + 1e-3 max |ref|, the bar of every
-conv kernel), BN partial-sum totals within fp32 rounding of the fp32 output's sums.  The route
-is checked through the partial-sum row count (one row per sample x sub group x plane)."""
+via MedicalNet) -- forward, input gradient (the same kernel over reversed taps), weight
+gradient and the eval-mode epilogue, against a plain PyTorch conv of the same bf16 operands:
+outputs and input gradients within one bf16 rounding of an fp32 conv (2^-7 |ref| + 1e-3
+max |ref|, the bar of every conv kernel), BN partial-sum totals within fp32 rounding of the
+fp32 output's sums, the weight gradient within 1e-3 |ref| + 1e-4 sum |gY| |X| of a float64
+one.  The route is checked through the partial-sum row count (one row per sample x sub group
+x plane) and the profiler's kernel names."""
 import pytest
 import torch
 
@@ -19,6 +21,17 @@ BF = torch.bfloat16
 
 def _variant(v):
     return _lib.load().mmad_set_kernel_variant(b"lattice5", v)
+
+
+def _kernels_of(fn):
+    """names of the GPU kernels fn launches (None where the profiler records none)"""
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events()
+             if e.device_type == torch.autograd.DeviceType.CUDA]
+    return names or None
 
 
 def _close(got, ref, name):
@@ -47,14 +60,17 @@ def test_lattice5_matches_fp32(name, xs, co, d):
     prev = _variant(2)
     try:
         xg = x.clone().requires_grad_(True)
-        y, stats = V.conv3d(xg, w.clone(), None, (1,) * 3, (d,) * 3, (d,) * 3, BF,
-                            want_stats=True)
+        wg = w.clone().requires_grad_(True)
+        y, stats = V.conv3d(xg, wg, None, (1,) * 3, (d,) * 3, (d,) * 3, BF, want_stats=True)
         gy = (torch.rand(y.shape, generator=g, device=DEV) * 2 - 1).to(BF) \
             .contiguous(memory_format=CL)
-        y.backward(gy)
-        torch.cuda.synchronize()
+        kernels = _kernels_of(lambda: y.backward(gy))
     finally:
         _variant(prev)
+    if kernels is not None:
+        assert any("lattice5_wgrad_kernel" in k for k in kernels), "weight gradient not routed"
+        if xs[1] % 128 == 0:                 # (dX of 64 channels: 128-channel tiles only)
+            assert any("lattice5_conv_kernel" in k for k in kernels), "input gradient not routed"
     assert stats.shape[0] == xs[0] * (d ** 3 // 16) * 5, "not routed to the lattice5 kernel"
     xr = x.float().requires_grad_(True)
     yr = torch.nn.functional.conv3d(xr, w.to(BF).float(), None, 1, d, d)
@@ -66,6 +82,13 @@ def test_lattice5_matches_fp32(name, xs, co, d):
     mag = torch.stack((yd.abs().sum(dim=(0, 2, 3, 4)), (yd * yd).sum(dim=(0, 2, 3, 4))))
     ref = torch.stack((yd.sum(dim=(0, 2, 3, 4)), (yd * yd).sum(dim=(0, 2, 3, 4))))
     assert ((tot.double() - ref).abs() <= 1e-3 * mag + 1e-6).all(), "BN partial sums"
+    # weight gradient (lattice5_wgrad_kernel + the transposing slab reduction) against a
+    # float64 one of the same bf16 operands: 1e-3 |ref| + 1e-4 sum |gY| |X|
+    xd, gd = x.double(), gy.double()
+    wr = torch.nn.grad.conv3d_weight(xd, w.shape, gd, 1, d, d)
+    mag = torch.nn.grad.conv3d_weight(xd.abs(), w.shape, gd.abs(), 1, d, d)
+    err = (wg.grad.double() - wr).abs()
+    assert (err <= 1e-3 * wr.abs() + 1e-4 * mag).all(), f"weight gradient: max {err.max().item():.3e}"
 
 
 def test_lattice5_eval_epilogue_residual_relu():
