@@ -53,14 +53,21 @@ constexpr uint32_t PW_OOB = 0x80000000u;
 // consecutive 16-voxel rows (y, y + 1) of one plane, as 2 segments of 16 (the 16-lane groups
 // lk = 0, 1 read segment 0, lk = 2, 3 segment 1); the y tile is the whole 16-row plane and an
 // image row group holds 18 x positions (x = -1 .. 16), 18 rows of them.
-// MODE: 0 the 32-wide form, 1 LAT, 2 W16
+// W40 (MODE 3, round 5): 40-wide volumes (config 5's layer1 at 40^3, 160^3 input): a row is
+// 5 segments of 8 voxels and a K step is 4 consecutive segments of the y tile in row-major
+// order (every 4 rows = 20 segments = 5 K steps, none wasted); an image row group holds the
+// 5 segments with their own x halos (x' = -1 .. 8 per segment, 50 positions; the halos
+// between segments are real voxels, the row ends zero), so lane group lk reads its segment
+// at a per-K-step lane offset (5 of them, the pattern's period) plus the tap's immediate.
+// MODE: 0 the 32-wide form, 1 LAT, 2 W16, 3 W40
 template <int MODE>
 struct PWC {
-  static constexpr bool LAT = MODE == 1, W16 = MODE == 2;
-  static constexpr int XR = LAT ? 40 : W16 ? 18 : PW_XW + 2;  // image positions per y row
+  static constexpr bool LAT = MODE == 1, W16 = MODE == 2, W40 = MODE == 3;
+  static constexpr int XR = LAT ? 40 : W16 ? 18 : W40 ? 50 : PW_XW + 2;  // positions per y row
+  static constexpr int SPP = W40 ? 5 : 4;                    // dY stages per output plane
   static constexpr int YRI = W16 ? 18 : PW_YR;               // image y rows
-  static constexpr int XROWS = YRI * XR;                     // 400 / 324 / 340 rows of 64 B
-  static constexpr int XDMA = (XROWS + 15) / 16;             // 25 / 21 / 22 DMA instructions
+  static constexpr int XROWS = YRI * XR;                     // 400 / 324 / 340 / 500 rows
+  static constexpr int XDMA = (XROWS + 15) / 16;             // 25 / 21 / 22 / 32 DMAs
   static constexpr int XSLOT = XDMA * 1024;
   static constexpr int Y_OFF = PW_XSLOTS * XSLOT;
   static constexpr int LDS = Y_OFF + PW_YSLOTS * PW_YST;
@@ -80,8 +87,8 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
                                                          const u16* __restrict__ dy,
                                                          float* __restrict__ ws) {
   using C = PWC<MODE>;
-  constexpr bool LAT = C::LAT, W16 = C::W16;
-  constexpr int XR = C::XR;
+  constexpr bool LAT = C::LAT, W16 = C::W16, W40 = C::W40;
+  constexpr int XR = C::XR, SPP = C::SPP;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -98,7 +105,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   const int zi = split % nzr, yt = (split / nzr) % nyt, n = split / (nzr * nyt);
   const int rz = LAT ? yt : 0;                    // (first) class group
   const int co0 = cot * 64, ci0 = cit * PW_KC, y0 = LAT || W16 ? 0 : yt * PW_TY, z0 = zi * g.zr;
-  constexpr int VW = LAT || W16 ? 16 : PW_XW;      // voxels per volume row
+  constexpr int VW = LAT || W16 ? 16 : W40 ? 40 : PW_XW;   // voxels per volume row
 
   const int64_t vox = LAT ? (int64_t)16 * 16 * 16 : (int64_t)g.D * g.H * VW;
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
@@ -127,6 +134,11 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
       const int yv = row / XR - 1, xv = row % XR - 1;
       const bool ok = row < C::XROWS && (unsigned)yv < (unsigned)g.H && (unsigned)xv < 16u;
       return ok ? (uint32_t)(((yv * 16 + xv) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
+    } else if constexpr (W40) {
+      // image row = (y - y0 + 1) * 50 + segment * 10 + x' + 1, voxel x = 8 segment + x'
+      const int yv = y0 - 1 + row / XR, ps = row % XR, xv = 8 * (ps / 10) + ps % 10 - 1;
+      const bool ok = row < C::XROWS && (unsigned)yv < (unsigned)g.H && (unsigned)xv < 40u;
+      return ok ? (uint32_t)(((yv * 40 + xv) * g.Cs + ci0 + (lane & 3) * 8) * 2) : PW_OOB;
     } else {
       const int yv = y0 - 1 + row / XR, xv = row % XR - 1;
       const bool ok = row < C::XROWS && (unsigned)yv < (unsigned)g.H &&
@@ -160,12 +172,19 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   const int yvox = LAT ? ((((yr >> 3) & 3) >> 1) + 2 * (yr >> 5)) * 16 + (((yr >> 3) & 3) & 1) +
                              2 * (yr & 7)
                        : yr;
-  const uint32_t ylane = (uint32_t)((yvox * g.Nd + co0 + ((lane & 7) ^ pw_wsz128(yr)) * 8) * 2);
+  const uint32_t ylane = (uint32_t)(((W40 ? (lane >> 3) : yvox) * g.Nd + co0 +
+                                     ((lane & 7) ^ pw_wsz128(yr)) * 8) * 2);
   auto issue_y = [&](int o, int m, int sl, int rz) {
-    const uint32_t base =
-        LAT ? (uint32_t)(((rz + 2 * (z0 + o)) * 16 + 4 * m) * 16) * (uint32_t)g.Nd * 2
-        : W16 ? (uint32_t)(((z0 + o) * g.H + 4 * m) * 16) * (uint32_t)g.Nd * 2
-            : (uint32_t)(((z0 + o) * g.H + y0 + 2 * m) * PW_XW) * (uint32_t)g.Nd * 2;
+    uint32_t base;
+    if constexpr (W40) {
+      // wave w: segment j = 4 (2m + w / 4) + w % 4 of the y tile (row j / 5, x 8 (j % 5))
+      const int j = 4 * (2 * m + (wave >> 2)) + (wave & 3);
+      base = (uint32_t)((((z0 + o) * g.H + y0 + j / 5) * 40 + 8 * (j % 5)) * g.Nd * 2);
+    } else {
+      base = LAT ? (uint32_t)(((rz + 2 * (z0 + o)) * 16 + 4 * m) * 16) * (uint32_t)g.Nd * 2
+             : W16 ? (uint32_t)(((z0 + o) * g.H + 4 * m) * 16) * (uint32_t)g.Nd * 2
+                   : (uint32_t)(((z0 + o) * g.H + y0 + 2 * m) * PW_XW) * (uint32_t)g.Nd * 2;
+    }
     buf_lds16_asm(base + ylane, rsy, smem_l + (uint32_t)(C::Y_OFF + sl * PW_YST + wave * 1024));
   };
 
@@ -184,8 +203,17 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   // (LAT: the 16-lane group lk reads segment lk, whose image positions start at 10 lk)
   // (W16: groups lk = 0, 1 read x 0-7, 8-15 of segment 0 -- image row y -- and lk = 2, 3 those
   // of segment 1, one image row group (18 positions) further)
-  const uint32_t xb = (uint32_t)((LAT ? 10 * lk + q4 : W16 ? 18 * (lk >> 1) + 8 * (lk & 1) + q4 : rsel) *
+  const uint32_t xb = (uint32_t)((LAT ? 10 * lk + q4 : W16 ? 18 * (lk >> 1) + 8 * (lk & 1) + q4
+                                  : W40 ? q4 : rsel) *
                                      64 + cf * 32 + 8 * p4);
+  // W40: lane group lk's segment of K step kt (of the 5-step period): image position of its
+  // first voxel (segment 4 kt + lk of the period's 4 rows)
+  uint32_t xk[W40 ? 5 : 1];
+#pragma unroll
+  for (int kt = 0; kt < (W40 ? 5 : 1); ++kt) {
+    const int j = 4 * kt + lk;
+    xk[kt] = W40 ? (uint32_t)(((j / 5) * XR + (j % 5) * 10) * 64) : 0u;
+  }
   f32x4 acc[4][7];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -205,7 +233,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   };
   prologue(rz);
   const int ng = LAT ? g.ng : 1;
-  const int nstage = ng * g.zr * 4;
+  const int nstage = ng * g.zr * SPP;
 
   struct PFr { bf16x8 a[4], b[7]; };
   auto run = [&](auto tgc) {
@@ -219,7 +247,8 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
     auto y_on = [](int t, int yl) constexpr {
       return !LAT || ((unsigned)(yl + (t / 3) % 3 - 1) < 8u);
     };
-    // one K step = output row YL of the current plane (compile time)
+    // one K step = output row YL of the current plane (compile time); W40: K step YL of the
+    // plane's 10
     auto kread = [&](const char* yimg, auto qc, auto ylc, PFr& f) {
       constexpr int Q = decltype(qc)::value, YL = decltype(ylc)::value;
 #pragma unroll
@@ -232,8 +261,14 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
         if constexpr (K < NT && y_on(TG * 7 + K, YL)) {
           constexpr int t = TG * 7 + K;
           constexpr int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;   // 0..2 (shift + 1)
-          constexpr int r0 = ((W16 ? 2 : 1) * YL + ky) * XR + kx;
-          const char* img = xbase[kz] + r0 * 64;
+          const char* img;
+          if constexpr (W40) {
+            constexpr int r0 = ((YL / 5) * 4 + ky) * XR + kx;
+            img = xbase[kz] + xk[YL % 5] + r0 * 64;
+          } else {
+            constexpr int r0 = ((W16 ? 2 : 1) * YL + ky) * XR + kx;
+            img = xbase[kz] + r0 * 64;
+          }
           f.b[K] = __builtin_shufflevector(tr8(img), tr8(img + 4 * 64), 0, 1, 2, 3, 4, 5, 6, 7);
         }
       };
@@ -285,7 +320,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
       const bool xnext = v + 3 < ng * gstride;   // stream entry v + 3 exists
       auto stage = [&](auto mc) {
         constexpr int M = decltype(mc)::value;
-        const int s = o * 4 + M;
+        const int s = o * SPP + M;
         // dY(s) landed (and at M = 0 the planes of o, issued a plane earlier); younger: dY(s+1)
         // and, at stages 1 and 2, the X plane issued at stage 0 right after stage 2's dY
         // (the second group's first stage: everything, its entries 1 and 2 included)
@@ -300,8 +335,8 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
         }
         raw_barrier();
         if (s + 2 < nstage) {
-          const int p2 = (s + 2) / 4, g2 = p2 >= g.zr ? 1 : 0;
-          issue_y(p2 - g2 * g.zr, (s + 2) % 4, (s + 2) % PW_YSLOTS, rz + g2);
+          const int p2 = (s + 2) / SPP, g2 = p2 >= g.zr ? 1 : 0;
+          issue_y(p2 - g2 * g.zr, (s + 2) % SPP, (s + 2) % PW_YSLOTS, rz + g2);
         }
         if (M == 0 && xnext) issue_x(v + 3, rz);
         // (opaque, defined after the barrier: otherwise the dY fragment addresses of all four
@@ -320,6 +355,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
       stage(std::integral_constant<int, 1>{});
       stage(std::integral_constant<int, 2>{});
       stage(std::integral_constant<int, 3>{});
+      if constexpr (SPP == 5) stage(std::integral_constant<int, 4>{});
     }
   };
   switch (tg) {                                  // wave-uniform
@@ -377,6 +413,20 @@ bool w16_geo(const mmad_patch::Geo& q) {
          q.pd == 1 && q.ph == 1 && q.pw == 1 && q.Ds == q.Dd && q.Hs == q.Hd && q.Ws == q.Wd &&
          q.Wd == 16 && q.Hd == 16 && q.Dd >= 4;
 }
+// MMAD_PWGRAD_W40=0 keeps the 40-wide convs on the row-gather wgrad_kernel (A/B switch)
+bool w40_on() {
+  static const bool v = [] {
+    const char* e = getenv("MMAD_PWGRAD_W40");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return v;
+}
+// the 40-wide form: dense 3^3, padding 1, stride 1 on volumes 40 voxels wide, H % 8 == 0
+bool w40_geo(const mmad_patch::Geo& q) {
+  return q.KD == 3 && q.KH == 3 && q.KW == 3 && q.dd == 1 && q.dh == 1 && q.dw == 1 &&
+         q.pd == 1 && q.ph == 1 && q.pw == 1 && q.Ds == q.Dd && q.Hs == q.Hd && q.Ws == q.Wd &&
+         q.Wd == 40 && q.Hd % PW_TY == 0 && q.Dd >= 4;
+}
 // the residue-class form: 3^3 dilation 2, padding 2, stride 1 on a 16^3 grid (8^3 classes)
 bool lat_geo(const mmad_patch::Geo& q) {
   return q.KD == 3 && q.KH == 3 && q.KW == 3 && q.dd == 2 && q.dh == 2 && q.dw == 2 &&
@@ -426,6 +476,12 @@ bool ok(const mmad_patch::Geo& q) {
     const int zr = pw_zr(q);
     return q.Dd % zr == 0 && zr >= 2;
   }
+  if (w40_geo(q)) {
+    if (!w40_on() || (int64_t)q.Dd * q.Hd * 40 * std::max(q.Cs, q.Nd) * 2 >= (int64_t(1) << 30))
+      return false;
+    const int zr = pw_zr(q);
+    return q.Dd % zr == 0 && zr >= 2;
+  }
   if (q.KD != 3 || q.KH != 3 || q.KW != 3 || q.dd != 1 || q.dh != 1 || q.dw != 1) return false;
   if (q.pd != 1 || q.ph != 1 || q.pw != 1) return false;
   if (q.Ds != q.Dd || q.Hs != q.Hd || q.Ws != q.Wd || q.Wd != PW_XW) return false;
@@ -454,9 +510,11 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
       hipFuncSetAttribute((const void*)pwgrad_kernel<1>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, PWC<1>::LDS) == hipSuccess &&
       hipFuncSetAttribute((const void*)pwgrad_kernel<2>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, PWC<2>::LDS) == hipSuccess;
+                          hipFuncAttributeMaxDynamicSharedMemorySize, PWC<2>::LDS) == hipSuccess &&
+      hipFuncSetAttribute((const void*)pwgrad_kernel<3>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, PWC<3>::LDS) == hipSuccess;
   if (!attr) return MMAD_EUNSUPPORTED;
-  const int mode = lat_geo(q) ? 1 : w16_geo(q) ? 2 : 0;
+  const int mode = lat_geo(q) ? 1 : w16_geo(q) ? 2 : w40_geo(q) ? 3 : 0;
   PWG g{};
   g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.D = q.Dd; g.H = q.Hd; g.K = 27 * q.Cs;
   g.zr = pw_zr(q);
@@ -468,6 +526,9 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
                        as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
   else if (mode == 2)
     hipLaunchKernelGGL(pwgrad_kernel<2>, dim3((unsigned)nblk), dim3(PW_NTHR), PWC<2>::LDS,
+                       as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  else if (mode == 3)
+    hipLaunchKernelGGL(pwgrad_kernel<3>, dim3((unsigned)nblk), dim3(PW_NTHR), PWC<3>::LDS,
                        as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
   else
     hipLaunchKernelGGL(pwgrad_kernel<0>, dim3((unsigned)nblk), dim3(PW_NTHR), PWC<0>::LDS,
