@@ -184,7 +184,15 @@ __global__ __launch_bounds__(NTHR) void lattice5_conv_kernel(
   const int d = g.d, E = g.E;
   const int n0 = nt * BW;
   const int64_t vol = (int64_t)E * E * E;
-  const u16* __restrict__ srcn = src + (int64_t)n * vol * g.Cs;
+  // both operands through buffer resources with 32-bit byte offsets (a scalar plane / stage
+  // part + a constant lane part; no 64-bit lane addresses, no generic-pointer casts per DMA)
+  const __amdgpu_buffer_rsrc_t rss = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(src + (int64_t)n * vol * g.Cs), 0,
+      (int)__builtin_amdgcn_readfirstlane((uint32_t)(vol * g.Cs * 2)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)wgt, 0, (int)__builtin_amdgcn_readfirstlane((uint32_t)g.Nd * g.Kpad * 2),
+      0x00020000);
+  const uint32_t lds0 = lds_addr_of(smem);
 
   // ---- plane DMA: instruction k of wave w = position w + 8k (clamped: surplus slots repeat
   // the last position, the same bytes to the same place, so every wave issues PI); lane >> 2
@@ -199,20 +207,19 @@ __global__ __launch_bounds__(NTHR) void lattice5_conv_kernel(
       const int pos = min(wave + NW * k, NP - 1), ty = pos / S, tx = pos % S;
       const int row = pos * NS + s;
       const int vox = (rz * E + ry + d * ty) * E + rx + d * tx;
-      pofs[k] = (uint32_t)(vox * g.Cs + ((lane & 3) ^ swz(row)) * 8);
+      pofs[k] = (uint32_t)(vox * g.Cs + ((lane & 3) ^ swz(row)) * 8) * 2u;
     }
   }
   // ---- weight DMA: instruction q = wave + NW h: tap q / 8, rows 16 (q % 8) ..
   uint32_t wofs[WI];
-  int wq_off[WI];
 #pragma unroll
   for (int h = 0; h < WI; ++h) {
     const int q = wave + NW * h;
     const int tk = q / (BW / 16), rb = q % (BW / 16);
     const int row = rb * 16 + (lane >> 2);
-    wofs[h] = (uint32_t)((n0 + row) * g.Kpad + (((lane & 3) ^ swz(row)) * 8) + tk * g.Cs);
-    wq_off[h] = tk * BTAP + rb * 1024;
+    wofs[h] = (uint32_t)((n0 + row) * g.Kpad + (((lane & 3) ^ swz(row)) * 8) + tk * g.Cs) * 2u;
   }
+  const uint32_t zstep = (uint32_t)(d * E * E * g.Cs * 2);   // bytes from plane tz to tz + 1
 
   const int wn = wave & 1, wm = wave >> 1;
   const int lr = lane & 15, lk = lane >> 4;
@@ -226,25 +233,30 @@ __global__ __launch_bounds__(NTHR) void lattice5_conv_kernel(
     const int tz = zb == 0 ? 4 * rep : zb;
     const int kz0 = tz == 0 ? 0 : -1;               // first kz inside the sub-lattice
     const int nz = (tz == 0 || tz == S - 1) ? 2 : 3;
-    const int nplanes = g.nchunk * nz, nstage = 3 * nplanes;
-    // plane i = (chunk i / nz, kz = kz0 + i % nz) -> ring slot i % 3
-    auto issue_plane = [&](int i) {
-      const int c = i / nz, z = tz + kz0 + i % nz;
-      const u16* base = srcn + (int64_t)z * d * E * E * g.Cs + c * KC;
-      char* pb = smem + (i % NPS) * PLB;
+    const int nplanes = g.nchunk * nz;
+    // plane i = (chunk c, kz index kzi) -> ring slot i % 3; stage (i, ky) reads plane i and
+    // the weights of taps 9 (kz + 1) + 3 (ky + 1) .. + 2 from weight slot ky + 1 (a plane's
+    // three stages use the three slots in order, so the slot is a compile-time constant)
+    auto issue_plane = [&](int c, int kzi, int slot) {
+      const uint32_t zoff = (uint32_t)(tz + kz0 + kzi) * zstep + (uint32_t)(c * KC * 2);
+      const uint32_t pb = lds0 + (uint32_t)(slot * PLB);
 #pragma unroll
       for (int k = 0; k < PI; ++k) {
         const int pos = min(wave + NW * k, NP - 1);
-        glds16_asm(base + pofs[k], lds_addr_of(pb + pos * 1024));
+        buf_lds16_asm(pofs[k] + zoff, rss, pb + (uint32_t)(pos * 1024));
       }
     };
-    // stage s = 3 i + (ky + 1) of plane i: taps t0 = 9 (kz + 1) + 3 (ky + 1) .. + 2
-    auto issue_stage_b = [&](int s) {
-      const int i = s / 3, c = i / nz, kz = kz0 + i % nz, ky = s % 3 - 1;
-      const u16* base = wgt + (9 * (kz + 1) + 3 * (ky + 1)) * g.Cs + c * KC;
-      char* sb = ring + (s % NSTL) * BSLOT;
+    auto issue_w = [&](int c, int kzi, auto kyc) {
+      constexpr int KY = decltype(kyc)::value;
+      const uint32_t toff =
+          (uint32_t)(((9 * (kz0 + kzi + 1) + 3 * (KY + 1)) * g.Cs + c * KC) * 2);
+      constexpr uint32_t sb = (uint32_t)(RING_OFF + (KY + 1) * BSLOT);
 #pragma unroll
-      for (int h = 0; h < WI; ++h) glds16_asm(base + wofs[h], lds_addr_of(sb + wq_off[h]));
+      for (int h = 0; h < WI; ++h) {
+        const int q = wave + NW * h;
+        const uint32_t dst = (uint32_t)((q / (BW / 16)) * BTAP + (q % (BW / 16)) * 1024);
+        buf_lds16_asm(wofs[h] + toff, rsw, lds0 + sb + dst);
+      }
     };
 
     f32x4 acc[NF][TN];
@@ -253,36 +265,55 @@ __global__ __launch_bounds__(NTHR) void lattice5_conv_kernel(
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // prologue: planes 0, 1 and the weights of stages 0, 1.  Group s (issued after stage
-    // s's barrier): plane s / 3 + 2 when s % 3 == 0 (its slot's last reader, plane s / 3 - 1,
-    // finished at stage s - 1) and the weights of stage s + 2 (into stage s - 1's slot)
-    issue_plane(0);
-    if (nplanes > 1) issue_plane(1);
-    issue_stage_b(0);
-    if (nstage > 1) issue_stage_b(1);
-    auto group_ops = [&](int s) {
-      return (s + 2 < nstage ? WI : 0) + ((s % 3 == 0 && s / 3 + 2 < nplanes) ? PI : 0);
-    };
+    // prologue: planes 0, 1 and the weights of plane 0's stages ky = -1, 0.  After stage
+    // (i, ky)'s barrier: ky = -1 issues plane i + 2 (slot of plane i - 1, last read at stage
+    // (i - 1, +1)) and the weights of (i, +1) (slot 2, last read at (i - 1, +1)); ky = 0 the
+    // weights of (i + 1, -1) (slot 0); ky = +1 those of (i + 1, 0) (slot 1).  Each stage waits
+    // for its weights; younger than them is the previous stage's group only.
+    issue_plane(0, 0, 0);
+    issue_plane(nz > 1 ? 0 : 1, nz > 1 ? 1 : 0, 1);
+    issue_w(0, 0, std::integral_constant<int, -1>{});
+    issue_w(0, 0, std::integral_constant<int, 0>{});
     auto run = [&](auto wmc) {
       constexpr int WM = decltype(wmc)::value;
+      int c = 0, kzi = 0, ps = 0;                   // plane i = (c, kzi) in slot ps
       for (int i = 0; i < nplanes; ++i) {
-        const char* pl = smem + (i % NPS) * PLB + a_lane;
+        // planes i + 1 and i + 2
+        const bool w1 = kzi + 1 == nz;
+        const int c1 = w1 ? c + 1 : c, k1 = w1 ? 0 : kzi + 1;
+        const bool w2 = k1 + 1 == nz;
+        const int c2 = w2 ? c1 + 1 : c1, k2 = w2 ? 0 : k1 + 1;
+        const int ps2 = ps == 0 ? 2 : ps - 1;       // (i + 2) % 3
+        const bool more1 = i + 1 < nplanes, more2 = i + 2 < nplanes;
+        const char* pl = smem + ps * PLB + a_lane;
         auto stage = [&](auto kyc) {
           constexpr int KY = decltype(kyc)::value;
-          const int s = 3 * i + KY + 1;
-          // younger than this stage's weights: group s - 1 (or, at s = 0, stage 1's weights);
-          // a plane is issued six stages before its first reader, ahead of its weights
-          wait_ops(s == 0 ? (nstage > 1 ? WI : 0) : group_ops(s - 1));
+          if constexpr (KY == -1) {
+            wait_vm_lgkm0<WI>();
+          } else if constexpr (KY == 0) {
+            if (more2) wait_vm_lgkm0<WI + PI>();
+            else wait_vm_lgkm0<WI>();
+          } else {
+            if (more1) wait_vm_lgkm0<WI>();
+            else wait_vm_lgkm0<0>();
+          }
           raw_barrier();
-          if (s % 3 == 0 && s / 3 + 2 < nplanes) issue_plane(s / 3 + 2);
-          if (s + 2 < nstage) issue_stage_b(s + 2);
-          int boff = RING_OFF + (s % NSTL) * BSLOT;
-          asm volatile("" : "+s"(boff));
-          stage_body<WM, KY>(acc, smem + boff + b_lane, pl);
+          if constexpr (KY == -1) {
+            if (more2) issue_plane(c2, k2, ps2);
+            issue_w(c, kzi, std::integral_constant<int, 1>{});
+          } else if constexpr (KY == 0) {
+            if (more1) issue_w(c1, k1, std::integral_constant<int, -1>{});
+          } else {
+            if (more1) issue_w(c1, k1, std::integral_constant<int, 0>{});
+          }
+          stage_body<WM, KY>(acc, smem + RING_OFF + (KY + 1) * BSLOT + b_lane, pl);
         };
         stage(std::integral_constant<int, -1>{});
         stage(std::integral_constant<int, 0>{});
         stage(std::integral_constant<int, 1>{});
+        c = c1;
+        kzi = k1;
+        ps = ps == 2 ? 0 : ps + 1;
       }
     };
     switch (wm) {                                     // wave-uniform

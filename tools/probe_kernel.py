@@ -1,5 +1,5 @@
-"""Run one conv pass of one ResNet-10 @128^3 layer (batch 8, bf16) a few times, for rocprofv3
-counter passes on a single kernel:
+"""Run one conv pass of one ResNet-10 @128^3 layer (batch 8, bf16; c5* layers: config 5's
+160^3 geometry) a few times, for rocprofv3 counter passes on a single kernel:
 
     rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY ... -d gpurun_out/pmc_x -o run \
         --output-format csv -- python3 tools/probe_kernel.py --layer l4c2 --op wgrad
@@ -22,6 +22,11 @@ LAYERS = {
     "l3c2": (256, 256, 16, 3, 1, 2, 2),
     "l4c1": (256, 512, 16, 3, 1, 4, 4),
     "l4c2": (512, 512, 16, 3, 1, 4, 4),
+    # BASELINE config 5 (160^3 input): layer4 on 20^3 (lattice5.hip), layer3, layer1 at 40^3
+    "c5l4c1": (256, 512, 20, 3, 1, 4, 4),
+    "c5l4c2": (512, 512, 20, 3, 1, 4, 4),
+    "c5l3c2": (256, 256, 20, 3, 1, 2, 2),
+    "c5l1c": (64, 64, 40, 3, 1, 1, 1),
 }
 
 
