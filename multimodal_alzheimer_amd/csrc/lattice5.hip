@@ -540,14 +540,16 @@ __global__ __launch_bounds__(NTHR) void lattice5_wgrad_kernel(LW5 g, const u16* 
       (void*)src, 0, (int)__builtin_amdgcn_readfirstlane(g.xbytes), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
       (void*)dy, 0, (int)__builtin_amdgcn_readfirstlane(g.ybytes), 0x00020000);
-  auto issue_x = [&](int e) {
-    const int gi = g0 + e / S, pz = e % S;
-    char* slot = smem + (e % WXSLOTS) * WPLANE;
-    const uint32_t zb = (uint32_t)(grp_vox(gi, pz, 0, 0) * g.Cs) * 2u;
+  const uint32_t lds0 = lds_addr_of(smem);
+  const uint32_t zsx = (uint32_t)(d * E * E * g.Cs * 2), zsy = (uint32_t)(d * E * E * g.Nd * 2);
+  // X plane z of a sub group whose first voxel is gx bytes into X, into ring slot `slot`
+  auto issue_x = [&](uint32_t gx, int z, int slot) {
+    const uint32_t zb = gx + (uint32_t)z * zsx;
+    const uint32_t lb = lds0 + (uint32_t)(slot * WPLANE);
 #pragma unroll
     for (int k = 0; k < PI; ++k) {
       const int pos = min(wave + NW * k, NP - 1);
-      buf_lds16_asm(zb + xl[k], rsx, lds_addr_of(slot + pos * 1024));
+      buf_lds16_asm(zb + xl[k], rsx, lb + (uint32_t)(pos * 1024));
     }
   };
   // dY of a stage: one instruction per wave, rows 8w .. 8w + 7 = K step q = w >> 2, half
@@ -556,12 +558,25 @@ __global__ __launch_bounds__(NTHR) void lattice5_wgrad_kernel(LW5 g, const u16* 
   const int yq = wave >> 2, yh = (wave >> 1) & 1;
   const uint32_t ylane = (uint32_t)(sub_part(yrow & 15) * g.Nd + co0 +
                                     (((lane & 7) ^ wsz128(yrow)) * 8)) * 2u;
-  auto issue_y = [&](int o, auto mc, int sl) {
+  // this wave's dY position of stage M, as a byte offset inside a plane (wave-uniform)
+  uint32_t py[WST];
+#pragma unroll
+  for (int m = 0; m < WST; ++m) {
+    const int p = yq == 0 ? (yh == 0 ? kpos_dma(2 * m, 0) : kpos_dma(2 * m, 1))
+                          : (yh == 0 ? kpos_dma(2 * m + 1, 0) : kpos_dma(2 * m + 1, 1));
+    py[m] = (uint32_t)((d * (p / S) * E + d * (p % S)) * g.Nd * 2);
+  }
+  // dY of stage M of plane z of a sub group whose first voxel is gy bytes into dY
+  auto issue_y = [&](uint32_t gy, int z, auto mc, int sl) {
     constexpr int M = decltype(mc)::value;
-    const int p = yq == 0 ? (yh == 0 ? kpos_dma(2 * M, 0) : kpos_dma(2 * M, 1))
-                          : (yh == 0 ? kpos_dma(2 * M + 1, 0) : kpos_dma(2 * M + 1, 1));
-    const uint32_t pb = (uint32_t)(grp_vox(g0 + o / S, o % S, p / S, p % S) * g.Nd) * 2u;
-    buf_lds16_asm(pb + ylane, rsy, lds_addr_of(smem + WY_OFF + sl * WYST + wave * 1024));
+    buf_lds16_asm(gy + (uint32_t)z * zsy + py[M] + ylane, rsy,
+                  lds0 + (uint32_t)(WY_OFF + sl * WYST + wave * 1024));
+  };
+  // first voxel of sub group gi (its first class), as byte offsets into X and dY
+  auto grp_off = [&](int gi, uint32_t& gx, uint32_t& gy) {
+    const int64_t v = grp_vox(gi, 0, 0, 0);
+    gx = (uint32_t)(v * g.Cs * 2);
+    gy = (uint32_t)(v * g.Nd * 2);
   };
 
   const int cf = wave & 1, tg = wave >> 1;          // ci half, tap group
@@ -590,10 +605,14 @@ __global__ __launch_bounds__(NTHR) void lattice5_wgrad_kernel(LW5 g, const u16* 
 #pragma unroll
     for (int k = 0; k < 7; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue_x(0);
-  if (nplane_out > 1) issue_x(1);
-  issue_y(0, std::integral_constant<int, 0>{}, 0);
-  issue_y(0, std::integral_constant<int, 1>{}, 1);
+  {
+    uint32_t gx0, gy0;
+    grp_off(g0, gx0, gy0);
+    issue_x(gx0, 0, 0);
+    issue_x(gx0, 1, 1);                             // (nplane_out >= 5)
+    issue_y(gy0, 0, std::integral_constant<int, 0>{}, 0);
+    issue_y(gy0, 0, std::integral_constant<int, 1>{}, 1);
+  }
 
   struct WFr { bf16x8 a[4], b[7]; };
   auto run = [&](auto tgc) {
@@ -655,27 +674,37 @@ __global__ __launch_bounds__(NTHR) void lattice5_wgrad_kernel(LW5 g, const u16* 
       one(std::integral_constant<int, 6>{});
     };
 
+    // sub group offsets: this one and the next (zero past the stream's end: never issued)
+    uint32_t gxc = 0, gyc = 0, gxn = 0, gyn = 0;
     // output plane o of the block's stream, TZ = its z position in the sub group
     auto plane = [&](int o, auto tzc) {
       constexpr int TZ = decltype(tzc)::value;
       const bool xnow = o + 2 < nplane_out;         // X plane o + 2 issued at stage 0
       const bool lastp = o + 1 == nplane_out;
+      const int o3 = o % WYSLOTS;                   // stage o * 7 + M sits in slot (o + M) % 3
       uint32_t xq[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) xq[k] = (uint32_t)(((o + k + 3) & 3) * WPLANE);
       auto stage = [&](auto mc) {
         constexpr int M = decltype(mc)::value;
-        const int s = o * WST + M;
-        const int sl = s % WYSLOTS;
+        const int sl = (o3 + M) % WYSLOTS;
+        const int sl2 = (o3 + M + 2) % WYSLOTS;
         // dY of this stage landed (issued two stages ago); younger: the next stage's dY and,
         // at stages 1 and 2, the X plane issued at stage 0 after stage 2's dY
         if ((M == 1 || M == 2) && xnow) wait_vm_lgkm0<PI + 1>();
         else if (lastp && M == WST - 1) wait_vm_lgkm0<0>();
         else wait_vm_lgkm0<1>();
         raw_barrier();
-        if constexpr (M + 2 < WST) issue_y(o, std::integral_constant<int, M + 2>{}, (s + 2) % WYSLOTS);
-        else if (!lastp) issue_y(o + 1, std::integral_constant<int, M + 2 - WST>{}, (s + 2) % WYSLOTS);
-        if (M == 0 && xnow) issue_x(o + 2);
+        if constexpr (M + 2 < WST) {
+          issue_y(gyc, TZ, std::integral_constant<int, M + 2>{}, sl2);
+        } else if (!lastp) {
+          if constexpr (TZ + 1 < S) issue_y(gyc, TZ + 1, std::integral_constant<int, M + 2 - WST>{}, sl2);
+          else issue_y(gyn, 0, std::integral_constant<int, M + 2 - WST>{}, sl2);
+        }
+        if (M == 0 && xnow) {
+          if constexpr (TZ + 2 < S) issue_x(gxc, TZ + 2, (o + 2) % WXSLOTS);
+          else issue_x(gxn, TZ + 2 - S, (o + 2) % WXSLOTS);
+        }
         // (opaque after the barrier, so that no stage's fragment addresses are computed
         // early and held in VGPRs)
         int yoff = WY_OFF + sl * WYST;
@@ -713,7 +742,9 @@ __global__ __launch_bounds__(NTHR) void lattice5_wgrad_kernel(LW5 g, const u16* 
       stage(std::integral_constant<int, 5>{});
       stage(std::integral_constant<int, 6>{});
     };
-    for (int og = 0; og < nplane_out; og += S) {    // a sub group's 5 planes
+    for (int og = 0, gi = g0; og < nplane_out; og += S, ++gi) {   // a sub group's 5 planes
+      grp_off(gi, gxc, gyc);
+      if (og + S < nplane_out) grp_off(gi + 1, gxn, gyn);
       plane(og + 0, std::integral_constant<int, 0>{});
       plane(og + 1, std::integral_constant<int, 1>{});
       plane(og + 2, std::integral_constant<int, 2>{});
