@@ -488,6 +488,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int r0, int col) {
 struct LWG {
   int nb, Cs, Nd, d, K;
   int groups_per_split;
+  uint32_t xbytes, ybytes;                  // operand sizes (buffer-resource ranges)
 };
 
 __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* __restrict__ src,
@@ -533,29 +534,37 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
   // X stream entry e = (group g0 + e / 4, plane e % 4) into slot e % 4: 4 instructions per
   // wave of 16 rows x 64 B (row = pos * 32 + sub)
   const int xrow_l = lane >> 2;
-  int64_t xlane[4];
+  // (round 5) both operands through buffer resources with 32-bit byte offsets (wgrad_ok
+  // bounds the tensors): a scalar plane / stage part plus a constant lane part -- no 64-bit
+  // lane addresses or generic-to-LDS casts in the stage loop
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)src, 0, (int)__builtin_amdgcn_readfirstlane(g.xbytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dy, 0, (int)__builtin_amdgcn_readfirstlane(g.ybytes), 0x00020000);
+  const uint32_t lds0 = lds_addr_of(smem);
+  uint32_t xlane[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int row = (wave * 4 + k) * 16 + xrow_l;
     const int pos = row / NS, sb = row % NS;
     const int chunk = (lane & 3) ^ wsz64(row);
-    xlane[k] = (sub_part(sb) + (int64_t)d * (pos / S) * E + d * (pos % S)) * g.Cs + ci0 +
-               chunk * 8;
+    xlane[k] = (uint32_t)(((sub_part(sb) + (int64_t)d * (pos / S) * E + d * (pos % S)) * g.Cs +
+                           ci0 + chunk * 8) * 2);
   }
   auto issue_x = [&](int e) {
     const int gi = g0 + e / S, pz = e % S;
-    char* slot = smem + (e % WXSLOTS) * WPLANE;
-    const u16* base = src + grp_vox(gi, pz, 0, 0) * g.Cs;
+    const uint32_t slot = lds0 + (uint32_t)((e % WXSLOTS) * WPLANE);
+    const uint32_t zb = (uint32_t)(grp_vox(gi, pz, 0, 0) * g.Cs * 2);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      glds16_asm(base + xlane[k], lds_addr_of(slot + (wave * 4 + k) * 1024));
+      buf_lds16_asm(zb + xlane[k], rsx, slot + (uint32_t)((wave * 4 + k) * 1024));
   };
   // dY stage s = (output plane s / 8, positions 2*(s%8), +1): one instruction per wave of
   // 8 rows x 128 B (row = q * 32 + sub; position 2m + q = (ty, tx) = (m / 2, 2 (m % 2) + q))
   const int yrow = wave * 8 + (lane >> 3);
   const int ychunk = (lane & 7) ^ wsz128(yrow);
-  const int64_t ylane = (sub_part(yrow % NS) + (int64_t)d * (yrow / NS)) * g.Nd + co0 +
-                        ychunk * 8;
+  const uint32_t ylane = (uint32_t)(((sub_part(yrow % NS) + (int64_t)d * (yrow / NS)) * g.Nd +
+                                     co0 + ychunk * 8) * 2);
 
 
   const int cf = wave & 1, tg = wave >> 1;          // ci half, tap group
@@ -592,8 +601,9 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
   };
   // dY of stage (plane o, pair m) into ring slot sl
   auto issue_y_at = [&](int64_t plane_vox0, int m, int sl) {
-    const u16* base = dy + (plane_vox0 + (int64_t)d * (m / 2) * E + 2 * d * (m % 2)) * g.Nd;
-    glds16_asm(base + ylane, lds_addr_of(smem + WY_OFF + sl * WYST + wave * 1024));
+    const uint32_t base =
+        (uint32_t)((plane_vox0 + (int64_t)d * (m / 2) * E + 2 * d * (m % 2)) * g.Nd * 2);
+    buf_lds16_asm(base + ylane, rsy, lds0 + (uint32_t)(WY_OFF + sl * WYST + wave * 1024));
   };
   auto plane_y0 = [&](int o) -> int64_t { return grp_vox(g0 + o / S, o % S, 0, 0); };
 
@@ -995,7 +1005,8 @@ bool wgrad_ok(const mmad_patch::Geo& q) {
   if ((d * d * d) % NS || q.Cs % KC || q.Nd % 64 || (d != 4 && d != 8)) return false;
   const int64_t tiles = (int64_t)(q.Cs / KC) * (q.Nd / 64) * wgrad_splits(q);
   if (lattice_mode() == 1 && tiles < 256) return false;
-  return (int64_t)q.nb * E * E * E * std::max(q.Cs, q.Nd) < (int64_t(1) << 40);
+  // 32-bit byte offsets into X and dY (buffer resources)
+  return (int64_t)q.nb * E * E * E * std::max(q.Cs, q.Nd) * 2 < (int64_t(1) << 31);
 }
 
 int64_t wgrad_workspace(const mmad_patch::Geo& q) {
@@ -1015,6 +1026,9 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
   LWG g{};
   g.nb = q.nb; g.Cs = q.Cs; g.Nd = q.Nd; g.d = q.dd; g.K = 27 * q.Cs;
   g.groups_per_split = q.nb * q.dd * q.dd * q.dd / NS / sp;
+  const int64_t vox = (int64_t)q.nb * S * q.dd * S * q.dd * S * q.dd;
+  g.xbytes = (uint32_t)(vox * q.Cs * 2);
+  g.ybytes = (uint32_t)(vox * q.Nd * 2);
   const int64_t nblk = (int64_t)(q.Cs / KC) * (q.Nd / 64) * sp;
   hipLaunchKernelGGL(lattice_wgrad_kernel, dim3((unsigned)nblk), dim3(NTHR), WLDS,
                      as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);

@@ -272,8 +272,14 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
     const u16* base = srcn + (int64_t)z * PV * g.Cs + c * KC;
     char* pb = smem + ((3 * c + jj) & 3) * ZPL;
 #pragma unroll
-    for (int k = 0; k < PI; ++k)
-      glds16_asm(base + pofs[k], lds_addr_of(pb + (wave * PI + k) * 1024));
+    for (int k = 0; k < PI; ++k) {
+      // (opaque lane offset: otherwise the compiler keeps every DMA's 64-bit lane address
+      // live across the chunk loop, and the extra VGPRs spill -- a scratch reload in the loop
+      // waits out every DMA in flight)
+      uint32_t o = pofs[k];
+      asm volatile("" : "+v"(o));
+      glds16_asm(base + o, lds_addr_of(pb + (wave * PI + k) * 1024));
+    }
   };
   // ---- weight DMA: stage (chunk c, kz, ky) -> taps t0 .. t0 + 2 into ring slot sl;
   // instruction q = wave + NW h: tap q / (BW/16), rows 16 * (q % (BW/16)) ..
@@ -293,8 +299,11 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
     const u16* base = wgt + (r * 3) * g.Cs + c * KC;   // taps (kz,ky) row: t0 = 3 r
     char* sb = ring + (s % NSTL) * C::BSLOT;
 #pragma unroll
-    for (int h = 0; h < C::WI; ++h)
-      glds16_asm(base + wofs[h], lds_addr_of(sb + wq_off[h]));
+    for (int h = 0; h < C::WI; ++h) {
+      uint32_t o = wofs[h];
+      asm volatile("" : "+v"(o));
+      glds16_asm(base + o, lds_addr_of(sb + wq_off[h]));
+    }
   };
 
   // waves w and w + 4 share a SIMD: give them diagonals wm and wm + 2
