@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for spec in "$@"; do
   IFS=: read L OP K <<< "$spec"
   echo "== $L $OP $K" | tee -a $OUT/pmc.txt
-  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/kt_$L$OP -o run --output-format csv -- python3 tools/probe_kernel.py --layer $L --op $OP > $OUT/kt_$L$OP.log 2>&1 || { echo "trace failed"; exit 1; }
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/kt_$L$OP -o run --output-format csv -- python3 tools/probe_kernel.py --layer $L --op $OP $PROBE_ARGS > $OUT/kt_$L$OP.log 2>&1 || { echo "trace failed"; exit 1; }
   python3 - $OUT/kt_$L$OP $K <<'PY' | tee -a $OUT/pmc.txt
 import csv, sys
 d, key = sys.argv[1], sys.argv[2]

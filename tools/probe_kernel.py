@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--stats", action="store_true", help="fwd: BN partial sums too")
     ap.add_argument("--relu", action="store_true",
                     help="operands ReLU'd (about half zeros, like a post-BN activation)")
+    ap.add_argument("--raw", action="store_true",
+                    help="stem: read the raw f64 volume (mmad_conv3d_*_raw, the bench's route)")
     ap.add_argument("--time", action="store_true",
                     help="print the median launch time (HIP events) instead of only running")
     a = ap.parse_args()
@@ -51,7 +53,7 @@ def main():
     lib = _lib.load()
     w = torch.randn(ws, device="cuda") * 0.02
     if ci == 1:
-        raw = torch.rand(xs, device="cuda")
+        raw = torch.rand(xs, device="cuda", dtype=torch.float64 if a.raw else torch.float32)
         x = torch.empty(lib.mmad_conv_unfolded_elems(d), dtype=dtype, device="cuda")
         _lib.call("mmad_conv_unfold_input", d, _lib.dtype_code(raw.dtype), _lib.ptr(raw), dt,
                   _lib.ptr(x), _lib.stream())
@@ -75,7 +77,14 @@ def main():
     for _ in range(a.reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        if a.op == "fwd":
+        if a.op == "fwd" and a.raw:
+            _lib.call("mmad_conv3d_fwd_raw", d, _lib.dtype_code(raw.dtype), _lib.ptr(raw), dt,
+                      _lib.ptr(wp), None, _lib.ptr(y), None if st is None else _lib.ptr(st),
+                      _lib.stream())
+        elif a.op == "wgrad" and a.raw:
+            _lib.call("mmad_conv3d_wgrad_raw", d, _lib.dtype_code(raw.dtype), _lib.ptr(raw), dt,
+                      _lib.ptr(y), _lib.ptr(dw), None, _lib.ptr(wsp), _lib.stream(), None)
+        elif a.op == "fwd":
             _lib.call("mmad_conv3d_fwd", d, dt, _lib.ptr(x), _lib.ptr(wp), None, _lib.ptr(y),
                       None if st is None else _lib.ptr(st), _lib.stream())
         elif a.op == "dgrad":
