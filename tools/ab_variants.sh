@@ -10,3 +10,6 @@ for i in 1 2; do
     MMAD_LIB_PATH=variants/$v/libmmad_hip.so timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-roofline > gpurun_out/$TAG/${v}_$i.json 2> gpurun_out/$TAG/${v}_$i.err
   done
 done
+for f in gpurun_out/$TAG/*.json; do
+  python3 -c "import json; d=json.load(open('$f')); print('$f', round(d['value'], 2), round(d['ms_per_step'], 4))"
+done
