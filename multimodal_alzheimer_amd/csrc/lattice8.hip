@@ -10,8 +10,7 @@
 // (position-major), so the tile needs no y/x halo -- a y or x shift that leaves the plane
 // is padding.  A stage is one input plane tz+kz (32 input channels, 32 KiB) and its 9 taps'
 // weights (64 output channels x 32 input channels = 4 KiB a tap), double-buffered: the next
-// stage's plane and weights load during this stage's MFMAs (L8_STAGE9=0 keeps the older
-// loop: the three planes tz-1..tz+1 resident, 3-tap weight stages on a 3-slot ring).
+// stage's plane and weights load during this stage's MFMAs.
 //  * a 16-row MFMA fragment is 2 x-neighbouring positions x 8 classes: a y shift out of
 //    the plane drops the whole fragment (compile-time per wave row, skipped); an x shift
 //    out of the plane drops half the lanes, which then read a zero row (one select);
@@ -37,18 +36,17 @@ constexpr int KC8 = RB8 / 2;
 constexpr int PLANE8 = PL8 * RB8;          // 32 KiB
 constexpr int BN8 = 64;                    // output channels per tile
 constexpr int BTAP8 = BN8 * RB8;           // 4 KiB
-// L8_STAGE9 (default 1): a stage is a whole kz plane of 9 taps (3 ky rows x 3 kx), streamed
-// with its input plane through a 2-slot plane ring and a 2-slot weight ring (36 KiB a slot),
-// so a tile runs nchunk * nkz stages with one barrier each instead of three times as many.
-// Measured r03l8s9 in the config-2 step: the four layer3 launches 52.1 / 91.7 / 88.0 / 59.1
-// us (3-tap stages, L8_STAGE9=0) -> 47.2 / 81.2 / 76.0 / 47.1 us
-#ifndef L8_STAGE9
-#define L8_STAGE9 1
-#endif
-constexpr int TPS8 = L8_STAGE9 ? 9 : 3;
-constexpr int BSLOT8 = TPS8 * BTAP8;       // 12 KiB (36 KiB for 9-tap stages)
-constexpr int NSL8 = L8_STAGE9 ? 2 : 3;
-constexpr int NPL8 = L8_STAGE9 ? 2 : 3;    // plane slots
+// A stage is a whole kz plane of 9 taps (3 ky rows x 3 kx), streamed with its input plane
+// through a 2-slot plane ring and a 2-slot weight ring (36 KiB a slot), so a tile runs
+// nchunk * nkz stages with one barrier each.  Measured r03l8s9 in the config-2 step: the four
+// layer3 launches 52.1 / 91.7 / 88.0 / 59.1 us with 3-tap stages -> 47.2 / 81.2 / 76.0 /
+// 47.1 us; a software-pipelined 3-tap loop (the barrier between the kx = 0 and kx = +1 MFMAs,
+// as latticezp.hip) measured 1-2 % slower than the 3-tap barrier-first loop (r03e); both
+// removed.
+constexpr int TPS8 = 9;
+constexpr int BSLOT8 = TPS8 * BTAP8;       // 36 KiB
+constexpr int NSL8 = 2;                    // weight slots
+constexpr int NPL8 = 2;                    // plane slots
 constexpr int RING8 = NPL8 * PLANE8;
 constexpr int ZERO8 = RING8 + NSL8 * BSLOT8;
 constexpr int MAIN8 = ZERO8 + RB8;
@@ -56,12 +54,6 @@ constexpr int CROW8 = BN8 * 2 + 16;
 constexpr int EPI8 = PL8 * CROW8 + 7 * 2 * BN8 * 4;   // + partial sums of up to 7 wave rows
 constexpr int LDS8 = MAIN8 > EPI8 ? MAIN8 : EPI8;
 constexpr int NT8 = 512;
-// L8_PIPE (default 0): the pipelined stage loop (run_pipe); measured r03e in the config-2
-// step 1-2 % slower than the barrier-first loop on all four layer3 launches (55.9 / 102.3 /
-// 96.5 / 66.0 us against 54.4 / 100.1 / 94.5 / 64.6) -- kept for A/B, not shipped.
-#ifndef L8_PIPE
-#define L8_PIPE 0
-#endif
 
 struct L8 {
   int nb, Cs, Nd, Kpad, nbn, nchunk;
@@ -214,24 +206,10 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
                    lds_addr_of(pb + (wave * 4 + k) * 1024));
     }
   };
-  auto issue_plane = [&](int p, int cc) { issue_plane_at(p, p, cc); };
-  // ---- weight DMA: 3 taps x BW rows x 64 B = 6*TN instructions; wave w issues q = w
-  // and q = w + 8 (while < 6*TN); instruction q = tap q / (2TN), rows (q % 2TN) * 16 ..
-  constexpr int NQ = 3 * BW / 16;
-  constexpr int QB = BW / 16;                      // 16-row weight pieces per tap
-  const int nbi = (wave < NQ ? 1 : 0) + (wave + 8 < NQ ? 1 : 0);
-  const u16* wq[2];
-  int wslot_off[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int q = min(wave + 8 * h, NQ - 1);
-    const int row = (q % QB) * 16 + lrow;
-    wq[h] = wgt + (int64_t)(n0 + row) * g.Kpad + ((lane & 3) ^ swz8(row)) * 8 +
-            (q / QB) * g.Cs;
-    wslot_off[h] = (q / QB) * BTAP8 + (q % QB) * 1024;
-  }
-  // 9-tap stage weights (L8_STAGE9): taps t0 .. t0 + 8 of chunk cc into slot sl; 9 * BW / 16
-  // instructions, WI9 per wave (surplus ones repeat the last: the same bytes, same place)
+  // ---- weight DMA, a stage's 9 taps: taps t0 .. t0 + 8 of chunk cc into slot sl; 9 * BW / 16
+  // instructions of 16 rows x 64 B, WI9 per wave (surplus ones repeat the last: the same
+  // bytes, same place); QB 16-row pieces per tap
+  constexpr int QB = BW / 16;
   constexpr int NQ9 = 9 * BW / 16, WI9 = (NQ9 + 7) / 8;
   auto issue_b9 = [&](int cc, int t0, int sl) {
 #pragma unroll
@@ -243,31 +221,8 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
       glds16_asm(src9, lds_addr_of(ring + sl * BSLOT8 + (q / QB) * BTAP8 + (q % QB) * 1024));
     }
   };
-  auto issue_b = [&](int cc, int t, int sl) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      if (wave + 8 * h < NQ)
-        glds16_asm(wq[h] + t * g.Cs + cc * KC8, lds_addr_of(ring + sl * BSLOT8 + wslot_off[h]));
-  };
-
   const int kz0 = tz == 0 ? 0 : -1, kz1 = tz == NZ - 1 ? 0 : 1;
   const int nkz = kz1 - kz0 + 1;
-  const int nspc = nkz * 3;
-  const int nstage = g.nchunk * nspc;
-  auto stage_w = [&](int s, int& cc, int& t) {
-    cc = s / nspc;
-    const int r = s - cc * nspc;
-    t = (kz0 + r / 3 + 1) * 9 + (r % 3) * 3;        // first tap (kx = -1) of the stage
-  };
-  auto plane_due = [&](int s, int& p, int& cc) -> bool {
-    if (s < 1) return false;
-    const int c = (s - 1) / nspc, r = (s - 1) - c * nspc;
-    if (r % 3 != 2 || c + 1 >= g.nchunk) return false;
-    p = kz0 + r / 3 + 1;
-    cc = c + 1;
-    return true;
-  };
-
   const int wm = wave % NWM, wn = wave / NWM;
   const int lr = lane & 15, lk = lane >> 4;
   const bool lhi = (lr >> 3) != 0;
@@ -282,139 +237,7 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: chunk-0 planes, weights of stages 0 and 1 (L8_PIPE: and 2, in run_pipe;
-  // L8_STAGE9: stage 0's plane and weights, in run9)
-  if (!L8_STAGE9)
-  for (int p = 0; p < 3; ++p)
-    if (p - 1 >= kz0 && p - 1 <= kz1) issue_plane(p, 0);
-  for (int s = 0; s < 2 && s < nstage && !L8_STAGE9; ++s) {
-    int cc, t;
-    stage_w(s, cc, t);
-    issue_b(cc, t, s);
-  }
-  int pl_at[2] = {0, 0};                            // plane instructions issued at s-1, s-2
-  // Stage bookkeeping kept incrementally (no run-time division in the loop: stage_w /
-  // plane_due divide by nspc, and a scalar division is a ~30-instruction sequence that ran
-  // twice per stage): the weights issued at stage s are those of stage s + 2 = (wc, wr) =
-  // divmod(s + 2, nspc); the plane check looks at stage s - 1 = (pcn, prn).
-  int wc = 2 / nspc, wr = 2 % nspc, pcn = 0, prn = -1;
-  auto one_stage = [&](int s, int slot_next) {
-    // B(s) landed; younger: B(s+1) and any plane issued after B(s) (stages s-1, s-2)
-    const int younger = (s + 1 < nstage ? nbi : 0) + pl_at[0] + pl_at[1];
-    switch (younger) {
-      case 0: wait_vm_lgkm0<0>(); break;
-      case 1: wait_vm_lgkm0<1>(); break;
-      case 2: wait_vm_lgkm0<2>(); break;
-      case 4: wait_vm_lgkm0<4>(); break;
-      case 5: wait_vm_lgkm0<5>(); break;
-      default: wait_vm_lgkm0<6>(); break;
-    }
-    raw_barrier();
-    pl_at[1] = pl_at[0];
-    pl_at[0] = 0;
-    if (s + 2 < nstage)                             // wr < 9: constant-divisor arithmetic
-      issue_b(wc, (kz0 + wr / 3 + 1) * 9 + (wr % 3) * 3, slot_next);
-    if (++wr == nspc) { wr = 0; ++wc; }
-    if (prn >= 0 && prn % 3 == 2 && pcn + 1 < g.nchunk) {
-      issue_plane(kz0 + prn / 3 + 1, pcn + 1);
-      pl_at[0] = 4;
-    }
-    if (++prn == nspc) { prn = 0; ++pcn; }
-  };
-  auto run = [&](auto wmc) {
-    constexpr int WM = decltype(wmc)::value;
-    // stage s0 = 3 * group: its three stages use weight slots 0, 1, 2 (NSL8 = 3) and issue
-    // the weights of stages s0 + 2 .. s0 + 4 into slots 2, 0, 1
-    static_assert(NSL8 == 3, "slot pattern");
-    int s0 = 0;
-    for (int c = 0; c < g.nchunk; ++c)
-      for (int kzi = 0; kzi < nkz; ++kzi, s0 += 3) {
-        const char* pl = smem + (kz0 + kzi + 1) * PLANE8;
-        one_stage(s0, 2);
-        stage8<TN, WM, -1, WR>(acc, ring + 0 * BSLOT8 + b_lane, pl, ao, zp, lhi);
-        one_stage(s0 + 1, 0);
-        stage8<TN, WM, 0, WR>(acc, ring + 1 * BSLOT8 + b_lane, pl, ao, zp, lhi);
-        one_stage(s0 + 2, 1);
-        stage8<TN, WM, 1, WR>(acc, ring + 2 * BSLOT8 + b_lane, pl, ao, zp, lhi);
-      }
-  };
-  // L8_PIPE: stage s's barrier sits between its kx = 0 and kx = +1 MFMAs.  Before it each
-  // wave waits for stage s + 1's weights (issued three stages ahead, in group s - 2) and its
-  // own LDS reads of stage s; after it the DMA group of stage s goes out (weights of stage
-  // s + 3 into stage s's slot, free now, and -- after a kz plane's last stage -- that plane
-  // of the next chunk, first read nspc - 2 >= 4 stages later), then stage s + 1's kx = -1
-  // fragments are read behind stage s's kx = +1 MFMAs: the MFMA pipe runs across barriers.
-  auto run_pipe = [&](auto wmc) {
-    constexpr int WM = decltype(wmc)::value;
-    auto plane_due2 = [&](int s, int& p, int& cc) -> bool {
-      const int c = s / nspc, r = s - c * nspc;
-      if (r % 3 != 2 || c + 1 >= g.nchunk) return false;
-      p = kz0 + r / 3 + 1;
-      cc = c + 1;
-      return true;
-    };
-    if (2 < nstage) {
-      int cc, t;
-      stage_w(2, cc, t);
-      issue_b(cc, t, 2);
-    }
-    if (2 < nstage && nbi == 2) wait_vm_lgkm0<4>();
-    else if (2 < nstage && nbi == 1) wait_vm_lgkm0<2>();
-    else wait_vm_lgkm0<0>();
-    raw_barrier();
-    Fr8<TN, NFR> f0, f1;
-    read8<TN, WM, -1, -1, WR>(ring + b_lane, smem + (kz0 + 1) * PLANE8, ao, zp, lhi, f0);
-    int pl_prev = 0;                                // plane instructions of group s - 1
-    auto barrier_dma = [&](int s) {
-      const int younger = (s + 2 < nstage ? nbi : 0) + pl_prev;
-      switch (younger) {
-        case 0: wait_vm_lgkm0<0>(); break;
-        case 1: wait_vm_lgkm0<1>(); break;
-        case 2: wait_vm_lgkm0<2>(); break;
-        case 4: wait_vm_lgkm0<4>(); break;
-        case 5: wait_vm_lgkm0<5>(); break;
-        default: wait_vm_lgkm0<6>(); break;
-      }
-      raw_barrier();
-      if (s + 3 < nstage) {
-        int cc, t;
-        stage_w(s + 3, cc, t);
-        issue_b(cc, t, s % NSL8);
-      }
-      int p, pc;
-      pl_prev = 0;
-      if (plane_due2(s, p, pc)) {
-        issue_plane(p, pc);
-        pl_prev = 4;
-      }
-    };
-    const int ngrp = nstage / 3;
-    for (int g2 = 0; g2 < ngrp; ++g2) {
-      const int kz = kz0 + g2 % nkz, kzn = kz0 + (g2 + 1) % nkz;
-      const char* pl = smem + (kz + 1) * PLANE8;
-      const char* pln = smem + (kzn + 1) * PLANE8;
-      const int s0 = g2 * 3;
-      auto stage = [&](auto kyc, int s, Fr8<TN, NFR>& fa, Fr8<TN, NFR>& fb) {
-        constexpr int KY = decltype(kyc)::value;
-        constexpr int KYN = KY < 1 ? KY + 1 : -1;
-        int boff = RING8 + (s % NSL8) * BSLOT8, bnof = RING8 + ((s + 1) % NSL8) * BSLOT8;
-        asm volatile("" : "+s"(boff), "+s"(bnof));
-        const char* bsl = smem + boff + b_lane;
-        read8<TN, WM, KY, 0, WR>(bsl, pl, ao, zp, lhi, fb);
-        mma8<TN, WM, KY, WR>(acc, fa);
-        read8<TN, WM, KY, 1, WR>(bsl, pl, ao, zp, lhi, fa);
-        mma8<TN, WM, KY, WR>(acc, fb);
-        barrier_dma(s);
-        read8<TN, WM, KYN, -1, WR>(smem + bnof + b_lane, KY < 1 ? pl : pln, ao, zp, lhi, fb);
-        mma8<TN, WM, KY, WR>(acc, fa);
-      };
-      stage(std::integral_constant<int, -1>{}, s0, f0, f1);
-      stage(std::integral_constant<int, 0>{}, s0 + 1, f1, f0);
-      stage(std::integral_constant<int, 1>{}, s0 + 2, f0, f1);
-      f0 = f1;
-    }
-  };
-  // L8_STAGE9: stage e = (chunk c, kz): plane e and its 9 taps' weights land in slot e & 1,
+  // stage e = (chunk c, kz): plane e and its 9 taps' weights land in slot e & 1,
   // issued at the top of stage e - 1 (after its barrier, when slot (e - 1) & 1 = (e + 1) & 1
   // has been read by every wave), so the top of stage e waits for everything issued
   auto run9 = [&](auto wmc) {
@@ -440,11 +263,7 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
       }
   };
   auto dispatch = [&](auto wmc) {
-    if constexpr (decltype(wmc)::value < NWM) {
-      if constexpr (L8_STAGE9) run9(wmc);
-      else if constexpr (L8_PIPE) run_pipe(wmc);
-      else run(wmc);
-    }
+    if constexpr (decltype(wmc)::value < NWM) run9(wmc);
   };
   switch (wm) {                                     // wave-uniform
     case 0: dispatch(std::integral_constant<int, 0>{}); break;

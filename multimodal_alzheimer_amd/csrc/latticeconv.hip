@@ -430,8 +430,8 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
 // dW[co][tap][ci] = sum over output voxels v of dY[v][co] * X[v + tap][ci], v walked as
 // (sub group, plane tz, position, 32 subs): a K step of 32 voxels is 32 subs at ONE output
 // position, so a tap's X rows for that step are the 32 subs at one shifted position of one
-// input plane -- or, when the shift leaves the 4^3 sub-lattice, the zero padding, read from
-// a 2 KiB zero block (uniform address select, no branch: those MFMAs add zeros).
+// input plane -- or, when the shift leaves the 4^3 sub-lattice, padding: those (tap, K step)
+// pairs are skipped at compile time (position, tap group and plane are template constants).
 //  * block = 64 output channels x 32 input channels x all 27 taps over a split of the sub
 //    groups; 8 waves = 2 (16-channel ci halves) x 4 tap groups of 7 (6); per wave 4 x 7
 //    accumulator tiles;
@@ -442,26 +442,16 @@ __global__ __launch_bounds__(NTHR) void lattice_conv_kernel(LG g, const u16* __r
 //  * both operands are m-major images read with transposing ds_read_b64_tr_b16 fragment
 //    reads (as conv.hip's wgrad_kernel); fp32 partial slabs [split][co][tap*Cs + ci] are
 //    summed and transposed by conv.hip's wgrad_reduce_t_kernel.
-// LW_PIPE (default 0): the pipelined stage loop below (run_pipe); measured r03e in the
-// config-2 step: layer4.0.conv2 wgrad 266.5 us against 241.0 for the barrier-first loop
-// (run), layer4.0.conv1 138.1 against 125.7 -- kept for A/B, not shipped.  LW_ZSKIP (with
-// LW_PIPE): z-padding taps skipped by a uniform branch instead of the zero block.
-#ifndef LW_PIPE
-#define LW_PIPE 0
-#endif
-#ifndef LW_ZSKIP
-#define LW_ZSKIP 1
-#endif
-#ifndef LW_TZ
-#define LW_TZ 1
-#endif
+// (A software-pipelined stage loop -- the barrier between a stage's two positions, as in
+// latticezp.hip -- measured slower in the config-2 step, r03e: layer4.0.conv2 wgrad 266.5 us
+// against 241.0 for this barrier-first loop, conv1 138.1 against 125.7; removed.)
 constexpr int WXROW = 64;                 // X rows: 32 ci x 2 B
 constexpr int WYROW = 128;                // dY rows: 64 co x 2 B
 constexpr int WPLANE = PL * WXROW;        // 32 KiB
 constexpr int WXSLOTS = 4;
 constexpr int WYST = 2 * NS * WYROW;      // 8 KiB: 2 positions per stage
 constexpr int WYSLOTS = 3;
-constexpr int WZERO_OFF = WXSLOTS * WPLANE;
+constexpr int WZERO_OFF = WXSLOTS * WPLANE;  // 2 KiB spare (the former padding-row block)
 constexpr int WY_OFF = WZERO_OFF + NS * WXROW;
 constexpr int WLDS = WY_OFF + WYSLOTS * WYST;
 
@@ -512,10 +502,6 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
   const int nplane_out = g.groups_per_split * S;    // output planes of this block
   const int nstage = nplane_out * 8;                // 2 positions per stage
   const int64_t plane_vox = (int64_t)d * E * E;
-
-  // zero block (the padding rows)
-  for (int i = tid; i < NS * WXROW / 16; i += NTHR)
-    *reinterpret_cast<u32x4*>(smem + WZERO_OFF + i * 16) = u32x4{0u, 0u, 0u, 0u};
 
   // sub s of group gi -> voxel of (plane z, position ty, tx) = a group-uniform part
   // (scalar, recomputed per stage / plane) + a per-lane sub part (constant: a group holds
@@ -615,9 +601,8 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
 
   // The wave's tap group TG is a compile-time constant of its code path, and so is each
   // K step's position: a tap whose (y, x) shift leaves the sub-lattice at that position has
-  // neither fragment reads nor MFMAs (no branches in the MFMA stream, 31 % fewer X reads).
-  // A tap whose z shift leaves it (first / last plane of a sub group) reads the zero block
-  // and its MFMAs add exact zeros.
+  // neither fragment reads nor MFMAs (no branches in the MFMA stream, 31 % fewer X reads);
+  // nor has a tap whose z shift leaves it (first / last plane of a sub group).
   struct WFr { bf16x8 a[4], b[7]; };
   auto run = [&](auto tgc) {
     constexpr int TG = decltype(tgc)::value;
@@ -629,17 +614,14 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       constexpr int py = POS / S + ky, px = POS % S + kx;
       return K < NT && py >= 0 && py < S && px >= 0 && px < S;
     };
-    // LW_TZ: the plane's z position in its sub group is a compile-time constant too, so a
-    // tap whose z shift leaves the sub-lattice has no reads and no MFMAs either (the plane
-    // loop is unrolled by the 4 planes of a sub group); LW_TZ = 0 reads the zero block and
-    // adds zero products instead
+    // the plane's z position in its sub group is a compile-time constant too, so a tap
+    // whose z shift leaves the sub-lattice has no reads and no MFMAs either (the plane loop
+    // is unrolled by the 4 planes of a sub group)
     auto z_on = [](auto kc, auto tzc) constexpr {
       constexpr int K = decltype(kc)::value, TZ = decltype(tzc)::value;
       constexpr int kz = (TG * 7 + K) / 9 - 1;
-      return TZ < 0 || (TZ + kz >= 0 && TZ + kz < S);
+      return TZ + kz >= 0 && TZ + kz < S;
     };
-    bool zok[7];
-    int pbase = 0;                                  // plane tz's X offset in the ring
     auto kread = [&](const char* yimg, auto qc, auto posc, auto tzc, WFr& f) {
       constexpr int Q = decltype(qc)::value, POS = decltype(posc)::value;
       constexpr int TZ = decltype(tzc)::value;
@@ -654,9 +636,7 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
           constexpr int t = TG * 7 + K;
           constexpr int dk = (t / 9 - 1) * WPLANE + (((t / 3) % 3 - 1) * S + t % 3 - 1) * NS * WXROW +
                              POS * NS * WXROW;
-          const char* img;
-          if constexpr (TZ >= 0) img = smem + TZ * WPLANE + dk;
-          else img = smem + (zok[K] ? pbase + dk : WZERO_OFF);
+          const char* img = smem + TZ * WPLANE + dk;
           f.b[K] = __builtin_shufflevector(tr8(img + xb_lo), tr8(img + xb_hi), 0, 1, 2, 3, 4, 5,
                                            6, 7);
         }
@@ -688,16 +668,9 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       one(std::integral_constant<int, 6>{});
     };
 
-    // plane o of the block's stream; tzc = its z position in the sub group (-1: run time)
+    // plane o of the block's stream; tzc = its z position in the sub group
     auto plane = [&](int o, auto tzc) {
-      const int tz = o % S;
       const bool xnow = o + 2 < nplane_out;         // X plane o + 2 issued at stage 0
-      pbase = tz * WPLANE;
-#pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        const int kz = (TG * 7 + k) / 9 - 1;
-        zok[k] = (unsigned)(tz + kz) < (unsigned)S;
-      }
       const int64_t y_here = plane_y0(o);
       const int64_t y_next = o + 1 < nplane_out ? plane_y0(o + 1) : y_here;
       const int sl0 = (o * 8) % WYSLOTS;
@@ -736,150 +709,18 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       stage(std::integral_constant<int, 6>{});
       stage(std::integral_constant<int, 7>{});
     };
-    if constexpr (LW_TZ) {
-      for (int og = 0; og < nplane_out; og += S) {  // a sub group's 4 planes
-        plane(og + 0, std::integral_constant<int, 0>{});
-        plane(og + 1, std::integral_constant<int, 1>{});
-        plane(og + 2, std::integral_constant<int, 2>{});
-        plane(og + 3, std::integral_constant<int, 3>{});
-      }
-    } else {
-      for (int o = 0; o < nplane_out; ++o) plane(o, std::integral_constant<int, -1>{});
-    }
-  };
-  // LW_PIPE: the barrier of stage s sits between its two positions' MFMAs.  Stage s reads
-  // its second position's fragments behind the first position's MFMAs, waits for stage
-  // s + 1's dY (and every LDS read of stage s), takes the barrier, issues its DMA group (dY
-  // of stage s + 3 into stage s's slot, free now; X plane o + 2 at a plane's first stage)
-  // and reads stage s + 1's first-position fragments behind its second position's MFMAs:
-  // the MFMA pipe runs across the barrier.  X plane o + 2 is issued 8 stages before its first
-  // reader's barrier and ahead of that barrier's dY, so the same wait covers it.  A tap whose
-  // z shift leaves the sub-lattice (first / last plane of a sub group) is skipped by a
-  // wave-uniform branch -- reads and MFMAs -- instead of adding the zero block's products:
-  // the reads run a phase ahead of their MFMAs, so the branches cost no overlap.
-  auto run_pipe = [&](auto tgc) {
-    constexpr int TG = decltype(tgc)::value;
-    constexpr int NT = TG == 3 ? 6 : 7;
-    auto yx_on = [](auto kc, auto posc) constexpr {
-      constexpr int K = decltype(kc)::value, POS = decltype(posc)::value;
-      constexpr int t = TG * 7 + K;
-      constexpr int ky = (t / 3) % 3 - 1, kx = t % 3 - 1;
-      constexpr int py = POS / S + ky, px = POS % S + kx;
-      return K < NT && py >= 0 && py < S && px >= 0 && px < S;
-    };
-    auto kread = [&](const char* yimg, auto qc, auto posc, int pb, const bool (&zk)[7], WFr& f) {
-      constexpr int Q = decltype(qc)::value, POS = decltype(posc)::value;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        f.a[i] = __builtin_shufflevector(tr8(yimg + Q * NS * WYROW + ya_lo[i]),
-                                         tr8(yimg + Q * NS * WYROW + ya_hi[i]), 0, 1, 2, 3, 4,
-                                         5, 6, 7);
-      auto one = [&](auto kc) {
-        constexpr int K = decltype(kc)::value;
-        if constexpr (yx_on(kc, posc)) {
-          constexpr int t = TG * 7 + K;
-          constexpr int dk = (t / 9 - 1) * WPLANE + (((t / 3) % 3 - 1) * S + t % 3 - 1) * NS * WXROW +
-                             POS * NS * WXROW;
-          if (!LW_ZSKIP || zk[K]) {                    // wave-uniform: z padding skipped
-            const char* img = smem + (zk[K] ? pb + dk : WZERO_OFF);
-            f.b[K] = __builtin_shufflevector(tr8(img + xb_lo), tr8(img + xb_hi), 0, 1, 2, 3, 4,
-                                             5, 6, 7);
-          }
-        }
-      };
-      one(std::integral_constant<int, 0>{});
-      one(std::integral_constant<int, 1>{});
-      one(std::integral_constant<int, 2>{});
-      one(std::integral_constant<int, 3>{});
-      one(std::integral_constant<int, 4>{});
-      one(std::integral_constant<int, 5>{});
-      one(std::integral_constant<int, 6>{});
-    };
-    auto kmma = [&](const WFr& f, auto posc, const bool (&zk)[7]) {
-      auto one = [&](auto kc) {
-        constexpr int K = decltype(kc)::value;
-        if constexpr (yx_on(kc, posc)) {
-          if (!LW_ZSKIP || zk[K]) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              acc[i][K] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[K], acc[i][K], 0,
-                                                                  0, 0);
-          }
-        }
-      };
-      one(std::integral_constant<int, 0>{});
-      one(std::integral_constant<int, 1>{});
-      one(std::integral_constant<int, 2>{});
-      one(std::integral_constant<int, 3>{});
-      one(std::integral_constant<int, 4>{});
-      one(std::integral_constant<int, 5>{});
-      one(std::integral_constant<int, 6>{});
-    };
-    auto zflags = [&](int tz, bool (&zk)[7]) {
-#pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        const int kz = (TG * 7 + k) / 9 - 1;
-        zk[k] = (unsigned)(tz + kz) < (unsigned)S;
-      }
-    };
-    issue_y_at(plane_y0(0), 2, 2);                  // the prologue's third dY stage
-    wait_vm_lgkm0<2>();                             // X planes 0, 1 and dY stage 0
-    raw_barrier();
-    WFr f0, f1;
-    bool zok[7], zn[7];
-    zflags(0, zok);
-    kread(smem + WY_OFF, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0,
-          zok, f0);
-    for (int o = 0; o < nplane_out; ++o) {
-      const int tz = o % S;
-      const bool xnow = o + 2 < nplane_out;         // X plane o + 2 issued at stage 0
-      const bool lastp = o + 1 == nplane_out;
-      const int pbase = tz * WPLANE, pnext = ((o + 1) % S) * WPLANE;
-      zflags(tz, zok);
-      zflags((o + 1) % S, zn);
-      const int64_t y_here = plane_y0(o);
-      const int64_t y_next = lastp ? y_here : plane_y0(o + 1);
-      const int sl0 = (o * 8) % WYSLOTS;
-      auto stage = [&](auto mc) {
-        constexpr int M = decltype(mc)::value;
-        const int sl = (sl0 + M) % WYSLOTS;
-        int yoff = WY_OFF + sl * WYST, ynof = WY_OFF + ((sl + 1) % WYSLOTS) * WYST;
-        asm volatile("" : "+s"(yoff), "+s"(ynof));
-        kread(smem + yoff, std::integral_constant<int, 1>{},
-              std::integral_constant<int, 2 * M + 1>{}, pbase, zok, f1);
-        kmma(f0, std::integral_constant<int, 2 * M>{}, zok);
-        // barrier of stage s: dY of stage s + 1 (issued in group s - 2) landed; younger are
-        // group s - 1's dY (stage s + 2) and, after a plane's first stage, its X plane
-        if (M == 1 && xnow) wait_vm_lgkm0<5>();
-        else if (lastp && M >= 6) wait_vm_lgkm0<0>();
-        else wait_vm_lgkm0<1>();
-        raw_barrier();
-        if (M + 3 < 8) issue_y_at(y_here, M + 3, sl);
-        else if (!lastp) issue_y_at(y_next, M - 5, sl);
-        if (M == 0 && xnow) issue_x(o + 2);
-        if constexpr (M < 7)
-          kread(smem + ynof, std::integral_constant<int, 0>{},
-                std::integral_constant<int, 2 * M + 2>{}, pbase, zok, f0);
-        else
-          kread(smem + ynof, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
-                pnext, zn, f0);
-        kmma(f1, std::integral_constant<int, 2 * M + 1>{}, zok);
-      };
-      stage(std::integral_constant<int, 0>{});
-      stage(std::integral_constant<int, 1>{});
-      stage(std::integral_constant<int, 2>{});
-      stage(std::integral_constant<int, 3>{});
-      stage(std::integral_constant<int, 4>{});
-      stage(std::integral_constant<int, 5>{});
-      stage(std::integral_constant<int, 6>{});
-      stage(std::integral_constant<int, 7>{});
+    for (int og = 0; og < nplane_out; og += S) {    // a sub group's 4 planes
+      plane(og + 0, std::integral_constant<int, 0>{});
+      plane(og + 1, std::integral_constant<int, 1>{});
+      plane(og + 2, std::integral_constant<int, 2>{});
+      plane(og + 3, std::integral_constant<int, 3>{});
     }
   };
   switch (tg) {                                     // wave-uniform
-    case 0: LW_PIPE ? run_pipe(std::integral_constant<int, 0>{}) : run(std::integral_constant<int, 0>{}); break;
-    case 1: LW_PIPE ? run_pipe(std::integral_constant<int, 1>{}) : run(std::integral_constant<int, 1>{}); break;
-    case 2: LW_PIPE ? run_pipe(std::integral_constant<int, 2>{}) : run(std::integral_constant<int, 2>{}); break;
-    default: LW_PIPE ? run_pipe(std::integral_constant<int, 3>{}) : run(std::integral_constant<int, 3>{}); break;
+    case 0: run(std::integral_constant<int, 0>{}); break;
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    default: run(std::integral_constant<int, 3>{}); break;
   }
 
   // partial slab [split][co][tap * Cs + ci]

@@ -22,8 +22,9 @@
 //    accumulators (one wave per SIMD with 256 accumulators in AGPRs fared worse still: the
 //    MFMA results rotate through registers and spill the overflow to VGPRs);
 //  * a stage = (channel chunk, kz, ky): the three kx taps' weights (3 x BW rows x 64 B)
-//    through a 3-slot ring, two stages in flight; both output planes use the same kz
-//    weights, so every B fragment feeds 16 A fragments;
+//    through a 4-slot ring, three stages in flight; both output planes use the same kz
+//    weights, so every B fragment feeds 8 A fragments of the wave (16 of the SIMD pair);
+//    the stage loop is software-pipelined across its barriers (see run_pipe);
 //  * input planes (16 subs x 16 positions x 32 channels = 16 KiB) through a 4-slot ring:
 //    per chunk the pair reads 3 real planes (tz0 - 1 .. tz0 + 2 minus the padding one), each
 //    loaded once and read by every kz whose shift lands on it; planes of the next chunk
@@ -142,21 +143,6 @@ __device__ __forceinline__ void mma_a(f32x4 (&acc)[NF][TN], const bf16x8 (&a)[NF
   }
 }
 
-// One stage (kz, ky; kx = -1, 0, 1), rolling registers: each A fragment register is refilled
-// for the next tap right after the current tap's MFMAs have read it, so one set of A
-// fragments and two sets of B fragments are live, and each refill has the other fragments'
-// MFMAs (and the partner wave) to land behind.
-// `dma` (the stage's LDS-DMA issues) runs after the first tap's fragment reads are issued:
-// the ~60-cycle issue of each DMA then overlaps those reads' latency instead of delaying
-// them behind the barrier.  ZP_EARLY_READS: 1 (default) for the 64-channel form only -- the
-// 128-channel form has no registers to spare for it (256 VGPRs and spills inside the main
-// loop); 2 both forms; 0 neither (barrier -> DMA -> reads).
-#ifndef ZP_EARLY_READS
-#define ZP_EARLY_READS 1
-#endif
-#ifndef ZP_PIPE
-#define ZP_PIPE 1
-#endif
 // ZP_PIN 1: a scheduling barrier after each fragment's (MFMAs, refill) pair keeps the
 // compiler from hoisting the refills (their latency is covered by the other fragments'
 // MFMAs anyway) and so from inflating the live fragment registers into spills
@@ -168,35 +154,7 @@ __device__ __forceinline__ void mma_a(f32x4 (&acc)[NF][TN], const bf16x8 (&a)[NF
 #else
 #define ZP_PIN() (void)0
 #endif
-template <int TN, int WM, int P, int KZ, int KY, typename DMA>
-__device__ __forceinline__ void stage_body(f32x4 (&acc)[NF][TN], const char* bsl,
-                                           const char* const (&pl)[3], DMA&& dma) {
-  constexpr bool EARLY = ZP_EARLY_READS == 2 || (ZP_EARLY_READS == 1 && TN == 2);
-  bf16x8 a[NF], b0[TN], b1[TN];
-  if constexpr (!EARLY) dma();
-  read_b<TN, -1>(bsl, b0);
-  [&]<int... F>(std::integer_sequence<int, F...>) {
-    (read_a<WM, P, KZ, KY, -1, F>(pl, a), ...);
-  }(std::make_integer_sequence<int, NF>{});
-  read_b<TN, 0>(bsl, b1);
-  if constexpr (EARLY) dma();
-  [&]<int... F>(std::integer_sequence<int, F...>) {
-    ((mma_a<TN, WM, P, KZ, KY, -1, F>(acc, a, b0), read_a<WM, P, KZ, KY, 0, F>(pl, a)), ...);
-  }(std::make_integer_sequence<int, NF>{});
-  read_b<TN, 1>(bsl, b0);
-  [&]<int... F>(std::integer_sequence<int, F...>) {
-    ((mma_a<TN, WM, P, KZ, KY, 0, F>(acc, a, b1), read_a<WM, P, KZ, KY, 1, F>(pl, a)), ...);
-  }(std::make_integer_sequence<int, NF>{});
-  [&]<int... F>(std::integer_sequence<int, F...>) {
-    (mma_a<TN, WM, P, KZ, KY, 1, F>(acc, a, b0), ...);
-  }(std::make_integer_sequence<int, NF>{});
-}
-
-// planes issued at chunk-relative stage R of a non-last chunk (pair P): count
-template <int P, int R>
-__device__ constexpr int planes_at() {
-  return P == 0 ? (R == 0 ? 2 : R == 6 ? 1 : 0) : (R == 0 || R == 3 || R == 6 ? 1 : 0);
-}
+// planes issued at chunk-relative stage r of a non-last chunk (pair p): count
 __host__ __device__ constexpr int planes_at_rt(int p, int r) {
   return p == 0 ? (r == 0 ? 2 : r == 6 ? 1 : 0) : (r == 0 || r == 3 || r == 6 ? 1 : 0);
 }
@@ -318,80 +276,13 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
     for (int j = 0; j < TN; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: the first chunk's planes needed before its plane issues (pair 0: planes 0, 1;
-  // pair 1: all three), then the weights of stages 0 and 1 (and 2 for ZP_PIPE)
+  // pair 1: all three), then the weights of the first NSTL stages
   issue_plane(0, 0);
   issue_plane(0, 1);
   if (pair == 1) issue_plane(0, 2);
-  issue_stage_b(0);
-  issue_stage_b(1);
-  if constexpr (ZP_PIPE)
-    for (int t = 2; t < NSTL; ++t) issue_stage_b(t);
+  for (int t = 0; t < NSTL; ++t) issue_stage_b(t);
 
-  // Stage s = 9c + R (R = 3 (kz+1) + ky+1) waits for its weights (issued at stage s - 2);
-  // younger are the ops issued at stage s - 1: its planes and the weights of stage s + 1.
-  // A plane is older than the weights of the stage that first reads it (issued 3 or more
-  // stages ahead), so the same wait covers it.  Issue schedule per chunk c (slot reuse
-  // checked against each plane's last reader):
-  //   pair 0: R 0 -> (c, 2), (c + 1, 0); R 6 -> (c + 1, 1)
-  //   pair 1: R 0 -> (c + 1, 0); R 3 -> (c + 1, 1); R 6 -> (c + 1, 2)
-  auto run = [&](auto wmc, auto pc) {
-    constexpr int WM = decltype(wmc)::value, P = decltype(pc)::value;
-    for (int c = 0; c < g.nchunk; ++c) {
-      const bool more = c + 1 < g.nchunk;
-      const int sb0 = 3 * c;
-      const char* const pl[3] = {smem + ((sb0 + 0) & 3) * ZPL + a_lane,
-                                 smem + ((sb0 + 1) & 3) * ZPL + a_lane,
-                                 smem + ((sb0 + 2) & 3) * ZPL + a_lane};
-      auto stage = [&](auto rc) {
-        constexpr int R = decltype(rc)::value;
-        constexpr int KZ = R / 3 - 1, KY = R % 3 - 1;
-        const int s = 9 * c + R;
-        // younger than this stage's weights: stage s-1's planes (R - 1 of this chunk) and
-        // the weights of stage s + 1
-        constexpr int PY = R >= 1 ? planes_at<P, R - 1>() : 0;
-        if (s == 0) {
-          wait_vm_lgkm0<C::WI>();
-        } else if (s + 1 >= nstage) {
-          wait_vm_lgkm0<0>();
-        } else if (more) {
-          wait_vm_lgkm0<C::WI + PI * PY>();
-        } else {
-          // last chunk: pair 0 still issued (c, 2) at R 0; nothing else of chunk c + 1
-          constexpr int PYL = (P == 0 && R == 1) ? 1 : 0;
-          wait_vm_lgkm0<C::WI + PI * PYL>();
-        }
-        raw_barrier();
-        auto dma = [&]() {
-          if constexpr (P == 0) {
-            if constexpr (R == 0) {
-              issue_plane(c, 2);
-              if (more) issue_plane(c + 1, 0);
-            } else if constexpr (R == 6) {
-              if (more) issue_plane(c + 1, 1);
-            }
-          } else {
-            if constexpr (R == 0 || R == 3 || R == 6) {
-              if (more) issue_plane(c + 1, R / 3);
-            }
-          }
-          if (s + 2 < nstage) issue_stage_b(s + 2);
-        };
-        int boff = C::RING_OFF + (s % NSTL) * C::BSLOT;
-        asm volatile("" : "+s"(boff));              // per-stage base stays opaque (no early
-        stage_body<TN, WM, P, KZ, KY>(acc, smem + boff + b_lane, pl, dma);   // hoisting)
-      };
-      stage(std::integral_constant<int, 0>{});
-      stage(std::integral_constant<int, 1>{});
-      stage(std::integral_constant<int, 2>{});
-      stage(std::integral_constant<int, 3>{});
-      stage(std::integral_constant<int, 4>{});
-      stage(std::integral_constant<int, 5>{});
-      stage(std::integral_constant<int, 6>{});
-      stage(std::integral_constant<int, 7>{});
-      stage(std::integral_constant<int, 8>{});
-    }
-  };
-  // ZP_PIPE: the stage boundary is one more step of the rolling pipeline.  Stage s's
+  // The stage loop: the stage boundary is one more step of the rolling pipeline.  Stage s's
   // barrier sits between its kx = 0 and kx = +1 taps: before it each wave waits for the
   // weights of stage s + 1 (and every LDS read of stage s); after it the DMA group of stage
   // s goes out (its planes and the weights of stage s + 3 into stage s's weight slot, free
@@ -400,7 +291,10 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
   // boundaries: no wave waits on its first fragment reads after a barrier.  A plane first
   // read by stage t is issued in a DMA group <= t - 3, before the weights of stage t, so the
   // wait at barrier t - 1 covers it; a slot is refilled in group s only when its last reader
-  // is stage s or earlier (the pair schedules above satisfy both).
+  // is stage s or earlier.  Plane issue schedule per chunk c (stage R = 3 (kz+1) + ky+1; slot
+  // reuse checked against each plane's last reader):
+  //   pair 0: R 0 -> (c, 2), (c + 1, 0); R 6 -> (c + 1, 1)
+  //   pair 1: R 0 -> (c + 1, 0); R 3 -> (c + 1, 1); R 6 -> (c + 1, 2)
   auto run_pipe = [&](auto wmc, auto pc) {
     constexpr int WM = decltype(wmc)::value, P = decltype(pc)::value;
     bf16x8 a[NF], b0[TN], b1[TN];
@@ -493,13 +387,8 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
     chunk(g.nchunk - 1, std::false_type{});
   };
   auto by_pair = [&](auto wmc) {
-    if constexpr (ZP_PIPE) {
-      if (pair == 0) run_pipe(wmc, std::integral_constant<int, 0>{});
-      else run_pipe(wmc, std::integral_constant<int, 1>{});
-    } else {
-      if (pair == 0) run(wmc, std::integral_constant<int, 0>{});
-      else run(wmc, std::integral_constant<int, 1>{});
-    }
+    if (pair == 0) run_pipe(wmc, std::integral_constant<int, 0>{});
+    else run_pipe(wmc, std::integral_constant<int, 1>{});
   };
   switch (wm) {                                     // wave-uniform
     case 0: by_pair(std::integral_constant<int, 0>{}); break;

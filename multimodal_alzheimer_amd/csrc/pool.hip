@@ -368,113 +368,6 @@ __global__ __launch_bounds__(256) void bnpool3_fwd_rows_kernel(
   }
 }
 
-// k = 3, stride 2, pad 1, bf16, 8 channels per thread: a thread walks a run of outputs along
-// x and keeps the window column it shares with the previous output (x = 2 ow - 1) in
-// registers, so each output loads 18 input vectors instead of 27; the next output's 18 loads
-// are issued before the current output's compare chain.  Same keys (value << 16 | 31 -
-// window index), clamped duplicates at the borders (identical keys) and outputs as
-// bnpool3_fwd_one_bf16: the results are bit-identical to bnpool3_fwd_rows_kernel's.
-// Block: 2^cv_shift channel vectors x 2 runs (the two halves of the output row) x
-// 256 / 2^(cv_shift+1) output rows; blockIdx.y = n * do + od.
-__global__ __launch_bounds__(256) void bnpool3s2_fwd_run_kernel(
-    PoolG g, int cv_shift, int run, const u16* __restrict__ y, const float* __restrict__ scale,
-    const float* __restrict__ shift, u16* __restrict__ out, uint8_t* __restrict__ am,
-    u16* __restrict__ ymax) {
-  const int cmask = (1 << cv_shift) - 1;
-  const int c0 = (threadIdx.x & cmask) * 8;
-  const int half = (threadIdx.x >> cv_shift) & 1;
-  const int oh = blockIdx.x * (256 >> (cv_shift + 1)) + (threadIdx.x >> (cv_shift + 1));
-  const int od = blockIdx.y % g.do_;
-  const int64_t nb = blockIdx.y / g.do_;
-  const int ow0 = half * run, ow1 = min(ow0 + run, g.wo);
-  if (oh >= g.ho || ow0 >= ow1) return;
-  f32x2 sc2[4], sh2[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    sc2[p] = (f32x2){scale[c0 + 2 * p], scale[c0 + 2 * p + 1]};
-    sh2[p] = (f32x2){shift[c0 + 2 * p], shift[c0 + 2 * p + 1]};
-  }
-  // window rows j = kd * 3 + ky (clamped to the volume; a clamped row repeats its edge row
-  // with that row's own tag, as bnpool3_fwd_one_bf16 does)
-  const int z0 = od * 2 - 1, y0 = oh * 2 - 1;
-  const u16* rowp[9];
-  uint32_t rtag[9];
-#pragma unroll
-  for (int j = 0; j < 9; ++j) {
-    const int zc = min(max(z0 + j / 3, 0), g.di - 1), yc = min(max(y0 + j % 3, 0), g.hi - 1);
-    rowp[j] = y + (((nb * g.di + zc) * g.hi + yc) * (int64_t)g.wi) * g.c + c0;
-    rtag[j] = 31 - ((zc - z0) * 9 + (yc - y0) * 3);
-  }
-  auto ld = [&](u32x4 (&col)[9], int x) {
-#pragma unroll
-    for (int j = 0; j < 9; ++j)
-      col[j] = *reinterpret_cast<const u32x4*>(rowp[j] + (int64_t)x * g.c);
-  };
-  const int xmax = g.wi - 1;
-  u32x4 cp[9], c1[9], c2[9];
-  int xp = max(2 * ow0 - 1, 0);                     // column kx = 0 of window ow0 (clamped)
-  ld(cp, xp);
-  ld(c1, min(2 * ow0, xmax));
-  ld(c2, min(2 * ow0 + 1, xmax));
-  for (int ow = ow0; ow < ow1; ++ow) {
-    const int x0 = 2 * ow - 1;
-    const int xa = max(x0, 0), xb = min(x0 + 1, xmax), xc = min(x0 + 2, xmax);
-    u32x4 n1[9], n2[9];
-    if (ow + 1 < ow1) {
-      ld(n1, min(2 * ow + 2, xmax));
-      ld(n2, min(2 * ow + 3, xmax));
-    }
-    uint32_t key[8], rb[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { key[e] = 0; rb[e] = 0; }
-    auto take = [&](const u32x4 (&col)[9], uint32_t kxt) {
-#pragma unroll
-      for (int j = 0; j < 9; ++j) {
-        const uint32_t tag = rtag[j] - kxt;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const uint32_t word = col[j][p];
-          const f32x2 a = {__uint_as_float(word << 16), __uint_as_float(word & 0xffff0000u)};
-          const f32x2 s = __builtin_elementwise_fma(a, sc2[p], sh2[p]);
-          const s16x2 v = __builtin_elementwise_max(
-              __builtin_bit_cast(s16x2, __builtin_convertvector(s, bf16x2)), (s16x2){0, 0});
-          const uint32_t pk = __builtin_bit_cast(uint32_t, v);
-          const uint32_t k0 = (pk << 16) | tag, k1 = (pk & 0xffff0000u) | tag;
-          if (k0 > key[2 * p]) { key[2 * p] = k0; rb[2 * p] = word; }
-          if (k1 > key[2 * p + 1]) { key[2 * p + 1] = k1; rb[2 * p + 1] = word; }
-        }
-      }
-    };
-    // the window-relative x of each column (clamped columns keep their own position)
-    take(cp, (uint32_t)(xa - x0));
-    take(c1, (uint32_t)(xb - x0));
-    take(c2, (uint32_t)(xc - x0));
-    const int64_t ovox = ((nb * g.do_ + od) * g.ho + oh) * g.wo + ow;
-    u32x4 o, r;
-    uint64_t packed = 0;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      o[p] = (key[2 * p] >> 16) | (key[2 * p + 1] & 0xffff0000u);
-      r[p] = (rb[2 * p] & 0xffffu) | (rb[2 * p + 1] & 0xffff0000u);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t vb = key[e] >> 16;
-      const bool pos = vb != 0 && vb <= 0x7f80u;
-      packed |= (uint64_t)((31 - (key[e] & 31)) | (pos ? 0x80 : 0)) << (8 * e);
-    }
-    *reinterpret_cast<u32x4*>(out + ovox * g.c + c0) = o;
-    *reinterpret_cast<u32x4*>(ymax + ovox * g.c + c0) = r;
-    *reinterpret_cast<uint64_t*>(am + ovox * g.c + c0) = packed;
-#pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      cp[j] = c2[j];
-      c1[j] = n1[j];
-      c2[j] = n2[j];
-    }
-  }
-}
-
 // k = 3, stride 2, pad 1 form of bnpool_bwd_apply_kernel, one thread per 2x2x2 input cell
 // {2a, 2a+1}^3: input 2a lies only in window a, input 2a+1 in windows a and a+1, so the
 // cell's 8 inputs share the 8 windows {a, a+1}^3, loaded once (not ~3.4x per input).  All
@@ -871,10 +764,10 @@ bool rows_on() {
 }
 
 // MMAD_POOL_RUN: 2 (default) the z-walking bnpool3s2_fwd_zwalk_kernel for the stem pool (k 3,
-// s 2, p 1, bf16), 1 the column-carrying bnpool3s2_fwd_run_kernel, 0 the per-output rows
-// kernel; mmad_set_kernel_variant("pool_run", v).  Measured r03e at config 2: run kernel
-// 124.5 us against the rows kernel's 110.8 (r03a) -- its 2 waves per SIMD do not keep enough
-// loads in flight; kept for A/B.
+// s 2, p 1, bf16), any other value the per-output rows kernel; mmad_set_kernel_variant(
+// "pool_run", v).  (A column-carrying form -- each thread walking a run of outputs along x --
+// measured 124.5 us against the rows kernel's 110.8 at config 2, r03e: its 2 waves per SIMD
+// did not keep enough loads in flight; removed.)
 std::atomic<int> g_pool_run{-1};
 int pool_run_mode() {
   int v = g_pool_run.load(std::memory_order_relaxed);
@@ -940,15 +833,6 @@ int bnpool_fwd(const PoolG& g, const void* y, const float* scale, const float* s
                          dim3((unsigned)cdiv(g.do_, ods), (unsigned)g.ho, (unsigned)g.n),
                          dim3(256), 0, st, g, ilog2(cv), ods, (const u16*)y, scale, shift,
                          (u16*)out, am, (u16*)ymax);
-      return launch_status();
-    }
-    if (g.c % VEC == 0 && g.k == 3 && g.s == 2 && g.p == 1 && is_pow2(cv) && cv <= 64 &&
-        pool_run_mode() == 1 && (int64_t)g.n * g.do_ < 65536 && g.wo >= 2) {
-      const int cvs = ilog2(cv), rows = 256 >> (cvs + 1);
-      hipLaunchKernelGGL(bnpool3s2_fwd_run_kernel,
-                         dim3((unsigned)cdiv(g.ho, rows), (unsigned)(g.n * g.do_)), dim3(256), 0,
-                         st, g, cvs, (g.wo + 1) / 2, (const u16*)y, scale, shift, (u16*)out, am,
-                         (u16*)ymax);
       return launch_status();
     }
   }
