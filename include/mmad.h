@@ -55,13 +55,13 @@ int mmad_abi_version(void);                 /* == MMAD_ABI_VERSION */
 const char* mmad_strerror(int status);
 /* Kernel-variant switch (the run-time twin of the MMAD_* environment A/B switches; no
  * reference counterpart): "lattice_zp" = 1 plane-pair residue-class conv (default), 0 the
- * one-plane form, 2 plane-pair at any size; "lattice" / "lattice8" = 1 residue-class convs
- * where their tiles fill the CUs (default), 2 at any size, 0 off; "pool_run" = the stem
- * BN+ReLU+max-pool forward: 2 the z-walking kernel (default), 1 the column-carrying kernel,
- * 0 the per-output rows kernel; "patchz" = 1 the
- * persistent z-walking layer1 conv where its work items fill the CUs (default), 2 at any
- * size, 0 the per-box patch conv; "patchz_bs" = 1 its weight-stationary form, 0 (default)
- * the weight-streaming form.  value < 0 only queries.
+ * one-plane form, 2 plane-pair at any size; "lattice" / "lattice8" / "lattice5" = 1
+ * residue-class convs where their tiles fill the CUs (default), 2 at any size, 0 off;
+ * "pool_run" = the stem BN+ReLU+max-pool forward: 2 the z-walking kernel (default), other
+ * values the per-output rows kernel; "patchz" = 1 the persistent z-walking layer1 conv where
+ * its work items fill the CUs (default), 2 at any size, 0 the per-box patch conv;
+ * "pw_wg3_dedup" = 1 the stride-2 3^3 weight gradient on 16-wide rows with de-duplicated
+ * input columns (default), 0 its three-image form.  value < 0 only queries.
  * Returns the previous value, -1 for an unknown name.  Not thread-safe against concurrent
  * launches. */
 int mmad_set_kernel_variant(const char* name, int value);

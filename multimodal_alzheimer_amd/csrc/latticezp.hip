@@ -39,6 +39,7 @@
 
 #include "common.h"
 #include "patchconv.h"
+#include "pointwise.h"
 
 namespace {
 
@@ -554,5 +555,6 @@ extern "C" int mmad_set_kernel_variant(const char* name, int value) {
   if (std::strcmp(name, "lattice5") == 0) return mmad_lattice5::set_mode(value);
   if (std::strcmp(name, "pool_run") == 0) return mmad_pool::set_run_mode(value);
   if (std::strcmp(name, "patchz") == 0) return mmad_patchz::set_mode(value);
+  if (std::strcmp(name, "pw_wg3_dedup") == 0) return mmad_pw::set_wg3_dedup(value);
   return -1;
 }

@@ -27,4 +27,7 @@ int fwd(const mmad_conv_desc* d, const void* x, const void* wp, const float* bia
 bool wgrad_ok(const mmad_conv_desc* d, int dtype);
 int64_t wgrad_splits(const mmad_conv_desc* d);
 int wgrad(const mmad_conv_desc* d, const void* x, const void* dy, float* ws, void* stream);
+// the de-duplicated X rows of the 16-wide stride-2 3^3 weight gradient: 1 on (default), 0 off
+// (mmad_set_kernel_variant("pw_wg3_dedup", v)); returns the previous setting
+int set_wg3_dedup(int v);
 }  // namespace mmad_pw

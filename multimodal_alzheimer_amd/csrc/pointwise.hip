@@ -18,6 +18,7 @@
 // W[co][ci] with the forward-packed weights [co][ci] as the B rows, N tiles of 256 columns
 // in blockIdx.y, and the BN partial sums of the fp32 accumulators written per 128-row tile
 // (the implicit GEMM ran this K = 128 / 256 GEMM latency-bound: 31.4 / 17.6 us).
+#include <atomic>
 #include <cstdlib>
 
 #include "common.h"
@@ -284,13 +285,20 @@ struct WGC {
   static constexpr int XQ = XIMG / 1024;              // DMA instructions per X image
 };
 
-// MODE 0: stride 1, X row = m; 1: stride 2 1^3, X row = s2_src(m); 2: stride 2 3^3 (NTAP 3)
+// MODE 0: stride 1, X row = m; 1: stride 2 1^3, X row = s2_src(m); 2: stride 2 3^3 (NTAP 3);
+// 4: MODE 2 on 16-wide output rows (layer2.0.conv1 at 128^3) with de-duplicated X rows: a
+// stage is exactly two output rows, and the kx = 0 and kx = 2 taps read the same odd input
+// columns shifted by one (x = 2 ox - 1 and 2 ox + 1), so the stage's X image holds the even
+// columns once (32 rows, kx = 1) and the 17 odd columns x = -1, 1, .., 31 of each of the two
+// rows once (34 rows, read by kx = 0 at row 17 r + ox and by kx = 2 at row 17 r + ox + 1):
+// 66 gathered rows instead of 96.  Same voxel pairs in the same K order: dW bit-identical
 template <int CIT, int MODE, int NTAP = 1>
 __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, float* __restrict__ out, int Ci,
     int Co, int kper, int ntiles, PwS2 s2, uint32_t xbytes, uint32_t ybytes, int mrows) {
   using C = WGC<CIT, NTAP>;
-  static_assert(MODE != 2 || NTAP == 3, "the 3^3 form takes the three kx taps");
+  static_assert((MODE != 2 && MODE != 4) || NTAP == 3, "the 3^3 forms take the three kx taps");
+  static_assert(MODE != 4 || (CIT == 64 && C::XQ == 4), "MODE 4: 128-byte X rows");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -301,7 +309,8 @@ __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
   const int tile = lin % ntiles, split = lin / ntiles;
   const int nci = Ci / CIT, nco = Co / 128;
   const int ci0 = (tile % nci) * CIT, co0 = ((tile / nci) % nco) * 128;
-  const int kzy = MODE == 2 ? tile / (nci * nco) : 0;          // (kz, ky) of the 3^3 form
+  constexpr bool T3 = MODE == 2 || MODE == 4;                  // the 3^3 forms
+  const int kzy = T3 ? tile / (nci * nco) : 0;                 // (kz, ky) of the 3^3 form
   const int kz = kzy / 3, ky = kzy % 3;
   const int64_t m0 = (int64_t)split * kper;
   const int nstage = (int)(min((int64_t)kper, (int64_t)mrows - m0) / WG_KS);   // last: ragged
@@ -313,6 +322,18 @@ __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
   // dY / stride-1 X by a constant, the strided X rows as a mixed-radix (x, y, z, n) add of
   // the 32-voxel step with at most one carry per digit (no divisions in the loop)
   constexpr uint32_t OOB = 0x80000000u;
+  // MODE 4 (xbytes <= 2^30): a lane without a column carries OOB_L, a stage row outside the
+  // volume gets OOB_S as its scalar part; every sum stays below 2^32 and every sum with
+  // either part is past the buffer
+  constexpr uint32_t OOB_L = 0x80000000u, OOB_S = 0x40000000u;
+  // MODE 4: the stage's first output row (wave-uniform), advanced two rows a stage
+  int soy = 0, soz = 0, son = 0;
+  if constexpr (MODE == 4) {
+    const int64_t t1 = m0 / s2.Wo;
+    soy = (int)(t1 % s2.Ho);
+    soz = (int)((t1 / s2.Ho) % s2.Do);
+    son = (int)(t1 / s2.Ho / s2.Do);
+  }
   const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
       (void*)dy, 0, (int)__builtin_amdgcn_readfirstlane((int)ybytes), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
@@ -323,12 +344,38 @@ __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
   const int stz = MODE ? st2 % s2.Do : 0, stn = MODE ? st2 / s2.Do : 0;
   uint32_t off[C::WI], lofs[C::WI], cix[C::WI];
   int ox[C::WI], oy[C::WI], oz[C::WI], on[C::WI], tapx[C::WI];
+  int ixc[C::WI];                                   // MODE 4: the lane's output row of the stage
   bool isx[C::WI];
 #pragma unroll
   for (int h = 0; h < C::WI; ++h) {
     const int q = wave + 4 * h;
     lofs[h] = (uint32_t)(q * 1024);
+    ixc[h] = -1;
     int row, ch;
+    if (MODE == 4 && q >= 8) {
+      // pieces 8..11: even columns (row k = 16 r + ox -> x = 2 ox); 12..16: odd columns
+      // (row j = 17 r + u, u < 17 -> x = 2 u - 1; rows 34.. of piece 16 unused); 17..19 unused.
+      // The lane keeps its column's byte offset (OOB_L when it has none) and its output row
+      // r of the stage; the stage's (n, z, y) part is a wave-uniform scalar (see issue)
+      const bool even = q < 12;
+      row = even ? 8 * (q - 8) + (lane >> 3) : 8 * (q - 12) + (lane >> 3);
+      ch = (lane & 7) ^ pw_tsw128(row);
+      isx[h] = true;
+      tapx[h] = 0;
+      int ix = -1, r = 0;
+      if (even) {
+        r = row >> 4;
+        ix = 2 * (row & 15);
+      } else if (q < 17 && row < 34) {
+        r = row / 17;
+        ix = 2 * (row % 17) - 1;                    // -1: the padding column
+      }
+      ixc[h] = r;
+      off[h] = (unsigned)ix < (unsigned)s2.Wi ? (uint32_t)(ix * Ci + ci0 + ch * 8) * 2u : OOB_L;
+      cix[h] = 0;
+      ox[h] = oy[h] = oz[h] = on[h] = 0;
+      continue;
+    }
     if (q < 8) {
       row = 4 * q + (lane >> 4);
       ch = (lane & 15) ^ pw_tsw256(row);
@@ -355,6 +402,23 @@ __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
   const uint32_t smem_l = lds_addr_of(smem);
   auto issue = [&](int s) {
     const uint32_t slot = smem_l + (uint32_t)((s % C::NS) * C::SLOT);
+    // MODE 4: the stage's two output rows' input-row byte offsets (or OOB_S), scalar
+    uint32_t srow0 = 0, srow1 = 0;
+    if constexpr (MODE == 4) {
+      const int iz = 2 * soz + kz - 1, iy0 = 2 * soy + ky - 1;
+      const bool vz = (unsigned)iz < (unsigned)s2.Di;
+      const int base = ((son * s2.Di + iz) * s2.Hi + iy0) * s2.Wi * Ci * 2;
+      srow0 = vz && (unsigned)iy0 < (unsigned)s2.Hi ? (uint32_t)base : OOB_S;
+      srow1 = vz && (unsigned)(iy0 + 2) < (unsigned)s2.Hi
+                  ? (uint32_t)(base + 2 * s2.Wi * Ci * 2) : OOB_S;
+      soy += 2;                                      // two output rows a stage (Wo = 16)
+      const int cy = soy >= s2.Ho;
+      soy -= cy ? s2.Ho : 0;
+      soz += cy;
+      const int cz = soz >= s2.Do;
+      soz -= cz ? s2.Do : 0;
+      son += cz;
+    }
 #pragma unroll
     for (int h = 0; h < C::WI; ++h) {
       if (!isx[h]) {
@@ -363,6 +427,10 @@ __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
       } else if (MODE == 0) {
         buf_lds16_asm(off[h], rsx, slot + lofs[h]);
         off[h] += xstep;
+      } else if (MODE == 4) {
+        uint32_t vo = off[h] + (ixc[h] ? srow1 : srow0);
+        asm volatile("" : "+v"(vo));                // (a lane offset: keep it in a VGPR)
+        buf_lds16_asm(vo, rsx, __builtin_amdgcn_readfirstlane(slot + lofs[h]));
       } else {
         const int dz = MODE == 2 ? kz - 1 : 0, dyy = MODE == 2 ? ky - 1 : 0;
         const int dx = MODE == 2 ? tapx[h] - 1 : 0;
@@ -404,6 +472,24 @@ __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
     xb_lo[j] = (uint32_t)(C::YIMG + rlo * C::XROW + (((col >> 3) ^ slo) << 4) + (col & 7) * 2);
     xb_hi[j] = (uint32_t)(C::YIMG + rhi * C::XROW + (((col >> 3) ^ shi) << 4) + (col & 7) * 2);
   }
+  // MODE 4: per tap, the X rows of this lane's K rows rlo / rhi (k = 16 r + ox): kx = 1 the
+  // even image's row k, kx = 0 / 2 the odd image's row 17 r + ox / + 1
+  uint32_t xm_lo[3][C::TJ], xm_hi[3][C::TJ];
+  if constexpr (MODE == 4) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int j = 0; j < C::TJ; ++j) {
+        const int col = wn * (CIT / 2) + j * 16 + 4 * p4;
+        auto at = [&](int k) {
+          const int r = t == 1 ? k : 17 * (k >> 4) + (k & 15) + (t == 2 ? 1 : 0);
+          const int img = C::YIMG + (t == 1 ? 0 : C::XIMG);
+          return (uint32_t)(img + r * C::XROW + (((col >> 3) ^ pw_tsw128(r)) << 4) + (col & 7) * 2);
+        };
+        xm_lo[t][j] = at(rlo);
+        xm_hi[t][j] = at(rhi);
+      }
+  }
   auto tr8 = [](const char* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_AS bf16x4*)p);
   };
@@ -439,9 +525,15 @@ __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
     for (int t = 0; t < NTAP; ++t) {
       bf16x8 b[C::TJ];
 #pragma unroll
-      for (int j = 0; j < C::TJ; ++j)
-        b[j] = __builtin_shufflevector(tr8(slot + t * C::XIMG + xb_lo[j]),
-                                       tr8(slot + t * C::XIMG + xb_hi[j]), 0, 1, 2, 3, 4, 5, 6, 7);
+      for (int j = 0; j < C::TJ; ++j) {
+        if constexpr (MODE == 4)
+          b[j] = __builtin_shufflevector(tr8(slot + xm_lo[t][j]), tr8(slot + xm_hi[t][j]), 0, 1,
+                                         2, 3, 4, 5, 6, 7);
+        else
+          b[j] = __builtin_shufflevector(tr8(slot + t * C::XIMG + xb_lo[j]),
+                                         tr8(slot + t * C::XIMG + xb_hi[j]), 0, 1, 2, 3, 4, 5, 6,
+                                         7);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -452,7 +544,7 @@ __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
 
   // acc[t][i][j][r]: co = wm*64 + i*16 + 4 lk + r, ci = wn*CIT/2 + j*16 + (lane & 15);
   // slab column tap * Ci + ci (taps = 27 for the 3^3 form, tap = (kz*3 + ky)*3 + kx)
-  const int K = MODE == 2 ? 27 * Ci : Ci;
+  const int K = T3 ? 27 * Ci : Ci;
   float* o = out + (int64_t)split * Co * K;
   const int lr = lane & 15;
 #pragma unroll
@@ -465,9 +557,23 @@ __global__ __launch_bounds__(WG_NTHR, 1) void pw_wgrad_kernel(
         for (int r = 0; r < 4; ++r) {
           const int co = co0 + wm * 64 + i * 16 + 4 * lk + r;
           const int ci = ci0 + wn * (CIT / 2) + j * 16 + lr;
-          const int col = MODE == 2 ? (kzy * 3 + t) * Ci + ci : ci;
+          const int col = T3 ? (kzy * 3 + t) * Ci + ci : ci;
           o[(int64_t)co * K + col] = acc[t][i][j][r];
         }
+}
+
+// MMAD_PW_WG3_DEDUP=0 keeps the three gathered X images per stage for 16-wide rows (A/B);
+// mmad_set_kernel_variant("pw_wg3_dedup", v) overrides it at run time
+std::atomic<int> g_wg3_dedup{-1};
+bool wg3_dedup() {
+  int v = g_wg3_dedup.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("MMAD_PW_WG3_DEDUP");
+    int expect = -1;
+    g_wg3_dedup.compare_exchange_strong(expect, e == nullptr || atoi(e) != 0 ? 1 : 0);
+    v = g_wg3_dedup.load(std::memory_order_relaxed);
+  }
+  return v != 0;
 }
 
 bool pw_wgrad_on() {
@@ -579,6 +685,12 @@ int64_t wg_tiles(const mmad_conv_desc* d) {
 }
 }  // namespace
 
+int set_wg3_dedup(int v) {
+  const int prev = wg3_dedup() ? 1 : 0;
+  if (v >= 0) g_wg3_dedup.store(v ? 1 : 0, std::memory_order_relaxed);
+  return prev;
+}
+
 bool wgrad_ok(const mmad_conv_desc* d, int dtype) {
   if (!pw_on() || !pw_wgrad_on() || dtype != MMAD_BF16) return false;
   const bool one = d->kd == 1 && d->kh == 1 && d->kw == 1 && !d->pd && !d->ph && !d->pw &&
@@ -624,7 +736,13 @@ int wgrad(const mmad_conv_desc* d, const void* x, const void* dy, float* ws, voi
                        q, (uint32_t)(mi * d->ci * 2), (uint32_t)(m * d->co * 2), (int)m);
     return launch_status();
   };
-  if (wg3_geom(d)) return go(pw_wgrad_kernel<64, 2, 3>, WGC<64, 3>::LDS);
+  if (wg3_geom(d)) {
+    // 16-wide output rows (and an even row count): every 32-voxel stage is two whole rows
+    if (d->wo == 16 && d->ho % 2 == 0 && kper % 32 == 0 && mi * d->ci * 2 <= (int64_t(1) << 30) &&
+        wg3_dedup())
+      return go(pw_wgrad_kernel<64, 4, 3>, WGC<64, 3>::LDS);
+    return go(pw_wgrad_kernel<64, 2, 3>, WGC<64, 3>::LDS);
+  }
   const bool s2 = s2_geom(d);
   if (wg_cit(d) == 128)
     return s2 ? go(pw_wgrad_kernel<128, 1>, WGC<128>::LDS) : go(pw_wgrad_kernel<128, 0>, WGC<128>::LDS);

@@ -105,8 +105,8 @@ def test_pointwise_wgrad_vs_float64(xs, co, s):
 
 
 @pytest.mark.parametrize("xs,co", [((2, 64, 32, 32, 32), 128), ((2, 64, 15, 16, 16), 128),
-                                   ((1, 128, 16, 16, 16), 256)],
-                         ids=["layer2_conv1", "odd_depth", "wide_ci"])
+                                   ((1, 128, 16, 16, 16), 256), ((3, 64, 10, 32, 31), 128)],
+                         ids=["layer2_conv1", "odd_depth", "wide_ci", "rows16_ragged"])
 def test_stride2_3cube_wgrad_vs_float64(xs, co):
     """the stride-2 3^3 weight gradient (pw_wgrad_kernel's 3-tap form + transposing slab
     reduction; layer2.0.conv1) against torch's float64 weight gradient of the same bf16
@@ -144,3 +144,23 @@ def test_deferred_stem_reduce_bit_identical():
         grads.append(conv.weight.grad.clone())
     assert torch.equal(grads[0], grads[1])
 
+
+
+@pytest.mark.parametrize("xs,co", [((2, 64, 32, 32, 32), 128), ((3, 64, 10, 32, 31), 128),
+                                   ((1, 64, 6, 4, 32), 128), ((1, 64, 9, 31, 32), 128)],
+                         ids=["layer2_conv1", "rows16_ragged", "two_rows", "odd_height"])
+def test_stride2_3cube_wgrad_dedup_bit_identical(xs, co):
+    """16-wide output rows: the de-duplicated X-row form of the stride-2 3^3 weight gradient
+    (pw_wgrad_kernel MODE 4: the even input columns and the 17 odd ones of each output row
+    staged once, read by kx = 1 and by kx = 0 / 2 at a one-row offset) gives exactly the
+    three-image form's dW (MODE 2): the same voxel pairs summed in the same order."""
+    lib = _lib.load()
+    x, w = _operands(xs, (co, xs[1], 3, 3, 3), 13)
+    prev = lib.mmad_set_kernel_variant(b"pw_wg3_dedup", 0)
+    try:
+        ref, gy, _ = _wgrad(x, w, 2, 1, 1)
+        lib.mmad_set_kernel_variant(b"pw_wg3_dedup", 1)
+        got, _, _ = _wgrad(x, w, 2, 1, 1, gy)
+    finally:
+        lib.mmad_set_kernel_variant(b"pw_wg3_dedup", prev)
+    assert torch.equal(got, ref), f"max |diff| {(got - ref).abs().max().item():.3e}"
