@@ -153,8 +153,10 @@ __global__ __launch_bounds__(NTHR) void patchz_conv_kernel(PZ g, const u16* __re
   // ---- weight DMA: tap t's 64 x 64 slice, wave w rows 8w .. 8w + 7 (one instruction)
   const int lrow = lane >> 3;
   const u16* wrow = wgt + (int64_t)(n0 + wave * 8 + lrow) * g.Kpad + (((lane & 7) ^ lrow) * 8);
-  auto issue_w = [&](int gt) __attribute__((always_inline)) {                  // global tap counter -> slot gt % NST
-    glds16_asm(wrow + (gt % TAPS) * 64,
+  // global tap counter gt -> slot gt % NST; wt = gt % TAPS, a compile-time constant at every
+  // call (a run-time modulo by 27 per tap was ~20 scalar instructions in the tap loop)
+  auto issue_w = [&](int gt, int wt) __attribute__((always_inline)) {
+    glds16_asm(wrow + wt * 64,
                lds_addr_of(smem + RING_OFF + (gt & (NST - 1)) * WSLOT + wave * 1024));
   };
 
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(NTHR) void patchz_conv_kernel(PZ g, const u16* __re
   // ---- prologue: the first box's six planes, weights of taps 0..3
   for (int q = 0; q < 6; ++q) issue_plane(q);
 #pragma unroll
-  for (int t = 0; t < NST; ++t) issue_w(t);
+  for (int t = 0; t < NST; ++t) issue_w(t, t);
   wait_vm_lgkm0<NST - 1>();
   raw_barrier();
   read_frags(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0, 0, fa0, fb0);
@@ -355,7 +357,7 @@ __global__ __launch_bounds__(NTHR) void patchz_conv_kernel(PZ g, const u16* __re
         } else if constexpr (NEXT && T == 18) {
           issue_plane(q0 + 9);
         }
-        if constexpr (!(LAST && T + 4 >= TAPS)) issue_w(gt + 4);
+        if constexpr (!(LAST && T + 4 >= TAPS)) issue_w(gt + 4, (T + 4) % TAPS);
         if constexpr (T + 1 < TAPS)
           read_frags(std::integral_constant<int, T + 1>{}, std::integral_constant<int, 0>{}, q0,
                      gt + 1, fa0, fb0);
