@@ -481,6 +481,10 @@ struct LWG {
   uint32_t xbytes, ybytes;                  // operand sizes (buffer-resource ranges)
 };
 
+// DD = the dilation (4 or 8), a template constant: the sub-group / class digit arithmetic of
+// every plane's DMA bases then divides by constants (run-time divisions by d, d^2 and d^3 / 32
+// were ~35 scalar instructions each, several per plane)
+template <int DD>
 __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* __restrict__ src,
                                                              const u16* __restrict__ dy,
                                                              float* __restrict__ ws) {
@@ -496,7 +500,7 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
   const int t2 = tile / nco;
   const int cit = t2 % nci, split = t2 / nci;
   const int co0 = cot * 64, ci0 = cit * KC;
-  const int d = g.d, E = S * d;
+  constexpr int d = DD, E = S * d;
   const int gpn = d * d * d / NS;
   const int g0 = split * g.groups_per_split;
   const int nplane_out = g.groups_per_split * S;    // output planes of this block
@@ -859,9 +863,11 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
           void* stream) {
   if (mmad_lattice5::wgrad_ok(q)) return mmad_lattice5::wgrad(q, x, dy, ws, splits, stream);
   if (!wgrad_ok(q)) return MMAD_EUNSUPPORTED;
-  static const bool attr = hipFuncSetAttribute((const void*)lattice_wgrad_kernel,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               WLDS) == hipSuccess;
+  static const bool attr =
+      hipFuncSetAttribute((const void*)lattice_wgrad_kernel<4>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, WLDS) == hipSuccess &&
+      hipFuncSetAttribute((const void*)lattice_wgrad_kernel<8>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, WLDS) == hipSuccess;
   if (!attr) return MMAD_EUNSUPPORTED;
   const int sp = wgrad_splits(q);
   LWG g{};
@@ -871,8 +877,12 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
   g.xbytes = (uint32_t)(vox * q.Cs * 2);
   g.ybytes = (uint32_t)(vox * q.Nd * 2);
   const int64_t nblk = (int64_t)(q.Cs / KC) * (q.Nd / 64) * sp;
-  hipLaunchKernelGGL(lattice_wgrad_kernel, dim3((unsigned)nblk), dim3(NTHR), WLDS,
-                     as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  if (q.dd == 4)
+    hipLaunchKernelGGL(lattice_wgrad_kernel<4>, dim3((unsigned)nblk), dim3(NTHR), WLDS,
+                       as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  else
+    hipLaunchKernelGGL(lattice_wgrad_kernel<8>, dim3((unsigned)nblk), dim3(NTHR), WLDS,
+                       as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
   *splits = sp;
   return launch_status();
 }

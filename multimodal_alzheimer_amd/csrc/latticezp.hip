@@ -253,10 +253,11 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
     wq_off[h] = tk * C::BTAP + rb * 1024;
   }
   const int nstage = g.nchunk * 9;
-  auto issue_stage_b = [&](int s) {
-    const int c = s / 9, r = s % 9;
+  // (stage s = 9 c + r; the callers pass c and r, known up to c at compile time, so the
+  // stage loop has no run-time division by 9; slot = s % NSTL)
+  auto issue_stage_b = [&](int c, int r, int slot) {
     const u16* base = wgt + (r * 3) * g.Cs + c * KC;   // taps (kz,ky) row: t0 = 3 r
-    char* sb = ring + (s % NSTL) * C::BSLOT;
+    char* sb = ring + slot * C::BSLOT;
 #pragma unroll
     for (int h = 0; h < C::WI; ++h) {
       uint32_t o = wofs[h];
@@ -281,7 +282,7 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
   issue_plane(0, 0);
   issue_plane(0, 1);
   if (pair == 1) issue_plane(0, 2);
-  for (int t = 0; t < NSTL; ++t) issue_stage_b(t);
+  for (int t = 0; t < NSTL; ++t) issue_stage_b(t / 9, t % 9, t % NSTL);
 
   // The stage loop: the stage boundary is one more step of the rolling pipeline.  Stage s's
   // barrier sits between its kx = 0 and kx = +1 taps: before it each wave waits for the
@@ -364,7 +365,10 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
           } else {
             if constexpr ((R == 0 || R == 3 || R == 6) && MORE) issue_plane(c + 1, R / 3);
           }
-          if constexpr (MORE || R + NSTL < 9) issue_stage_b(s + NSTL);
+          if constexpr (MORE || R + NSTL < 9) {
+            constexpr int RN = R + NSTL;             // stage s + NSTL = 9 (c + RN / 9) + RN % 9
+            issue_stage_b(c + RN / 9, RN % 9, ((9 % NSTL) * c + RN) % NSTL);
+          }
         };
         read_b<TN, -1>(bsn, b1);
         [&]<int... F>(std::integer_sequence<int, F...>) {
