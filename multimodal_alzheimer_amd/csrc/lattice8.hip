@@ -160,32 +160,32 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
 
   // ---- patch DMA: plane slot p <- plane tz - 1 + p, chunk cc; 4 instructions per wave of
   // 16 rows x 64 B (row = pos * 8 + class)
+  // (both grids through a per-sample buffer resource: a lane's 32-bit byte offset in the
+  // sample, plus a wave-uniform plane / chunk part per stage -- no 64-bit lane addresses in
+  // the stage loop)
   const int lrow = lane >> 2;
-  int64_t pvox[4];
-  int pch[4];
   int rzk[4];                                       // RAG: class z residue, -huge off-grid
-  uint32_t pofs[4];                                 // RAG: byte offset in this sample
+  uint32_t pofs[4];                                 // byte offset in this sample
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int row = (wave * 4 + k) * 16 + lrow;
     const int pos = row >> 3, c = row & 7;
     const int ty = pos >> 3, tx = pos & 7;
-    pch[k] = (lane & 3) ^ swz8(row);
+    const int pch = (lane & 3) ^ swz8(row);
     if constexpr (RAG) {
       const int y = ((c >> 1) & 1) + 2 * ty, x = (c & 1) + 2 * tx;
-      pofs[k] = (uint32_t)((((c >> 2) * g.H + y) * g.W + x) * g.Cs + pch[k] * 8) * 2u;
+      pofs[k] = (uint32_t)((((c >> 2) * g.H + y) * g.W + x) * g.Cs + pch * 8) * 2u;
       rzk[k] = (y < g.H && x < g.W) ? (c >> 2) : -(1 << 20);
-      pvox[k] = 0;
     } else {
-      pvox[k] = (((int64_t)n * E + (c >> 2)) * E + ((c >> 1) & 1) + 2 * ty) * E + (c & 1) + 2 * tx;
-      pofs[k] = 0;
+      const int v = ((c >> 2) * E + ((c >> 1) & 1) + 2 * ty) * E + (c & 1) + 2 * tx;
+      pofs[k] = (uint32_t)(v * g.Cs + pch * 8) * 2u;
       rzk[k] = 0;
     }
   }
   const int64_t svox = RAG ? (int64_t)g.D * g.H * g.W : (int64_t)E * E * E;
-  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(src + (int64_t)n * svox * g.Cs), 0,
-      RAG ? (int)__builtin_amdgcn_readfirstlane((uint32_t)(svox * g.Cs * 2)) : 0, 0x00020000);
+      (int)__builtin_amdgcn_readfirstlane((uint32_t)(svox * g.Cs * 2)), 0x00020000);
   // input plane tz - 1 + zr (zr = kz + 1) of channel chunk cc into plane slot p
   auto issue_plane_at = [&](int p, int zr, int cc) {
     char* pb = smem + p * PLANE8;
@@ -199,11 +199,13 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
         buf_lds16_asm(ok ? pofs[k] + zoff : OOB, rsx, lds_addr_of(pb + (wave * 4 + k) * 1024));
       }
     } else {
-      const int64_t zoff = (int64_t)2 * (tz - 1 + zr) * E * E;
+      const uint32_t zoff = (uint32_t)(2 * (tz - 1 + zr) * E * E * g.Cs + cc * KC8) * 2u;
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        glds16_asm(src + (pvox[k] + zoff) * g.Cs + cc * KC8 + pch[k] * 8,
-                   lds_addr_of(pb + (wave * 4 + k) * 1024));
+      for (int k = 0; k < 4; ++k) {
+        uint32_t o = pofs[k];
+        asm volatile("" : "+v"(o));                 // (opaque: no hoisted per-stage copies)
+        buf_lds16_asm(o + zoff, rsx, lds_addr_of(pb + (wave * 4 + k) * 1024));
+      }
     }
   };
   // ---- weight DMA, a stage's 9 taps: taps t0 .. t0 + 8 of chunk cc into slot sl; 9 * BW / 16
@@ -211,14 +213,26 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   // bytes, same place); QB 16-row pieces per tap
   constexpr int QB = BW / 16;
   constexpr int NQ9 = 9 * BW / 16, WI9 = (NQ9 + 7) / 8;
+  // (lane byte offsets into the packed weights, fixed; the stage adds (t0 Cs + cc KC8) * 2)
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)wgt, 0, (int)__builtin_amdgcn_readfirstlane((uint32_t)(g.Nd * g.Kpad * 2)),
+      0x00020000);
+  uint32_t wofs9[WI9];
+#pragma unroll
+  for (int h = 0; h < WI9; ++h) {
+    const int q = min(wave + 8 * h, NQ9 - 1);
+    const int row = (q % QB) * 16 + lrow;
+    wofs9[h] = (uint32_t)((n0 + row) * g.Kpad + ((lane & 3) ^ swz8(row)) * 8 + (q / QB) * g.Cs) *
+               2u;
+  }
   auto issue_b9 = [&](int cc, int t0, int sl) {
+    const uint32_t so = (uint32_t)(t0 * g.Cs + cc * KC8) * 2u;
 #pragma unroll
     for (int h = 0; h < WI9; ++h) {
       const int q = min(wave + 8 * h, NQ9 - 1);
-      const int row = (q % QB) * 16 + lrow;
-      const u16* src9 = wgt + (int64_t)(n0 + row) * g.Kpad + ((lane & 3) ^ swz8(row)) * 8 +
-                        (t0 + q / QB) * g.Cs + cc * KC8;
-      glds16_asm(src9, lds_addr_of(ring + sl * BSLOT8 + (q / QB) * BTAP8 + (q % QB) * 1024));
+      uint32_t o = wofs9[h];
+      asm volatile("" : "+v"(o));
+      buf_lds16_asm(o + so, rsw, lds_addr_of(ring + sl * BSLOT8 + (q / QB) * BTAP8 + (q % QB) * 1024));
     }
   };
   const int kz0 = tz == 0 ? 0 : -1, kz1 = tz == NZ - 1 ? 0 : 1;
@@ -434,7 +448,9 @@ bool ok(const mmad_patch::Geo& q) {
   // one 512-thread block per CU: with too few tiles even at 32 channels the row-gather
   // GEMM's more, smaller blocks win
   if (lattice8_mode() == 1 && (int64_t)q.nb * planes8(q) * (q.Nd / 32) < 256) return false;
-  return (int64_t)q.nb * q.Ds * q.Hs * q.Ws * q.Cs < (int64_t(1) << 40);
+  // 32-bit buffer offsets: one sample's input, the packed weights
+  return (int64_t)q.Ds * q.Hs * q.Ws * q.Cs * 2 < (int64_t(1) << 31) &&
+         (int64_t)q.Nd * q.Kpad * 2 < (int64_t(1) << 31);
 }
 
 int64_t tiles(const mmad_patch::Geo& q) { return (int64_t)q.nb * planes8(q); }

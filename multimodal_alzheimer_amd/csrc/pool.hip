@@ -660,8 +660,12 @@ __global__ void gap_bwd_kernel(int n, int64_t S, int C, float inv, const float* 
 struct PlaneMax {
   uint32_t key[8], rb[8];
 };
-__device__ __forceinline__ void plane_max(const PoolG& g, const u16* __restrict__ yp, int y0,
-                                          int x0, int c0, const f32x2* sc2, const f32x2* sh2,
+// (window loads through the sample's buffer resource: the plane's byte offset is a scalar,
+// the thread's 9 in-plane byte offsets `wofs` are fixed for its whole z walk -- no per-load
+// 64-bit address arithmetic in this VALU-bound loop)
+__device__ __forceinline__ void plane_max(const PoolG& g, __amdgpu_buffer_rsrc_t rs,
+                                          uint32_t plane_off, const uint32_t (&wofs)[9], int y0,
+                                          int x0, const f32x2* sc2, const f32x2* sh2,
                                           PlaneMax& m) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) { m.key[e] = 0; m.rb[e] = 0; }
@@ -671,7 +675,8 @@ __device__ __forceinline__ void plane_max(const PoolG& g, const u16* __restrict_
   for (int w = 0; w < 9; ++w) {
     const int yc = min(max(y0 + w / 3, 0), g.hi - 1), xc = min(max(x0 + w % 3, 0), g.wi - 1);
     tag[w] = 31 - 18 - ((yc - y0) * 3 + (xc - x0));     // kd = 2 part; + 9 (2 - kd) later
-    raw[w] = *reinterpret_cast<const u32x4*>(yp + ((int64_t)yc * g.wi + xc) * g.c + c0);
+    raw[w] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rs, wofs[w], __builtin_amdgcn_readfirstlane(plane_off), 0));
   }
 #pragma unroll
   for (int w = 0; w < 9; ++w) {
@@ -721,15 +726,24 @@ __global__ __launch_bounds__(256, POOL_ZW_WAVES) void bnpool3s2_fwd_zwalk_kernel
   }
   const int y0 = 2 * oh - 1, x0 = 2 * ow - 1;
   const int64_t plane = (int64_t)g.hi * g.wi * g.c;
-  const u16* __restrict__ yn = y + nb * g.di * plane;
+  const uint32_t pbytes = (uint32_t)(plane * 2);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(y + nb * g.di * plane), 0, (int)__builtin_amdgcn_readfirstlane(pbytes * g.di),
+      0x00020000);
+  uint32_t wofs[9];
+#pragma unroll
+  for (int w = 0; w < 9; ++w) {
+    const int yc = min(max(y0 + w / 3, 0), g.hi - 1), xc = min(max(x0 + w % 3, 0), g.wi - 1);
+    wofs[w] = (uint32_t)((yc * g.wi + xc) * g.c + c0) * 2u;
+  }
   PlaneMax prev;                                   // plane 2 od - 1 (the previous od's last)
   bool prev_ok = 2 * od0 - 1 >= 0;
-  if (prev_ok) plane_max(g, yn + (2 * od0 - 1) * plane, y0, x0, c0, sc2, sh2, prev);
+  if (prev_ok) plane_max(g, rs, (uint32_t)(2 * od0 - 1) * pbytes, wofs, y0, x0, sc2, sh2, prev);
   for (int od = od0; od < od1; ++od) {
     PlaneMax a, b;
-    plane_max(g, yn + (2 * od) * plane, y0, x0, c0, sc2, sh2, a);
+    plane_max(g, rs, (uint32_t)(2 * od) * pbytes, wofs, y0, x0, sc2, sh2, a);
     const bool b_ok = 2 * od + 1 < g.di;
-    if (b_ok) plane_max(g, yn + (2 * od + 1) * plane, y0, x0, c0, sc2, sh2, b);
+    if (b_ok) plane_max(g, rs, (uint32_t)(2 * od + 1) * pbytes, wofs, y0, x0, sc2, sh2, b);
     PlaneMax best;                                 // kd = 1: always inside the volume
 #pragma unroll
     for (int e = 0; e < 8; ++e) { best.key[e] = a.key[e] + 9; best.rb[e] = a.rb[e]; }
@@ -826,7 +840,8 @@ int bnpool_fwd(const PoolG& g, const void* y, const float* scale, const float* s
   const int cv = g.c / VEC;
   if constexpr (sizeof(T) == 2) {
     if (g.c % VEC == 0 && g.k == 3 && g.s == 2 && g.p == 1 && is_pow2(cv) &&
-        pool_run_mode() == 2 && cv * g.wo <= 256 && g.ho < 65536 && g.n < 65536) {
+        pool_run_mode() == 2 && cv * g.wo <= 256 && g.ho < 65536 && g.n < 65536 &&
+        (int64_t)g.di * g.hi * g.wi * g.c * 2 < (int64_t(1) << 31)) {   // (32-bit offsets)
       // z segments of 4 outputs (one extra plane each): >= 8 blocks per CU at the stem
       const int ods = POOL_ZW_ODS;
       hipLaunchKernelGGL(bnpool3s2_fwd_zwalk_kernel,
