@@ -35,7 +35,7 @@ constexpr int PW_YR = PW_TY + 2;                 // y rows per plane image
 constexpr int PW_XSLOTS = 4;
 constexpr int PW_YROW = 128;                     // dY rows: 64 co x 2 B
 constexpr int PW_YST = 2 * PW_XW * PW_YROW;      // 8 KiB: 2 K steps per stage
-constexpr int PW_YSLOTS = 3;
+constexpr int PW_YSLOTS = 4;                     // (4: the slot of stage s is s & 3, no run-time mod 3)
 constexpr int PW_NTHR = 512;
 constexpr uint32_t PW_OOB = 0x80000000u;
 // LAT = false: the 32-wide volume (layer1); a K step is one 32-voxel row and an image row
