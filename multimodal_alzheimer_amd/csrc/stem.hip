@@ -793,6 +793,9 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const TI* __r
                                                           float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int YIN = (YT - 1) * SH + KH, RSTEP = SD * YIN;
+  // ring planes (geom_for's g.rz = kd + sd) as a compile-time constant: the per-z-step slot
+  // arithmetic (mod RZW) then needs no run-time scalar division
+  constexpr int RZW = KD + SD;
   constexpr int DYB = YT * XW * CO * 2;
   constexpr int NH = (RSTEP + 16 + 7) / 8;          // DMA slots per wave per step
   constexpr uint32_t OOB = 0x80000000u;
@@ -848,25 +851,25 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const TI* __r
   // unfolded into the ring at the end of the current step
   RawV<TI> rv[NH];
   auto raw_commit_step = [&](int ozn) __attribute__((always_inline)) {
-    int sbn = (ozn * SD) % g.rz;
+    int sbn = (ozn * SD) % RZW;
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       const int f = wave + 8 * h;
       if (f < RSTEP) {
         int slot = sbn + KD - SD + f / YIN;
-        slot -= slot >= g.rz ? g.rz : 0;
+        slot -= slot >= RZW ? RZW : 0;
         raw_row_commit<TI>(rv[h], lane, g.wo, smem + (slot * YIN + f % YIN) * ROWB_W);
       }
     }
   };
   auto load_step = [&](int ozn, bool urows = true) __attribute__((always_inline)) {
-    int sbn = (ozn * SD) % g.rz;
+    int sbn = (ozn * SD) % RZW;
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       const int f = wave + 8 * h;
       if (f < RSTEP) {
         int slot = sbn + KD - SD + f / YIN;
-        slot -= slot >= g.rz ? g.rz : 0;
+        slot -= slot >= RZW ? RZW : 0;
         if constexpr (RAW) {
           if (urows) rv[h] = raw_row_load<TI>(rsu, voff[h] + (uint32_t)ozn * ustep);
         } else {
@@ -902,7 +905,7 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const TI* __r
         const int f = wave + 8 * h;
         if (f < KD * YIN)
           raw_row_commit<TI>(pr[h], lane, g.wo,
-                             smem + (((oz0 * SD + f / YIN) % g.rz) * YIN + f % YIN) * ROWB_W);
+                             smem + (((oz0 * SD + f / YIN) % RZW) * YIN + f % YIN) * ROWB_W);
       }
       load_step(oz0, false);                     // (its dY tile; its U rows are in)
     } else {
@@ -912,7 +915,7 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const TI* __r
         const bool ok = (unsigned)zi < (unsigned)g.di && (unsigned)yi < (unsigned)g.hi &&
                         lane < g.tw && x0 + lane < g.wo;
         buf_lds16_asm(ok ? (uint32_t)(((zi * g.hi + yi) * g.wo + x0 + lane) * 16) : OOB, rsu,
-                      ring_l + (uint32_t)((((oz0 * SD + kd) % g.rz) * YIN + f % YIN) * ROWB_W));
+                      ring_l + (uint32_t)((((oz0 * SD + kd) % RZW) * YIN + f % YIN) * ROWB_W));
       }
       load_step(oz0);
     }
@@ -956,13 +959,13 @@ __global__ __launch_bounds__(512) void stem_wgrad2_kernel(StemG g, const TI* __r
     if (oz + 1 < oz1) load_step(oz + 1);          // lands while the MFMAs of oz run
 #endif
 
-    const int sbase = (oz * SD) % g.rz;
+    const int sbase = (oz * SD) % RZW;
     const char* dyt = smem + g.ring_off + (oz & 1) * DYB;
     const char* pl[7];
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
       int slot = sbase + kdj[j];
-      slot -= slot >= g.rz ? g.rz : 0;
+      slot -= slot >= RZW ? RZW : 0;
       pl[j] = smem + slot * YIN * ROWB_W + rowj[j];
     }
     auto rd = [&](const char* a) __attribute__((always_inline)) {
