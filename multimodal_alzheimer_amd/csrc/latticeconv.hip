@@ -543,7 +543,7 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
   }
   auto issue_x = [&](int e) {
     const int gi = g0 + e / S, pz = e % S;
-    const uint32_t slot = lds0 + (uint32_t)((e % WXSLOTS) * WPLANE);
+    const uint32_t slot = lds0 + (uint32_t)(((unsigned)e % WXSLOTS) * WPLANE);
     const uint32_t zb = (uint32_t)(grp_vox(gi, pz, 0, 0) * g.Cs * 2);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -677,10 +677,10 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
       const bool xnow = o + 2 < nplane_out;         // X plane o + 2 issued at stage 0
       const int64_t y_here = plane_y0(o);
       const int64_t y_next = o + 1 < nplane_out ? plane_y0(o + 1) : y_here;
-      const int sl0 = (o * 8) % WYSLOTS;
+      const int sl0 = (int)((unsigned)(o * 8) % WYSLOTS);   // (unsigned: no signed fixup)
       auto stage = [&](auto mc) {
         constexpr int M = decltype(mc)::value;
-        const int sl = (sl0 + M) % WYSLOTS;
+        const int sl = (int)((unsigned)(sl0 + M) % WYSLOTS);
         // dY of this stage landed (issued two stages ago); younger: the next stage's dY and,
         // at stages 1 and 2, the X plane issued at stage 0 right after stage 2's dY
         const bool last = o + 1 == nplane_out && M == 7;
@@ -688,8 +688,8 @@ __global__ __launch_bounds__(NTHR) void lattice_wgrad_kernel(LWG g, const u16* _
         else if (last) wait_vm_lgkm0<0>();
         else wait_vm_lgkm0<1>();
         raw_barrier();
-        if (M < 6) issue_y_at(y_here, M + 2, (sl + 2) % WYSLOTS);
-        else if (o + 1 < nplane_out) issue_y_at(y_next, M - 6, (sl + 2) % WYSLOTS);
+        if (M < 6) issue_y_at(y_here, M + 2, (int)((unsigned)(sl + 2) % WYSLOTS));
+        else if (o + 1 < nplane_out) issue_y_at(y_next, M - 6, (int)((unsigned)(sl + 2) % WYSLOTS));
         if (M == 0 && xnow) issue_x(o + 2);
         // (opaque, defined after the barrier, so the fragment addresses of later stages are
         // not computed early and held in VGPRs)

@@ -325,8 +325,8 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
         constexpr int KZ = R / 3 - 1, KY = R % 3 - 1;
         constexpr int KZN = R < 8 ? (R + 1) / 3 - 1 : -1, KYN = R < 8 ? (R + 1) % 3 - 1 : -1;
         const int s = 9 * c + R;
-        int boff = C::RING_OFF + (s % NSTL) * C::BSLOT;
-        int bnof = C::RING_OFF + ((s + 1) % NSTL) * C::BSLOT;
+        int boff = C::RING_OFF + (int)((unsigned)s % NSTL) * C::BSLOT;   // (s >= 0: no
+        int bnof = C::RING_OFF + (int)((unsigned)(s + 1) % NSTL) * C::BSLOT;  // signed fixup)
         asm volatile("" : "+s"(boff), "+s"(bnof));  // per-stage bases stay opaque
         const char* bsl = smem + boff + b_lane;
         const char* bsn = smem + bnof + b_lane;
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
           }
           if constexpr (MORE || R + NSTL < 9) {
             constexpr int RN = R + NSTL;             // stage s + NSTL = 9 (c + RN / 9) + RN % 9
-            issue_stage_b(c + RN / 9, RN % 9, ((9 % NSTL) * c + RN) % NSTL);
+            issue_stage_b(c + RN / 9, RN % 9, (int)((unsigned)((9 % NSTL) * c + RN) % NSTL));
           }
         };
         read_b<TN, -1>(bsn, b1);

@@ -151,7 +151,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
   // entries back to back: entry e = g (zr + 2) + e', e' = input plane z0 - 1 + e' of group g
   const int gstride = g.zr + 2;
   auto issue_x = [&](int e, int rz) {            // stream entry e = input plane z0 - 1 + e
-    const uint32_t slot = smem_l + (uint32_t)((e % PW_XSLOTS) * C::XSLOT);
+    const uint32_t slot = smem_l + (uint32_t)(((unsigned)e % PW_XSLOTS) * C::XSLOT);
     if (LAT && e >= gstride) {
       e -= gstride;
       rz += 1;
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
       }
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        uint32_t b = (uint32_t)(((v + j) % PW_XSLOTS) * C::XSLOT) + xb;
+        uint32_t b = (uint32_t)(((unsigned)(v + j) % PW_XSLOTS) * C::XSLOT) + xb;
         asm volatile("v_mov_b32 %0, %1" : "=v"(b) : "v"(b));
         xbase[j] = smem + b;
       }
@@ -335,13 +335,13 @@ __global__ __launch_bounds__(PW_NTHR) void pwgrad_kernel(PWG g, const u16* __res
         }
         raw_barrier();
         if (s + 2 < nstage) {
-          const int p2 = (s + 2) / SPP, g2 = p2 >= g.zr ? 1 : 0;
-          issue_y(p2 - g2 * g.zr, (s + 2) % SPP, (s + 2) % PW_YSLOTS, rz + g2);
+          const int p2 = (int)((unsigned)(s + 2) / SPP), g2 = p2 >= g.zr ? 1 : 0;
+          issue_y(p2 - g2 * g.zr, (int)((unsigned)(s + 2) % SPP), (int)((unsigned)(s + 2) % PW_YSLOTS), rz + g2);
         }
         if (M == 0 && xnext) issue_x(v + 3, rz);
         // (opaque, defined after the barrier: otherwise the dY fragment addresses of all four
         // stages are computed at the plane start and held -- 64 VGPRs, spilled)
-        int yoff = C::Y_OFF + (s % PW_YSLOTS) * PW_YST;
+        int yoff = C::Y_OFF + (int)((unsigned)s % PW_YSLOTS) * PW_YST;
         asm volatile("" : "+s"(yoff));
         const char* yimg = smem + yoff;
         PFr f0, f1;
