@@ -492,6 +492,9 @@ struct LW5 {
   uint32_t xbytes, ybytes;                // operand sizes (buffer-resource ranges)
 };
 
+// DD: the dilation as a template constant (4, 8; 0 = run time), so the per-sub-group class
+// digits (grp_vox / grp_off, every 5 planes) divide by constants
+template <int DD>
 __global__ __launch_bounds__(NTHR) void lattice5_wgrad_kernel(LW5 g, const u16* __restrict__ src,
                                                               const u16* __restrict__ dy,
                                                               float* __restrict__ ws) {
@@ -507,7 +510,8 @@ __global__ __launch_bounds__(NTHR) void lattice5_wgrad_kernel(LW5 g, const u16* 
   const int t2 = tile / nco;
   const int cit = t2 % nci, split = t2 / nci;
   const int co0 = cot * 64, ci0 = cit * KC;
-  const int d = g.d, E = g.E;
+  const int d = DD ? DD : g.d, E = DD ? S * DD : g.E;
+  const int GG = DD ? DD * DD * DD / NS : g.G;        // sub groups per sample
   const int g0 = split * g.groups_per_split;
   const int nplane_out = g.groups_per_split * S;
 
@@ -518,7 +522,7 @@ __global__ __launch_bounds__(NTHR) void lattice5_wgrad_kernel(LW5 g, const u16* 
   // class digits never carry into the group's (16-aligned classes, d^2 >= 16), so sub s adds
   // a constant
   auto grp_vox = [&](int gi, int z, int ty, int tx) -> int64_t {
-    const int n = gi / g.G, q = (gi % g.G) * NS;
+    const int n = gi / GG, q = (gi % GG) * NS;
     const int rz = q / (d * d), ry = (q / d) % d, rx = q % d;
     return (((int64_t)n * E + rz + d * z) * E + ry + d * ty) * E + rx + d * tx;
   };
@@ -874,9 +878,12 @@ int64_t wgrad_workspace(const mmad_patch::Geo& q) {
 int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, int* splits,
           void* stream) {
   if (!wgrad_ok(q)) return MMAD_EUNSUPPORTED;
-  static const bool attr = hipFuncSetAttribute((const void*)lattice5_wgrad_kernel,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               WLDS) == hipSuccess;
+  auto at = [](const void* k) {
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, WLDS) == hipSuccess;
+  };
+  static const bool attr = at((const void*)lattice5_wgrad_kernel<4>) &&
+                           at((const void*)lattice5_wgrad_kernel<8>) &&
+                           at((const void*)lattice5_wgrad_kernel<0>);
   if (!attr) return MMAD_EUNSUPPORTED;
   const int sp = wgrad_splits(q);
   LW5 g{};
@@ -887,8 +894,15 @@ int wgrad(const mmad_patch::Geo& q, const void* x, const void* dy, float* ws, in
   g.xbytes = (uint32_t)(vox * q.Cs * 2);
   g.ybytes = (uint32_t)(vox * q.Nd * 2);
   const int64_t nblk = (int64_t)(q.Cs / KC) * (q.Nd / 64) * sp;
-  hipLaunchKernelGGL(lattice5_wgrad_kernel, dim3((unsigned)nblk), dim3(NTHR), WLDS,
-                     as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  if (q.dd == 4)
+    hipLaunchKernelGGL(lattice5_wgrad_kernel<4>, dim3((unsigned)nblk), dim3(NTHR), WLDS,
+                       as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  else if (q.dd == 8)
+    hipLaunchKernelGGL(lattice5_wgrad_kernel<8>, dim3((unsigned)nblk), dim3(NTHR), WLDS,
+                       as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
+  else
+    hipLaunchKernelGGL(lattice5_wgrad_kernel<0>, dim3((unsigned)nblk), dim3(NTHR), WLDS,
+                       as_stream(stream), g, (const u16*)x, (const u16*)dy, ws);
   *splits = sp;
   return launch_status();
 }
