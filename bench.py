@@ -93,9 +93,10 @@ def kernel_roofline(op, events, batch, size, dtype, where):
     from the HIP event pairs volume_ops recorded around each call on its own stream.
 
     The residue-class kernels skip the MACs that land in the zero padding: per dimension 10
-    of the 12 (position, tap) pairs of a 4-point sub-lattice are real.  The forward skips
-    them in all three dimensions ((10/12)^3 = 57.9 % of the dense MACs run), the weight
-    gradient in y and x only (its z-padding taps read a zero block: (10/12)^2 = 69.4 %).
+    of the 12 (position, tap) pairs of a 4-point sub-lattice are real.  Both kernels skip
+    them in all three dimensions at compile time ((10/12)^3 = 57.9 % of the dense MACs run;
+    the weight gradient's plane loop is unrolled by the 4 planes of a sub group, so its
+    z-padding taps have no MFMAs either -- rounds 4-5 priced it at (10/12)^2 by mistake).
     ``frac`` = executed FLOP/s / peak (what the MFMA pipes did); ``dense_frac`` prices the
     dense count, as cuDNN / MIOpen report conv FLOPs, and can exceed 1."""
     _, flops = dominant_desc(batch, size)
@@ -105,7 +106,7 @@ def kernel_roofline(op, events, batch, size, dtype, where):
     peak = PEAK_BF16 if dtype == torch.bfloat16 else PEAK_F32
     s = size // 8
     lattice = s == 16 and dtype == torch.bfloat16
-    executed = flops * ((10 / 12) ** (3 if op == "fwd" else 2) if lattice else 1.0)
+    executed = flops * ((10 / 12) ** 3 if lattice else 1.0)
     vox = batch * s ** 3 * 512 * 2                         # one bf16 activation tensor
     wbytes = 512 * 512 * 27 * (2 if op == "fwd" else 4)    # bf16 packed in / fp32 dW out
     algo = 2 * vox + wbytes                                # X + Y (or dY) + weights
