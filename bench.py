@@ -52,7 +52,10 @@ from multimodal_alzheimer_amd.data_parallel import (GradAllReduce,  # noqa: E402
                                                     broadcast_module_state)
 
 W2 = [0.20314960629921264, 0.7968503937007874]
-FLOP_PER_VOL = {128: 424.7e9}            # fwd+bwd ResNet-10 @128^3
+# fwd+bwd ResNet-10 @128^3, dense MACs of the ops the step runs (413.2 GFLOP,
+# i.e. without the stem's input gradient, which the step never computes -- the 424.7 of
+# rounds 1-5 counted it)
+FLOP_PER_VOL = {128: 413.2e9}
 M2_BYTES_PER_VOL = 1.163e9               # unfused eager byte model
 PEAK_BF16 = 2.5e15                       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32 = 157.3e12
@@ -254,12 +257,12 @@ def main():
     elif args.workload == "fusion":
         model = M.PET_MRI_ResNet_Fusion(dict(hparams(args.precision), fl_gamma=2)).cuda()
     else:
-        model = M.All_Modalities_Fusion(dict(hparams(args.precision), fl_gamma=2,
+        model = M.Tri_ResNet_Tabular_Fusion(dict(hparams(args.precision), fl_gamma=2,
                                              resnet_depth_mri=34, resnet_depth_pet=18)).cuda()
     opt = model.configure_optimizers()
-    # config 5 is graphed at one rank (its multi-rank launch modes are not rehearsed)
-    use_graph = not args.eager and (args.graph or args.workload in ("mri", "fusion") or
-                                    (args.workload == "three" and not dp))
+    # every workload replays HIP graphs, at N > 1 too (the launch modes of configs 3-5 are
+    # rehearsed at world size 2 in tests/test_dp_graph_world2_gpu.py)
+    use_graph = not args.eager
     mode = "inside" if args.graph else "after" if args.after else args.collectives
     if not use_graph:
         mode = "eager"
@@ -430,6 +433,8 @@ def main():
         per_gpu = value / world
         result["step_mfma_frac"] = per_gpu * FLOP_PER_VOL[S] / (
             PEAK_BF16 if cdtype == torch.bfloat16 else PEAK_F32)
+        result["step_mfma_frac_basis"] = ("dense GFLOP per volume of the ops run (413.2, "
+                                          "SURVEY.md 8d; no stem dgrad) / dense bf16 peak")
         result["hbm_roofline_frac_m2"] = per_gpu * M2_BYTES_PER_VOL / PEAK_HBM
     result["config"]["step_launch"] = (
         "eager" if not use_graph else "hip graph replay" if reducer is None else

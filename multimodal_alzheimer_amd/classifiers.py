@@ -9,6 +9,9 @@ Same class names, constructor signatures, hparams keys, ``general_step`` contrac
   pkg/models/pet_models/pet_cnn.py                 Small_PET_CNN, Random_Benchmark_All_CN
   pkg/models/pet_models/pet_resnet_cnn.py          PET_CNN_ResNet
   pkg/models/fusion_models/anat_pet_fusion.py      Anat_PET_CNN
+  pkg/models/fusion_models/tabular_mri_fusion.py   Tabular_MRT_Model
+  pkg/models/fusion_models/pet_tabular_fusion.py   PET_TABULAR_CNN
+  pkg/models/fusion_models/all_modalities_fusion.py All_Modalities_Fusion
   pkg/loss_functions/focalloss.py                  FocalLoss
 
 but every forward / backward op runs on the MI355X kernels of libmmad_hip.so.
@@ -18,8 +21,12 @@ Additions beyond the reference (documented build extensions, BASELINE configs 3-
   * resnet_depth 34 (n_in 512) is accepted (the reference match rejects it,
     anat_cnn.py:37-46);
   * PET_MRI_ResNet_Fusion -- "ResNet-10 x2 + MLP head" (config 3/4);
-  * All_Modalities_Fusion -- MRI ResNet + PET ResNet + tabular MLP (config 5; the
-    reference's TabPFN branch is replaced, no reference parity).
+  * Tri_ResNet_Tabular_Fusion -- MRI ResNet + PET ResNet + tabular MLP trained in one
+    stage (config 5's network; not a reference class).
+
+The stage-2 / stage-3 tabular fusion classes (Tabular_MRT_Model, PET_TABULAR_CNN,
+All_Modalities_Fusion) follow the reference; their TabPFN feature extractor comes from
+tabular.py (tabpfn, or a registered backend).
 """
 import os
 from abc import ABC, abstractmethod
@@ -29,6 +36,7 @@ import torch.nn as nn
 from torch.optim.lr_scheduler import ReduceLROnPlateau
 
 from . import head_ops
+from . import tabular
 from . import layers as Lyr
 from . import medicalnet
 from .lightning_compat import (LightningModule, MulticlassF1Score, MulticlassMatthewsCorrCoef)
@@ -837,14 +845,17 @@ class Tabular_MLP(nn.Module):
         return self.net(x.reshape(x.shape[0], -1))
 
 
-class All_Modalities_Fusion(Base_Model):
-    """Three-branch late fusion (all_modalities_fusion.py:12-137), BUILD EXTENSION form.
+class Tri_ResNet_Tabular_Fusion(Base_Model):
+    """BUILD EXTENSION -- BASELINE config 5 "MRI ResNet-34 + PET ResNet-18 + tabular MLP,
+    160^3" (SURVEY.md sec. 7), trained end to end in one stage.
 
-    The reference fuses three stage-2 models, two of which embed TabPFN
-    (tabpfn==0.1.8, absent offline, CPU round-trip); BASELINE config 5 replaces that with
-    a tabular MLP.  Branches: MRI ResNet (``resnet_depth_mri``, default 34), PET ResNet
-    (``resnet_depth_pet``, default 18), Tabular_MLP -> 64-d each -> cat 192 ->
-    Linear(192,64) -> ReLU -> Linear(64,C) (the reference's stage-3 head, :50-57).
+    Not the reference's ``All_Modalities_Fusion`` (that class fuses three *trained stage-2
+    models* loaded from checkpoints, two of them TabPFN-based; it is restated below under
+    its own name).  Branches: MRI ResNet (``resnet_depth_mri``, default 34), PET ResNet
+    (``resnet_depth_pet``, default 18), both cut to conv_seg[:2] and reduced 512 -> 64 + ReLU
+    (as reduce_dim_mri, anat_pet_fusion.py:49), Tabular_MLP -> 64 -> cat (pet, mri, tab) 192
+    -> Linear(192, 64) -> ReLU -> Linear(64, C) (the reference's stage-3 head,
+    all_modalities_fusion.py:50-57).
     """
 
     def __init__(self, hparams):
@@ -892,4 +903,199 @@ class All_Modalities_Fusion(Base_Model):
             for p in m.parameters():
                 p.requires_grad = bool(lr_pre) or m in (self.model_tabular,)
                 groups.append({"params": p, "lr": lr_pre or self.hparams["lr"]})
+        return _with_scheduler(_adam(groups, self.hparams, self.device), self.hparams)
+
+
+# ------------------------------------------------------- stage-2 / stage-3 tabular fusion
+def _tabpfn_params(classifier):
+    """Parameters of TabPFN's transformer (``model_tabular.model[2]``), which the reference
+    hands to Adam at lr_pretrained (tabular_mri_fusion.py:113-116); none for a stand-in
+    that is not an nn.Module."""
+    net = classifier.model[2] if getattr(classifier, "model", None) is not None else None
+    return list(net.parameters()) if isinstance(net, nn.Module) else []
+
+
+class _TabularStage2(Base_Model):
+    """Shared forward / step of the two TabPFN stage-2 models (tabular_mri_fusion.py:50-93,
+    pet_tabular_fusion.py:69-116): TabPFN decoder features of the CPU copy of the batch
+    (``tabular.decoder_features``), ``reduce_tab``, the volume branch, cat, ``model_fuse``."""
+
+    def _tab_features(self, x_tabular):
+        acts = tabular.decoder_features(self.model_tabular, x_tabular,
+                                        self.hparams["ensemble_size"],
+                                        self.tabular_training_size)
+        dev = next(self.reduce_tab.parameters()).device
+        return acts.to(device=dev, dtype=torch.float32)
+
+    def _tab_groups(self, stage1):
+        groups = [{"params": p, "lr": self.hparams["lr"]}
+                  for m in (self.model_fuse, self.reduce_tab) for p in m.parameters()]
+        if self.hparams.get("lr_pretrained"):
+            groups += [{"params": p, "lr": self.hparams["lr_pretrained"]}
+                       for p in list(stage1.parameters()) + _tabpfn_params(self.model_tabular)]
+        return groups
+
+
+class Tabular_MRT_Model(_TabularStage2):
+    """Stage-2 MRI + tabular fusion (pkg/models/fusion_models/tabular_mri_fusion.py:11-129):
+    Anat_CNN from ``path_mri`` (or hparams['path_mri']) cut to conv_seg[:2] (512-d), TabPFN
+    decoder features [B, 1024] -> reduce_tab = Linear(1024, 512) + ReLU, cat (tabular, mri)
+    1024 -> model_fuse = Linear(1024, 64) -> ReLU -> Linear(64, C).  TabPFN comes from
+    ``tabular.load_model`` (fails loudly when neither tabpfn nor a registered backend is
+    present).  The MRI output is flattened per sample (the reference's ``.squeeze()``,
+    :77, which equals it for batches > 1)."""
+
+    def __init__(self, hparams, path_mri=None):
+        super().__init__(hparams)
+        self.model_mri = Anat_CNN.load_from_checkpoint(path_mri or hparams["path_mri"])
+        self.model_mri.model.conv_seg = self.model_mri.model.conv_seg[:2]
+        self.model_tabular, self.tabular_training_size = tabular.load_model(
+            tabular.TRAINPATH, hparams["n_classes"] == 2, ensemble_size=hparams["ensemble_size"])
+        if not hparams.get("lr_pretrained"):
+            _freeze(self.model_mri)         # (TabPFN's own freeze is a no-op typo, :29-30)
+        self.stage2out = Lyr.Linear(512 + 512, 64)
+        self.cls2 = Lyr.Linear(64, hparams["n_classes"])
+        self.relu = Lyr.ReLU()
+        self.reduce_tab = nn.Sequential(Lyr.Linear(1024, 512), self.relu)
+        self.model_fuse = nn.Sequential(self.stage2out, self.relu, self.cls2)
+        self.criterion = make_criterion(hparams)
+        Lyr.set_compute_dtype(self, Lyr.precision_dtype(hparams))
+
+    def forward(self, x_tabular, x_mri):
+        bs = x_mri.shape[0]
+        out_tabular = self.reduce_tab(self._tab_features(x_tabular))
+        out_mri = self.model_mri(x_mri).reshape(bs, -1)
+        return self.model_fuse(head_ops.concat_features(out_tabular, out_mri))
+
+    def general_step(self, batch, batch_idx, mode):
+        batch = self.prepare_batch(batch)
+        x_mri = batch["mri"].unsqueeze(1)
+        y = batch["label"]
+        x_tab = cast(batch["tabular"].unsqueeze(1), torch.float32)
+        y_hat, loss = _logits_and_loss(self.criterion, self(x_tab, x_mri), y)
+        self.log(mode + "_loss", loss, on_step=True, prog_bar=True)
+        return {"loss": loss, "outputs": y_hat, "labels": y}
+
+    def configure_optimizers(self):
+        return _with_scheduler(_adam(self._tab_groups(self.model_mri), self.hparams,
+                                     self.device), self.hparams)
+
+
+class PET_TABULAR_CNN(_TabularStage2):
+    """Stage-2 PET + tabular fusion (pkg/models/fusion_models/pet_tabular_fusion.py:15-148):
+    Small_PET_CNN from ``path_pet`` (or hparams['path_pet']) cut after GAP + flatten
+    (``model[:-3]`` for 2 classes, ``model[:-1]`` otherwise, :28-31), TabPFN decoder
+    features -> reduce_tab (``simple_dim_red``: Linear(1024, 512) ReLU Linear(512, 64) ReLU,
+    else Linear(1024, 64) ReLU, :54-57), cat (pet, tabular) 128 -> model_fuse =
+    Linear(128, 64) -> ReLU -> Linear(64, C)."""
+
+    def __init__(self, hparams, path_pet=None):
+        super().__init__(hparams)
+        pet = Small_PET_CNN.load_from_checkpoint(path_pet or hparams["path_pet"])
+        self.model_pet = pet.model[:-3] if hparams["n_classes"] == 2 else pet.model[:-1]
+        self.model_tabular, self.tabular_training_size = tabular.load_model(
+            tabular.TRAINPATH, hparams["n_classes"] == 2, ensemble_size=hparams["ensemble_size"])
+        if not hparams.get("lr_pretrained"):
+            _freeze(self.model_pet)
+        self.stage2out = Lyr.Linear(64 + 64, 64)
+        self.cls2 = Lyr.Linear(64, hparams["n_classes"])
+        self.relu = Lyr.ReLU()
+        if self.hparams["simple_dim_red"]:
+            self.reduce_tab = nn.Sequential(Lyr.Linear(1024, 512), self.relu,
+                                            Lyr.Linear(512, 64), self.relu)
+        else:
+            self.reduce_tab = nn.Sequential(Lyr.Linear(1024, 64), self.relu)
+        self.model_fuse = nn.Sequential(self.stage2out, self.relu, self.cls2)
+        self.criterion = make_criterion(hparams)
+        Lyr.set_compute_dtype(self, Lyr.precision_dtype(hparams))
+
+    def forward(self, x_pet, x_tabular):
+        out_pet = self.model_pet(x_pet)
+        out_tab = self.reduce_tab(self._tab_features(x_tabular))
+        return self.model_fuse(head_ops.concat_features(out_pet, out_tab))
+
+    def general_step(self, batch, batch_idx, mode):
+        batch = self.prepare_batch(batch)
+        x_pet = batch["pet1451"].unsqueeze(1)
+        y = batch["label"]
+        x_tab = cast(batch["tabular"].unsqueeze(1), torch.float32)
+        y_hat, loss = _logits_and_loss(self.criterion, self(x_pet, x_tab), y)
+        self.log(mode + "_loss", loss, on_step=True, prog_bar=True)
+        return {"loss": loss, "outputs": y_hat, "labels": y}
+
+    def configure_optimizers(self):
+        return _with_scheduler(_adam(self._tab_groups(self.model_pet), self.hparams,
+                                     self.device), self.hparams)
+
+
+class All_Modalities_Fusion(Base_Model):
+    """Stage-3 fusion of the three stage-2 models (pkg/models/fusion_models/
+    all_modalities_fusion.py:12-137).
+
+    * stage-2 models from checkpoints (:17-26): ``Anat_PET_CNN`` from
+      hparams['path_anat_pet'] (with path_pet / path_anat), ``Tabular_MRT_Model`` from
+      'path_anat_tab' (path_mri = path_anat), ``PET_TABULAR_CNN`` from 'path_pet_tab'
+      (path_pet); each one's classifier cut off, ``model_fuse[:-2]`` = its stage2out alone
+      (64-d, no ReLU; :29-31);
+    * without lr_pretrained the stage-2 reduce / fuse layers are frozen (:34-47);
+    * cat (anat_pet, anat_tab, pet_tab) 192 -> model_fuse = stage3out Linear(192, 64) ->
+      ReLU -> cls3 Linear(64, C) (:50-57, :74-79); focal loss or weighted CE (:60-64);
+    * Adam over model_fuse at lr, plus the stage-1/2 parts at lr_pretrained (:98-137; the
+      reference lists ``model_tabular`` -- a TabPFNClassifier, not a Module -- which raises
+      there; its transformer's parameters are taken here, as the stage-2 models do).
+
+    The two tabular stage-2 models need TabPFN (``tabular.load_model``: tabpfn, or a
+    registered backend, else ``TabPFNUnavailable``).  The config-5 benchmark network
+    (ResNet-34 + ResNet-18 + tabular MLP, one stage) is ``Tri_ResNet_Tabular_Fusion``.
+    """
+
+    def __init__(self, hparams):
+        super().__init__(hparams)
+        self.model_anat_pet = Anat_PET_CNN.load_from_checkpoint(
+            hparams["path_anat_pet"], path_pet=hparams["path_pet"],
+            path_anat=hparams["path_anat"])
+        self.model_anat_tab = Tabular_MRT_Model.load_from_checkpoint(
+            hparams["path_anat_tab"], path_mri=hparams["path_anat"])
+        self.model_pet_tab = PET_TABULAR_CNN.load_from_checkpoint(
+            hparams["path_pet_tab"], path_pet=hparams["path_pet"])
+        for m in (self.model_anat_pet, self.model_anat_tab, self.model_pet_tab):
+            m.model_fuse = m.model_fuse[:-2]
+        if not hparams.get("lr_pretrained"):
+            _freeze(self.model_anat_pet.reduce_dim_mri, self.model_anat_pet.model_fuse,
+                    self.model_anat_tab.reduce_tab, self.model_anat_tab.model_fuse,
+                    self.model_pet_tab.model_fuse, self.model_pet_tab.reduce_tab)
+        self.stage3out = Lyr.Linear(64 + 64 + 64, 64)
+        self.cls3 = Lyr.Linear(64, hparams["n_classes"])
+        self.relu = Lyr.ReLU()
+        self.model_fuse = nn.Sequential(self.stage3out, self.relu, self.cls3)
+        self.criterion = make_criterion(hparams)
+        Lyr.set_compute_dtype(self, Lyr.precision_dtype(hparams))
+
+    def forward(self, x_pet, x_mri, x_tab):
+        out_anat_pet = self.model_anat_pet(x_pet, x_mri)
+        out_anat_tab = self.model_anat_tab(x_tab, x_mri)
+        out_pet_tab = self.model_pet_tab(x_pet, x_tab)
+        out = head_ops.concat_features(out_anat_pet, out_anat_tab, out_pet_tab)
+        return self.model_fuse(out)
+
+    def general_step(self, batch, batch_idx, mode):
+        batch = self.prepare_batch(batch)
+        x_pet = batch["pet1451"].unsqueeze(1)
+        x_mri = batch["mri"].unsqueeze(1)
+        x_tab = cast(batch["tabular"].unsqueeze(1), torch.float32)
+        y = batch["label"]
+        y_hat, loss = _logits_and_loss(self.criterion, self(x_pet, x_mri, x_tab), y)
+        self.log(mode + "_loss", loss, on_step=True, prog_bar=True)
+        return {"loss": loss, "outputs": y_hat, "labels": y}
+
+    def configure_optimizers(self):
+        groups = [{"params": p, "lr": self.hparams["lr"]} for p in self.model_fuse.parameters()]
+        if self.hparams.get("lr_pretrained"):
+            ap, pt, at = self.model_anat_pet, self.model_pet_tab, self.model_anat_tab
+            prev = [ap.model_pet, ap.model_mri, ap.stage2out, ap.reduce_dim_mri,
+                    pt.model_pet, pt.model_tabular, pt.stage2out, pt.reduce_tab,
+                    at.model_mri, at.model_tabular, at.stage2out, at.reduce_tab]
+            for m in prev:
+                ps = m.parameters() if isinstance(m, nn.Module) else _tabpfn_params(m)
+                groups += [{"params": p, "lr": self.hparams["lr_pretrained"]} for p in ps]
         return _with_scheduler(_adam(groups, self.hparams, self.device), self.hparams)

@@ -1920,8 +1920,8 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
   void* const stream = st;
   void* const rstream = rst;
   int rc;
-  // (1x1x1 weight gradients stay here: hipBLASLt's heuristic offers no split-K algorithm
-  // for K = all voxels at this size and its single-pass one ran 5x slower than wgrad_kernel)
+  // (the bf16 1x1x1 and stride-2 3^3 weight gradients leave below for pw_wgrad_kernel,
+  // pointwise.hip; what stays on wgrad_kernel is fp32 and the geometries it declines)
   if (raw_dtype >= 0 && !(unfolded(d) && mmad_stem::fwd_ok(d, dtype) && g.K == 392))
     return MMAD_EUNSUPPORTED;                    // raw input: the stem kernel or nothing
   if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && (stem_kernel_on() || raw_dtype >= 0) &&

@@ -1097,13 +1097,22 @@ bool raw_ok(const mmad_conv_desc* d, int in_dtype) {
          (int64_t)d->do_ * d->ho * d->wo * CO * 2 < (int64_t(1) << 30);
 }
 
+// the hoisted weight gradient's buffer offsets are 32-bit
+static bool wg2_small(const StemG& g) {
+  return (int64_t)g.di * g.hi * g.wo * 16 < (int64_t(1) << 30) &&
+         (int64_t)g.do_ * g.ho * g.wo * CO * 2 < (int64_t(1) << 30);
+}
+
 bool fwd_ok(const mmad_conv_desc* d, int dtype) {
   StemG g;
   int blocks;
   size_t lds;
   if (dtype != MMAD_BF16 || !geom_for(d, g, blocks, lds)) return false;
-  // column tiles: the y-quad forward and the hoisted weight gradient only
-  return g.nxt == 1 || (quad_on() && wg2_on() && geom_for(d, g, blocks, lds, true));
+  if (g.nxt == 1) return true;
+  // column tiles: the y-quad forward and the hoisted weight gradient only -- and the
+  // weight gradient's 32-bit offsets must hold, or the backward would have no stem route
+  // (so the whole conv takes the generic unfold path from the forward on)
+  return quad_on() && wg2_on() && wg2_small(g) && geom_for(d, g, blocks, lds, true);
 }
 
 int64_t fwd_stats_rows(const mmad_conv_desc* d) {
@@ -1142,9 +1151,7 @@ int wgrad(const mmad_conv_desc* d, const void* x_unf, const void* dy, float* ws,
                          attr((const void*)stem_wgrad2_kernel<7, 7, 2, 2, u16>) &&
                          attr((const void*)stem_wgrad2_kernel<7, 7, 2, 2, double>);
   if (!ok || wl > 160 * 1024) return MMAD_EUNSUPPORTED;
-  // (the hoisted form's buffer offsets are 32-bit)
-  const bool small = (int64_t)g.di * g.hi * g.wo * 16 < (int64_t(1) << 30) &&
-                     (int64_t)g.do_ * g.ho * g.wo * CO * 2 < (int64_t(1) << 30);
+  const bool small = wg2_small(g);
   if (in_dtype == MMAD_F64)
     hipLaunchKernelGGL((stem_wgrad2_kernel<7, 7, 2, 2, double>), dim3((unsigned)blocks),
                        dim3(512), wl, as_stream(stream), g, (const double*)x_unf, (const u16*)dy,

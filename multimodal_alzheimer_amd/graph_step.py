@@ -161,6 +161,7 @@ class StagedBackward:
                 p.grad = g
             else:
                 p.grad.add_(g)
+        volume_ops.check_deferred_adoption()
         keep = [(t, g) for t, g in zip(nxt, out[:len(nxt)]) if g is not None]
         self._grads = ([t for t, _ in keep], [g for _, g in keep])
         if k == self.n - 1:

@@ -79,8 +79,36 @@ WGRAD_PROBES = {}
 # (mmad_wgrad_reduce_batch, bit-identical sums).  graph_step captures the backward this way
 # and flushes at its end (per stage when staged), so the replay has one reduction launch
 # instead of one per conv.  Nothing may read a queued dW before the flush: eager backward
-# hooks that all-reduce buckets keep it off.
-_WGRAD_DEFER = {"on": False, "jobs": [], "keep": []}
+# hooks that all-reduce buckets keep it off, a weight with tensor / post-accumulate hooks is
+# never deferred, and every deferred dW must end up as its parameter's ``.grad`` itself
+# (``check_deferred_adoption``: an AccumulateGrad that cloned it, or a second contribution
+# summed into it, would have read it before the flush -- that raises).
+_WGRAD_DEFER = {"on": False, "jobs": [], "keep": [], "adopt": []}
+
+
+def _deferrable(wparam):
+    """a weight gradient may queue its slab reduction: the weight is a leaf parameter with
+    no gradient yet and no hook that would read dW during the backward, and the wgrad runs
+    on the main stream (MMAD_WGRAD_STREAM keeps deferral off: the flush runs on the main
+    stream, the workspace would belong to the side stream)"""
+    if not _WGRAD_DEFER["on"] or WGRAD_STREAM or wparam is None or not wparam.is_leaf:
+        return False
+    if wparam.grad is not None or getattr(wparam, "_backward_hooks", None):
+        return False
+    return not getattr(wparam, "_post_accumulate_grad_hooks", None)
+
+
+def check_deferred_adoption():
+    """Every weight whose dW reduction was deferred holds that very tensor as ``.grad`` (host
+    side, pointer compare).  Anything else means a copy or a sum read dW before the flush."""
+    pending = _WGRAD_DEFER["adopt"]
+    bad = [p for p, ptr in pending if p.grad is None or p.grad.data_ptr() != ptr]
+    pending.clear()
+    if bad:
+        raise RuntimeError(
+            f"{len(bad)} deferred weight gradient(s) were not adopted as .grad as-is (copied "
+            f"or summed before the batched slab reduction ran); shapes "
+            f"{[tuple(p.shape) for p in bad[:4]]}.  Run with MMAD_DEFER_WGRAD=0.")
 
 
 class deferred_wgrad_reduce:
@@ -97,6 +125,10 @@ class deferred_wgrad_reduce:
     def __exit__(self, *exc):
         flush_wgrad_reduce()
         _WGRAD_DEFER["on"] = self.prev
+        if exc[0] is None:
+            check_deferred_adoption()
+        else:
+            _WGRAD_DEFER["adopt"].clear()
         return False
 
 
@@ -509,14 +541,16 @@ def _wgrad(ctx, d, dt, src, gy, weight, wparam=None, rside=None):
     # a dW that autograd will not adopt as-is (an existing .grad it is added into, or the
     # channel-padded copy cut below) is read on the main stream: no split then
     raw = getattr(ctx, "raw", None)
-    if raw is not None and _WGRAD_DEFER["on"] and not ctx.has_bias and not padded and \
-            (wparam is None or wparam.grad is None):
+    defer = not ctx.has_bias and not padded and _deferrable(wparam)
+    if raw is not None and defer:
         job = L.WgradJob()
         L.call("mmad_conv3d_wgrad_raw_deferred", d, raw, L.ptr(src), dt, L.ptr(gy), L.ptr(dw),
                L.ptr(ws), C.byref(job), L.stream())
         if job.kind:
             _WGRAD_DEFER["jobs"].append(job)
             _WGRAD_DEFER["keep"].append(ws)
+            # the address only: an extra reference to dW would make AccumulateGrad copy it
+            _WGRAD_DEFER["adopt"].append((wparam, dw.data_ptr()))
     elif raw is not None:
         # the raw stem input (see _Conv3dFn.forward); slab reduction on rside when given
         split = rside is not None and (wparam is None or wparam.grad is None)
@@ -536,14 +570,15 @@ def _wgrad(ctx, d, dt, src, gy, weight, wparam=None, rside=None):
             if t is not None:
                 t.record_stream(rside)
         _queue_join(torch.cuda.current_stream(), rside)
-    elif _WGRAD_DEFER["on"] and not ctx.has_bias and not padded and \
-            (wparam is None or wparam.grad is None):
+    elif defer:
         job = L.WgradJob()
         L.call("mmad_conv3d_wgrad_deferred", d, dt, L.ptr(src), L.ptr(gy), L.ptr(dw), L.ptr(ws),
                C.byref(job), L.stream())
         if job.kind:
             _WGRAD_DEFER["jobs"].append(job)
             _WGRAD_DEFER["keep"].append(ws)
+            # the address only: an extra reference to dW would make AccumulateGrad copy it
+            _WGRAD_DEFER["adopt"].append((wparam, dw.data_ptr()))
     else:
         probe = WGRAD_PROBES.get(_desc_tuple(d)) if WGRAD_PROBES else None
         if probe is not None:

@@ -168,6 +168,114 @@ class AnatPETCNNRef(nn.Module):
         return {"loss": self.criterion(y_hat, y), "outputs": y_hat, "labels": y}
 
 
+def tabpfn_features(classifier, x_tab, num_ensemble, training_size):
+    """tabular_mri_fusion.py:58-74 (= pet_tabular_fusion.py:80-97): hook TabPFN's first
+    decoder Linear, predict_proba on the CPU copy, average the test rows over the ensemble
+    members (dl_approach.py:71-78)."""
+    acts = {}
+    h = classifier.model[2].decoder[0].register_forward_hook(
+        lambda mod, inp, out: acts.__setitem__("dec", out.detach()))
+    classifier.predict_proba(x_tab.cpu().squeeze(dim=1), normalize_with_test=False)
+    h.remove()
+    out = None
+    for i in range(num_ensemble):
+        a = acts["dec"][training_size:, i:i + 1, :]
+        out = a if out is None else out + a
+    return torch.transpose(out / num_ensemble, 0, 1).squeeze(dim=0)
+
+
+class TabularMRTRef(nn.Module):
+    """Tabular_MRT_Model (pkg/models/fusion_models/tabular_mri_fusion.py:11-93): stage-1
+    Anat_CNN cut to conv_seg[:2]; TabPFN features -> reduce_tab Linear(1024,512)+ReLU;
+    cat(tabular, mri) -> Linear(1024,64) -> ReLU -> Linear(64,C).  ``tabpfn`` = (fitted
+    classifier, n_train) as dl_approach.load_model returns it."""
+
+    def __init__(self, hparams, mri_stage1, tabpfn):
+        super().__init__()
+        self.hparams = dict(hparams)
+        self.model_mri = mri_stage1
+        self.model_mri.model.conv_seg = self.model_mri.model.conv_seg[:2]
+        self.model_tabular, self.tabular_training_size = tabpfn
+        self.stage2out = nn.Linear(512 + 512, 64)
+        self.cls2 = nn.Linear(64, hparams["n_classes"])
+        self.relu = nn.ReLU()
+        self.reduce_tab = nn.Sequential(nn.Linear(1024, 512), self.relu)
+        self.model_fuse = nn.Sequential(self.stage2out, self.relu, self.cls2)
+        self.criterion = make_criterion(hparams)
+
+    def forward(self, x_tabular, x_mri):
+        acts = tabpfn_features(self.model_tabular, x_tabular, self.hparams["ensemble_size"],
+                               self.tabular_training_size)
+        out_tabular = self.reduce_tab(acts.to(self.stage2out.weight.dtype))
+        out_mri = self.model_mri(x_mri).squeeze()
+        return self.model_fuse(torch.cat((out_tabular, out_mri), dim=1))
+
+
+class PETTabularRef(nn.Module):
+    """PET_TABULAR_CNN (pkg/models/fusion_models/pet_tabular_fusion.py:15-104): stage-1
+    Small_PET_CNN cut after GAP+Flatten (model[:-3] / [:-1], :28-31); TabPFN features ->
+    reduce_tab (simple_dim_red: 1024->512->64 with ReLUs, else 1024->64 + ReLU, :54-57);
+    cat(pet, tabular) -> Linear(128,64) -> ReLU -> Linear(64,C)."""
+
+    def __init__(self, hparams, pet_stage1, tabpfn):
+        super().__init__()
+        self.hparams = dict(hparams)
+        self.model_pet = (pet_stage1.model[:-3] if hparams["n_classes"] == 2
+                          else pet_stage1.model[:-1])
+        self.model_tabular, self.tabular_training_size = tabpfn
+        self.stage2out = nn.Linear(64 + 64, 64)
+        self.cls2 = nn.Linear(64, hparams["n_classes"])
+        self.relu = nn.ReLU()
+        if hparams["simple_dim_red"]:
+            self.reduce_tab = nn.Sequential(nn.Linear(1024, 512), self.relu,
+                                            nn.Linear(512, 64), self.relu)
+        else:
+            self.reduce_tab = nn.Sequential(nn.Linear(1024, 64), self.relu)
+        self.model_fuse = nn.Sequential(self.stage2out, self.relu, self.cls2)
+        self.criterion = make_criterion(hparams)
+
+    def forward(self, x_pet, x_tabular):
+        out_pet = self.model_pet(x_pet)
+        acts = tabpfn_features(self.model_tabular, x_tabular, self.hparams["ensemble_size"],
+                               self.tabular_training_size)
+        out_tab = self.reduce_tab(acts.to(self.stage2out.weight.dtype))
+        return self.model_fuse(torch.cat((out_pet, out_tab), dim=1))
+
+
+class AllModalitiesFusionRef(nn.Module):
+    """All_Modalities_Fusion (pkg/models/fusion_models/all_modalities_fusion.py:12-96):
+    the three stage-2 models with their classifiers cut (model_fuse[:-2] = stage2out
+    alone, :29-31), cat(anat_pet, anat_tab, pet_tab) 192 -> Linear(192,64) -> ReLU ->
+    Linear(64,C) (:50-57, :74-79)."""
+
+    def __init__(self, hparams, anat_pet, anat_tab, pet_tab):
+        super().__init__()
+        self.hparams = dict(hparams)
+        self.model_anat_pet, self.model_anat_tab, self.model_pet_tab = anat_pet, anat_tab, pet_tab
+        for m in (anat_pet, anat_tab, pet_tab):
+            m.model_fuse = m.model_fuse[:-2]
+        self.stage3out = nn.Linear(64 + 64 + 64, 64)
+        self.cls3 = nn.Linear(64, hparams["n_classes"])
+        self.relu = nn.ReLU()
+        self.model_fuse = nn.Sequential(self.stage3out, self.relu, self.cls3)
+        self.criterion = make_criterion(hparams)
+
+    def forward(self, x_pet, x_mri, x_tab):
+        out = torch.cat((self.model_anat_pet(x_pet, x_mri), self.model_anat_tab(x_tab, x_mri),
+                         self.model_pet_tab(x_pet, x_tab)), dim=1)
+        return self.model_fuse(out)
+
+    def inputs(self, batch, dtype=torch.float32):
+        return (batch["pet1451"].unsqueeze(1).to(dtype), batch["mri"].unsqueeze(1).to(dtype),
+                batch["tabular"].unsqueeze(1).to(torch.float32))
+
+    def general_step(self, batch, batch_idx=0, mode="train"):
+        """all_modalities_fusion.py:81-96."""
+        y_hat = self(*self.inputs(batch)).to(dtype=torch.double)
+        return {"loss": self.criterion(y_hat, batch["label"]), "outputs": y_hat,
+                "labels": batch["label"]}
+
+
 class ResNetPairFusionRef(nn.Module):
     """BUILD EXTENSION (BASELINE config 3/4): "ResNet-10 x2 + MLP head".
 
@@ -213,9 +321,9 @@ class TabularMLPRef(nn.Module):
         return self.net(x.reshape(x.shape[0], -1))
 
 
-class AllModalitiesRef(nn.Module):
-    """BUILD EXTENSION (BASELINE config 5): the stage-3 head of All_Modalities_Fusion
-    (all_modalities_fusion.py:50-79: three 64-d stage-2 features -> cat 192 ->
+class TriResNetTabularRef(nn.Module):
+    """BUILD EXTENSION (BASELINE config 5, ``Tri_ResNet_Tabular_Fusion``): the stage-3 head
+    of All_Modalities_Fusion (all_modalities_fusion.py:50-79: three 64-d features -> cat 192 ->
     Linear(192,64) -> ReLU -> Linear(64,C)) over an MRI ResNet, a PET ResNet (both cut to
     conv_seg[:2] and reduced 512 -> 64 + ReLU as reduce_dim_mri, anat_pet_fusion.py:49) and
     the tabular MLP that replaces the TabPFN branch.  Concat order pet, mri, tabular (the

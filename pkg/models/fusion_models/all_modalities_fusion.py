@@ -1,1 +1,2 @@
-from multimodal_alzheimer_amd.classifiers import All_Modalities_Fusion, Tabular_MLP  # noqa: F401
+from multimodal_alzheimer_amd.classifiers import (All_Modalities_Fusion, PET_TABULAR_CNN,  # noqa: F401
+                                                  Tabular_MRT_Model)

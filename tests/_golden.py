@@ -54,6 +54,72 @@ def fmf_hparams(mode, n_classes=2, **kw):
     return h
 
 
+TAB_SEED, TAB_ROWS = 4242, 16        # make_golden.install_tabpfn_standin
+
+
+def amf_hparams(lr_pretrained):
+    """Stage-2 / stage-3 hparams of the all_modalities_fusion case (mirror of
+    make_golden.amf_hparams; the paths are file names inside the checkpoint directory)."""
+    common = dict(ensemble_size=4, lr_pretrained=lr_pretrained)
+    return {
+        "anat_pet.ckpt": anat_hparams(10, fl_gamma=2, path_pet="pet.ckpt", path_mri="mri.ckpt",
+                                      **common),
+        "anat_tab.ckpt": anat_hparams(10, path_mri="mri.ckpt", **common),
+        "pet_tab.ckpt": anat_hparams(10, fl_gamma=1, simple_dim_red=True, path_pet="pet.ckpt",
+                                     **common),
+        "stage3": anat_hparams(10, fl_gamma=2, path_anat_pet="anat_pet.ckpt",
+                               path_anat_tab="anat_tab.ckpt", path_pet_tab="pet_tab.ckpt",
+                               path_pet="pet.ckpt", path_anat="mri.ckpt", **common),
+    }
+
+
+def tabpfn_backend():
+    from oracle import tabpfn_standin
+    return tabpfn_standin.make_backend(TAB_SEED, TAB_ROWS)
+
+
+def amf_checkpoint_chain(tmp_dir, lr_pretrained=1e-5):
+    """The reference's three-stage chain on the drop-in classes, through PL checkpoint
+    files: stage-1 Small_PET_CNN / Anat_CNN saved, stage-2 Anat_PET_CNN /
+    Tabular_MRT_Model / PET_TABULAR_CNN built from those paths and saved, then
+    All_Modalities_Fusion(hparams) loading all five (all_modalities_fusion.py:17-26).
+    TabPFN is the oracle stand-in (registered with tabular.set_backend).  Returns the
+    stage-3 model (on the CPU, weights as built)."""
+    import multimodal_alzheimer_amd as M
+    from multimodal_alzheimer_amd import tabular
+    tabular.set_backend(tabpfn_backend())
+    hp = amf_hparams(lr_pretrained)
+    path = {k: os.path.join(tmp_dir, k) for k in
+            ("pet.ckpt", "mri.ckpt", "anat_pet.ckpt", "anat_tab.ckpt", "pet_tab.ckpt")}
+
+    def fix(h):
+        return {k: (path[v] if isinstance(v, str) and v in path else v) for k, v in h.items()}
+
+    torch.manual_seed(0)
+    M.Small_PET_CNN(pet_hparams()).save_checkpoint(path["pet.ckpt"])
+    M.Anat_CNN(anat_hparams(10)).save_checkpoint(path["mri.ckpt"])
+    h = fix(hp["anat_pet.ckpt"])
+    M.Anat_PET_CNN(h, path_pet=h["path_pet"], path_anat=h["path_mri"]).save_checkpoint(
+        path["anat_pet.ckpt"])
+    h = fix(hp["anat_tab.ckpt"])
+    M.Tabular_MRT_Model(h, path_mri=h["path_mri"]).save_checkpoint(path["anat_tab.ckpt"])
+    h = fix(hp["pet_tab.ckpt"])
+    M.PET_TABULAR_CNN(h, path_pet=h["path_pet"]).save_checkpoint(path["pet_tab.ckpt"])
+    return M.All_Modalities_Fusion(fix(hp["stage3"]))
+
+
+def build_amf_oracle(h3):
+    hp = amf_hparams(1e-5)
+    load = tabpfn_backend()
+    ap = models_ref.AnatPETCNNRef(hp["anat_pet.ckpt"], models_ref.SmallPETCNNRef(pet_hparams()),
+                                  models_ref.AnatCNNRef(anat_hparams(10)))
+    at = models_ref.TabularMRTRef(hp["anat_tab.ckpt"], models_ref.AnatCNNRef(anat_hparams(10)),
+                                  load(None, True, 4))
+    pt = models_ref.PETTabularRef(hp["pet_tab.ckpt"], models_ref.SmallPETCNNRef(pet_hparams()),
+                                  load(None, True, 4))
+    return models_ref.AllModalitiesFusionRef(h3, ap, at, pt)
+
+
 def batch_for(shape, n_classes, seed, keys=("mri",)):
     b = {"label": torch.from_numpy(prng.labels(seed + 7, shape[0], n_classes))}
     for i, k in enumerate(keys):
@@ -111,6 +177,8 @@ CASES = {
                       "smallpet", 20, ("pet1451",)),
     "anat_pet_fusion": (lambda: anat_hparams(10, fl_gamma=2), "fusion", 22,
                         ("pet1451", "mri")),
+    "all_modalities_fusion": (lambda: amf_hparams(1e-5)["stage3"], "amf", 42,
+                              ("pet1451", "mri")),
     "early_fusion": (lambda: ef_hparams(), "ef", 24, ("pet1451", "mri")),
     "early_fusion_bn3": (lambda: ef_hparams(n_classes=3, batchnorm=True, conv_out=[16, 32, 64],
                                             filter_size=[5, 5, 3], linear_out=None),
@@ -137,6 +205,8 @@ def build_oracle(name):
         pet = models_ref.SmallPETCNNRef(pet_hparams())
         mri = models_ref.AnatCNNRef(anat_hparams(10))
         return models_ref.AnatPETCNNRef(h, pet, mri)
+    if kind == "amf":
+        return build_amf_oracle(h)
     if kind == "ef":
         return models_ref.EarlyFusionRef(h)
     if kind == "fmf":
@@ -145,10 +215,14 @@ def build_oracle(name):
 
 
 def batch_of(name, g):
-    _, _, bseed, keys = CASES[name]
+    _, kind, bseed, keys = CASES[name]
     shape = tuple(int(v) for v in g["shape"])
     n_classes = g["train_logits"].shape[1]
-    return batch_for(shape, n_classes, bseed, keys)
+    b = batch_for(shape, n_classes, bseed, keys)
+    if kind == "amf":                      # make_golden.amf_batch
+        from oracle import tabpfn_standin
+        b["tabular"] = tabpfn_standin.training_table(bseed + 50, shape[0])[0]
+    return b
 
 
 def fusion_via_stage1_checkpoints(tmp_dir):

@@ -377,6 +377,107 @@ def anat_pet_fusion():
     return out
 
 
+TAB_SEED, TAB_ROWS = 4242, 16        # the TabPFN stand-in's seed / training rows
+
+
+def install_tabpfn_standin():
+    """The stage-2 tabular fusion models import pkg.models.tabular_models.dl_approach, which
+    imports ``tabpfn`` (absent offline) and, through data_preparation, the reference
+    DataLoader module (nibabel, torchvision.transforms: absent, untouched here).  The
+    reference modules themselves run; only TabPFN is the build-defined stand-in of
+    oracle/tabpfn_standin.py, and ``get_data`` (the training rows of the ADNI table) returns
+    the stand-in's synthetic table."""
+    from oracle import tabpfn_standin
+    tp = types.ModuleType("tabpfn")
+    tp.TabPFNClassifier = tabpfn_standin.TabPFNClassifier
+    sys.modules["tabpfn"] = tp
+    if "nibabel" not in sys.modules:
+        sys.modules["nibabel"] = types.ModuleType("nibabel")
+    tv = sys.modules.setdefault("torchvision", types.ModuleType("torchvision"))
+    tvt = types.ModuleType("torchvision.transforms")
+    tvt.ToTensor = tvt.Normalize = object
+    tv.transforms = tvt
+    sys.modules["torchvision.transforms"] = tvt
+    import pkg.models.tabular_models.dl_approach as dl
+    assert dl.__file__.startswith(REF), dl.__file__
+    dl.get_data = lambda path, binary_classification: tabpfn_standin.training_table(
+        TAB_SEED, TAB_ROWS, 9, 2 if binary_classification else 3)
+    return dl
+
+
+def amf_batch(n, size, seed):
+    """pet1451 / mri volumes as batch_for, plus the 9 tabular features (float64)."""
+    from oracle import tabpfn_standin
+    b = batch_for((n, size, size, size), 2, seed, keys=("pet1451", "mri"))
+    b["tabular"] = tabpfn_standin.training_table(seed + 50, n)[0]
+    return b
+
+
+def amf_hparams(lr_pretrained):
+    """Stage-2 / stage-3 hparams of the all-modalities case (paths are registry keys)."""
+    common = dict(ensemble_size=4, lr_pretrained=lr_pretrained)
+    return {
+        "anat_pet.ckpt": anat_hparams(10, fl_gamma=2, path_pet="pet.ckpt", path_mri="mri.ckpt",
+                                      **common),
+        "anat_tab.ckpt": anat_hparams(10, path_mri="mri.ckpt", **common),
+        "pet_tab.ckpt": anat_hparams(10, fl_gamma=1, simple_dim_red=True, path_pet="pet.ckpt",
+                                     **common),
+        "stage3": anat_hparams(10, fl_gamma=2, path_anat_pet="anat_pet.ckpt",
+                               path_anat_tab="anat_tab.ckpt", path_pet_tab="pet_tab.ckpt",
+                               path_pet="pet.ckpt", path_anat="mri.ckpt", **common),
+    }
+
+
+@case
+def all_modalities_fusion():
+    """The reference's stage-3 ``All_Modalities_Fusion`` (all_modalities_fusion.py:12-96)
+    over its real stage-2 classes -- Anat_PET_CNN, Tabular_MRT_Model, PET_TABULAR_CNN -- and
+    their stage-1 Small_PET_CNN / Anat_CNN, every ``load_from_checkpoint`` answered from a
+    registry of freshly built models (the weights then come from the prng, as everywhere).
+    Only TabPFN is the stand-in (install_tabpfn_standin).  lr_pretrained is set at both
+    stages so nothing is frozen and every part gets a gradient (the cuts, the concat order
+    and the stage-3 head are all on the gradient path); the trainable-parameter names of
+    the default (frozen) build are recorded beside it (``frozen_trainable``)."""
+    install_tabpfn_standin()
+    from pkg.models.pet_models.pet_cnn import Small_PET_CNN
+    from pkg.models.mri_models.anat_cnn import Anat_CNN
+    from pkg.models.fusion_models.anat_pet_fusion import Anat_PET_CNN
+    from pkg.models.fusion_models.tabular_mri_fusion import Tabular_MRT_Model
+    from pkg.models.fusion_models.pet_tabular_fusion import PET_TABULAR_CNN
+    from pkg.models.fusion_models.all_modalities_fusion import All_Modalities_Fusion
+
+    def build(lr_pretrained):
+        hp = amf_hparams(lr_pretrained)
+        registry = {"pet.ckpt": (Small_PET_CNN, pet_hparams()),
+                    "mri.ckpt": (Anat_CNN, anat_hparams(10)),
+                    "anat_pet.ckpt": (Anat_PET_CNN, hp["anat_pet.ckpt"]),
+                    "anat_tab.ckpt": (Tabular_MRT_Model, hp["anat_tab.ckpt"]),
+                    "pet_tab.ckpt": (PET_TABULAR_CNN, hp["pet_tab.ckpt"])}
+        classes = (Small_PET_CNN, Anat_CNN, Anat_PET_CNN, Tabular_MRT_Model, PET_TABULAR_CNN)
+        orig = {c: c.__dict__.get("load_from_checkpoint") for c in classes}
+        for c in classes:
+            c.load_from_checkpoint = classmethod(
+                lambda cls, path, **kw: registry[path][0](dict(registry[path][1]), **kw))
+        try:
+            return All_Modalities_Fusion(hp["stage3"])
+        finally:
+            for c, f in orig.items():
+                if f is None:
+                    del c.load_from_checkpoint
+
+    torch.manual_seed(0)
+    frozen = build(None)
+    torch.manual_seed(0)
+    m = build(1e-5)
+    load_prng_weights(m, 41)
+    out = {"seed": np.array(41), "shape": np.array([2, 32, 32, 32])}
+    run_case(m, amf_batch(2, 32, 42), out)
+    out["frozen_trainable"] = np.array([n for n, p in frozen.named_parameters()
+                                        if p.requires_grad])
+    out["frozen_state_dict_keys"] = np.array(list(frozen.state_dict().keys()))
+    return out
+
+
 def ef_hparams(n_classes=2, **kw):
     """train_early_fusion.py:236-254 best configuration, dropout keys removed."""
     h = {"n_classes": n_classes, "conv_out": [8, 16, 32, 64], "filter_size": [7, 5, 3, 3],

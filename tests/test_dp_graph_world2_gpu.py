@@ -1,5 +1,6 @@
 """bench.py's N > 1 launch modes at world size 2 on BASELINE config 3/4's model
-(PET_MRI_ResNet_Fusion: PET + MRI ResNet-10 x2 + MLP head, focal loss), SURVEY.md §8(e).
+(PET_MRI_ResNet_Fusion: PET + MRI ResNet-10 x2 + MLP head, focal loss) and on config 5's
+(Tri_ResNet_Tabular_Fusion: MRI ResNet-34 + PET ResNet-18 + tabular MLP), SURVEY.md §8(e).
 
 Two processes share the test box's one GPU (RCCL refuses two ranks on one device, so the
 collective is gloo over the same CUDA tensors); everything else is the benched path:
@@ -11,7 +12,7 @@ collective is gloo over the same CUDA tensors); everything else is the benched p
 Each rank trains on its own shard (fp32, 32^3, 2 pairs per rank) for 3 replays.  Checked:
   * every rank's averaged gradient of replay 3 == the mean of the two per-replica
     gradients computed in one process from the same pre-replay weights (1e-5 relative);
-  * each replica's replay-3 logits == the CPU oracle (oracle ResNetPairFusionRef) on that
+  * each replica's replay-3 logits == the CPU oracle (oracle ResNetPairFusionRef / TriResNetTabularRef) on that
     replica's shard at the same weights (1e-4, argmax exact);
   * replays 1-3 are bit-identical (losses, parameters, BN running statistics) to eager
     steps of an identical model with the eager hook-driven all-reduce.
@@ -29,29 +30,33 @@ DEV = "cuda"
 N_PER_RANK, SIZE, STEPS, WARM = 2, 32, 3, 2
 
 
-def _model():
+def _build(kind, product):
+    from tests.test_fusion_configs_gpu import _hp, _pair, _three
+    return (_pair if kind == "pair" else _three)(_hp(kind), product)
+
+
+def _model(kind):
     from tests import _golden as G
-    from tests.test_fusion_configs_gpu import _hp, _live, _pair
-    ref = _pair(_hp("pair"), False)
+    from tests.test_fusion_configs_gpu import _live
+    ref = _build(kind, False)
     G.load_prng_weights(ref, 81)
     _live(ref)
-    import multimodal_alzheimer_amd as M
-    m = M.PET_MRI_ResNet_Fusion(_hp("pair"))
+    m = _build(kind, True)
     m.load_state_dict(ref.state_dict())
     return m
 
 
-def _batches(rank):
+def _batches(rank, kind):
     from tests.test_fusion_configs_gpu import _batch
     out = []
     for i in range(STEPS):
-        b = _batch(2 * N_PER_RANK, SIZE, 90 + 3 * i, False)
+        b = _batch(2 * N_PER_RANK, SIZE, 90 + 3 * i, kind == "three")
         sl = slice(N_PER_RANK * rank, N_PER_RANK * (rank + 1))
         out.append({k: v[sl] for k, v in b.items()})
     return out
 
 
-def _worker(rank, world, port, out_dir, mode):
+def _worker(rank, world, port, out_dir, mode, kind):
     import torch.distributed as dist
     from multimodal_alzheimer_amd.data_parallel import GradAllReduce
     from multimodal_alzheimer_amd.graph_step import GraphedTrainStep, backward_stages
@@ -59,9 +64,9 @@ def _worker(rank, world, port, out_dir, mode):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        a = _model().to(DEV)
+        a = _model(kind).to(DEV)
         b = copy.deepcopy(a)
-        batches = [{k: v.to(DEV) for k, v in bt.items()} for bt in _batches(rank)]
+        batches = [{k: v.to(DEV) for k, v in bt.items()} for bt in _batches(rank, kind)]
 
         # graph-replayed (the benched mode)
         opt_a = a.configure_optimizers()
@@ -112,13 +117,14 @@ def _worker(rank, world, port, out_dir, mode):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("kind", ["pair", "three"])
 @pytest.mark.parametrize("mode", ["staged", "after"])
-def test_graphed_dp_world2_fusion(tmp_path, mode):
+def test_graphed_dp_world2_fusion(tmp_path, mode, kind):
     from oracle import models_ref  # noqa: F401  (the checker only)
-    from tests.test_fusion_configs_gpu import _hp, _pair
     ctx = mp.get_context("spawn")
-    port = 29100 + os.getpid() % 400 + (0 if mode == "staged" else 450)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), mode))
+    port = (29100 + os.getpid() % 400 + (0 if mode == "staged" else 450) +
+            (0 if kind == "pair" else 900))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), mode, kind))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -136,19 +142,17 @@ def test_graphed_dp_world2_fusion(tmp_path, mode):
         assert torch.equal(res[0]["pre"][k], res[1]["pre"][k]), k
         assert torch.equal(res[0]["final"][k], res[1]["final"][k]), k
 
-    import multimodal_alzheimer_amd as M
     per = []
-    h = _hp("pair")
     for r in range(2):
-        batch = _batches(r)[STEPS - 1]
-        m = M.PET_MRI_ResNet_Fusion(h)
+        batch = _batches(r, kind)[STEPS - 1]
+        m = _build(kind, True)
         m.load_state_dict(res[0]["pre"])
         m = m.to(DEV)
         o = m.general_step({k: v.to(DEV) for k, v in batch.items()}, 0, "train")
         o["loss"].backward()
         torch.cuda.synchronize()
         per.append({k: p.grad.detach().cpu() for k, p in m.named_parameters()})
-        ref = _pair(h, False)
+        ref = _build(kind, False)
         ref.load_state_dict(res[0]["pre"])
         rr = ref.general_step(batch, 0, "train")
         got, exp = res[r]["logits"].numpy(), rr["outputs"].detach().numpy()

@@ -149,18 +149,20 @@ def test_full_size_fp32_matches_reference(name):
             f"{pname}: max err {err.max():.3e} vs bound {bound:.3e} (reference fp32 {e_ref:.3e})"
         st = g["grad/stats/" + pname]
         got = np.array([np.abs(full).sum(), np.sqrt((full * full).sum())])
-        # within 2e-3 of the reference's fp32 sums -- or, where fp32 noise compounds through a
-        # deep chain (ResNet-34's 36 layers: ReLU masks flipped by pre-activations within fp32
-        # rounding of 0), of the float64 sums within 2e-3 + the larger of twice the reference
-        # fp32 path's own deviation from them and the normwise error of this tensor's sampled
-        # elements (which passed their element bar above)
+        # within 2e-3 of the reference's fp32 sums.  Only for the 36-layer ResNet-34 chain
+        # (anat_r34_160, whose "reference" is the oracle's fp32 run), where fp32 noise
+        # compounds (ReLU masks flipped by pre-activations within fp32 rounding of 0), the
+        # float64 sums may stand in: within 2e-3 + the larger of twice the fp32 reference's
+        # own deviation from them and a fixed 2e-2 -- a bound that does not depend on this
+        # implementation's error, so a regression cannot widen it
         st64 = g["grad64/stats/" + pname][1:]
         ok32 = np.all(np.abs(got - st[1:]) <= 2e-3 * np.abs(st[1:]) + 1e-6 * gscale)
-        ref_dev = np.abs(st[1:] - st64) / np.abs(st64)
-        nrm = np.linalg.norm(ours - exact) / max(np.linalg.norm(exact), 1e-30)
-        ok64 = np.all(np.abs(got - st64) <=
-                      (2e-3 + np.maximum(2 * ref_dev, nrm)) * np.abs(st64) + 1e-6 * gscale)
-        assert ok32 or ok64, (pname, got, st[1:], st64, nrm)
+        ok64 = False
+        if name == "anat_r34_160":
+            ref_dev = np.abs(st[1:] - st64) / np.abs(st64)
+            ok64 = np.all(np.abs(got - st64) <=
+                          (2e-3 + np.maximum(2 * ref_dev, 2e-2)) * np.abs(st64) + 1e-6 * gscale)
+        assert ok32 or ok64, (pname, got, st[1:], st64, np.abs(got - st64) / np.abs(st64))
         n += 1
     assert n >= 20
 

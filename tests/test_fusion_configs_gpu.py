@@ -3,7 +3,7 @@ PET+MRI late fusion (ResNet-10 x2 + MLP head) and the three-branch fusion (MRI R
 PET ResNet-18 + tabular MLP), on the MI355X through libmmad_hip.so.
 
   * fp32 at 32^3 against the CPU oracle's restatement of the same networks
-    (oracle/models_ref.py ResNetPairFusionRef / AllModalitiesRef): logits 1e-4, argmax,
+    (oracle/models_ref.py ResNetPairFusionRef / TriResNetTabularRef): logits 1e-4, argmax,
     loss, and every gradient within the f64 bar of test_model_parity_gpu;
   * bf16 at the configs' full sizes (128^3 pairs, batch 8; 160^3, batch 2) against the
     fp32 HIP path on the same weights: finite, bounded logit drift, loss."""
@@ -29,8 +29,8 @@ def _pair(h, product):
 
 def _three(h, product):
     if product:
-        return M.All_Modalities_Fusion(h)
-    return models_ref.AllModalitiesRef(h, models_ref.AnatCNNRef(_stage1(h, 34)),
+        return M.Tri_ResNet_Tabular_Fusion(h)
+    return models_ref.TriResNetTabularRef(h, models_ref.AnatCNNRef(_stage1(h, 34)),
                                        models_ref.PETResNetRef(_stage1(h, 18)))
 
 

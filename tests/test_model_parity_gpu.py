@@ -29,6 +29,10 @@ def build_product(name):
         return M.PET_MRI_EF(h)
     if kind == "fmf":
         return M.PET_MRI_FMF(h)
+    if kind == "amf":                      # stage 1 -> 2 -> 3 through checkpoint files
+        import tempfile
+        with tempfile.TemporaryDirectory() as d:
+            return G.amf_checkpoint_chain(d)
     pet = M.Small_PET_CNN(G.pet_hparams())
     mri = M.Anat_CNN(G.anat_hparams(10))
     return M.Anat_PET_CNN(h, pet_model=pet, mri_model=mri)
@@ -216,7 +220,7 @@ def test_two_backbone_fusion_and_three_branch_run():
     assert m.model_pet.model.conv1.weight.grad is not None
     assert m.model_mri.model.conv1.weight.grad is not None
     h5 = G.anat_hparams(10, precision="bf16", resnet_depth_mri=34, resnet_depth_pet=18)
-    m5 = M.All_Modalities_Fusion(h5).to(DEV)
+    m5 = M.Tri_ResNet_Tabular_Fusion(h5).to(DEV)
     b["tabular"] = torch.rand(2, 9, dtype=torch.float64, device=DEV)
     o5 = m5.general_step(b, 0, "train")
     o5["loss"].backward()

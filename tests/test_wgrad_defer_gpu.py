@@ -164,3 +164,37 @@ def test_stride2_3cube_wgrad_dedup_bit_identical(xs, co):
     finally:
         lib.mmad_set_kernel_variant(b"pw_wg3_dedup", prev)
     assert torch.equal(got, ref), f"max |diff| {(got - ref).abs().max().item():.3e}"
+
+
+def test_hooked_weight_is_not_deferred():
+    """a tensor hook on the weight reads dW during the backward, before any flush: such a
+    weight keeps the immediate reduction (bit-identical dW, the hook sees the final dW)"""
+    name, xs, ws, s, p, d = ROUTES[0]
+    x, w = _operands(xs, ws, 21)
+    ref, gy, _ = _wgrad(x, w, s, p, d)
+    wg = w.clone().requires_grad_(True)
+    seen = []
+    wg.register_hook(lambda g: seen.append(g.clone()))
+    y = V.conv3d(x, wg, None, (s,) * 3, (p,) * 3, (d,) * 3, BF)
+    with V.deferred_wgrad_reduce(True):
+        y.backward(gy)
+        queued = len(V._WGRAD_DEFER["jobs"])
+    torch.cuda.synchronize()
+    assert queued == 0
+    assert torch.equal(wg.grad, ref) and torch.equal(seen[0], ref)
+
+
+def test_summed_deferred_gradient_raises():
+    """a weight used by two convs gets the SUM of two deferred dWs, computed by autograd
+    before the flush: the adoption check refuses it instead of returning garbage"""
+    name, xs, ws, s, p, d = ROUTES[0]
+    x, w = _operands(xs, ws, 22)
+    wg = w.clone().requires_grad_(True)
+    y = V.conv3d(x, wg, None, (s,) * 3, (p,) * 3, (d,) * 3, BF)
+    y2 = V.conv3d(x, wg, None, (s,) * 3, (p,) * 3, (d,) * 3, BF)
+    gy = torch.ones_like(y)
+    with pytest.raises(RuntimeError, match="not adopted"):
+        with V.deferred_wgrad_reduce(True):
+            torch.autograd.backward([y, y2], [gy, gy])
+    torch.cuda.synchronize()
+    assert not V._WGRAD_DEFER["jobs"] and not V._WGRAD_DEFER["adopt"]
