@@ -163,6 +163,19 @@ int mmad_bn_fold(int c, const float* gamma, const float* beta, const float* runn
                  float* bias, void* stream);
 int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy,
                       const void* w_packed_t, void* dx, void* stream);
+/* Input gradient of a conv whose input was relu(bn(y)) -- a BN+ReLU without residual, as
+ * MedicalNet's BasicBlock runs bn1 -> relu -> conv2 (reference call site anat_cnn.py:30-31;
+ * replaces the column-sum pass of that BN's backward, mmad_bn_relu_bwd_reduce) -- with the
+ * BN backward's partial sums from the dgrad epilogue: parts [rows][2][ci] holds per tile
+ * (sum g', sum g' * xhat), g' = dx * (fma(y, scale, shift) > 0), xhat = (y - mean) * invstd,
+ * g = dx as stored (bf16); feed them to mmad_bn_bwd_finalize with nparts = rows.
+ * rows = mmad_conv3d_dgrad_bnsum_rows(d, dtype): -1 when this conv's dgrad route has no such
+ * epilogue (then mmad_conv3d_dgrad + mmad_bn_relu_bwd_reduce).  bf16 only; y NDHWC like dx,
+ * scale / shift / mean / invstd [ci] fp32, 16-byte aligned. */
+int64_t mmad_conv3d_dgrad_bnsum_rows(const mmad_conv_desc* d, int dtype);
+int mmad_conv3d_dgrad_bnsum(const mmad_conv_desc* d, int dtype, const void* dy, const void* wpt,
+                            void* dx, const void* y, const float* scale, const float* shift,
+                            const float* mean, const float* invstd, float* parts, void* stream);
 int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype); /* bytes */
 int mmad_conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* dy,
                       float* dw, float* dbias, void* workspace, void* stream);

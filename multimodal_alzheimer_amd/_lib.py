@@ -94,6 +94,8 @@ _SIGS = {
     "mmad_conv3d_stats_rows": (_i64, [_P, _i32]),
     "mmad_conv3d_fwd": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_conv3d_dgrad": (_i32, [_P, _i32, _vp, _vp, _vp, _vp]),
+    "mmad_conv3d_dgrad_bnsum_rows": (_i64, [_P, _i32]),
+    "mmad_conv3d_dgrad_bnsum": (_i32, [_P, _i32] + [_vp] * 10),
     "mmad_conv3d_wgrad_workspace": (_i64, [_P, _i32]),
     "mmad_conv3d_wgrad": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmad_conv3d_wgrad_split": (_i32, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -1861,6 +1861,58 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
                           as_stream(stream));
 }
 
+// dgrad routes whose epilogue also writes the BN-backward partial sums of the BN+ReLU that
+// produced the conv's input (bnsum.h): 1 = the plane-pair residue-class kernel (layer4),
+// 2 = the dilation-2 residue-class kernel (layer3), 3 = the patch conv (layer2's 128-channel
+// stride-1 conv; not its persistent z-walking form)
+static int bnsum_route(const mmad_conv_desc* d, int dtype, mmad_patch::Geo* qo) {
+  if (dtype != MMAD_BF16 || !desc_ok(d) || unfolded(d) || !dgrad_as_fwd(d)) return 0;
+  if (mmad_pw::ok(d, dtype)) return 0;
+  const Geom gf = dgrad_fwd_geom(d, dtype);
+  if (!geom_ok(gf, dtype)) return 0;
+  const mmad_patch::Geo q = patch_geo(gf);
+  int route = 0;
+  if (use_lattice(gf, dtype)) {
+    if (!mmad_lattice5::ok(q) && mmad_lattice_zp::ok(q)) route = 1;
+  } else if (use_lattice8(gf, dtype)) {
+    route = 2;
+  } else if (use_patch(gf, dtype) && !mmad_patchz::ok(q)) {
+    route = 3;
+  }
+  if (route) *qo = q;
+  return route;
+}
+
+int64_t mmad_conv3d_dgrad_bnsum_rows(const mmad_conv_desc* d, int dtype) {
+  mmad_patch::Geo q{};
+  switch (bnsum_route(d, dtype, &q)) {
+    case 1: return mmad_lattice_zp::tiles(q);
+    case 2: return mmad_lattice8::tiles(q);
+    case 3: return mmad_patch::tiles(q);
+    default: return -1;
+  }
+}
+
+int mmad_conv3d_dgrad_bnsum(const mmad_conv_desc* d, int dtype, const void* dy, const void* wpt,
+                            void* dx, const void* y, const float* scale, const float* shift,
+                            const float* mean, const float* invstd, float* parts, void* stream) {
+  if (!dy || !wpt || !dx || !y || !scale || !shift || !mean || !invstd || !parts)
+    return MMAD_ENULL;
+  mmad_patch::Geo q{};
+  const int route = bnsum_route(d, dtype, &q);
+  if (route == 0) return MMAD_EUNSUPPORTED;
+  if (((uintptr_t)scale | (uintptr_t)shift | (uintptr_t)mean | (uintptr_t)invstd) & 15)
+    return MMAD_EBADSHAPE;                        // (16-byte constant loads)
+  q.bny = y;
+  q.bnsc = scale; q.bnsh = shift; q.bnmu = mean; q.bnis = invstd;
+  q.bnparts = parts;
+  switch (route) {
+    case 1: return mmad_lattice_zp::fwd(q, dy, wpt, nullptr, dx, nullptr, stream);
+    case 2: return mmad_lattice8::fwd(q, dy, wpt, nullptr, dx, nullptr, stream);
+    default: return mmad_patch::fwd(q, dy, wpt, nullptr, dx, nullptr, stream);
+  }
+}
+
 int64_t mmad_conv3d_wgrad_workspace(const mmad_conv_desc* d, int dtype) {
   if (!desc_ok(d)) return -1;
   const Geom g = fwd_geom(d, dtype);

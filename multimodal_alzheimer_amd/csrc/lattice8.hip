@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "bnsum.h"
 #include "common.h"
 #include "patchconv.h"
 
@@ -60,6 +61,9 @@ struct L8 {
   const u16* res;
   int relu;
   int D, H, W, nz;                         // ragged grids: extents, planes per class
+  const u16* bny;                          // dgrad: BN-backward sums epilogue (bnsum.h)
+  const float *bnsc, *bnsh, *bnmu, *bnis;
+  float* bnparts;
 };
 
 __device__ __forceinline__ int swz8(int row) { return 3 * ((row >> 3) & 1); }
@@ -341,6 +345,27 @@ __global__ __launch_bounds__(NT8) void lattice8_conv_kernel(L8 g, const u16* __r
   }
   __syncthreads();
   constexpr int CPR = BW / 8;
+  static_assert(NT8 % CPR == 0, "a thread keeps one channel vector in the store loop");
+  if (g.bny != nullptr) {                           // (block-uniform) dgrad + BN-backward sums
+    BnSum bs;
+    bs.init(g.bnsc, g.bnsh, g.bnmu, g.bnis, n0 + (tid % CPR) * 8);
+#pragma unroll
+    for (int hh = 0; hh < PL8 * CPR / NT8; ++hh) {
+      const int qd = tid + NT8 * hh;
+      const int row = qd / CPR, c8 = qd % CPR;
+      const int64_t dv = dst_vox(row);
+      if (RAG && dv < 0) continue;
+      const int64_t o = dv * g.Nd + n0 + c8 * 8;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
+                                                      row * CROW8 + c8 * 16);
+      const u32x4 yv = *reinterpret_cast<const u32x4*>(g.bny + o);
+      *reinterpret_cast<u32x4*>(dst + o) = v;
+      bs.add(v, yv);
+    }
+    __syncthreads();                                // ctile reads done: reuse it below
+    bnsum_flush(bs, reinterpret_cast<float*>(smem), CPR, NT8, g.bnparts, n * NZ + tz, g.Nd, n0);
+    return;
+  }
 #pragma unroll
   for (int hh = 0; hh < PL8 * CPR / NT8; ++hh) {
     const int qd = tid + NT8 * hh;
@@ -483,6 +508,11 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
   g.res = reinterpret_cast<const u16*>(q.res);
   g.relu = q.relu;
   g.D = q.Ds; g.H = q.Hs; g.W = q.Ws; g.nz = nz;
+  g.bny = reinterpret_cast<const u16*>(q.bny);
+  g.bnsc = q.bnsc; g.bnsh = q.bnsh; g.bnmu = q.bnmu; g.bnis = q.bnis;
+  g.bnparts = q.bnparts;
+  if (g.bny != nullptr && (stats != nullptr || g.res != nullptr || g.relu || bias != nullptr))
+    return MMAD_EUNSUPPORTED;                       // (one epilogue at a time)
   const int64_t nblk = (int64_t)q.nb * nz * g.nbn;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(NT8), LDS8, as_stream(stream), g,

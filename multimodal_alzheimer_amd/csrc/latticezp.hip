@@ -37,6 +37,7 @@
 #include <type_traits>
 #include <utility>
 
+#include "bnsum.h"
 #include "common.h"
 #include "patchconv.h"
 #include "pointwise.h"
@@ -84,6 +85,9 @@ struct ZG {
   int xcd2;                                 // two channel tiles per XCD (see the tile map)
   const u16* res;
   int relu;
+  const u16* bny;                           // dgrad: BN-backward sums epilogue (bnsum.h)
+  const float *bnsc, *bnsh, *bnmu, *bnis;
+  float* bnparts;
 };
 
 __device__ __forceinline__ int swz(int row) { return 3 * ((row >> 3) & 1); }
@@ -115,9 +119,17 @@ __device__ constexpr int frag_pos() {
   return (I + KY) * S + ((I + WM) & 3) + KX;
 }
 constexpr int NF = 8;                     // A fragments per wave: 2 planes x 4 positions
+// timing skeletons (wrong results): 1 = only the kx = -1 A fragments are read, 2 = no A
+// reads, 3 = no A / B reads and no stage waits or barriers
+#ifndef ZP_SKEL
+#define ZP_SKEL 0
+#endif
 
 template <int TN, int KX>
 __device__ __forceinline__ void read_b(const char* bsl, bf16x8 (&b)[TN]) {
+#if ZP_SKEL >= 3
+  return;
+#endif
 #pragma unroll
   for (int j = 0; j < TN; ++j)
     b[j] = *reinterpret_cast<const bf16x8*>(bsl + (KX + 1) * ZC<TN>::BTAP + j * 16 * RBL);
@@ -127,7 +139,9 @@ __device__ __forceinline__ void read_b(const char* bsl, bf16x8 (&b)[TN]) {
 template <int WM, int P, int KZ, int KY, int KX, int F>
 __device__ __forceinline__ void read_a(const char* const (&pl)[3], bf16x8 (&a)[NF]) {
   constexpr int L = F / 4, I = F % 4;
-  if constexpr (frag_ok<WM, P, KZ, KY, KX, L, I>()) {
+  // ZP_SKEL 1 (timing skeleton, wrong results): only the kx = -1 fragments are read
+  if constexpr (frag_ok<WM, P, KZ, KY, KX, L, I>() && (ZP_SKEL != 1 || KX == -1) &&
+                ZP_SKEL < 2) {
     constexpr int ps = frag_pos<WM, I, KY, KX>();
     a[F] = *reinterpret_cast<const bf16x8*>(pl[plane_idx<P, L, KZ>()] + ps * 16 * RBL);
   }
@@ -346,14 +360,15 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
         {
           constexpr int YF = zp_younger(P, R, MORE, true, C::WI, PI);
           constexpr int YO = zp_younger(P, R, MORE, false, C::WI, PI);
-          if constexpr (YF == YO) {
+          if constexpr (ZP_SKEL >= 3) {
+          } else if constexpr (YF == YO) {
             wait_vm_lgkm0<YO>();
           } else {
             if (c == 0) wait_vm_lgkm0<YF>();
             else wait_vm_lgkm0<YO>();
           }
         }
-        raw_barrier();
+        if constexpr (ZP_SKEL < 3) raw_barrier();
         auto dma = [&]() {
           if constexpr (P == 0) {
             if constexpr (R == 0) {
@@ -435,6 +450,26 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
   }
   __syncthreads();
   constexpr int CPR = C::BW / 8;
+  static_assert(NTHR % CPR == 0, "a thread keeps one channel vector in the store loop");
+  if (g.bny != nullptr) {                           // (block-uniform) dgrad + BN-backward sums
+    BnSum bs;
+    bs.init(g.bnsc, g.bnsh, g.bnmu, g.bnis, n0 + (tid % CPR) * 8);
+#pragma unroll 4
+    for (int hh = 0; hh < ROWS * CPR / NTHR; ++hh) {
+      const int qd = tid + NTHR * hh;
+      const int row = qd / CPR, c8 = qd % CPR;
+      const int64_t o = dst_vox(row) * g.Nd + n0 + c8 * 8;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
+                                                      row * C::CROW + c8 * 16);
+      const u32x4 yv = *reinterpret_cast<const u32x4*>(g.bny + o);
+      *reinterpret_cast<u32x4*>(dst + o) = v;
+      bs.add(v, yv);
+    }
+    __syncthreads();                                // ctile reads done: reuse it below
+    bnsum_flush(bs, reinterpret_cast<float*>(smem), CPR, NTHR, g.bnparts, gid * 2 + pair, g.Nd,
+                n0);
+    return;
+  }
 #pragma unroll 4
   for (int hh = 0; hh < ROWS * CPR / NTHR; ++hh) {
     const int qd = tid + NTHR * hh;
@@ -531,6 +566,11 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
   g.nbn = q.Nd / (w ? 128 : 64);
   g.res = reinterpret_cast<const u16*>(q.res);
   g.relu = q.relu;
+  g.bny = reinterpret_cast<const u16*>(q.bny);
+  g.bnsc = q.bnsc; g.bnsh = q.bnsh; g.bnmu = q.bnmu; g.bnis = q.bnis;
+  g.bnparts = q.bnparts;
+  if (g.bny != nullptr && (stats != nullptr || g.res != nullptr || g.relu || bias != nullptr))
+    return MMAD_EUNSUPPORTED;                       // (one epilogue at a time)
   const int64_t nblk = mmad_lattice_zp::tiles(q) * g.nbn;
   static const int xcd2 = [] { const char* e = getenv("MMAD_ZP_XCD2"); return e ? atoi(e) : 1; }();
   g.xcd2 = xcd2 && g.nbn == 4 && (nblk / 4) % 4 == 0 && nblk % 8 == 0 ? 1 : 0;

@@ -14,6 +14,15 @@ struct Geo {
   int KD, KH, KW, pd, ph, pw, dd, dh, dw;
   const void* res = nullptr;      // eval-mode epilogue: residual (output-shaped) and ReLU
   int relu = 0;
+  // dgrad epilogue (bnsum.h): the BN-backward partial sums of the BN+ReLU whose output was
+  // this conv's input -- its input y (output-shaped), scale / shift (the ReLU mask), mean /
+  // invstd, and the partial rows [tiles][2][Nd] to write (bny == nullptr: off)
+  const void* bny = nullptr;
+  const float* bnsc = nullptr;
+  const float* bnsh = nullptr;
+  const float* bnmu = nullptr;
+  const float* bnis = nullptr;
+  float* bnparts = nullptr;
 };
 // true when the geometry is handled (and the kernel is switched on, MMAD_PATCH)
 bool ok(const Geo& g);

@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "bnsum.h"
 #include "common.h"
 #include "patchconv.h"
 
@@ -58,6 +59,9 @@ struct PG {
   int ring_off;              // LDS byte offset of the weight ring
   const u16* res;            // eval-mode epilogue extras (see patchconv.h)
   int relu;
+  const u16* bny;            // dgrad: BN-backward sums epilogue (bnsum.h)
+  const float *bnsc, *bnsh, *bnmu, *bnis;
+  float* bnparts;
 };
 
 __device__ const u32x4 g_zero16[8] = {};
@@ -270,6 +274,28 @@ __global__ __launch_bounds__(WGM * WGN * 64) void patch_conv_kernel(PG g, const 
   constexpr int CPR = BN / 8;
   u16* __restrict__ dstb = dst + vbase * g.Nd + n0;
   const u16* __restrict__ resb = g.res != nullptr ? g.res + vbase * g.Nd + n0 : nullptr;
+  static_assert(NTHR % CPR == 0, "a thread keeps one channel vector in the store loop");
+  if (g.bny != nullptr) {                      // (block-uniform) dgrad + BN-backward sums
+    BnSum bs;
+    bs.init(g.bnsc, g.bnsh, g.bnmu, g.bnis, n0 + (tid % CPR) * 8);
+    const u16* __restrict__ yb = g.bny + vbase * g.Nd + n0;
+#pragma unroll
+    for (int h = 0; h < TV * CPR / NTHR; ++h) {
+      const int q = tid + NTHR * h;
+      const int row = q / CPR, c8 = q % CPR;
+      if (row_ok(row)) {
+        const int o = row_off(row) * g.Nd + c8 * 8;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(ctile) +
+                                                        row * CROW + c8 * 16);
+        const u32x4 yv = *reinterpret_cast<const u32x4*>(yb + o);
+        *reinterpret_cast<u32x4*>(dstb + o) = v;
+        bs.add(v, yv);
+      }
+    }
+    __syncthreads();                           // ctile reads done: reuse it below
+    bnsum_flush(bs, reinterpret_cast<float*>(smem), CPR, NTHR, g.bnparts, mt, g.Nd, n0);
+    return;
+  }
 #pragma unroll
   for (int h = 0; h < TV * CPR / NTHR; ++h) {
     const int q = tid + NTHR * h;
@@ -349,6 +375,9 @@ PG make_pg(const mmad_patch::Geo& q, int TZ) {
   g.ring_off = g.prow8 * 1024;
   g.res = reinterpret_cast<const u16*>(q.res);
   g.relu = q.relu;
+  g.bny = reinterpret_cast<const u16*>(q.bny);
+  g.bnsc = q.bnsc; g.bnsh = q.bnsh; g.bnmu = q.bnmu; g.bnis = q.bnis;
+  g.bnparts = q.bnparts;
   return g;
 }
 
@@ -405,6 +434,8 @@ int fwd(const Geo& q, const void* src, const void* wp, const float* bias, void* 
   if (mmad_patchz::ok(q)) return mmad_patchz::fwd(q, src, wp, bias, dst, stats, stream);
   const int tz = tz_for(q);
   const PG g = make_pg(q, tz);
+  if (g.bny != nullptr && (stats != nullptr || g.res != nullptr || g.relu || bias != nullptr))
+    return MMAD_EUNSUPPORTED;                  // (one epilogue at a time)
   hipStream_t st = as_stream(stream);
   if (tz == 4) return launch<64, 8, 1, 3, 4>(g, src, wp, bias, dst, stats, st);
   return launch<64, 4, 1, 3, 2>(g, src, wp, bias, dst, stats, st);

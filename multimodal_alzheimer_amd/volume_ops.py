@@ -14,6 +14,7 @@ Reference ops replaced (file:line in the reference tree):
 """
 import ctypes as C
 import os
+import weakref
 
 import torch
 
@@ -450,6 +451,10 @@ class _Conv3dFn(torch.autograd.Function):
         else:
             _check_vol(x, cdtype)
             src = x
+        ctx.bnsum = None
+        if BNSUM and _BNSUM_SRC and ctx.needs_input_grad[0] and cdtype == torch.bfloat16 \
+                and isinstance(x, torch.Tensor):
+            ctx.bnsum = _bnsum_source(x, d, dt)
         wp, wpt = packed if packed is not None else (None, None)
         if wp is None:
             wp = pack_weight(d, dt, wsrc, cdtype, False)
@@ -500,7 +505,18 @@ class _Conv3dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             wpt = ctx.wpt if ctx.wpt is not None else pack_weight(d, dt, weight, cdtype, True)
             dx = _empty_vol(d.n, d.ci, d.di, d.hi, d.wi, cdtype, gy.device)
-            L.call("mmad_conv3d_dgrad", d, dt, L.ptr(gy), L.ptr(wpt), L.ptr(dx), L.stream())
+            if ctx.bnsum is not None:
+                # the input's BN backward sums from the dgrad epilogue (see BNSUM above)
+                yb, mu, ist, sc, sh = ctx.bnsum
+                rows = L.load().mmad_conv3d_dgrad_bnsum_rows(d, dt)
+                parts = torch.empty((rows, 2, d.ci), dtype=torch.float32, device=gy.device)
+                L.call("mmad_conv3d_dgrad_bnsum", d, dt, L.ptr(gy), L.ptr(wpt), L.ptr(dx),
+                       L.ptr(yb), L.ptr(sc), L.ptr(sh), L.ptr(mu), L.ptr(ist), L.ptr(parts),
+                       L.stream())
+                _BNSUM_PARTS[id(dx)] = (weakref.ref(dx), parts)
+            else:
+                L.call("mmad_conv3d_dgrad", d, dt, L.ptr(gy), L.ptr(wpt), L.ptr(dx),
+                       L.stream())
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             main = torch.cuda.current_stream()
             side = grad_stream(gy.device) if WGRAD_STREAM else main
@@ -778,8 +794,49 @@ def take_twin(x):
 
 
 def clear_twins():
-    """drop twins nobody took (called at the start of each backbone forward)"""
+    """drop twins nobody took (called at the start of each backbone forward); also the
+    BN-backward-sum registrations of the previous step"""
     _TWINS.clear()
+    _BNSUM_SRC.clear()
+    _BNSUM_PARTS.clear()
+
+
+# ---- BN-backward sums from the consumer's dgrad epilogue (round 6) --------------------
+# MedicalNet's BasicBlock runs bn1 -> relu -> conv2; conv2's input gradient is exactly what
+# bn1's backward column-sums.  Where conv2's dgrad route has the epilogue for it
+# (mmad_conv3d_dgrad_bnsum_rows > 0; bnsum.h), the dgrad writes those partial rows itself and
+# the BN backward skips its column-sum pass over g and y:
+#   * _BNActFn.forward (BN+ReLU with the mask taken from y) registers its output;
+#   * _Conv3dFn.forward finds its input registered and keeps the BN's (y, mean, invstd,
+#     scale, shift);
+#   * _Conv3dFn.backward runs mmad_conv3d_dgrad_bnsum and files the parts under the input
+#     gradient it returns;
+#   * _BNActFn.backward uses them when its incoming gradient IS that tensor (any other
+#     gradient -- a sum with a second consumer's, a copy -- takes the column-sum pass).
+# Measured (round 6, profiles/r06/r06e_bnsum_ab.txt, same box, replayed config-2 step): the
+# three column sums go (14.1 + 8.3 + 6.3 us) but the dgrads grow by 12.9 / 4.3 / 4.1 us --
+# their epilogue is the tail of a one-tile-per-CU launch, so the extra read of y (33.5 MB at
+# layer4, all CUs at once) is exposed -- and the applies that follow lose the cache hits the
+# column-sum pass gave them: kernel sum 2987.4 -> 2986.0 us, no gain; loading y ahead of the
+# accumulator staging made it worse (2971.7 -> 2996.7, r06f).  So it is OFF by default;
+# MMAD_BNSUM=1 (or volume_ops.BNSUM = True) switches it on (A/B; tests/test_bnsum_gpu.py
+# checks the fused path either way).
+BNSUM = os.environ.get("MMAD_BNSUM", "0") == "1"
+_BNSUM_SRC = {}          # id(out) -> (weakref(out), (y, mean, invstd, scale, shift))
+_BNSUM_PARTS = {}        # id(dx) -> (weakref(dx), parts)
+
+
+def _bnsum_source(x, d, dt):
+    """the BN+ReLU constants behind conv input x, if its dgrad can fold that BN's sums"""
+    ent = _BNSUM_SRC.get(id(x))
+    if ent is None or ent[0]() is not x:
+        return None
+    return ent[1] if L.load().mmad_conv3d_dgrad_bnsum_rows(d, dt) > 0 else None
+
+
+def _bnsum_parts(g):
+    ent = _BNSUM_PARTS.pop(id(g), None)
+    return ent[1] if ent is not None and ent[0]() is g else None
 
 
 def _sum_grads(g, g2):
@@ -813,18 +870,25 @@ def _mask_from_y_ok(y):
 
 
 def _bn_backward(g, relu_out, y, mean, invstd, gamma, batch_stats, want_gmask,
-                 params=(None, None), mask_affine=None, g2=None):
+                 params=(None, None), mask_affine=None, g2=None, pre_parts=None):
     """BN (+ReLU) backward.  ``mask_affine`` = (scale, shift) of a BN+ReLU without residual:
     the ReLU mask is then recomputed from y (mmad_bn_relu_bwd_*) instead of read from
-    ``relu_out``.  ``g2``: a twin's gradient, summed into g by the kernels."""
+    ``relu_out``.  ``g2``: a twin's gradient, summed into g by the kernels.  ``pre_parts``:
+    the column sums already written by the consumer's dgrad epilogue (BNSUM)."""
     m, c = _rows(y)
     dev = y.device
     dt = L.dtype_code(y.dtype)
     if g2 is not None and (mask_affine is not None or not _mask_from_y_ok(y)):
         g, g2 = _sum_grads(g, g2), None
-    nparts = L.load().mmad_bn_bwd_parts(m, c)
-    parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
-    if mask_affine is not None:
+    if pre_parts is not None:
+        parts = pre_parts
+        nparts = parts.shape[0]
+    else:
+        nparts = L.load().mmad_bn_bwd_parts(m, c)
+        parts = torch.empty((nparts, 2, c), dtype=torch.float32, device=dev)
+    if pre_parts is not None:
+        pass
+    elif mask_affine is not None:
         sc, sh = mask_affine
         L.call("mmad_bn_relu_bwd_reduce", dt, m, c, L.ptr(g), L.ptr(y), L.ptr(mean),
                L.ptr(invstd), L.ptr(sc), L.ptr(sh), L.ptr(parts), L.stream())
@@ -886,7 +950,7 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, parts, gamma, beta, res, res_parts, rgamma, rbeta, cfg):
-        bn, relu, training, rbn, twin = cfg
+        bn, relu, training, rbn, twin, bnsum = cfg
         L.require_device(y)
         rscale = rshift = rmean = rinvstd = None
         rbatch = False
@@ -903,6 +967,8 @@ class _BNActFn(torch.autograd.Function):
                L.ptr(shift), L.ptr(res), L.ptr(rscale), L.ptr(rshift), int(relu), L.ptr(out),
                L.stream())
         masky = relu and res is None and y.dim() == 5 and _mask_from_y_ok(y)
+        if masky and bnsum and not twin and y.dtype == torch.bfloat16:
+            _BNSUM_SRC[id(out)] = (weakref.ref(out), (y, mean, invstd, scale, shift))
         ctx.save_for_backward(y, out if relu and not masky else None, mean, invstd, gamma,
                               res if rbn is not None else None, rmean, rinvstd, rgamma)
         ctx.mask_affine = (scale, shift) if masky else None
@@ -940,9 +1006,11 @@ class _BNActFn(torch.autograd.Function):
                     drb if ctx.needs_input_grad[7] else None, None)
         if g2 is not None and has_rbn:      # per-BN calls below both read g
             g, g2 = _sum_grads(g, g2), None
+        pre = _bnsum_parts(g) if ctx.mask_affine is not None and g2 is None and \
+            _BNSUM_PARTS else None
         dy, dgamma, dbeta, gmask = _bn_backward(g, out, y, mean, invstd, gam, batch,
                                                 has_res and not has_rbn, ctx.params[0],
-                                                ctx.mask_affine, g2)
+                                                ctx.mask_affine, g2, pre)
         dres = drg = drb = None
         if has_rbn:
             rg = None if rgamma is None else rgamma.detach()
@@ -979,7 +1047,8 @@ def batchnorm_act(y, bn, parts=None, relu=False, res=None, res_bn=None, res_part
     out = _BNActFn.apply(y, parts, bn.weight, bn.bias, res, res_parts,
                          None if res_bn is None else res_bn.weight,
                          None if res_bn is None else res_bn.bias,
-                         (bn, relu, training, res_bn, twin))
+                         (bn, relu, training, res_bn, twin,
+                          BNSUM and torch.is_grad_enabled()))
     if twin:
         out, alias = out
         _register_twin(out, alias)
