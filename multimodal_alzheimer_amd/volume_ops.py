@@ -85,6 +85,9 @@ WGRAD_PROBES = {}
 # (``check_deferred_adoption``: an AccumulateGrad that cloned it, or a second contribution
 # summed into it, would have read it before the flush -- that raises).
 _WGRAD_DEFER = {"on": False, "jobs": [], "keep": [], "adopt": []}
+# MMAD_REDUCE_EACH=1 (diagnostic): the queued reductions run one launch per job, so a kernel
+# trace times each conv's share of the batched reduction
+_REDUCE_EACH = os.environ.get("MMAD_REDUCE_EACH", "0") == "1"
 
 
 def _deferrable(wparam):
@@ -139,8 +142,13 @@ def flush_wgrad_reduce():
     jobs = _WGRAD_DEFER["jobs"]
     if not jobs:
         return
-    arr = (L.WgradJob * len(jobs))(*jobs)
-    L.call("mmad_wgrad_reduce_batch", len(jobs), arr, L.stream())
+    if _REDUCE_EACH:                       # diagnostic: one launch per job (per-job timing)
+        for j in jobs:
+            one = (L.WgradJob * 1)(j)
+            L.call("mmad_wgrad_reduce_batch", 1, one, L.stream())
+    else:
+        arr = (L.WgradJob * len(jobs))(*jobs)
+        L.call("mmad_wgrad_reduce_batch", len(jobs), arr, L.stream())
     # (stream-ordered: the workspaces return to the caching allocator only for work queued
     # after this launch)
     jobs.clear()

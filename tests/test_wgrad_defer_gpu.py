@@ -198,3 +198,4 @@ def test_summed_deferred_gradient_raises():
             torch.autograd.backward([y, y2], [gy, gy])
     torch.cuda.synchronize()
     assert not V._WGRAD_DEFER["jobs"] and not V._WGRAD_DEFER["adopt"]
+
