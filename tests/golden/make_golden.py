@@ -746,6 +746,45 @@ def anat_r34_160():
     return out
 
 
+TRI160 = (2, 160, 160, 160)
+
+
+def tri_hparams():
+    """config 5's network: MRI ResNet-34 + PET ResNet-18 + tabular MLP (as
+    tests/test_fusion_configs_gpu._hp("three"))."""
+    return anat_hparams(10, fl_gamma=2, resnet_depth_mri=34, resnet_depth_pet=18)
+
+
+def tri_ref(h):
+    st = dict(h, linear_out=[], conv_out=[], filter_size=[], batchnorm_begin=False,
+              batchnorm_dense=False)
+    return models_ref.TriResNetTabularRef(h, models_ref.AnatCNNRef(dict(st, resnet_depth=34)),
+                                          models_ref.PETResNetRef(dict(st, resnet_depth=18)))
+
+
+@case
+def tri_160():
+    """BASELINE config 5's whole network at its full size (Tri_ResNet_Tabular_Fusion, a build
+    extension: MRI ResNet-34 + PET ResNet-18 + tabular MLP, 2 x 160^3 pairs + 9 tabular
+    features, focal loss gamma 2).  No reference class exists for it, so the "reference" is
+    the oracle restatement (oracle/models_ref.py TriResNetTabularRef) in fp32, with its float64
+    and CPU-autocast bf16 evaluations beside it: the GPU test measures the HIP path against an
+    independent CPU implementation at full size (its branches are pinned to the reference
+    code by pet_r18_160 and, for the ResNet-34 wiring, by anat_r34_160)."""
+    from oracle import tabpfn_standin
+    h = tri_hparams()
+    batch = batch_for(TRI160, 2, 1701, keys=("pet1451", "mri"))
+    batch["tabular"] = tabpfn_standin.training_table(1751, TRI160[0])[0]
+    torch.manual_seed(0)
+    m = tri_ref(h)
+    load_prng_weights(m, 1700)
+    out = {"seed": np.array(1700), "shape": np.array(TRI160)}
+    calibrate_bn(m, batch, out)
+    mixed_head(m, m.cls3, "cls3.", batch, out)
+    run_full_case(m, tri_ref(h), batch, lambda b: m.inputs(b, torch.float64), out)
+    return out
+
+
 def main(names=None):
     install_stubs()
     torch.set_num_threads(min(8, os.cpu_count() or 1))

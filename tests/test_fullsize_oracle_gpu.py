@@ -73,9 +73,15 @@ BUILD = {
                     ("pet1451",), 1501),
     "anat_r34_160": (lambda p: M.Anat_CNN(G.anat_hparams(34, fl_gamma=2, precision=p)),
                      ("mri",), 1601),
+    # config 5's whole network (build extension) against the oracle restatement at 2 x 160^3
+    "tri_160": (lambda p: M.Tri_ResNet_Tabular_Fusion(G.anat_hparams(
+        10, fl_gamma=2, resnet_depth_mri=34, resnet_depth_pet=18, precision=p)),
+        ("pet1451", "mri"), 1701),
 }
-CASES = ["anat_r10_128", "pair_r10_128", "pet_r18_160", "anat_r34_160"]
-IDS = ["config2", "config3", "config5_pet", "config5_mri"]
+CASES = ["anat_r10_128", "pair_r10_128", "pet_r18_160", "anat_r34_160", "tri_160"]
+IDS = ["config2", "config3", "config5_pet", "config5_mri", "config5_tri"]
+# cases whose gradient sums may fall back to the float64 bar (the 36-layer ResNet-34 chain)
+DEEP = ("anat_r34_160", "tri_160")
 
 
 @pytest.fixture(autouse=True)
@@ -97,7 +103,11 @@ def _build(name, precision):
     assert list(m.state_dict()) == [str(k) for k in g["state_dict_keys"]]
     G.load_fixture_weights(m, g)
     shape = tuple(int(v) for v in g["shape"])
-    batch = {k: v.to(DEV) for k, v in G.batch_for(shape, 2, bseed, keys).items()}
+    batch = G.batch_for(shape, 2, bseed, keys)
+    if name == "tri_160":                 # make_golden.tri_160: 9 tabular features
+        from oracle import tabpfn_standin
+        batch["tabular"] = tabpfn_standin.training_table(bseed + 50, shape[0])[0]
+    batch = {k: v.to(DEV) for k, v in batch.items()}
     return g, m.to(DEV), batch
 
 
@@ -150,7 +160,7 @@ def test_full_size_fp32_matches_reference(name):
         st = g["grad/stats/" + pname]
         got = np.array([np.abs(full).sum(), np.sqrt((full * full).sum())])
         # within 2e-3 of the reference's fp32 sums.  Only for the 36-layer ResNet-34 chain
-        # (anat_r34_160, whose "reference" is the oracle's fp32 run), where fp32 noise
+        # (anat_r34_160 / tri_160, whose "reference" is the oracle's fp32 run), where fp32 noise
         # compounds (ReLU masks flipped by pre-activations within fp32 rounding of 0), the
         # float64 sums may stand in: within 2e-3 + the larger of twice the fp32 reference's
         # own deviation from them and a fixed 2e-2 -- a bound that does not depend on this
@@ -158,7 +168,7 @@ def test_full_size_fp32_matches_reference(name):
         st64 = g["grad64/stats/" + pname][1:]
         ok32 = np.all(np.abs(got - st[1:]) <= 2e-3 * np.abs(st[1:]) + 1e-6 * gscale)
         ok64 = False
-        if name == "anat_r34_160":
+        if name in DEEP:
             ref_dev = np.abs(st[1:] - st64) / np.abs(st64)
             ok64 = np.all(np.abs(got - st64) <=
                           (2e-3 + np.maximum(2 * ref_dev, 2e-2)) * np.abs(st64) + 1e-6 * gscale)

@@ -82,3 +82,12 @@ def test_get_avg_activation():
     out = tabular.get_avg_activation(acts, 3, 2)
     np.testing.assert_array_equal(out.numpy(), acts[2:].mean(1).numpy())
     assert out.shape == (3, 4)
+
+
+def test_tri_resnet_tabular_keys_match_oracle_fixture():
+    """config 5's network (Tri_ResNet_Tabular_Fusion) has the state_dict of the oracle
+    restatement its full-size fixture (tri_160) was generated from"""
+    g = G.load("tri_160")
+    m = M.Tri_ResNet_Tabular_Fusion(G.anat_hparams(10, fl_gamma=2, resnet_depth_mri=34,
+                                                   resnet_depth_pet=18))
+    assert list(m.state_dict().keys()) == list(g["state_dict_keys"])
