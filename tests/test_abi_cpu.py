@@ -70,6 +70,21 @@ def test_host_side_shape_queries(lib):
     assert lib.mmad_conv_packed_elems(bad, _lib.F32, 0) == -1
 
 
+def test_wide_stem_routes_by_wgrad_offsets(lib):
+    """Column-tiled stems (wo > 64) take the stem kernels only when the hoisted weight
+    gradient's 32-bit buffer offsets hold (csrc/stem.hip wg2_small): a 400^3 sample (200^3
+    outputs x 64 ch x 2 B < 2^30) stays on the stem (one BN row per block), a 416^3 one
+    (208^3 outputs) goes to the implicit GEMM from the forward on (one row per 128-voxel
+    tile) -- so its backward never meets a stem wgrad that cannot run."""
+    from multimodal_alzheimer_amd.volume_ops import conv_desc
+    w = (64, 1, 7, 7, 7)
+    on = conv_desc((1, 1, 400, 400, 400), w, (2, 2, 2), (3, 3, 3), (1, 1, 1))
+    off = conv_desc((1, 1, 416, 416, 416), w, (2, 2, 2), (3, 3, 3), (1, 1, 1))
+    assert on.wo > 64 and off.wo > 64
+    assert lib.mmad_conv3d_stats_rows(on, _lib.BF16) == 400
+    assert lib.mmad_conv3d_stats_rows(off, _lib.BF16) == 208 ** 3 // 128
+
+
 def test_bad_arguments_are_rejected_without_launching(lib):
     from multimodal_alzheimer_amd.volume_ops import conv_desc
     d = conv_desc((1, 64, 8, 8, 8), (64, 64, 3, 3, 3), (1, 1, 1), (1, 1, 1), (1, 1, 1))
