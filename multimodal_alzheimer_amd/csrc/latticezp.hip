@@ -193,7 +193,11 @@ __host__ __device__ constexpr int zp_younger(int p, int r, bool more, bool first
   return n;
 }
 
-template <int TN>
+// BNS: the dgrad epilogue with the BN-backward sums (g.bny set) -- its own instantiation, so
+// the plain kernels keep their register allocation (compiled into one body, the BN-sum path
+// pushed the stage loops of two wave variants into in-loop scratch reloads, each of which
+// waits out every DMA in flight)
+template <int TN, bool BNS>
 __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __restrict__ src, const u16* __restrict__ wgt,
                        const float* __restrict__ bias, u16* __restrict__ dst,
                        float* __restrict__ stats) {
@@ -451,7 +455,7 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
   __syncthreads();
   constexpr int CPR = C::BW / 8;
   static_assert(NTHR % CPR == 0, "a thread keeps one channel vector in the store loop");
-  if (g.bny != nullptr) {                           // (block-uniform) dgrad + BN-backward sums
+  if constexpr (BNS) {                              // dgrad + BN-backward sums
     BnSum bs;
     bs.init(g.bnsc, g.bnsh, g.bnmu, g.bnis, n0 + (tid % CPR) * 8);
 #pragma unroll 4
@@ -469,7 +473,7 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
     bnsum_flush(bs, reinterpret_cast<float*>(smem), CPR, NTHR, g.bnparts, gid * 2 + pair, g.Nd,
                 n0);
     return;
-  }
+  } else {
 #pragma unroll 4
   for (int hh = 0; hh < ROWS * CPR / NTHR; ++hh) {
     const int qd = tid + NTHR * hh;
@@ -513,6 +517,7 @@ __global__ __launch_bounds__(NTHR) void lattice_zp_kernel(ZG g, const u16* __res
       }
     }
   }
+  }
 }
 
 // MMAD_LATTICE_ZP: 1 (default) plane-pair kernel where it fills the CUs, 0 the one-plane
@@ -553,11 +558,13 @@ int64_t tiles(const mmad_patch::Geo& q) { return (int64_t)q.nb * 8; }
 
 int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* bias, void* dst,
         float* stats, void* stream) {
-  static const bool attr =
-      hipFuncSetAttribute((const void*)lattice_zp_kernel<4>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, ZC<4>::LDS) == hipSuccess &&
-      hipFuncSetAttribute((const void*)lattice_zp_kernel<2>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, ZC<2>::LDS) == hipSuccess;
+  auto lds_attr = [](const void* k, int lds) {
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  };
+  static const bool attr = lds_attr((const void*)lattice_zp_kernel<4, false>, ZC<4>::LDS) &&
+                           lds_attr((const void*)lattice_zp_kernel<2, false>, ZC<2>::LDS) &&
+                           lds_attr((const void*)lattice_zp_kernel<4, true>, ZC<4>::LDS) &&
+                           lds_attr((const void*)lattice_zp_kernel<2, true>, ZC<2>::LDS);
   if (!attr) return MMAD_EUNSUPPORTED;
   const bool w = wide(q);
   ZG g{};
@@ -574,14 +581,18 @@ int fwd(const mmad_patch::Geo& q, const void* src, const void* wp, const float* 
   const int64_t nblk = mmad_lattice_zp::tiles(q) * g.nbn;
   static const int xcd2 = [] { const char* e = getenv("MMAD_ZP_XCD2"); return e ? atoi(e) : 1; }();
   g.xcd2 = xcd2 && g.nbn == 4 && (nblk / 4) % 4 == 0 && nblk % 8 == 0 ? 1 : 0;
-  if (w)
-    hipLaunchKernelGGL(lattice_zp_kernel<4>, dim3((unsigned)nblk), dim3(NTHR), ZC<4>::LDS,
-                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                       stats);
-  else
-    hipLaunchKernelGGL(lattice_zp_kernel<2>, dim3((unsigned)nblk), dim3(NTHR), ZC<2>::LDS,
-                       as_stream(stream), g, (const u16*)src, (const u16*)wp, bias, (u16*)dst,
-                       stats);
+  auto go = [&](auto kern, int lds) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(NTHR), lds, as_stream(stream), g,
+                       (const u16*)src, (const u16*)wp, bias, (u16*)dst, stats);
+  };
+  const bool bns = g.bny != nullptr;
+  if (w) {
+    if (bns) go(lattice_zp_kernel<4, true>, ZC<4>::LDS);
+    else go(lattice_zp_kernel<4, false>, ZC<4>::LDS);
+  } else {
+    if (bns) go(lattice_zp_kernel<2, true>, ZC<2>::LDS);
+    else go(lattice_zp_kernel<2, false>, ZC<2>::LDS);
+  }
   return launch_status();
 }
 
