@@ -15,6 +15,9 @@
  *   - The library never allocates, frees or synchronises device memory and keeps no
  *     mutable global state: every buffer (including workspaces sized by the
  *     *_workspace / *_parts queries) is owned by the caller.
+ *   - Activation, packed-weight and workspace buffers of the conv entry points are
+ *     16-byte aligned (they move as 16-byte vectors); a misaligned one is refused with
+ *     MMAD_EBADSHAPE before anything is launched.
  *   - Activations are NDHWC ("voxel-major": channels contiguous per voxel) in the
  *     compute dtype (MMAD_F32 or MMAD_BF16); a logical (N,C,D,H,W) torch tensor in
  *     torch.channels_last_3d memory format is exactly this layout.

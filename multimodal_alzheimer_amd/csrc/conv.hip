@@ -1452,6 +1452,13 @@ int big_cfg_for(const Geom& g, int dtype, int64_t m_max, int classes) {
     return g.Nd % 256 == 0 && cdiv(m_max, 256) * classes * (g.Nd / 256) >= 256 ? cfg : 0;
   return g.Nd % 256 == 0 && cdiv(m_max, 128) * classes * (g.Nd / 256) >= 256 ? cfg : 0;
 }
+// every activation / packed-weight operand is moved as 16-byte vectors (and LDS-DMA rows):
+// a misaligned base pointer is refused up front (MMAD_EBADSHAPE) instead of faulting
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+static bool al16(const void* a, const void* b, const void* c) {
+  return al16(a) && al16(b) && al16(c);
+}
+
 // MMAD_STEM=0 routes the MedicalNet stem through the generic implicit GEMM (A/B switch)
 bool stem_kernel_on() {
   static const bool v = [] { const char* e = getenv("MMAD_STEM"); return !e || atoi(e) != 0; }();
@@ -1771,6 +1778,7 @@ int mmad_conv3d_fwd(const mmad_conv_desc* d, int dtype, const void* x, const voi
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!x || !wp || !y) return MMAD_ENULL;
+  if (!al16(x, wp, y)) return MMAD_EBADSHAPE;
   if (unfolded(d) && mmad_stem::fwd_ok(d, dtype) && stem_kernel_on())
     return mmad_stem::fwd(d, x, wp, bias, y, stats, stream);
   const Geom g = fwd_geom(d, dtype);
@@ -1793,6 +1801,7 @@ int mmad_conv3d_fwd_ex(const mmad_conv_desc* d, int dtype, const void* x, const 
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!x || !wp || !y) return MMAD_ENULL;
+  if (!al16(x, wp, y) || !al16(res)) return MMAD_EBADSHAPE;
   if (res == nullptr && !relu) return mmad_conv3d_fwd(d, dtype, x, wp, bias, y, stats, stream);
   if (unfolded(d)) return MMAD_EUNSUPPORTED;     // the stem keeps its own epilogue
   Geom g = fwd_geom(d, dtype);
@@ -1826,6 +1835,7 @@ int mmad_conv3d_dgrad(const mmad_conv_desc* d, int dtype, const void* dy, const 
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!dy || !wpt || !dx) return MMAD_ENULL;
+  if (!al16(dy, wpt, dx)) return MMAD_EBADSHAPE;
   if (unfolded(d)) return MMAD_EUNSUPPORTED;   // the raw input never needs a gradient
   if (mmad_pw::ok(d, dtype)) {
     const int rc = mmad_pw::dgrad(d, dy, wpt, dx, stream);
@@ -1903,6 +1913,7 @@ int mmad_conv3d_dgrad_bnsum(const mmad_conv_desc* d, int dtype, const void* dy, 
   if (route == 0) return MMAD_EUNSUPPORTED;
   if (((uintptr_t)scale | (uintptr_t)shift | (uintptr_t)mean | (uintptr_t)invstd) & 15)
     return MMAD_EBADSHAPE;                        // (16-byte constant loads)
+  if (!al16(dy, wpt, dx) || !al16(y)) return MMAD_EBADSHAPE;
   q.bny = y;
   q.bnsc = scale; q.bnsh = shift; q.bnmu = mean; q.bnis = invstd;
   q.bnparts = parts;
@@ -1967,6 +1978,7 @@ int conv3d_wgrad(const mmad_conv_desc* d, int dtype, const void* x, const void* 
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (dtype != MMAD_F32 && dtype != MMAD_BF16) return MMAD_EBADDTYPE;
   if (!x || !dy || !dw || !workspace) return MMAD_ENULL;
+  if (!al16(x, dy, workspace)) return MMAD_EBADSHAPE;
   const Geom g = fwd_geom(d, dtype);
   if (!geom_ok(g, dtype) || g.Nd % (dtype == MMAD_BF16 ? 8 : 4)) return MMAD_EUNSUPPORTED;
   void* const stream = st;
@@ -2174,6 +2186,7 @@ int mmad_conv3d_fwd_raw(const mmad_conv_desc* d, int in_dtype, const void* x, in
                         void* stream) {
   if (!desc_ok(d)) return MMAD_EBADSHAPE;
   if (!x || !w_packed || !y) return MMAD_ENULL;
+  if (!al16(x, w_packed, y)) return MMAD_EBADSHAPE;
   if (!mmad_stem_raw_ok(d, in_dtype, dtype)) return MMAD_EUNSUPPORTED;
   return mmad_stem::fwd(d, x, w_packed, bias, y, stats, stream, in_dtype);
 }

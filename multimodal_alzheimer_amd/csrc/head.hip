@@ -614,7 +614,7 @@ int mmad_abi_version(void) { return MMAD_ABI_VERSION; }
 const char* mmad_strerror(int s) {
   switch (s) {
     case MMAD_OK: return "ok";
-    case MMAD_EBADSHAPE: return "bad shape / descriptor";
+    case MMAD_EBADSHAPE: return "bad shape / descriptor / buffer alignment";
     case MMAD_EBADDTYPE: return "unsupported dtype";
     case MMAD_ENULL: return "null pointer argument";
     case MMAD_EUNSUPPORTED: return "unsupported configuration";

@@ -91,3 +91,10 @@ def test_bad_arguments_are_rejected_without_launching(lib):
     assert lib.mmad_conv3d_fwd(d, 7, None, None, None, None, None, None) == 1002
     assert lib.mmad_conv3d_fwd(d, _lib.F32, None, None, None, None, None, None) == 1003
     assert lib.mmad_loss_fwd(0, 2, None, None, None, 0.0, 0, None, None, None) == 1001
+    # a misaligned operand is refused before anything is launched (16-byte vector moves);
+    # the pointer values are never dereferenced here
+    assert lib.mmad_conv3d_fwd(d, _lib.BF16, 0x1008, 0x2000, None, 0x3000, None, None) == 1001
+    assert lib.mmad_conv3d_dgrad(d, _lib.BF16, 0x1000, 0x2004, 0x3000, None) == 1001
+    assert lib.mmad_conv3d_wgrad(d, _lib.BF16, 0x1000, 0x2000, 0x3000, None, 0x4002,
+                                 None) == 1001
+    assert b"alignment" in lib.mmad_strerror(1001)
