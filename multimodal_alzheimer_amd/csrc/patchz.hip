@@ -176,6 +176,13 @@ __global__ __launch_bounds__(NTHR) void patchz_conv_kernel(PZ g, const u16* __re
 
   f32x4 acc[2][4];
   bf16x8 fa0[2], fb0[4], fa1[2], fb1[4];
+#if defined(PZ_NO_AREAD) || defined(PZ_NO_BREAD)
+  // (skeletons: the skipped fragments start as opaque register contents, so the MFMAs stay)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { asm volatile("" : "=v"(fa0[i])); asm volatile("" : "=v"(fa1[i])); }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { asm volatile("" : "=v"(fb0[j])); asm volatile("" : "=v"(fb1[j])); }
+#endif
   // fragments of K half K of tap T of the box whose first plane is q0
   auto read_frags = [&](auto tc, auto kc, int q0, int gt, bf16x8 (&A)[2], bf16x8 (&B)[4])
       __attribute__((always_inline)) {
@@ -185,12 +192,16 @@ __global__ __launch_bounds__(NTHR) void patchz_conv_kernel(PZ g, const u16* __re
     int wbase = __builtin_amdgcn_readfirstlane(RING_OFF + (gt & (NST - 1)) * WSLOT);
     asm volatile("" : "+s"(pbase), "+s"(wbase));
     const char* pa = smem + pbase + aoff[kx][K] + ky * PX * RB;
+#ifndef PZ_NO_AREAD   // timing skeleton (tools): no A fragment reads (stale registers)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       A[i] = *reinterpret_cast<const bf16x8*>(pa + i * 2 * PX * RB);
+#endif
     const char* pb = smem + wbase + boff[K];
+#ifndef PZ_NO_BREAD   // timing skeleton (tools): no B fragment reads (stale registers)
 #pragma unroll
     for (int j = 0; j < 4; ++j) B[j] = *reinterpret_cast<const bf16x8*>(pb + j * 16 * RB);
+#endif
   };
   auto mma = [&](const bf16x8 (&A)[2], const bf16x8 (&B)[4]) __attribute__((always_inline)) {
 #ifdef PZ_NO_MMA   // timing skeleton (tools): fragments consumed, no MFMA
