@@ -47,6 +47,18 @@ PartPlan part_plan(int64_t M) {
 // to gsum (the pool backward's input).
 // GB (DUAL only): g is a global-average-pool gradient given compactly as [N][C] rows, row r of
 // the BN input reading g[r / gS] (the pooled gradient's broadcast is never materialised)
+#ifndef BN_FOLD_PROBE
+#define BN_FOLD_PROBE 0
+#endif
+#if BN_FOLD_PROBE
+// BN-finalize fold measurement (build flag, never the default): after its partial rows every
+// block releases them and arrives on its 32-block group's counter; the group's last arriver
+// acquires and re-reads the group's rows -- the first level of a producer-side fold -- and
+// re-arms the counter.  The result goes to g_fold_sink so the reads stay.
+__device__ int g_fold_cnt[4096];
+__device__ float g_fold_sink[4096];
+#endif
+
 template <typename T, int MODE, int V, bool DUAL = false, bool G2 = false, bool GB = false>
 __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t rpp,
                                                      const T* __restrict__ y,
@@ -224,6 +236,29 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int C, int64_t r
       parts2[((int64_t)blockIdx.x * 2 + 1) * C + cb + c] = q2q;
     }
   }
+#if BN_FOLD_PROBE
+  __shared__ int last;
+  const int ngx = ((int)gridDim.x + 31) >> 5;
+  const int grp = (int)blockIdx.y * ngx + ((int)blockIdx.x >> 5);
+  const int gsize = min(32, (int)gridDim.x - (((int)blockIdx.x >> 5) << 5));
+  __threadfence();                                   // release this block's rows
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(&g_fold_cnt[grp & 4095], 1) == gsize - 1;
+  __syncthreads();
+  if (last) {
+    __threadfence();                                 // acquire the group's rows
+    for (int c = tid; c < CC; c += 256) {
+      float ss = 0.f, qq = 0.f;
+      const int p0 = ((int)blockIdx.x >> 5) << 5;
+      for (int k = 0; k < gsize; ++k) {
+        ss += parts[((int64_t)(p0 + k) * 2) * C + cb + c];
+        qq += parts[((int64_t)(p0 + k) * 2 + 1) * C + cb + c];
+      }
+      g_fold_sink[(grp * 64 + c) & 4095] = ss + qq;
+    }
+    if (tid == 0) g_fold_cnt[grp & 4095] = 0;          // re-arm
+  }
+#endif
 }
 
 // Fold groups of `group` partial rows into one (fixed order): keeps the finalize short
